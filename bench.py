@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py -- Mpackets/s of device-resident parse + 5-tuple classify on MI355X.
+
+One step = one pass of the hot path (fb_parse_classify_dev: parse_packet_pcap + the per-packet
+part of process_parsed_packet, src/packets.rs:202-802) over one batch of synthetic frames that
+is already resident in HBM.  Default workload = BASELINE.json configs[1] (C2): 1,048,576 x 64-B
+IPv4/TCP frames per GPU.  Batches rotate over R distinct device buffers so the working set
+(> 1 GB) exceeds the 256 MB Infinity Cache and the timing is HBM-bound, not MALL-bound.
+
+Multi-GPU: one process per GPU (torchrun); packets are sharded by index (each rank owns the
+contiguous range [rank*n, (rank+1)*n) of the virtual batch) with no data-path collective
+("scaling": "weak"); torch.distributed (gloo, CPU) only provides the barrier and the max over
+ranks of the timed region.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+WORKLOADS = {
+    2: "C2: 1,048,576 x 64-B IPv4/TCP frames per GPU, device-resident (BASELINE configs[1])",
+    3: "C3: 1,048,576-frame IMIX 64/576/1500 (7:4:1), IPv4+IPv6, TCP+UDP per GPU, device-resident",
+    4: "C4: 10,485,760-frame IMIX batch per GPU, device-resident",
+}
+
+
+def algorithmic_bytes(offsets, n_session, n_dns):
+    """B = sum(min(caplen,128)) + 4 B offset per frame (+1 sentinel)
+    + 56 B per emitted session record + 16 B per DNS record (no class array requested)."""
+    caplen = np.diff(offsets.astype(np.int64))
+    return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
+
+
+def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist):
+    from flodbadd_amd import synth
+    frames, offs = synth.generate(config_id, n, first=rank * n)
+    nbytes = frames.nbytes
+    stream = N.Stream()
+    bufs = []
+    for _ in range(rotate):
+        d_fr = N.DeviceBuffer(nbytes).upload(frames)
+        d_off = N.DeviceBuffer(offs.nbytes).upload(offs)
+        d_out = N.DeviceBuffer(n * N.PKT_OUT_DTYPE.itemsize)
+        d_dns = N.DeviceBuffer(n * N.DNS_OUT_DTYPE.itemsize)
+        d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        bufs.append((d_fr, d_off, d_out, d_dns, d_st))
+
+    def step(i):
+        d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
+        rc = lib.fb_parse_classify_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
+                                       d_st.ptr, stream.ptr)
+        if rc != 0:
+            raise RuntimeError(lib.fb_last_error().decode())
+
+    for i in range(warmup):
+        step(i)
+    stream.sync()
+    st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
+    if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
+        raise RuntimeError("bad batch stats: %s" % st)
+    ev0, ev1 = N.Event(), N.Event()
+    if dist:
+        dist.barrier()
+    stream.sync()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        step(i)
+    ev1.record(stream)
+    stream.sync()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ev_ms = ev0.elapsed_ms(ev1)
+    algo = algorithmic_bytes(offs, st[0]["n_session"], st[0]["n_dns"])
+    # make sure the last step's results are sane too
+    st2 = bufs[(steps - 1) % rotate][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
+    assert st2.tobytes() == st.tobytes()
+    for b in bufs:
+        for x in b:
+            x.free()
+    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo,
+                stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
+
+
+def cpu_baseline(frames, offs, seconds):
+    """The oracle (C restatement of src/packets.rs parse + classify, 1 thread) on the same batch,
+    repeated until `seconds` of CPU work: a bounded sample of the same workload."""
+    from oracle import coracle
+    cfg = coracle.make_cfg(1)  # FlodbaddCapture::new() default filter: GlobalOnly
+    n = len(offs) - 1
+    out = np.zeros(n, dtype=coracle.PKT_OUT_DTYPE)
+    dns = np.zeros(n, dtype=coracle.DNS_OUT_DTYPE)
+    st = np.zeros(1, dtype=coracle.STATS_DTYPE)
+    no, nd = C.c_uint32(), C.c_uint32()
+    L = coracle.lib()
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        L.orc_parse_classify(C.byref(cfg), frames.ctypes.data, frames.nbytes, offs.ctypes.data, n,
+                             out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), None, st.ctypes.data)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=round(passes * n / el / 1e6, 3), unit="Mpackets/s", cores=1, kind="port",
+                sample="%d passes over the %d-frame batch (%.1f s, 1 thread, C restatement oracle/oracle.c)"
+                       % (passes, n, el))
+
+
+def load_traffic(config_id):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(str(config_id), {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--packets", type=int, default=None, help="frames per GPU per step")
+    ap.add_argument("--rotate", type=int, default=None, help="distinct device batches cycled")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C3) measurement")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
+
+    from flodbadd_amd import _native as N
+    lib = N.gpu_lib()
+    ndev = N.device_count()
+    if ndev == 0:
+        raise SystemExit("no HIP device visible")
+    device = local % ndev
+    cfg = N.FbConfig()
+    cfg.abi_version = N.FB_ABI_VERSION
+    cfg.filter = N.FB_FILTER_GLOBAL_ONLY  # FlodbaddCapture::new() default (src/capture.rs:108)
+    cfg.max_batch_packets = 1 << 24
+    N.check(lib.fb_set_device(device))
+    ctx = lib.fb_create(device, C.byref(cfg))
+    if not ctx:
+        raise SystemExit("fb_create failed: %s" % lib.fb_last_error().decode())
+    ctx = C.c_void_p(ctx)
+
+    n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
+    rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
+    main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist)
+    per_launch_s = main_r["ev_ms"] / 1e3 / args.steps
+    achieved = main_r["algo_bytes"] / per_launch_s / 1e9
+    value = world * n * args.steps / main_r["elapsed"] / 1e6
+
+    extra = {}
+    if not args.no_imix and args.config == 2:
+        steps3 = max(args.steps // 2, 10)
+        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist)
+        pl3 = r3["ev_ms"] / 1e3 / steps3
+        extra["imix_c3"] = dict(value=round(world * (1 << 20) * steps3 / r3["elapsed"] / 1e6, 2),
+                                unit="Mpackets/s", ms_per_step=round(r3["elapsed"] * 1e3 / steps3, 4),
+                                roofline_achieved_GBs=round(r3["algo_bytes"] / pl3 / 1e9, 1),
+                                roofline_frac=round(r3["algo_bytes"] / pl3 / 1e9 / HBM_PEAK_GBS, 4),
+                                algo_bytes_per_launch=r3["algo_bytes"])
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(main_r["frames"], main_r["offs"], args.cpu_seconds)
+
+    lib.fb_destroy(ctx)
+    if rank == 0:
+        line = {
+            "metric": "Mpackets/s device-resident header parse + 5-tuple classify, 64B & IMIX frames",
+            "value": round(value, 2),
+            "unit": "Mpackets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(main_r["elapsed"] * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
+            "config": {"workload": WORKLOADS[args.config], "frames_per_gpu_per_step": n,
+                       "rotated_batches": rotate, "filter": "GlobalOnly",
+                       "parallelism": "packet-index shards x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
+                         "algo_bytes_per_launch": main_r["algo_bytes"],
+                         "kernel_ms_per_launch": round(per_launch_s * 1e3, 5)},
+            "cpu_baseline": cpu,
+            "batch_stats": main_r["stats"],
+        }
+        if extra:
+            line["extra"] = extra
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

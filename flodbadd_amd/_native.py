@@ -1,0 +1,243 @@
+"""ctypes binding of include/flodbadd_gpu.h (libflodbadd_gpu.so) + numpy record dtypes.
+
+The GPU library is the product path: there is no CPU fallback.  `gpu_lib()` raises
+NativeLibraryMissing if the in-tree .so is absent, and fb_create fails loudly without a gfx950.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+GPU_LIB_PATH = os.path.join(PKG, "libflodbadd_gpu.so")
+SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
+
+FB_ABI_VERSION = 1
+FB_MAX_BATCH_PACKETS = 1 << 30
+FB_MAX_LAN_V6 = 64
+FB_MAX_OWN_IPS = 64
+
+# fb_err
+FB_OK, FB_ERR_INVAL, FB_ERR_NOMEM, FB_ERR_HIP, FB_ERR_NODEV, FB_ERR_TABLE_FULL, FB_ERR_INTERNAL = 0, -1, -2, -3, -4, -5, -6
+# fb_filter (SessionFilter discriminants, src/sessions.rs:173-178)
+FB_FILTER_LOCAL_ONLY, FB_FILTER_GLOBAL_ONLY, FB_FILTER_ALL = 0, 1, 2
+# fb_class
+FB_CLASS_SESSION, FB_CLASS_DNS, FB_CLASS_DROP, FB_CLASS_FILTERED = 0, 1, 2, 3
+# fb_meta_bits
+META_HAS_FLAGS, META_SWAP, META_ORIGINATOR = 1, 2, 4
+META_LOCAL_SRC, META_LOCAL_DST, META_SELF_SRC, META_SELF_DST, META_DST_SERVICE = 8, 16, 32, 64, 128
+
+KEY_FIELDS = [("src_ip", "<u4", (4,)), ("dst_ip", "<u4", (4,)), ("src_port", "<u2"), ("dst_port", "<u2"),
+              ("protocol", "u1"), ("family", "u1"), ("padding", "<u2")]
+PKT_OUT_DTYPE = np.dtype(KEY_FIELDS + [
+    ("packet_length", "<u4"), ("ip_packet_length", "<u4"), ("tcp_flags", "u1"), ("meta", "u1"),
+    ("hist_char", "u1"), ("reserved", "u1"), ("pkt_index", "<u4")])
+DNS_OUT_DTYPE = np.dtype([("pkt_index", "<u4"), ("payload_offset", "<u4"), ("payload_length", "<u4"),
+                          ("protocol", "u1"), ("family", "u1"), ("reserved", "<u2")])
+STATS_FIELDS = ["total_processed", "tcp_processed", "udp_processed", "ipv4_processed", "ipv6_processed",
+                "new_sessions", "updated_sessions", "n_session", "n_dns", "n_drop", "n_filtered",
+                "bad_offsets", "error", "reserved0", "reserved1", "reserved2"]
+STATS_DTYPE = np.dtype([(f, "<u8") for f in STATS_FIELDS])
+FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
+    ("outbound_bytes", "<u8"), ("inbound_bytes", "<u8"), ("orig_pkts", "<u8"), ("resp_pkts", "<u8"),
+    ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8")])
+LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
+FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
+
+assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16
+assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 88
+assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
+
+
+class FbConfig(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("filter", C.c_uint32), ("service_bitmap", C.c_void_p),
+                ("lan_v6", C.c_void_p), ("n_lan_v6", C.c_uint32), ("n_own_ips", C.c_uint32),
+                ("own_ips", C.c_void_p), ("flow_capacity", C.c_uint64), ("max_batch_packets", C.c_uint32),
+                ("reserved0", C.c_uint32), ("max_batch_bytes", C.c_uint64)]
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+class FbError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("fb error %d: %s" % (code, msg))
+        self.code = code
+
+
+# Every symbol include/flodbadd_gpu.h declares: (name, restype, argtypes).
+_P, _U32, _U64, _I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+_PU32, _PU64 = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+GPU_SYMBOLS = [
+    ("fb_abi_version", _U32, []),
+    ("fb_last_error", C.c_char_p, []),
+    ("fb_create", _P, [_I, C.POINTER(FbConfig)]),
+    ("fb_destroy", _I, [_P]),
+    ("fb_set_filter", _I, [_P, _U32]),
+    ("fb_set_service_bitmap", _I, [_P, _P]),
+    ("fb_set_lan_v6", _I, [_P, _P, _U32]),
+    ("fb_set_own_ips", _I, [_P, _P, _U32]),
+    ("fb_parse_classify_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_parse_classify", _I, [_P, _P, _U64, _P, _U32, _P, _PU32, _P, _PU32, _P, _P, _P]),
+    ("fb_flow_update_dev", _I, [_P, _P, _P, _P]),
+    ("fb_process_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_flow_count", _I, [_P, _PU64, _P]),
+    ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
+    ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),
+    ("fb_flow_clear", _I, [_P, _P]),
+    ("fb_flow_hash", _U64, [_P]),
+    ("fb_dev_alloc", _I, [C.POINTER(C.c_void_p), _U64]),
+    ("fb_dev_free", _I, [_P]),
+    ("fb_host_alloc_pinned", _I, [C.POINTER(C.c_void_p), _U64]),
+    ("fb_host_free_pinned", _I, [_P]),
+    ("fb_memcpy_h2d", _I, [_P, _P, _U64, _P]),
+    ("fb_memcpy_d2h", _I, [_P, _P, _U64, _P]),
+    ("fb_memset_dev", _I, [_P, _I, _U64, _P]),
+    ("fb_stream_create", _I, [C.POINTER(C.c_void_p)]),
+    ("fb_stream_destroy", _I, [_P]),
+    ("fb_stream_sync", _I, [_P]),
+    ("fb_event_create", _I, [C.POINTER(C.c_void_p)]),
+    ("fb_event_destroy", _I, [_P]),
+    ("fb_event_record", _I, [_P, _P]),
+    ("fb_event_elapsed_ms", _I, [C.POINTER(C.c_float), _P, _P]),
+    ("fb_device_count", _I, [C.POINTER(C.c_int)]),
+    ("fb_set_device", _I, [_I]),
+]
+
+_gpu = None
+
+
+def gpu_lib():
+    """Load libflodbadd_gpu.so (raises NativeLibraryMissing if it was not built)."""
+    global _gpu
+    if _gpu is None:
+        if not os.path.exists(GPU_LIB_PATH):
+            raise NativeLibraryMissing(
+                "%s is missing: run `python -m flodbadd_amd.build` (there is no CPU fallback)" % GPU_LIB_PATH)
+        lib = C.CDLL(GPU_LIB_PATH)
+        for name, res, args in GPU_SYMBOLS:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.fb_abi_version() != FB_ABI_VERSION:
+            raise NativeLibraryMissing("ABI version mismatch")
+        _gpu = lib
+    return _gpu
+
+
+def check(rc):
+    if rc != FB_OK:
+        raise FbError(rc, gpu_lib().fb_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(a):
+    """ctypes void* of a numpy array's buffer (None for None)."""
+    if a is None:
+        return None
+    return C.c_void_p(a.ctypes.data)
+
+
+# ---- small device buffer / stream helpers ----------------------------------------------
+class DeviceBuffer:
+    """Raw device allocation (hipMalloc through the C ABI)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(gpu_lib().fb_dev_alloc(C.byref(p), self.nbytes))
+        self.ptr = p
+
+    def upload(self, arr, stream=None):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        check(gpu_lib().fb_memcpy_h2d(self.ptr, ptr(arr), arr.nbytes, stream))
+        if stream is None:
+            check(gpu_lib().fb_stream_sync(None))
+        return self
+
+    def download(self, arr, nbytes=None, stream=None):
+        nb = arr.nbytes if nbytes is None else int(nbytes)
+        check(gpu_lib().fb_memcpy_d2h(ptr(arr), self.ptr, nb, stream))
+        check(gpu_lib().fb_stream_sync(stream))
+        return arr
+
+    def memset(self, value=0, stream=None):
+        check(gpu_lib().fb_memset_dev(self.ptr, value, self.nbytes, stream))
+
+    def free(self):
+        if self.ptr:
+            gpu_lib().fb_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class PinnedBuffer:
+    """Page-locked host buffer exposed as a numpy uint8 array."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(gpu_lib().fb_host_alloc_pinned(C.byref(p), max(self.nbytes, 1)))
+        self.ptr = p
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(p.value))[: self.nbytes]
+
+    def free(self):
+        if self.ptr:
+            gpu_lib().fb_host_free_pinned(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        p = C.c_void_p()
+        check(gpu_lib().fb_stream_create(C.byref(p)))
+        self.ptr = p
+
+    def sync(self):
+        check(gpu_lib().fb_stream_sync(self.ptr))
+
+    def __del__(self):
+        try:
+            gpu_lib().fb_stream_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self):
+        p = C.c_void_p()
+        check(gpu_lib().fb_event_create(C.byref(p)))
+        self.ptr = p
+
+    def record(self, stream=None):
+        check(gpu_lib().fb_event_record(self.ptr, stream.ptr if isinstance(stream, Stream) else stream))
+
+    def elapsed_ms(self, end):
+        ms = C.c_float()
+        check(gpu_lib().fb_event_elapsed_ms(C.byref(ms), self.ptr, end.ptr))
+        return ms.value
+
+    def __del__(self):
+        try:
+            gpu_lib().fb_event_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+def device_count():
+    n = C.c_int(0)
+    check(gpu_lib().fb_device_count(C.byref(n)))
+    return n.value

@@ -1,0 +1,175 @@
+"""Host-side mirror of the reference's packet path surface, driving the C ABI.
+
+`FlodbaddGpuCapture` stands where `FlodbaddCapture` (src/capture.rs:70-2030) feeds frames to
+`parse_packet_pcap` + `process_parsed_packet` (src/capture.rs:1036-1061): it owns one fb_ctx
+(one per capture interface, like the reference's one processor task per interface), exposes
+the same knobs (`set_filter`/`get_filter`, capture.rs:185; own IPs, capture.rs:964-970;
+`init_local_cache`-style IPv6 LAN prefixes, ip.rs:164-191), and turns batches of frames into
+session records, DNS diversions and per-flow counters on the GPU.
+
+There is no CPU path: every method calls libflodbadd_gpu.so, which requires a gfx950 device.
+"""
+import ctypes as C
+import ipaddress
+
+import numpy as np
+
+from . import _native as N
+from .sessions import SessionFilter, flows_to_sessions, ip_to_words
+
+
+def lan_v6_table(prefixes):
+    """[(ipv6 address, prefix_len)] -> fb_lan_v6 array (apply_mask_v6, src/ip.rs:44-51)."""
+    t = np.zeros(len(prefixes), dtype=N.LAN_V6_DTYPE)
+    for i, (ip, pfx) in enumerate(prefixes):
+        net = ipaddress.IPv6Network("%s/%d" % (ipaddress.IPv6Address(ip), pfx), strict=False)
+        t[i]["net"] = ip_to_words(net.network_address)[0]
+        t[i]["prefix"] = pfx
+    return t
+
+
+def own_ip_table(ips):
+    t = np.zeros(len(ips), dtype=N.FB_IP_DTYPE)
+    for i, ip in enumerate(ips):
+        w, fam = ip_to_words(ip)
+        t[i]["addr"] = w
+        t[i]["family"] = fam
+    return t
+
+
+class BatchResult:
+    def __init__(self, records, dns, cls, stats):
+        self.records = records  # PKT_OUT_DTYPE, packet order
+        self.dns = dns          # DNS_OUT_DTYPE, packet order
+        self.cls = cls          # uint8 per frame (fb_class)
+        self.stats = stats      # dict of fb_batch_stats
+
+
+def stats_dict(arr):
+    return {k: int(arr[0][k]) for k in N.STATS_FIELDS if not k.startswith("reserved")}
+
+
+class FlodbaddGpuCapture:
+    def __init__(self, device=0, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 20,
+                 service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20):
+        lib = N.gpu_lib()
+        self._keep = []
+        cfg = N.FbConfig()
+        cfg.abi_version = N.FB_ABI_VERSION
+        cfg.filter = int(session_filter)
+        if service_bitmap is not None:
+            bm = np.ascontiguousarray(np.frombuffer(bytes(service_bitmap), dtype=np.uint8))
+            assert bm.size == 8192
+            self._keep.append(bm)
+            cfg.service_bitmap = bm.ctypes.data
+        lt = lan_v6_table(list(lan_v6))
+        ot = own_ip_table(list(own_ips))
+        self._keep += [lt, ot]
+        cfg.lan_v6 = lt.ctypes.data if len(lt) else None
+        cfg.n_lan_v6 = len(lt)
+        cfg.own_ips = ot.ctypes.data if len(ot) else None
+        cfg.n_own_ips = len(ot)
+        cfg.flow_capacity = int(flow_capacity)
+        cfg.max_batch_packets = int(max_batch_packets)
+        ctx = lib.fb_create(int(device), C.byref(cfg))
+        if not ctx:
+            raise N.FbError(N.FB_ERR_NODEV, lib.fb_last_error().decode(errors="replace"))
+        self.ctx = C.c_void_p(ctx)
+        self.filter = SessionFilter(session_filter)
+        self.device = device
+        self.flow_capacity = flow_capacity
+
+    # ---- configuration -------------------------------------------------------------------
+    def set_filter(self, flt):
+        N.check(N.gpu_lib().fb_set_filter(self.ctx, int(flt)))
+        self.filter = SessionFilter(flt)
+
+    def get_filter(self):
+        return self.filter
+
+    def set_service_bitmap(self, bitmap):
+        bm = np.ascontiguousarray(np.frombuffer(bytes(bitmap), dtype=np.uint8))
+        assert bm.size == 8192
+        N.check(N.gpu_lib().fb_set_service_bitmap(self.ctx, N.ptr(bm)))
+
+    def set_lan_v6(self, prefixes):
+        t = lan_v6_table(list(prefixes))
+        N.check(N.gpu_lib().fb_set_lan_v6(self.ctx, N.ptr(t) if len(t) else None, len(t)))
+
+    def set_own_ips(self, ips):
+        t = own_ip_table(list(ips))
+        N.check(N.gpu_lib().fb_set_own_ips(self.ctx, N.ptr(t) if len(t) else None, len(t)))
+
+    # ---- packet path -----------------------------------------------------------------------
+    def parse_classify(self, frames, offsets):
+        """Host-memory batch: parse_packet_pcap + per-packet classification for every frame."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n = offsets.size - 1
+        out = np.zeros(max(n, 1), dtype=N.PKT_OUT_DTYPE)
+        dns = np.zeros(max(n, 1), dtype=N.DNS_OUT_DTYPE)
+        cls = np.zeros(max(n, 1), dtype=np.uint8)
+        st = np.zeros(1, dtype=N.STATS_DTYPE)
+        n_out, n_dns = C.c_uint32(0), C.c_uint32(0)
+        N.check(N.gpu_lib().fb_parse_classify(self.ctx, N.ptr(frames), frames.nbytes, N.ptr(offsets), n,
+                                              N.ptr(out), C.byref(n_out), N.ptr(dns), C.byref(n_dns),
+                                              N.ptr(cls), N.ptr(st), None))
+        return BatchResult(out[: n_out.value], dns[: n_dns.value], cls[:n], stats_dict(st))
+
+    def process_frames(self, frames, offsets):
+        """parse + classify + flow-table upsert (the whole process_parsed_packet per frame)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n = offsets.size - 1
+        lib = N.gpu_lib()
+        d_fr = N.DeviceBuffer(max(frames.nbytes, 1)).upload(frames) if frames.nbytes else N.DeviceBuffer(1)
+        d_off = N.DeviceBuffer(offsets.nbytes).upload(offsets)
+        d_out = N.DeviceBuffer(max(n, 1) * N.PKT_OUT_DTYPE.itemsize)
+        d_dns = N.DeviceBuffer(max(n, 1) * N.DNS_OUT_DTYPE.itemsize)
+        d_cls = N.DeviceBuffer(max(n, 1))
+        d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        N.check(lib.fb_process_dev(self.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr,
+                                   d_cls.ptr, d_st.ptr, None))
+        st = d_st.download(np.zeros(1, dtype=N.STATS_DTYPE))
+        sd = stats_dict(st)
+        out = d_out.download(np.zeros(max(sd["n_session"], 1), dtype=N.PKT_OUT_DTYPE),
+                             sd["n_session"] * N.PKT_OUT_DTYPE.itemsize)[: sd["n_session"]]
+        dns = d_dns.download(np.zeros(max(sd["n_dns"], 1), dtype=N.DNS_OUT_DTYPE),
+                             sd["n_dns"] * N.DNS_OUT_DTYPE.itemsize)[: sd["n_dns"]]
+        cls = d_cls.download(np.zeros(max(n, 1), dtype=np.uint8), n)[:n]
+        if sd["error"]:
+            raise N.FbError(N.FB_ERR_INTERNAL, "device error word %d" % sd["error"])
+        return BatchResult(out, dns, cls, sd)
+
+    # ---- session table -----------------------------------------------------------------------
+    def flow_count(self):
+        n = C.c_uint64(0)
+        N.check(N.gpu_lib().fb_flow_count(self.ctx, C.byref(n), None))
+        return n.value
+
+    def export_flows(self):
+        cnt = self.flow_count()
+        out = np.zeros(max(cnt, 1), dtype=N.FLOW_REC_DTYPE)
+        n = C.c_uint64(0)
+        N.check(N.gpu_lib().fb_flow_export(self.ctx, N.ptr(out), cnt, C.byref(n), None))
+        return out[: n.value]
+
+    def get_sessions(self, is_lan=None):
+        """Sessions sorted by the derived Ord of Session (integer counters + derived f64s)."""
+        return flows_to_sessions(self.export_flows(), is_lan)
+
+    def clear_all_sessions(self):
+        """src/capture.rs:396 (`stop()` clears the table, capture.rs:383)."""
+        N.check(N.gpu_lib().fb_flow_clear(self.ctx, None))
+        N.check(N.gpu_lib().fb_stream_sync(None))
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            N.gpu_lib().fb_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,487 @@
+// fb_capi.hip -- C ABI (include/flodbadd_gpu.h) over the gfx950 kernels.
+//
+// Host-side counterpart of the reference capture task's per-packet calls
+// (src/capture.rs:1036-1061 / 1219-1249): a context owns the device-resident configuration
+// (service-port bitmap, filter, IPv6 LAN prefixes, own IPs), the look-back scratch, the flow
+// table and (lazily) host-mode staging buffers.  Every entry point returns an fb_err code;
+// nothing aborts.  No CPU fallback exists: without a gfx950 device fb_create fails.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "fb_internal.h"
+#include "service_ports_default.inc"  // kDefaultServiceBitmap[8192] (generated at build time)
+
+using namespace fbk;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return set_err(FB_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));    \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct fb_ctx {
+    int device = 0;
+    DevConfig* h_cfg = nullptr;  // host shadow
+    DevConfig* d_cfg = nullptr;
+    bool cfg_dirty = true;
+    unsigned long long* d_status = nullptr;
+    uint64_t status_tiles = 0;
+    uint32_t epoch = 0;
+    uint32_t* d_error = nullptr;
+    // flow table
+    FlowSlot* d_table = nullptr;
+    uint64_t table_cap = 0;
+    unsigned long long* d_partials = nullptr;
+    unsigned long long* d_n = nullptr;
+    // host-mode staging
+    uint8_t* s_frames = nullptr;
+    uint64_t s_frames_cap = 0;
+    uint32_t* s_offsets = nullptr;
+    fb_pkt_out* s_out = nullptr;
+    fb_dns_out* s_dns = nullptr;
+    uint8_t* s_cls = nullptr;
+    uint64_t s_pkts_cap = 0;
+    fb_batch_stats* s_stats = nullptr;
+};
+
+static constexpr uint32_t kFlowGrid = 1024;
+
+static int upload_cfg(fb_ctx* c, hipStream_t s) {
+    if (!c->cfg_dirty) return FB_OK;
+    HIP_TRY(hipStreamSynchronize(s));  // nothing on this stream may still read d_cfg
+    HIP_TRY(hipMemcpyAsync(c->d_cfg, c->h_cfg, sizeof(DevConfig), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->cfg_dirty = false;
+    return FB_OK;
+}
+
+static int ensure_status(fb_ctx* c, uint64_t tiles, hipStream_t s) {
+    if (tiles <= c->status_tiles && c->epoch < 0xFFFFFFF0u) return FB_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tiles > c->status_tiles) {
+        if (c->d_status) HIP_TRY(hipFree(c->d_status));
+        c->d_status = nullptr;
+        uint64_t want = std::max<uint64_t>(tiles, 1024);
+        if (hipMalloc(&c->d_status, want * kStatusWords * 8ull) != hipSuccess) {
+            c->status_tiles = 0;
+            return set_err(FB_ERR_NOMEM, "status buffer (%llu tiles)", (unsigned long long)want);
+        }
+        c->status_tiles = want;
+    }
+    HIP_TRY(hipMemset(c->d_status, 0, c->status_tiles * kStatusWords * 8ull));
+    c->epoch = 0;  // epoch 0 is never used by a launch
+    return FB_OK;
+}
+
+static void set_lan(DevConfig* d, const fb_lan_v6* nets, uint32_t n) {
+    d->n_lan_v6 = n;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t p = std::min<uint32_t>(nets[i].prefix, 128u);
+        for (int k = 0; k < 4; ++k) {
+            int bits = (int)p - 32 * k;
+            uint32_t m = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : 0xFFFFFFFFu << (32 - bits));
+            d->lan_v6[i].mask[k] = m;
+            d->lan_v6[i].net[k] = nets[i].net[k] & m;
+        }
+    }
+}
+
+extern "C" {
+
+uint32_t fb_abi_version(void) { return FB_ABI_VERSION; }
+const char* fb_last_error(void) { return g_err; }
+
+int fb_device_count(int* n) {
+    if (!n) return set_err(FB_ERR_INVAL, "n is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = e == hipSuccess ? c : 0;
+    return FB_OK;
+}
+
+fb_ctx* fb_create(int device, const fb_config* cfg) {
+    if (!cfg) { set_err(FB_ERR_INVAL, "cfg is NULL"); return nullptr; }
+    if (cfg->abi_version != FB_ABI_VERSION) {
+        set_err(FB_ERR_INVAL, "abi_version %u != %u", cfg->abi_version, FB_ABI_VERSION);
+        return nullptr;
+    }
+    if (cfg->filter > FB_FILTER_ALL || cfg->n_lan_v6 > FB_MAX_LAN_V6 || cfg->n_own_ips > FB_MAX_OWN_IPS ||
+        (cfg->n_lan_v6 && !cfg->lan_v6) || (cfg->n_own_ips && !cfg->own_ips)) {
+        set_err(FB_ERR_INVAL, "invalid fb_config field");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        set_err(FB_ERR_NODEV, "device %d not available (%d HIP devices)", device, ndev);
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_err(FB_ERR_NODEV, "device %d is not gfx950 (%s)", device, prop.gcnArchName);
+        return nullptr;
+    }
+    DeviceGuard g(device);
+    fb_ctx* c = new (std::nothrow) fb_ctx();
+    if (!c) { set_err(FB_ERR_NOMEM, "fb_ctx"); return nullptr; }
+    c->device = device;
+    c->h_cfg = new (std::nothrow) DevConfig();
+    bool ok = c->h_cfg != nullptr;
+    if (ok) {
+        memset(c->h_cfg, 0, sizeof(DevConfig));
+        memcpy(c->h_cfg->service_bitmap, cfg->service_bitmap ? cfg->service_bitmap : kDefaultServiceBitmap,
+               FB_SERVICE_BITMAP_BYTES);
+        c->h_cfg->filter = cfg->filter;
+        set_lan(c->h_cfg, cfg->lan_v6, cfg->n_lan_v6);
+        c->h_cfg->n_own = cfg->n_own_ips;
+        for (uint32_t i = 0; i < cfg->n_own_ips; ++i) c->h_cfg->own[i] = cfg->own_ips[i];
+    }
+    ok = ok && hipMalloc(&c->d_cfg, sizeof(DevConfig)) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_error, 16) == hipSuccess && hipMemset(c->d_error, 0, 16) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_partials, 2ull * kFlowGrid * 8ull) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_n, 16) == hipSuccess;
+    if (ok && cfg->flow_capacity) {
+        uint64_t cap = 1;
+        while (cap < cfg->flow_capacity) cap <<= 1;
+        c->table_cap = cap;
+        ok = hipMalloc(&c->d_table, cap * sizeof(FlowSlot)) == hipSuccess &&
+             hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess;
+    }
+    if (ok) {
+        uint64_t tiles = ((uint64_t)cfg->max_batch_packets + kTile - 1) / kTile;
+        ok = ensure_status(c, tiles, nullptr) == FB_OK && upload_cfg(c, nullptr) == FB_OK;
+    }
+    if (!ok) {
+        if (g_err[0] == 0) set_err(FB_ERR_NOMEM, "device allocation failed");
+        fb_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+int fb_destroy(fb_ctx* c) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    DeviceGuard g(c->device);
+    (void)hipDeviceSynchronize();
+    hipFree(c->d_cfg);
+    hipFree(c->d_status);
+    hipFree(c->d_error);
+    hipFree(c->d_table);
+    hipFree(c->d_partials);
+    hipFree(c->d_n);
+    hipFree(c->s_frames);
+    hipFree(c->s_offsets);
+    hipFree(c->s_out);
+    hipFree(c->s_dns);
+    hipFree(c->s_cls);
+    hipFree(c->s_stats);
+    delete c->h_cfg;
+    delete c;
+    return FB_OK;
+}
+
+int fb_set_filter(fb_ctx* c, uint32_t filter) {
+    if (!c || filter > FB_FILTER_ALL) return set_err(FB_ERR_INVAL, "bad ctx or filter");
+    if (c->h_cfg->filter != filter) { c->h_cfg->filter = filter; c->cfg_dirty = true; }
+    return FB_OK;
+}
+
+int fb_set_service_bitmap(fb_ctx* c, const uint8_t* bm) {
+    if (!c || !bm) return set_err(FB_ERR_INVAL, "bad ctx or bitmap");
+    memcpy(c->h_cfg->service_bitmap, bm, FB_SERVICE_BITMAP_BYTES);
+    c->cfg_dirty = true;
+    return FB_OK;
+}
+
+int fb_set_lan_v6(fb_ctx* c, const fb_lan_v6* nets, uint32_t n) {
+    if (!c || n > FB_MAX_LAN_V6 || (n && !nets)) return set_err(FB_ERR_INVAL, "bad lan_v6 table");
+    set_lan(c->h_cfg, nets, n);
+    c->cfg_dirty = true;
+    return FB_OK;
+}
+
+int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
+    if (!c || n > FB_MAX_OWN_IPS || (n && !ips)) return set_err(FB_ERR_INVAL, "bad own-ip table");
+    c->h_cfg->n_own = n;
+    for (uint32_t i = 0; i < n; ++i) c->h_cfg->own[i] = ips[i];
+    c->cfg_dirty = true;
+    return FB_OK;
+}
+
+int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes,
+                          const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns,
+                          uint8_t* d_class, fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_stats) return set_err(FB_ERR_INVAL, "ctx and d_stats are required");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "frames_bytes must be < 4 GiB");
+    if (n && !d_offsets) return set_err(FB_ERR_INVAL, "d_offsets is NULL");
+    if (n && frames_bytes && !d_frames) return set_err(FB_ERR_INVAL, "d_frames is NULL");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
+        return FB_OK;
+    }
+    const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
+    int rc = ensure_status(c, tiles, s);
+    if (rc) return rc;
+    rc = upload_cfg(c, s);
+    if (rc) return rc;
+    ParseParams p;
+    p.frames = d_frames;
+    p.offsets = d_offsets;
+    p.out = d_out;
+    p.dns = d_dns;
+    p.cls = d_class;
+    p.stats = d_stats;
+    p.status = c->d_status;
+    p.cfg = c->d_cfg;
+    p.frames_bytes = (uint32_t)frames_bytes;
+    p.n = n;
+    p.num_tiles = (uint32_t)tiles;
+    p.epoch = ++c->epoch;
+    p.error = c->d_error;
+    HIP_TRY(launch_parse_classify(p, s));
+    return FB_OK;
+}
+
+static int ensure_staging(fb_ctx* c, uint64_t n, uint64_t bytes) {
+    if (bytes > c->s_frames_cap) {
+        hipFree(c->s_frames);
+        c->s_frames = nullptr;
+        c->s_frames_cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes, 1 << 20);
+        if (hipMalloc(&c->s_frames, want) != hipSuccess) return set_err(FB_ERR_NOMEM, "staging frames");
+        c->s_frames_cap = want;
+    }
+    if (n > c->s_pkts_cap) {
+        hipFree(c->s_offsets); hipFree(c->s_out); hipFree(c->s_dns); hipFree(c->s_cls);
+        c->s_offsets = nullptr; c->s_out = nullptr; c->s_dns = nullptr; c->s_cls = nullptr;
+        c->s_pkts_cap = 0;
+        uint64_t want = std::max<uint64_t>(n, 4096);
+        if (hipMalloc(&c->s_offsets, (want + 1) * 4) != hipSuccess ||
+            hipMalloc(&c->s_out, want * sizeof(fb_pkt_out)) != hipSuccess ||
+            hipMalloc(&c->s_dns, want * sizeof(fb_dns_out)) != hipSuccess ||
+            hipMalloc(&c->s_cls, want) != hipSuccess)
+            return set_err(FB_ERR_NOMEM, "staging packets");
+        c->s_pkts_cap = want;
+    }
+    if (!c->s_stats && hipMalloc(&c->s_stats, sizeof(fb_batch_stats)) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "staging stats");
+    return FB_OK;
+}
+
+static int check_error_word(fb_ctx* c, hipStream_t s) {
+    uint32_t e = 0;
+    HIP_TRY(hipMemcpyAsync(&e, c->d_error, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (e) {
+        HIP_TRY(hipMemsetAsync(c->d_error, 0, 4, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->epoch = 0xFFFFFFFFu;  // force a scratch reset before the next launch
+        if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full");
+        return set_err(FB_ERR_INTERNAL, "kernel bounded spin expired (code %u)", e);
+    }
+    return FB_OK;
+}
+
+int fb_parse_classify(fb_ctx* c, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
+                      uint32_t n, fb_pkt_out* out, uint32_t* n_out, fb_dns_out* dns, uint32_t* n_dns,
+                      uint8_t* cls, fb_batch_stats* stats, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n too large");
+    if (frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "frames_bytes must be < 4 GiB");
+    if ((n && !offsets) || (frames_bytes && !frames)) return set_err(FB_ERR_INVAL, "NULL input");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_staging(c, n, frames_bytes);
+    if (rc) return rc;
+    if (frames_bytes) HIP_TRY(hipMemcpyAsync(c->s_frames, frames, frames_bytes, hipMemcpyHostToDevice, s));
+    if (n) HIP_TRY(hipMemcpyAsync(c->s_offsets, offsets, (uint64_t)(n + 1) * 4, hipMemcpyHostToDevice, s));
+    rc = fb_parse_classify_dev(c, c->s_frames, frames_bytes, c->s_offsets, n, out ? c->s_out : nullptr,
+                               dns ? c->s_dns : nullptr, cls ? c->s_cls : nullptr, c->s_stats, s);
+    if (rc) return rc;
+    fb_batch_stats st;
+    HIP_TRY(hipMemcpyAsync(&st, c->s_stats, sizeof(st), hipMemcpyDeviceToHost, s));
+    rc = check_error_word(c, s);  // synchronises the stream
+    if (rc) return rc;
+    if (out && st.n_session)
+        HIP_TRY(hipMemcpyAsync(out, c->s_out, st.n_session * sizeof(fb_pkt_out), hipMemcpyDeviceToHost, s));
+    if (dns && st.n_dns)
+        HIP_TRY(hipMemcpyAsync(dns, c->s_dns, st.n_dns * sizeof(fb_dns_out), hipMemcpyDeviceToHost, s));
+    if (cls && n) HIP_TRY(hipMemcpyAsync(cls, c->s_cls, n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n_out) *n_out = (uint32_t)st.n_session;
+    if (n_dns) *n_dns = (uint32_t)st.n_dns;
+    if (stats) *stats = st;
+    return FB_OK;
+}
+
+int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_recs || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_recs and d_stats are required");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    FlowParams p;
+    p.recs = d_recs;
+    p.stats = d_stats;
+    p.table = c->d_table;
+    p.mask = c->table_cap - 1;
+    p.partials = c->d_partials;
+    p.error = c->d_error;
+    p.max_recs = 0xFFFFFFFFu;
+    HIP_TRY(launch_flow_update(p, kFlowGrid, s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, kFlowGrid, c->d_error, s));
+    return FB_OK;
+}
+
+int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                   uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns, uint8_t* d_class,
+                   fb_batch_stats* d_stats, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    if (!d_out) return set_err(FB_ERR_INVAL, "d_out is required");
+    int rc = fb_parse_classify_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_dns, d_class, d_stats, stream);
+    if (rc || n == 0) return rc;
+    return fb_flow_update_dev(c, d_out, d_stats, stream);
+}
+
+int fb_flow_count(fb_ctx* c, uint64_t* n_flows, void* stream) {
+    if (!c || !n_flows) return set_err(FB_ERR_INVAL, "bad arguments");
+    *n_flows = 0;
+    if (!c->d_table) return FB_OK;
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long h = 0;
+    HIP_TRY(hipMemsetAsync(c->d_n, 0, 8, s));
+    HIP_TRY(launch_flow_count(c->d_table, c->table_cap, c->d_n, s));
+    HIP_TRY(hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_flows = h;
+    return FB_OK;
+}
+
+int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n, void* stream) {
+    if (!c || !d_n || (cap && !d_out)) return set_err(FB_ERR_INVAL, "bad arguments");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
+    if (!c->d_table) return FB_OK;
+    HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s));
+    return FB_OK;
+}
+
+int fb_flow_export(fb_ctx* c, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream) {
+    if (!c || !n || (cap && !out)) return set_err(FB_ERR_INVAL, "bad arguments");
+    *n = 0;
+    if (!c->d_table || cap == 0) return FB_OK;
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t total = 0;
+    int rc = fb_flow_count(c, &total, stream);
+    if (rc) return rc;
+    const uint64_t m = std::min(total, cap);
+    if (m == 0) return FB_OK;
+    fb_flow_rec* d_out = nullptr;
+    if (hipMalloc(&d_out, m * sizeof(fb_flow_rec)) != hipSuccess) return set_err(FB_ERR_NOMEM, "export buffer");
+    unsigned long long h = 0;
+    hipError_t e = hipMemsetAsync(c->d_n, 0, 8, s);
+    if (e == hipSuccess) e = launch_flow_export(c->d_table, c->table_cap, d_out, m, c->d_n, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, m * sizeof(fb_flow_rec), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d_out);
+    if (e != hipSuccess) return set_err(FB_ERR_HIP, "flow export: %s", hipGetErrorString(e));
+    *n = std::min<uint64_t>(h, m);
+    return FB_OK;
+}
+
+int fb_flow_clear(fb_ctx* c, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (!c->d_table) return FB_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemsetAsync(c->d_table, 0, c->table_cap * sizeof(FlowSlot), (hipStream_t)stream));
+    return FB_OK;
+}
+
+// ---- device-memory helpers -------------------------------------------------------------
+int fb_dev_alloc(void** p, uint64_t bytes) {
+    if (!p) return set_err(FB_ERR_INVAL, "p is NULL");
+    *p = nullptr;
+    if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess) return set_err(FB_ERR_NOMEM, "hipMalloc(%llu)", (unsigned long long)bytes);
+    return FB_OK;
+}
+int fb_dev_free(void* p) { HIP_TRY(hipFree(p)); return FB_OK; }
+int fb_host_alloc_pinned(void** p, uint64_t bytes) {
+    if (!p) return set_err(FB_ERR_INVAL, "p is NULL");
+    *p = nullptr;
+    if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "hipHostMalloc(%llu)", (unsigned long long)bytes);
+    return FB_OK;
+}
+int fb_host_free_pinned(void* p) { HIP_TRY(hipHostFree(p)); return FB_OK; }
+int fb_memcpy_h2d(void* d, const void* s, uint64_t b, void* st) {
+    HIP_TRY(hipMemcpyAsync(d, s, b, hipMemcpyHostToDevice, (hipStream_t)st));
+    return FB_OK;
+}
+int fb_memcpy_d2h(void* d, const void* s, uint64_t b, void* st) {
+    HIP_TRY(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToHost, (hipStream_t)st));
+    return FB_OK;
+}
+int fb_memset_dev(void* d, int v, uint64_t b, void* st) {
+    HIP_TRY(hipMemsetAsync(d, v, b, (hipStream_t)st));
+    return FB_OK;
+}
+int fb_stream_create(void** st) {
+    if (!st) return set_err(FB_ERR_INVAL, "NULL");
+    HIP_TRY(hipStreamCreateWithFlags((hipStream_t*)st, hipStreamNonBlocking));
+    return FB_OK;
+}
+int fb_stream_destroy(void* st) { HIP_TRY(hipStreamDestroy((hipStream_t)st)); return FB_OK; }
+int fb_stream_sync(void* st) { HIP_TRY(hipStreamSynchronize((hipStream_t)st)); return FB_OK; }
+int fb_event_create(void** ev) {
+    if (!ev) return set_err(FB_ERR_INVAL, "NULL");
+    HIP_TRY(hipEventCreate((hipEvent_t*)ev));
+    return FB_OK;
+}
+int fb_event_destroy(void* ev) { HIP_TRY(hipEventDestroy((hipEvent_t)ev)); return FB_OK; }
+int fb_event_record(void* ev, void* st) { HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)st)); return FB_OK; }
+int fb_event_elapsed_ms(float* ms, void* a, void* b) {
+    if (!ms) return set_err(FB_ERR_INVAL, "NULL");
+    HIP_TRY(hipEventSynchronize((hipEvent_t)b));
+    HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+    return FB_OK;
+}
+int fb_set_device(int d) { HIP_TRY(hipSetDevice(d)); return FB_OK; }
+
+}  // extern "C"

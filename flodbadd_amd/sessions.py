@@ -1,0 +1,162 @@
+"""Host-side session model, mirroring the reference's types (src/sessions.rs).
+
+Only data-model plumbing lives here: converting between the C-ABI `fb_session_key` layout and
+Session objects, derived statistics computed from integer counters, and the post-hoc
+bucket split `filter_sessions` (src/sessions.rs:678-692), which in the reference runs per
+query over the session list, not per packet.  Per-packet work never runs here.
+"""
+import enum
+import ipaddress
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from ._native import (FB_FILTER_ALL, FB_FILTER_GLOBAL_ONLY, FB_FILTER_LOCAL_ONLY, FLOW_REC_DTYPE,
+                      META_DST_SERVICE, META_HAS_FLAGS, META_LOCAL_DST, META_LOCAL_SRC, META_ORIGINATOR,
+                      META_SELF_DST, META_SELF_SRC, META_SWAP, PKT_OUT_DTYPE)
+
+
+class Protocol(enum.IntEnum):
+    """src/sessions.rs:17-21 (derived Ord: TCP < UDP)."""
+    TCP = 6
+    UDP = 17
+
+
+class SessionFilter(enum.IntEnum):
+    """src/sessions.rs:173-178 (same discriminant order)."""
+    LocalOnly = FB_FILTER_LOCAL_ONLY
+    GlobalOnly = FB_FILTER_GLOBAL_ONLY
+    All = FB_FILTER_ALL
+
+
+def ip_to_words(ip):
+    """session_to_key word format (src/l7_ebpf.rs:78-104): v4 numeric in word 0; v6 4 BE words."""
+    ip = ipaddress.ip_address(ip)
+    if ip.version == 4:
+        return (int(ip), 0, 0, 0), 2
+    v = int(ip)
+    return tuple((v >> (96 - 32 * k)) & 0xFFFFFFFF for k in range(4)), 10
+
+
+def words_to_ip(words, family):
+    if family == 2:
+        return ipaddress.IPv4Address(int(words[0]))
+    v = 0
+    for w in words:
+        v = (v << 32) | int(w)
+    return ipaddress.IPv6Address(v)
+
+
+@dataclass(frozen=True, order=False)
+class Session:
+    """The 5-tuple key, src/sessions.rs:23-30."""
+    protocol: Protocol
+    src_ip: object
+    src_port: int
+    dst_ip: object
+    dst_port: int
+
+    def sort_key(self):
+        """Derived Ord: protocol, src_ip (V4 < V6, then octets), src_port, dst_ip, dst_port."""
+        return (int(self.protocol), self.src_ip.version, int(self.src_ip), self.src_port,
+                self.dst_ip.version, int(self.dst_ip), self.dst_port)
+
+    def __lt__(self, other):
+        return self.sort_key() < other.sort_key()
+
+    def reversed(self):
+        return Session(self.protocol, self.dst_ip, self.dst_port, self.src_ip, self.src_port)
+
+    @staticmethod
+    def from_key(rec):
+        fam = int(rec["family"])
+        return Session(Protocol(int(rec["protocol"])), words_to_ip(rec["src_ip"], fam), int(rec["src_port"]),
+                       words_to_ip(rec["dst_ip"], fam), int(rec["dst_port"]))
+
+    def key_fields(self):
+        s, fam = ip_to_words(self.src_ip)
+        d, _ = ip_to_words(self.dst_ip)
+        return s, d, fam
+
+
+@dataclass
+class SessionPacketData:
+    """src/packets.rs:91-98 (per emitted record; raw session = key reversed when swapped)."""
+    session: Session
+    packet_length: int
+    ip_packet_length: int
+    flags: Optional[int]
+
+
+@dataclass
+class SessionStats:
+    """Integer counters of src/sessions.rs:73-96 + the two derived f64s
+    (src/packets.rs:122-135), recomputed from the final counters."""
+    inbound_bytes: int = 0
+    outbound_bytes: int = 0
+    orig_pkts: int = 0
+    resp_pkts: int = 0
+    orig_ip_bytes: int = 0
+    resp_ip_bytes: int = 0
+    history: str = ""
+    conn_state: Optional[str] = None
+
+    @property
+    def average_packet_size(self):
+        tp = self.orig_pkts + self.resp_pkts
+        return (self.inbound_bytes + self.outbound_bytes) / tp if tp > 0 else 0.0
+
+    @property
+    def inbound_outbound_ratio(self):
+        return self.inbound_bytes / self.outbound_bytes if self.outbound_bytes > 0 else 0.0
+
+
+@dataclass
+class SessionInfo:
+    """Subset of src/sessions.rs:40-61 that the GPU path owns."""
+    session: Session
+    stats: SessionStats = field(default_factory=SessionStats)
+    is_local_src: bool = False
+    is_local_dst: bool = False
+
+
+def records_to_packets(recs):
+    """fb_pkt_out records -> SessionPacketData (raw direction restored from the SWAP bit)."""
+    assert recs.dtype == PKT_OUT_DTYPE
+    out = []
+    for r in recs:
+        key = Session.from_key(r)
+        raw = key.reversed() if int(r["meta"]) & META_SWAP else key
+        flags = int(r["tcp_flags"]) if int(r["meta"]) & META_HAS_FLAGS else None
+        out.append(SessionPacketData(raw, int(r["packet_length"]), int(r["ip_packet_length"]), flags))
+    return out
+
+
+def flows_to_sessions(flows, is_lan=None):
+    """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session."""
+    assert flows.dtype == FLOW_REC_DTYPE
+    out = []
+    for r in flows:
+        st = SessionStats(int(r["inbound_bytes"]), int(r["outbound_bytes"]), int(r["orig_pkts"]),
+                          int(r["resp_pkts"]), int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]))
+        s = Session.from_key(r)
+        info = SessionInfo(s, st)
+        if is_lan is not None:
+            info.is_local_src, info.is_local_dst = is_lan(s.src_ip), is_lan(s.dst_ip)
+        out.append(info)
+    out.sort(key=lambda i: i.session.sort_key())
+    return out
+
+
+def filter_sessions(sessions: List[SessionInfo], flt: SessionFilter) -> List[SessionInfo]:
+    """src/sessions.rs:678-692 over SessionInfo.is_local_src/dst (set from the record meta bits)."""
+    if flt == SessionFilter.LocalOnly:
+        return [s for s in sessions if s.is_local_src and s.is_local_dst]
+    if flt == SessionFilter.GlobalOnly:
+        return [s for s in sessions if not (s.is_local_src and s.is_local_dst)]
+    return list(sessions)
+
+
+__all__ = ["Protocol", "SessionFilter", "Session", "SessionPacketData", "SessionStats", "SessionInfo",
+           "ip_to_words", "words_to_ip", "records_to_packets", "flows_to_sessions", "filter_sessions",
+           "META_HAS_FLAGS", "META_SWAP", "META_ORIGINATOR", "META_LOCAL_SRC", "META_LOCAL_DST",
+           "META_SELF_SRC", "META_SELF_DST", "META_DST_SERVICE"]

@@ -1,0 +1,73 @@
+"""Deterministic synthetic capture batches via libfb_synth.so.
+
+Configs (BASELINE.json `configs`):
+  C2: 1M x 64-B IPv4/TCP, flow pool 2^16             -> config_id 2, mode 0
+  C3: 1M IMIX 64/576/1500 (7:4:1), v4/v6, TCP/UDP     -> config_id 3, mode 1
+  C4: 10M IMIX + flow table, pool 2^20 (uniform/Zipf) -> config_id 4, mode 1
+  C5: 80M = 8 x 10M shards by packet index            -> config_id 5, mode 1
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._native import SYNTH_LIB_PATH, NativeLibraryMissing
+
+
+class SynthCfg(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_flows", C.c_uint32), ("mode", C.c_uint32),
+                ("v6_permille", C.c_uint32), ("udp_permille", C.c_uint32), ("dns_permille", C.c_uint32),
+                ("zipf", C.c_uint32), ("zipf_s", C.c_double)]
+
+
+CONFIGS = {
+    2: dict(n_flows=1 << 16, mode=0, v6_permille=0, udp_permille=0, dns_permille=5, zipf=0, zipf_s=1.1),
+    3: dict(n_flows=1 << 16, mode=1, v6_permille=200, udp_permille=300, dns_permille=5, zipf=0, zipf_s=1.1),
+    4: dict(n_flows=1 << 20, mode=1, v6_permille=200, udp_permille=300, dns_permille=5, zipf=0, zipf_s=1.1),
+    5: dict(n_flows=1 << 20, mode=1, v6_permille=200, udp_permille=300, dns_permille=5, zipf=0, zipf_s=1.1),
+}
+
+_lib = None
+
+
+def _synth():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SYNTH_LIB_PATH):
+            raise NativeLibraryMissing("%s missing: run `python -m flodbadd_amd.build`" % SYNTH_LIB_PATH)
+        lib = C.CDLL(SYNTH_LIB_PATH)
+        lib.fb_synth_plan.restype = C.c_uint64
+        lib.fb_synth_plan.argtypes = [C.POINTER(SynthCfg), C.c_uint64, C.c_uint32, C.c_void_p]
+        lib.fb_synth_fill.restype = C.c_int
+        lib.fb_synth_fill.argtypes = [C.POINTER(SynthCfg), C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int]
+        lib.fb_synth_flow_of.restype = C.c_uint32
+        lib.fb_synth_flow_of.argtypes = [C.POINTER(SynthCfg), C.c_uint64]
+        _lib = lib
+    return _lib
+
+
+def make_cfg(config_id, **overrides):
+    d = dict(CONFIGS[config_id])
+    d.update(overrides)
+    return SynthCfg(seed=0xF10DBADD ^ config_id, **d)
+
+
+def generate(config_id, n, first=0, threads=None, frames_out=None, **overrides):
+    """Return (frames uint8[bytes], offsets uint32[n+1]) for packets [first, first+n).
+
+    `frames_out`, if given, is a preallocated uint8 buffer (e.g. pinned) of sufficient size."""
+    cfg = make_cfg(config_id, **overrides)
+    lib = _synth()
+    offsets = np.empty(n + 1, dtype=np.uint32)
+    total = lib.fb_synth_plan(C.byref(cfg), first, n, offsets.ctypes.data)
+    if total >= 1 << 32:
+        raise ValueError("batch exceeds 4 GiB (u32 offsets)")
+    if frames_out is None:
+        frames = np.empty(max(total, 1), dtype=np.uint8)[:total]
+    else:
+        assert frames_out.nbytes >= total
+        frames = frames_out[:total]
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    lib.fb_synth_fill(C.byref(cfg), first, n, offsets.ctypes.data, frames.ctypes.data, threads)
+    return frames, offsets

@@ -1,0 +1,274 @@
+/*
+ * flodbadd_gpu.h -- C ABI of the MI355X (gfx950) packet-parse + flow-classification path.
+ *
+ * Drop-in boundary for edamametechnologies/flodbadd (reference @ 2025-07-18).  The reference
+ * calls two Rust functions per captured frame from its capture task:
+ *
+ *   src/capture.rs:1038  parse_packet_pcap(&data)          -> Option<ParsedPacket>
+ *   src/capture.rs:1046  process_parsed_packet(cp, &sessions, &current_sessions,
+ *                                              &own_ips, &filter, l7)
+ *   (async-capture twin at src/capture.rs:1224-1238)
+ *
+ * This header replaces that per-packet pair with batched, stream-ordered calls over a packed
+ * frame buffer.  Every entry point is plain C (pointers + sizes, no torch/HIP types in the
+ * signatures; streams are passed as `void*` = hipStream_t, NULL = the null stream).
+ *
+ * Conventions (mirroring the reference's error behaviour):
+ *   - Every int-returning function returns FB_OK (0) or a negative fb_err; nothing aborts.
+ *   - A frame the reference would reject (`parse_packet_pcap` returning None, src/packets.rs:
+ *     603-802) is NOT an error: it is classified FB_CLASS_DROP.  A session packet rejected by
+ *     the session filter (src/packets.rs:321-327) is FB_CLASS_FILTERED.  Port-53 traffic is
+ *     FB_CLASS_DNS (src/packets.rs:638-650, 681-686) and is listed in the DNS side output.
+ *   - A context is not thread-safe; use one per capture interface / stream, like the
+ *     reference's one processor task per interface (src/capture.rs:1027).
+ *   - Frames: `frames[offsets[i] .. offsets[i+1])` is frame i (caplen bytes, as libpcap hands
+ *     `packet.data` to the reference, src/capture.rs:1092).  offsets has n+1 entries.
+ *     A frame whose offsets are decreasing or exceed frames_bytes is classified DROP and
+ *     counted in fb_batch_stats.bad_offsets.  Batches are limited to FB_MAX_BATCH_PACKETS
+ *     packets and < 4 GiB of frame bytes (u32 offsets).
+ */
+#ifndef FLODBADD_GPU_H
+#define FLODBADD_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FB_ABI_VERSION 1u
+#define FB_MAX_BATCH_PACKETS (1u << 30)
+#define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
+#define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
+#define FB_SERVICE_BITMAP_BYTES 8192u
+
+/* Return codes. */
+enum fb_err {
+    FB_OK = 0,
+    FB_ERR_INVAL = -1,      /* bad argument (NULL, size limits, bad enum)                 */
+    FB_ERR_NOMEM = -2,      /* device or host allocation failed                           */
+    FB_ERR_HIP = -3,        /* HIP runtime error; fb_last_error() has the text             */
+    FB_ERR_NODEV = -4,      /* no gfx950 device / device index out of range                */
+    FB_ERR_TABLE_FULL = -5, /* flow table capacity exhausted (some packets not counted)    */
+    FB_ERR_INTERNAL = -6    /* kernel-side protocol failure (bounded spin expired)          */
+};
+
+/* SessionFilter, src/sessions.rs:173-178 (same discriminant order as the Rust enum). */
+enum fb_filter { FB_FILTER_LOCAL_ONLY = 0, FB_FILTER_GLOBAL_ONLY = 1, FB_FILTER_ALL = 2 };
+
+/* Per-packet class (the reference's Option<ParsedPacket> + filter outcome). */
+enum fb_class {
+    FB_CLASS_SESSION = 0,  /* ParsedPacket::SessionPacket that passed the filter -> out[]   */
+    FB_CLASS_DNS = 1,      /* ParsedPacket::DnsPacket -> dns[]                              */
+    FB_CLASS_DROP = 2,     /* parse_packet_pcap returned None                               */
+    FB_CLASS_FILTERED = 3  /* SessionPacket rejected by the Local/Global filter             */
+};
+
+/* fb_pkt_out.meta bits. */
+enum fb_meta_bits {
+    FB_META_HAS_FLAGS = 1u << 0,  /* SessionPacketData.flags is Some (TCP)                  */
+    FB_META_SWAP = 1u << 1,       /* canonical key = reversed raw 5-tuple                    */
+    FB_META_ORIGINATOR = 1u << 2, /* is_originator, src/packets.rs:316-319                   */
+    FB_META_LOCAL_SRC = 1u << 3,  /* is_lan_ip(key.src_ip), src/packets.rs:430               */
+    FB_META_LOCAL_DST = 1u << 4,  /* is_lan_ip(key.dst_ip), src/packets.rs:431               */
+    FB_META_SELF_SRC = 1u << 5,   /* own_ips.contains(key.src_ip), src/packets.rs:434        */
+    FB_META_SELF_DST = 1u << 6,   /* own_ips.contains(key.dst_ip), src/packets.rs:435        */
+    FB_META_DST_SERVICE = 1u << 7 /* dst_service is Some, src/packets.rs:441-464             */
+};
+
+/*
+ * Session key, byte-identical to the reference's only C-ABI 5-tuple:
+ * `struct session_key` (ebpf/l7_ebpf_program/src/l7_ebpf.c:26-34), mirrored by
+ * `SessionKey` + `session_to_key` (src/l7_ebpf.rs:33-42, 78-104):
+ *   IPv4: ip[0] = u32::from(Ipv4Addr) (numeric value, host byte order), ip[1..3] = 0.
+ *   IPv6: ip[k] = u32::from_be_bytes(octets[4k..4k+4]).
+ *   family from src_ip: 2 (AF_INET) / 10 (AF_INET6); protocol 6 (TCP) / 17 (UDP).
+ */
+typedef struct fb_session_key {
+    uint32_t src_ip[4];
+    uint32_t dst_ip[4];
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t protocol;
+    uint8_t family;
+    uint16_t padding; /* always 0 */
+} fb_session_key;     /* 40 bytes */
+
+/*
+ * One emitted session packet (class SESSION), in packet order.  Replaces the
+ * SessionPacketData that reaches the DashMap upsert (src/packets.rs:85-98, 329-535).
+ * `key` is the CANONICAL session key (src/packets.rs:245-311); the raw 5-tuple is `key`
+ * reversed when FB_META_SWAP is set.
+ */
+typedef struct fb_pkt_out {
+    fb_session_key key;        /*  0: canonical Session                                      */
+    uint32_t packet_length;    /* 40: L4 payload bytes (SessionPacketData.packet_length)       */
+    uint32_t ip_packet_length; /* 44: IPv4 total_length / IPv6 payload_length + 40             */
+    uint8_t tcp_flags;         /* 48: TCP flags byte (0 when !HAS_FLAGS)                       */
+    uint8_t meta;              /* 49: fb_meta_bits                                             */
+    uint8_t hist_char;         /* 50: map_tcp_flags() char (src/packets.rs:561-601), 0 for UDP */
+    uint8_t reserved;          /* 51: 0                                                        */
+    uint32_t pkt_index;        /* 52: index of the frame in the batch                          */
+} fb_pkt_out;                  /* 56 bytes */
+
+/* One DNS-diverted packet: payload = frames[payload_offset .. +payload_length). */
+typedef struct fb_dns_out {
+    uint32_t pkt_index;
+    uint32_t payload_offset; /* absolute byte offset in the frame buffer; TCP: after the 2-byte
+                                length prefix (src/packets.rs:646-647)                       */
+    uint32_t payload_length;
+    uint8_t protocol; /* 6 / 17 */
+    uint8_t family;   /* 2 / 10 */
+    uint16_t reserved;
+} fb_dns_out; /* 16 bytes */
+
+/* PACKET_STATS (src/packets.rs:28-83, 211-227, 336, 346) + batch bookkeeping. */
+typedef struct fb_batch_stats {
+    uint64_t total_processed; /* SessionPackets reaching process_parsed_packet (pre-filter)  */
+    uint64_t tcp_processed;
+    uint64_t udp_processed;
+    uint64_t ipv4_processed;
+    uint64_t ipv6_processed;
+    uint64_t new_sessions;     /* flow-table inserts  (fb_flow_update only)                   */
+    uint64_t updated_sessions; /* flow-table hits     (fb_flow_update only)                   */
+    uint64_t n_session;        /* records written to out[] (class SESSION)                    */
+    uint64_t n_dns;            /* records written to dns[] (class DNS)                        */
+    uint64_t n_drop;           /* parse_packet_pcap -> None                                   */
+    uint64_t n_filtered;       /* rejected by the session filter                              */
+    uint64_t bad_offsets;      /* frames with invalid offsets (counted in n_drop too)         */
+    uint64_t error;            /* nonzero: kernel protocol failure (see FB_ERR_INTERNAL)      */
+    uint64_t reserved[3];
+} fb_batch_stats; /* 128 bytes */
+
+/* IPv6 LAN network (init_local_cache, src/ip.rs:164-191): ip & mask(prefix) == net. */
+typedef struct fb_lan_v6 {
+    uint32_t net[4]; /* network address, session_key word format (already masked)          */
+    uint32_t prefix; /* 0..128                                                               */
+    uint32_t reserved[3];
+} fb_lan_v6; /* 32 bytes */
+
+/* One own address (FlodbaddInterface v4/v6 addresses, src/capture.rs:964-970). */
+typedef struct fb_ip {
+    uint32_t addr[4]; /* session_key word format */
+    uint32_t family;  /* 2 / 10 */
+    uint32_t reserved[3];
+} fb_ip; /* 32 bytes */
+
+typedef struct fb_config {
+    uint32_t abi_version;          /* must be FB_ABI_VERSION                                  */
+    uint32_t filter;               /* fb_filter; FlodbaddCapture::new() uses GLOBAL_ONLY      */
+    const uint8_t* service_bitmap; /* FB_SERVICE_BITMAP_BYTES; NULL -> built-in table
+                                      (src/port_vulns_db.rs, bit p <=> name(p) != "")        */
+    const fb_lan_v6* lan_v6;       /* may be NULL when n_lan_v6 == 0                          */
+    uint32_t n_lan_v6;             /* <= FB_MAX_LAN_V6                                        */
+    uint32_t n_own_ips;            /* <= FB_MAX_OWN_IPS                                       */
+    const fb_ip* own_ips;          /* may be NULL when n_own_ips == 0                         */
+    uint64_t flow_capacity;        /* flow-table slots (rounded up to a power of two, 0 = none)*/
+    uint32_t max_batch_packets;    /* host-mode staging capacity (packets per call)           */
+    uint32_t reserved0;
+    uint64_t max_batch_bytes;      /* host-mode staging capacity (frame bytes per call)       */
+} fb_config;
+
+/* Flow-table export record: canonical key + SessionStats integer counters
+ * (src/sessions.rs:76-82; update rules src/packets.rs:111-120, 383-391). */
+typedef struct fb_flow_rec {
+    fb_session_key key;      /*  0 */
+    uint64_t outbound_bytes; /* 40 */
+    uint64_t inbound_bytes;  /* 48 */
+    uint64_t orig_pkts;      /* 56 */
+    uint64_t resp_pkts;      /* 64 */
+    uint64_t orig_ip_bytes;  /* 72 */
+    uint64_t resp_ip_bytes;  /* 80 */
+} fb_flow_rec;               /* 88 bytes */
+
+typedef struct fb_ctx fb_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+uint32_t fb_abi_version(void);
+const char* fb_last_error(void); /* thread-local text of the last failure */
+fb_ctx* fb_create(int device, const fb_config* cfg); /* NULL on failure (see fb_last_error) */
+int fb_destroy(fb_ctx* ctx);
+
+/* ---- runtime configuration (each takes effect for the next call on the context) -------- */
+int fb_set_filter(fb_ctx* ctx, uint32_t filter);                 /* set_filter, capture.rs:185 */
+int fb_set_service_bitmap(fb_ctx* ctx, const uint8_t* bitmap);   /* CloudModel update, port_vulns.rs:350-380 */
+int fb_set_lan_v6(fb_ctx* ctx, const fb_lan_v6* nets, uint32_t n); /* init_local_cache, ip.rs:164 */
+int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
+
+/*
+ * Device-resident parse + classify (parse_packet_pcap + the per-packet part of
+ * process_parsed_packet).  All pointers are DEVICE pointers; the call is asynchronous on
+ * `stream`.  Outputs, all optional except d_stats:
+ *   d_out   : >= n fb_pkt_out, class-SESSION records, packet order (stable compaction)
+ *   d_dns   : >= n fb_dns_out, class-DNS records, packet order
+ *   d_class : n bytes, fb_class of every frame
+ *   d_stats : one fb_batch_stats (overwritten, not accumulated)
+ */
+int fb_parse_classify_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
+                          const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out,
+                          fb_dns_out* d_dns, uint8_t* d_class, fb_batch_stats* d_stats,
+                          void* stream);
+
+/*
+ * Host-memory variant: host buffers in, host buffers out (staged through the context's
+ * pinned buffers with hipMemcpyAsync H2D/D2H).  Synchronous: returns after the results are
+ * in host memory.  `out`/`dns` need room for n records; *n_out / *n_dns receive the counts.
+ * Any of out, dns, cls, stats may be NULL.
+ */
+int fb_parse_classify(fb_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes,
+                      const uint32_t* offsets, uint32_t n, fb_pkt_out* out, uint32_t* n_out,
+                      fb_dns_out* dns, uint32_t* n_dns, uint8_t* cls, fb_batch_stats* stats,
+                      void* stream);
+
+/*
+ * Flow-table upsert of SESSION records (the DashMap entry()/update_session_stats part of
+ * process_parsed_packet, src/packets.rs:329-535, integer counters only).  d_recs/d_n are
+ * device pointers; the record count is read on the device from d_stats->n_session of the
+ * fb_parse_classify_dev call that produced them, so no host round trip is needed.
+ * new_sessions / updated_sessions are ADDED into d_stats.
+ */
+int fb_flow_update_dev(fb_ctx* ctx, const fb_pkt_out* d_recs, fb_batch_stats* d_stats,
+                       void* stream);
+
+/* Fused device-resident parse + classify + flow upsert (no record round trip through HBM).
+ * Same outputs as fb_parse_classify_dev (d_out may be NULL) followed by fb_flow_update_dev. */
+int fb_process_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
+                   const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns,
+                   uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+
+int fb_flow_count(fb_ctx* ctx, uint64_t* n_flows, void* stream); /* synchronous */
+/* Copy every flow (slot order) to host memory; *n = flows written (<= cap). Synchronous. */
+int fb_flow_export(fb_ctx* ctx, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream);
+/* Same, into DEVICE memory; *d_n (device u64) receives the count. Asynchronous. */
+int fb_flow_export_dev(fb_ctx* ctx, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n,
+                       void* stream);
+int fb_flow_clear(fb_ctx* ctx, void* stream); /* clear_all_sessions, src/capture.rs:396 */
+/* The table's deterministic 64-bit key hash (the reference's DashMap uses SipHash with a random
+ * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */
+uint64_t fb_flow_hash(const fb_session_key* key);
+
+/* ---- small device-memory helpers (so hosts without a GPU runtime binding can drive the
+ *      device-resident entry points, e.g. through ctypes) ------------------------------- */
+int fb_dev_alloc(void** p, uint64_t bytes);
+int fb_dev_free(void* p);
+int fb_host_alloc_pinned(void** p, uint64_t bytes);
+int fb_host_free_pinned(void* p);
+int fb_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream); /* async */
+int fb_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream); /* async */
+int fb_memset_dev(void* dst, int value, uint64_t bytes, void* stream);       /* async */
+int fb_stream_create(void** stream);
+int fb_stream_destroy(void* stream);
+int fb_stream_sync(void* stream);
+int fb_event_create(void** ev);
+int fb_event_destroy(void* ev);
+int fb_event_record(void* ev, void* stream);
+int fb_event_elapsed_ms(float* ms, void* ev_start, void* ev_stop); /* syncs ev_stop */
+int fb_device_count(int* n);
+int fb_set_device(int device);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* FLODBADD_GPU_H */

@@ -1,0 +1,137 @@
+"""ctypes wrapper of oracle/liboracle.so (the C restatement).  TEST INFRASTRUCTURE ONLY:
+imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product package."""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+ROOT = os.path.dirname(HERE)
+BITMAP_PATH = os.path.join(ROOT, "flodbadd_amd", "data", "service_ports.bin")
+
+# Record layouts are defined once, in the product's binding of include/flodbadd_gpu.h.
+from flodbadd_amd._native import (DNS_OUT_DTYPE, FB_IP_DTYPE, FLOW_REC_DTYPE, LAN_V6_DTYPE,  # noqa: E402
+                                  PKT_OUT_DTYPE, STATS_DTYPE)
+
+
+class LanV6(C.Structure):
+    _fields_ = [("net", C.c_uint32 * 4), ("prefix", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
+class FbIp(C.Structure):
+    _fields_ = [("addr", C.c_uint32 * 4), ("family", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
+class OrcCfg(C.Structure):
+    _fields_ = [("filter", C.c_uint32), ("service_bitmap", C.c_uint8 * 8192), ("n_lan_v6", C.c_uint32),
+                ("lan_v6", LanV6 * 64), ("n_own_ips", C.c_uint32), ("own_ips", FbIp * 64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("%s missing: run `python -m flodbadd_amd.build`" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        P, U32, U64 = C.c_void_p, C.c_uint32, C.c_uint64
+        L.orc_parse_classify.restype = C.c_int
+        L.orc_parse_classify.argtypes = [P, P, U64, P, U32, P, C.POINTER(U32), P, C.POINTER(U32), P, P]
+        L.orc_flows_new.restype = P
+        L.orc_flows_free.argtypes = [P]
+        L.orc_flows_clear.argtypes = [P]
+        L.orc_flows_update.argtypes = [P, P, U64, P]
+        L.orc_flows_count.restype = U64
+        L.orc_flows_count.argtypes = [P]
+        L.orc_flows_export_sorted.restype = U64
+        L.orc_flows_export_sorted.argtypes = [P, P, U64]
+        L.orc_flows_history.restype = C.c_int64
+        L.orc_flows_history.argtypes = [P, P, C.c_char_p, U64, C.c_char_p, U64]
+        L.orc_pipeline.restype = U64
+        L.orc_pipeline.argtypes = [P, P, P, U64, P, U32, P, P]
+        L.orc_key_cmp.restype = C.c_int
+        L.orc_key_cmp.argtypes = [P, P]
+        _lib = L
+    return _lib
+
+
+def default_bitmap():
+    with open(BITMAP_PATH, "rb") as f:
+        return f.read()
+
+
+def make_cfg(session_filter=2, bitmap=None, lan_v6=None, own_ips=None):
+    """lan_v6 / own_ips are LAN_V6_DTYPE / FB_IP_DTYPE arrays (see flodbadd_amd.capture)."""
+    c = OrcCfg()
+    c.filter = int(session_filter)
+    bm = default_bitmap() if bitmap is None else bytes(bitmap)
+    C.memmove(c.service_bitmap, bm, 8192)
+    if lan_v6 is not None and len(lan_v6):
+        lan_v6 = np.ascontiguousarray(lan_v6, dtype=LAN_V6_DTYPE)
+        c.n_lan_v6 = len(lan_v6)
+        C.memmove(C.addressof(c.lan_v6), lan_v6.ctypes.data, lan_v6.nbytes)
+    if own_ips is not None and len(own_ips):
+        own_ips = np.ascontiguousarray(own_ips, dtype=FB_IP_DTYPE)
+        c.n_own_ips = len(own_ips)
+        C.memmove(C.addressof(c.own_ips), own_ips.ctypes.data, own_ips.nbytes)
+    return c
+
+
+def parse_classify(cfg, frames, offsets):
+    """Returns (records, dns, cls, stats) exactly as fb_parse_classify would."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    n = offsets.size - 1
+    out = np.zeros(max(n, 1), dtype=PKT_OUT_DTYPE)
+    dns = np.zeros(max(n, 1), dtype=DNS_OUT_DTYPE)
+    cls = np.zeros(max(n, 1), dtype=np.uint8)
+    st = np.zeros(1, dtype=STATS_DTYPE)
+    no, nd = C.c_uint32(), C.c_uint32()
+    lib().orc_parse_classify(C.byref(cfg), frames.ctypes.data, frames.nbytes, offsets.ctypes.data, n,
+                             out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), cls.ctypes.data,
+                             st.ctypes.data)
+    return out[: no.value], dns[: nd.value], cls[:n], st
+
+
+class Flows:
+    """The oracle's session table (DashMap restatement)."""
+
+    def __init__(self):
+        self.h = C.c_void_p(lib().orc_flows_new())
+
+    def update(self, recs, stats=None):
+        recs = np.ascontiguousarray(recs, dtype=PKT_OUT_DTYPE)
+        lib().orc_flows_update(self.h, recs.ctypes.data if recs.size else None, recs.size,
+                               stats.ctypes.data if stats is not None else None)
+
+    def count(self):
+        return lib().orc_flows_count(self.h)
+
+    def export_sorted(self):
+        n = self.count()
+        out = np.zeros(max(n, 1), dtype=FLOW_REC_DTYPE)
+        m = lib().orc_flows_export_sorted(self.h, out.ctypes.data, n)
+        return out[:m]
+
+    def history(self, key_rec):
+        """key_rec: a PKT_OUT_DTYPE or FLOW_REC_DTYPE element (uses its first 40 bytes)."""
+        kb = np.frombuffer(key_rec.tobytes()[:40], dtype=np.uint8).copy()
+        buf = C.create_string_buffer(1 << 16)
+        cs = C.create_string_buffer(8)
+        n = lib().orc_flows_history(self.h, kb.ctypes.data, buf, 1 << 16, cs, 8)
+        if n < 0:
+            return None, None
+        return buf.raw[:n].decode(), (cs.value.decode() or None)
+
+    def clear(self):
+        lib().orc_flows_clear(self.h)
+
+    def __del__(self):
+        try:
+            lib().orc_flows_free(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,484 @@
+/*
+ * oracle.c -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY
+ * (see oracle.h).  Plain C99, single-threaded, written for clarity rather than speed, but
+ * without gratuitous overhead so it can also serve as the bench's cpu_baseline ("port").
+ *
+ * Every function cites the reference lines it restates.  Byte-level decode follows
+ * pnet_packet 0.35.0 (Cargo.lock:2588), which is not vendored under /root/reference:
+ * the rules below are the published crate's accessor/payload semantics as restated in
+ * SURVEY.md §8a "a1 exact decode rules" -- parity of the decode step is UNPINNED by any
+ * reference test (no reference test builds raw frames).
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define TCP_FIN 0x01u
+#define TCP_SYN 0x02u
+#define TCP_RST 0x04u
+#define TCP_PSH 0x08u
+#define TCP_ACK 0x10u
+
+static uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* ---------------------------------------------------------------------------------------
+ * parse_packet_pcap, src/packets.rs:603-802.
+ * EthernetPacket::new needs >= 14 bytes; payload() is the rest of the frame (pnet ethernet).
+ * Ipv4Packet::new needs >= 20 bytes; payload() = packet[20+opt .. min(20+opt+plen, len)]
+ *   with opt = sat(ihl*4 - 20), plen = sat(total_length - ihl*4), empty if len <= 20+opt.
+ * Ipv6Packet::new needs >= 40 bytes; payload() = packet[40 .. min(40+payload_length, len)].
+ * TcpPacket::new needs >= 20 bytes; payload() = packet[20+opt ..] (opt = doff>5 ? doff*4-20 : 0),
+ *   empty if len <= 20+opt.  UdpPacket::new needs >= 8; payload() = packet[8..] (length
+ *   field ignored).
+ * ------------------------------------------------------------------------------------- */
+static uint32_t parse_l4(const uint8_t* frame, uint32_t l4_off, uint32_t l4_len, uint32_t proto,
+                         orc_parsed* o) {
+    const uint8_t* P = frame + l4_off;
+    if (proto == 6) { /* IpNextHeaderProtocols::Tcp, src/packets.rs:624-665 / 707-749 */
+        if (l4_len < 20) return ORC_NONE;            /* "Failed to parse TCP packet" */
+        uint32_t doff = P[12] >> 4;
+        uint32_t hs = 20 + (doff > 5 ? doff * 4 - 20 : 0);
+        uint32_t plen = l4_len <= hs ? 0 : l4_len - hs;
+        o->protocol = 6;
+        o->src_port = (uint16_t)be16(P);
+        o->dst_port = (uint16_t)be16(P + 2);
+        o->flags = P[13]; /* tcp.get_flags() is u8, src/packets.rs:635 */
+        o->has_flags = 1;
+        o->packet_length = plen;
+        if (o->src_port == 53 || o->dst_port == 53) { /* DNS over TCP, src/packets.rs:638-650 */
+            if (plen < 2) return ORC_NONE;           /* "DNS-over-TCP payload too short" */
+            o->dns_payload_offset = l4_off + hs + 2; /* drain(0..2) */
+            o->dns_payload_length = plen - 2;
+            return ORC_DNS;
+        }
+        return ORC_SESSION;
+    }
+    if (proto == 17) { /* IpNextHeaderProtocols::Udp, src/packets.rs:667-699 / 750-783 */
+        if (l4_len < 8) return ORC_NONE; /* "Failed to parse UDP packet" */
+        o->protocol = 17;
+        o->src_port = (uint16_t)be16(P);
+        o->dst_port = (uint16_t)be16(P + 2);
+        o->flags = 0;
+        o->has_flags = 0; /* flags: None */
+        o->packet_length = l4_len - 8;
+        if (o->src_port == 53 || o->dst_port == 53) { /* DNS over UDP, src/packets.rs:681-686 */
+            o->dns_payload_offset = l4_off + 8;
+            o->dns_payload_length = l4_len - 8;
+            return ORC_DNS;
+        }
+        return ORC_SESSION;
+    }
+    return ORC_NONE; /* `_ => None` */
+}
+
+uint32_t orc_parse_packet_pcap(const uint8_t* f, uint32_t L, orc_parsed* o) {
+    memset(o, 0, sizeof(*o));
+    if (L < 14) return ORC_NONE; /* "Failed to parse Ethernet packet", src/packets.rs:604-610 */
+    uint32_t et = be16(f + 12);
+    const uint8_t* ip = f + 14;
+    uint32_t n = L - 14;
+    uint32_t kind = ORC_NONE;
+    if (et == 0x0800) { /* EtherTypes::Ipv4, src/packets.rs:612 */
+        if (n < 20) return ORC_NONE;
+        uint32_t ihl4 = (ip[0] & 15u) * 4u; /* version is not checked by pnet */
+        uint32_t tot = be16(ip + 2);
+        uint32_t start = 20 + (ihl4 > 20 ? ihl4 - 20 : 0);
+        uint32_t plen = tot > ihl4 ? tot - ihl4 : 0;
+        uint32_t l4_len = 0;
+        if (n > start) {
+            uint32_t end = start + plen < n ? start + plen : n;
+            l4_len = end - start;
+        }
+        o->family = 2;
+        o->src_ip[0] = be32(ip + 12); /* u32::from(Ipv4Addr), src/l7_ebpf.rs:85 */
+        o->dst_ip[0] = be32(ip + 16);
+        o->ip_packet_length = tot; /* get_total_length(), src/packets.rs:620 */
+        kind = parse_l4(f, 14 + start, l4_len, ip[9], o);
+    } else if (et == 0x86DD) { /* EtherTypes::Ipv6, src/packets.rs:701 */
+        if (n < 40) return ORC_NONE;
+        uint32_t plen6 = be16(ip + 4);
+        uint32_t l4_len = 0;
+        if (n > 40) {
+            uint32_t end = 40 + plen6 < n ? 40 + plen6 : n;
+            l4_len = end - 40;
+        }
+        o->family = 10;
+        for (int k = 0; k < 4; ++k) {
+            o->src_ip[k] = be32(ip + 8 + 4 * k);
+            o->dst_ip[k] = be32(ip + 24 + 4 * k);
+        }
+        o->ip_packet_length = plen6 + 40; /* src/packets.rs:709 */
+        kind = parse_l4(f, 14 + 40, l4_len, ip[6], o); /* next header, no ext-hdr walk */
+    } else {
+        return ORC_NONE; /* `_ => None`, src/packets.rs:800 (VLAN, ARP, ... included) */
+    }
+    o->kind = kind;
+    return kind;
+}
+
+/* get_name_from_port(p) != "" (src/port_vulns.rs:213-228, src/packets.rs:233-237). */
+int orc_is_service_port(const orc_cfg* c, uint16_t p) {
+    return (c->service_bitmap[p >> 3] >> (p & 7)) & 1;
+}
+
+/* is_lan_ipv4_fast, src/ip.rs:55-91. */
+static int is_lan_v4(uint32_t v) {
+    if (v == 0 || v == 0xFFFFFFFFu) return 1;
+    if ((v >> 24) == 127) return 1;
+    if ((v >> 28) == 0xE) return 1;
+    if ((v >> 16) == 0xA9FE) return 1;
+    if ((v >> 24) == 10) return 1;
+    if ((v >> 24) == 172) {
+        uint32_t s = (v >> 16) & 0xFF;
+        if (s >= 16 && s <= 31) return 1;
+    }
+    if ((v >> 16) == 0xC0A8) return 1;
+    return 0;
+}
+
+/* is_local_ipv6 (src/ip.rs:112-134) then is_lan_ipv6_fast (src/ip.rs:139-156). */
+static int is_lan_v6(const orc_cfg* c, const uint32_t w[4]) {
+    uint32_t seg0 = w[0] >> 16;
+    if ((w[0] | w[1] | w[2] | w[3]) == 0) return 1;                        /* :: */
+    if (w[0] == 0 && w[1] == 0 && w[2] == 0 && w[3] == 1) return 1;        /* ::1 */
+    if ((seg0 & 0xffc0u) == 0xfe80u) return 1;                             /* fe80::/10 */
+    if ((seg0 & 0xff00u) == 0xff00u) return 1;                             /* ff00::/8 */
+    if ((seg0 & 0xfe00u) == 0xfc00u) return 1;                             /* fc00::/7 */
+    for (uint32_t i = 0; i < c->n_lan_v6; ++i) {
+        uint32_t pfx = c->lan_v6[i].prefix;
+        int match = 1;
+        for (int k = 0; k < 4; ++k) {
+            /* mask = !0u128 << (128 - prefix) (prefix 0 -> 0), src/ip.rs:143-147 */
+            int bits = (int)pfx - 32 * k;
+            uint32_t m = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : 0xFFFFFFFFu << (32 - bits));
+            if ((w[k] & m) != c->lan_v6[i].net[k]) { match = 0; break; }
+        }
+        if (match) return 1;
+    }
+    return 0;
+}
+
+/* is_lan_ip, src/ip.rs:199-242 (the known-local cache only memoises true results). */
+int orc_is_lan_ip(const orc_cfg* c, uint32_t family, const uint32_t ip[4]) {
+    return family == 2 ? is_lan_v4(ip[0]) : is_lan_v6(c, ip);
+}
+
+static int is_own_ip(const orc_cfg* c, uint32_t family, const uint32_t ip[4]) {
+    for (uint32_t i = 0; i < c->n_own_ips; ++i) {
+        const fb_ip* o = &c->own_ips[i];
+        if (o->family != family) continue;
+        if (family == 2 ? o->addr[0] == ip[0]
+                        : (o->addr[0] == ip[0] && o->addr[1] == ip[1] && o->addr[2] == ip[2] &&
+                           o->addr[3] == ip[3]))
+            return 1;
+    }
+    return 0;
+}
+
+/* map_tcp_flags, src/packets.rs:561-601. */
+char orc_map_tcp_flags(uint8_t fl, uint32_t plen, int orig) {
+    if ((fl & TCP_SYN) && !(fl & TCP_ACK)) return orig ? 'S' : 's';
+    if ((fl & TCP_SYN) && (fl & TCP_ACK)) return orig ? 'H' : 'h';
+    if (fl & TCP_FIN) return orig ? 'F' : 'f';
+    if (fl & TCP_RST) return orig ? 'R' : 'r';
+    if (plen > 0) return orig ? '>' : '<';
+    if (fl & TCP_ACK) return orig ? 'A' : 'a';
+    return '-';
+}
+
+/* Key canonicalisation + originator + filter: src/packets.rs:232-327. */
+uint32_t orc_classify(const orc_cfg* c, const orc_parsed* p, uint32_t pkt_index, fb_pkt_out* r) {
+    int S = orc_is_service_port(c, p->src_port);
+    int D = orc_is_service_port(c, p->dst_port);
+    int swap;
+    if (S && !D) {
+        swap = 1; /* source is likely a server (src/packets.rs:245-253) */
+    } else if (S && D) {
+        if (p->has_flags) {
+            if (p->protocol == 6 && (p->flags & TCP_SYN) && !(p->flags & TCP_ACK))
+                swap = 0; /* SYN without ACK (src/packets.rs:257-263) */
+            else if (p->protocol == 6 && (p->flags & TCP_SYN) && (p->flags & TCP_ACK))
+                swap = 1; /* SYN+ACK (src/packets.rs:264-275) */
+            else
+                swap = p->src_port < p->dst_port; /* port tiebreak (src/packets.rs:276-292) */
+        } else {
+            swap = p->src_port < p->dst_port; /* UDP tiebreak (src/packets.rs:294-307) */
+        }
+    } else {
+        swap = 0;
+    }
+    memset(r, 0, sizeof(*r));
+    const uint32_t* ks = swap ? p->dst_ip : p->src_ip;
+    const uint32_t* kd = swap ? p->src_ip : p->dst_ip;
+    for (int k = 0; k < 4; ++k) {
+        r->key.src_ip[k] = ks[k];
+        r->key.dst_ip[k] = kd[k];
+    }
+    r->key.src_port = swap ? p->dst_port : p->src_port;
+    r->key.dst_port = swap ? p->src_port : p->dst_port;
+    r->key.protocol = p->protocol;
+    r->key.family = p->family;
+    r->packet_length = p->packet_length;
+    r->ip_packet_length = p->ip_packet_length;
+    r->tcp_flags = p->has_flags ? p->flags : 0;
+    r->pkt_index = pkt_index;
+
+    /* is_originator, src/packets.rs:316-319: field-wise equality raw vs key. */
+    int orig = memcmp(p->src_ip, r->key.src_ip, 16) == 0 && p->src_port == r->key.src_port &&
+               memcmp(p->dst_ip, r->key.dst_ip, 16) == 0 && p->dst_port == r->key.dst_port;
+
+    uint8_t meta = 0;
+    if (p->has_flags) meta |= FB_META_HAS_FLAGS;
+    if (swap) meta |= FB_META_SWAP;
+    if (orig) meta |= FB_META_ORIGINATOR;
+    int lan_ks = orc_is_lan_ip(c, p->family, r->key.src_ip);
+    int lan_kd = orc_is_lan_ip(c, p->family, r->key.dst_ip);
+    if (lan_ks) meta |= FB_META_LOCAL_SRC;
+    if (lan_kd) meta |= FB_META_LOCAL_DST;
+    if (is_own_ip(c, p->family, r->key.src_ip)) meta |= FB_META_SELF_SRC;
+    if (is_own_ip(c, p->family, r->key.dst_ip)) meta |= FB_META_SELF_DST;
+    /* dst_service: name of key.dst_port (src/packets.rs:441-464) */
+    if (orc_is_service_port(c, r->key.dst_port)) meta |= FB_META_DST_SERVICE;
+    r->meta = meta;
+    r->hist_char = p->has_flags ? (uint8_t)orc_map_tcp_flags(p->flags, p->packet_length, orig) : 0;
+
+    /* Filter (src/packets.rs:321-327) on the raw packet's session; is_local_session! =
+     * is_lan(src) && is_lan(dst) (src/sessions.rs:660-672) -- symmetric, so key order is moot. */
+    int local = lan_ks && lan_kd;
+    if (c->filter == FB_FILTER_LOCAL_ONLY && !local) return FB_CLASS_FILTERED;
+    if (c->filter == FB_FILTER_GLOBAL_ONLY && local) return FB_CLASS_FILTERED;
+    return FB_CLASS_SESSION;
+}
+
+int orc_parse_classify(const orc_cfg* c, const uint8_t* frames, uint64_t frames_bytes,
+                       const uint32_t* offsets, uint32_t n, fb_pkt_out* out, uint32_t* n_out,
+                       fb_dns_out* dns, uint32_t* n_dns, uint8_t* cls, fb_batch_stats* st) {
+    fb_batch_stats s;
+    memset(&s, 0, sizeof(s));
+    uint32_t no = 0, nd = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t o0 = offsets[i], o1 = offsets[i + 1];
+        uint32_t k;
+        orc_parsed p;
+        if (o1 < o0 || (uint64_t)o1 > frames_bytes) {
+            s.bad_offsets++;
+            k = FB_CLASS_DROP;
+        } else {
+            uint32_t kind = orc_parse_packet_pcap(frames + o0, o1 - o0, &p);
+            if (kind == ORC_NONE) {
+                k = FB_CLASS_DROP;
+            } else if (kind == ORC_DNS) {
+                k = FB_CLASS_DNS;
+                if (dns) {
+                    fb_dns_out* d = &dns[nd];
+                    d->pkt_index = i;
+                    d->payload_offset = o0 + p.dns_payload_offset;
+                    d->payload_length = p.dns_payload_length;
+                    d->protocol = p.protocol;
+                    d->family = p.family;
+                    d->reserved = 0;
+                }
+                nd++;
+            } else {
+                /* PACKET_STATS increments precede the filter (src/packets.rs:211-227). */
+                s.total_processed++;
+                if (p.protocol == 6) s.tcp_processed++; else s.udp_processed++;
+                if (p.family == 2) s.ipv4_processed++; else s.ipv6_processed++;
+                fb_pkt_out rec;
+                k = orc_classify(c, &p, i, &rec);
+                if (k == FB_CLASS_SESSION) {
+                    if (out) out[no] = rec;
+                    no++;
+                }
+            }
+        }
+        if (k == FB_CLASS_DROP) s.n_drop++;
+        if (k == FB_CLASS_FILTERED) s.n_filtered++;
+        if (cls) cls[i] = (uint8_t)k;
+    }
+    s.n_session = no;
+    s.n_dns = nd;
+    if (n_out) *n_out = no;
+    if (n_dns) *n_dns = nd;
+    if (st) *st = s;
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------------------
+ * Session table: a restatement of the DashMap<Session, SessionInfo> upsert
+ * (src/packets.rs:329-535) keeping the integer counters (src/packets.rs:111-120, 383-391),
+ * the history string and conn_state (src/packets.rs:187-198, 410-426, 539-559).
+ * Open addressing with FNV-1a over the 40-byte key (the reference hashes with SipHash and a
+ * random key, so no hash value is a parity target -- only keys and counters are).
+ * ------------------------------------------------------------------------------------- */
+typedef struct orc_flow {
+    fb_flow_rec rec;
+    char* hist;
+    uint64_t hist_len, hist_cap;
+    char conn_state[4];
+    int ended; /* end_time.is_some() */
+    int used;
+} orc_flow;
+
+struct orc_flows {
+    orc_flow* slots;
+    uint64_t cap, count;
+};
+
+static uint64_t key_hash(const fb_session_key* k) {
+    const uint8_t* b = (const uint8_t*)k;
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < 40; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+orc_flows* orc_flows_new(void) {
+    orc_flows* f = (orc_flows*)calloc(1, sizeof(orc_flows));
+    f->cap = 1024;
+    f->slots = (orc_flow*)calloc(f->cap, sizeof(orc_flow));
+    return f;
+}
+
+void orc_flows_clear(orc_flows* f) {
+    for (uint64_t i = 0; i < f->cap; ++i) free(f->slots[i].hist);
+    memset(f->slots, 0, f->cap * sizeof(orc_flow));
+    f->count = 0;
+}
+
+void orc_flows_free(orc_flows* f) {
+    if (!f) return;
+    for (uint64_t i = 0; i < f->cap; ++i) free(f->slots[i].hist);
+    free(f->slots);
+    free(f);
+}
+
+static orc_flow* find_slot(orc_flow* slots, uint64_t cap, const fb_session_key* k) {
+    uint64_t i = key_hash(k) & (cap - 1);
+    for (;;) {
+        if (!slots[i].used || memcmp(&slots[i].rec.key, k, sizeof(*k)) == 0) return &slots[i];
+        i = (i + 1) & (cap - 1);
+    }
+}
+
+static void grow(orc_flows* f) {
+    uint64_t ncap = f->cap * 2;
+    orc_flow* ns = (orc_flow*)calloc(ncap, sizeof(orc_flow));
+    for (uint64_t i = 0; i < f->cap; ++i)
+        if (f->slots[i].used) *find_slot(ns, ncap, &f->slots[i].rec.key) = f->slots[i];
+    free(f->slots);
+    f->slots = ns;
+    f->cap = ncap;
+}
+
+/* determine_conn_state, src/packets.rs:539-559. */
+static void conn_state_of(const char* h, uint64_t n, char out[4]) {
+    int has[128] = {0};
+    for (uint64_t i = 0; i < n; ++i) has[(unsigned char)h[i] & 127] = 1;
+    const char* s;
+    if (has['S'] && has['H'] && has['F'] && has['f']) s = "SF";
+    else if (has['S'] && !has['h'] && !has['r']) s = "S0";
+    else if (has['R'] || has['r']) s = "REJ";
+    else if (has['S'] && has['H'] && !has['F'] && !has['f']) s = "S1";
+    else s = "-";
+    strcpy(out, s);
+}
+
+void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* st) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const fb_pkt_out* r = &recs[i];
+        if ((f->count + 1) * 2 > f->cap) grow(f);
+        orc_flow* s = find_slot(f->slots, f->cap, &r->key);
+        if (!s->used) { /* Entry::Vacant, src/packets.rs:344 */
+            memset(s, 0, sizeof(*s));
+            s->used = 1;
+            s->rec.key = r->key;
+            f->count++;
+            if (st) st->new_sessions++;
+        } else if (st) {
+            st->updated_sessions++; /* Entry::Occupied, src/packets.rs:332 */
+        }
+        if (r->meta & FB_META_ORIGINATOR) {
+            s->rec.outbound_bytes += r->packet_length;
+            s->rec.orig_pkts += 1;
+            s->rec.orig_ip_bytes += r->ip_packet_length;
+        } else {
+            s->rec.inbound_bytes += r->packet_length;
+            s->rec.resp_pkts += 1;
+            s->rec.resp_ip_bytes += r->ip_packet_length;
+        }
+        if (r->meta & FB_META_HAS_FLAGS) { /* history push, src/packets.rs:187-198, 410-426 */
+            if (s->hist_len + 1 > s->hist_cap) {
+                s->hist_cap = s->hist_cap ? s->hist_cap * 2 : 16;
+                s->hist = (char*)realloc(s->hist, s->hist_cap);
+            }
+            s->hist[s->hist_len++] = (char)r->hist_char;
+            if ((r->tcp_flags & (TCP_FIN | TCP_RST)) && !s->ended) {
+                s->ended = 1;
+                conn_state_of(s->hist, s->hist_len, s->conn_state);
+            }
+        }
+    }
+}
+
+uint64_t orc_flows_count(const orc_flows* f) { return f->count; }
+
+static int ip_cmp(uint32_t fam, const uint32_t* a, const uint32_t* b) {
+    int nw = fam == 2 ? 1 : 4;
+    for (int k = 0; k < nw; ++k)
+        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return 0;
+}
+
+int orc_key_cmp(const fb_session_key* a, const fb_session_key* b) {
+    if (a->protocol != b->protocol) return a->protocol < b->protocol ? -1 : 1; /* TCP < UDP */
+    if (a->family != b->family) return a->family < b->family ? -1 : 1;         /* V4 < V6 */
+    int c = ip_cmp(a->family, a->src_ip, b->src_ip);
+    if (c) return c;
+    if (a->src_port != b->src_port) return a->src_port < b->src_port ? -1 : 1;
+    c = ip_cmp(a->family, a->dst_ip, b->dst_ip);
+    if (c) return c;
+    if (a->dst_port != b->dst_port) return a->dst_port < b->dst_port ? -1 : 1;
+    return 0;
+}
+
+static int rec_cmp(const void* x, const void* y) {
+    return orc_key_cmp(&((const fb_flow_rec*)x)->key, &((const fb_flow_rec*)y)->key);
+}
+
+uint64_t orc_flows_export_sorted(const orc_flows* f, fb_flow_rec* out, uint64_t cap) {
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < f->cap && m < cap; ++i)
+        if (f->slots[i].used) out[m++] = f->slots[i].rec;
+    qsort(out, m, sizeof(fb_flow_rec), rec_cmp);
+    return m;
+}
+
+int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* buf, uint64_t cap,
+                          char* cs, uint64_t cs_cap) {
+    orc_flow* s = find_slot(f->slots, f->cap, key);
+    if (!s->used) return -1;
+    uint64_t m = s->hist_len < cap ? s->hist_len : cap;
+    if (m) memcpy(buf, s->hist, m);
+    if (cs && cs_cap) {
+        if (s->ended) {
+            strncpy(cs, s->conn_state, cs_cap - 1);
+            cs[cs_cap - 1] = 0;
+        } else {
+            cs[0] = 0;
+        }
+    }
+    return (int64_t)s->hist_len;
+}
+
+uint64_t orc_pipeline(const orc_cfg* c, orc_flows* fl, const uint8_t* frames, uint64_t fb,
+                      const uint32_t* offsets, uint32_t n, fb_pkt_out* scratch,
+                      fb_batch_stats* st) {
+    uint32_t no = 0;
+    orc_parse_classify(c, frames, fb, offsets, n, scratch, &no, NULL, NULL, NULL, st);
+    if (fl) orc_flows_update(fl, scratch, no, st);
+    return n;
+}

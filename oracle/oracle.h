@@ -1,0 +1,99 @@
+/*
+ * oracle.h -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ * The product path (flodbadd_amd/, libflodbadd_gpu.so) never links or calls it.
+ *
+ * Restates, from edamametechnologies/flodbadd @ 2025-07-18:
+ *   src/packets.rs:603-802   parse_packet_pcap (via pnet_packet 0.35.0 semantics, which are
+ *                            NOT vendored in the reference: byte-level decode parity is
+ *                            "unpinned" -- see DESIGN.md §Oracle)
+ *   src/packets.rs:202-537   process_parsed_packet (canonical key, originator, filter, upsert)
+ *   src/packets.rs:105-200   update_session_stats (integer counters + history)
+ *   src/packets.rs:539-601   determine_conn_state, map_tcp_flags
+ *   src/ip.rs:55-242         is_lan_ip
+ *   src/sessions.rs:658-692  is_local_session! / is_global_session! / filter_sessions
+ *   src/port_vulns.rs:213-228 get_name_from_port (as a 65536-bit "has a name" bitmap)
+ * Output records use the same C layout as include/flodbadd_gpu.h so results compare
+ * byte-for-byte.
+ */
+#ifndef FLODBADD_ORACLE_H
+#define FLODBADD_ORACLE_H
+
+#include <stdint.h>
+#include "../include/flodbadd_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Result kinds of parse_packet_pcap (Option<ParsedPacket>). */
+enum orc_kind { ORC_NONE = 0, ORC_SESSION = 1, ORC_DNS = 2 };
+
+/* SessionPacketData / DnsPacketData (src/packets.rs:85-102), flattened. */
+typedef struct orc_parsed {
+    uint32_t kind;
+    uint8_t protocol; /* 6 / 17 */
+    uint8_t family;   /* 2 / 10 */
+    uint8_t has_flags;
+    uint8_t flags;
+    uint32_t src_ip[4], dst_ip[4]; /* session_key word format */
+    uint16_t src_port, dst_port;
+    uint32_t packet_length;
+    uint32_t ip_packet_length;
+    uint32_t dns_payload_offset; /* relative to the frame start */
+    uint32_t dns_payload_length;
+} orc_parsed;
+
+typedef struct orc_cfg {
+    uint32_t filter;
+    uint8_t service_bitmap[FB_SERVICE_BITMAP_BYTES];
+    uint32_t n_lan_v6;
+    fb_lan_v6 lan_v6[FB_MAX_LAN_V6];
+    uint32_t n_own_ips;
+    fb_ip own_ips[FB_MAX_OWN_IPS];
+} orc_cfg;
+
+/* Single-frame decode. Returns kind. */
+uint32_t orc_parse_packet_pcap(const uint8_t* frame, uint32_t caplen, orc_parsed* out);
+
+int orc_is_service_port(const orc_cfg* cfg, uint16_t port);
+int orc_is_lan_ip(const orc_cfg* cfg, uint32_t family, const uint32_t ip[4]);
+char orc_map_tcp_flags(uint8_t flags, uint32_t packet_length, int is_originator);
+
+/* Per-packet classification (the stateless part of process_parsed_packet).
+ * Returns FB_CLASS_SESSION or FB_CLASS_FILTERED; fills *rec either way. */
+uint32_t orc_classify(const orc_cfg* cfg, const orc_parsed* p, uint32_t pkt_index,
+                      fb_pkt_out* rec);
+
+/* Whole batch, same contract as fb_parse_classify (any output pointer may be NULL). */
+int orc_parse_classify(const orc_cfg* cfg, const uint8_t* frames, uint64_t frames_bytes,
+                       const uint32_t* offsets, uint32_t n, fb_pkt_out* out, uint32_t* n_out,
+                       fb_dns_out* dns, uint32_t* n_dns, uint8_t* cls, fb_batch_stats* stats);
+
+/* ---- session table (DashMap<Session, SessionInfo> restated; integer part + history) ---- */
+typedef struct orc_flows orc_flows;
+orc_flows* orc_flows_new(void);
+void orc_flows_free(orc_flows* f);
+void orc_flows_clear(orc_flows* f);
+/* Upsert records in order; adds new/updated counts into stats (may be NULL). */
+void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* stats);
+uint64_t orc_flows_count(const orc_flows* f);
+/* Export sorted by the derived Ord of Session (src/sessions.rs:23-30). Returns count. */
+uint64_t orc_flows_export_sorted(const orc_flows* f, fb_flow_rec* out, uint64_t cap);
+/* History string + conn_state ('\0' when None) of one flow; returns history length, or -1. */
+int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* buf,
+                          uint64_t cap, char* conn_state, uint64_t cs_cap);
+
+/* Bench helper: parse+classify+upsert with a scratch record buffer; returns packets done. */
+uint64_t orc_pipeline(const orc_cfg* cfg, orc_flows* flows, const uint8_t* frames,
+                      uint64_t frames_bytes, const uint32_t* offsets, uint32_t n,
+                      fb_pkt_out* scratch, fb_batch_stats* stats);
+
+/* Derived Ord comparison of two keys (protocol, src_ip, src_port, dst_ip, dst_port). */
+int orc_key_cmp(const fb_session_key* a, const fb_session_key* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,84 @@
+"""CPU-side checks of the C-ABI boundary: the library loads (no GPU needed for dlopen) and exports
+exactly the functions include/flodbadd_gpu.h declares; record layouts match the header."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+from flodbadd_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "flodbadd_gpu.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(fb_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_all_bound_symbols():
+    declared = _declared_functions()
+    bound = sorted(n for n, _, _ in N.GPU_SYMBOLS)
+    assert declared == bound, (set(declared) ^ set(bound))
+
+
+def test_library_exports_every_declared_symbol():
+    from flodbadd_amd.build import build_gpu
+    build_gpu()
+    lib = N.gpu_lib()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", N.GPU_LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (fb_\w+)", out))
+    assert set(_declared_functions()) <= exported
+    assert lib.fb_abi_version() == N.FB_ABI_VERSION
+
+
+def test_no_gpu_means_loud_failure():
+    """Without a gfx950 device fb_create must fail (no CPU fallback anywhere)."""
+    lib = N.gpu_lib()
+    n = C.c_int(-1)
+    assert lib.fb_device_count(C.byref(n)) == 0
+    if n.value == 0:
+        cfg = N.FbConfig()
+        cfg.abi_version = N.FB_ABI_VERSION
+        cfg.filter = N.FB_FILTER_ALL
+        assert not lib.fb_create(0, C.byref(cfg))
+        assert lib.fb_last_error()
+
+
+def test_invalid_arguments_are_errors_not_aborts():
+    lib = N.gpu_lib()
+    assert lib.fb_set_filter(None, 0) == N.FB_ERR_INVAL
+    assert lib.fb_destroy(None) == N.FB_ERR_INVAL
+    assert lib.fb_parse_classify_dev(None, None, 0, None, 0, None, None, None, None, None) == N.FB_ERR_INVAL
+    cfg = N.FbConfig()
+    cfg.abi_version = 999
+    assert not lib.fb_create(0, C.byref(cfg))
+    assert b"abi_version" in lib.fb_last_error()
+
+
+def test_record_layouts():
+    assert N.PKT_OUT_DTYPE.itemsize == 56
+    assert N.PKT_OUT_DTYPE.fields["packet_length"][1] == 40
+    assert N.PKT_OUT_DTYPE.fields["pkt_index"][1] == 52
+    assert N.FLOW_REC_DTYPE.fields["outbound_bytes"][1] == 40
+    assert N.DNS_OUT_DTYPE.itemsize == 16
+    assert N.STATS_DTYPE.itemsize == 128
+
+
+def test_flow_hash_is_deterministic_and_host_side():
+    lib = N.gpu_lib()
+    k = np.zeros(1, dtype=N.PKT_OUT_DTYPE)
+    k[0]["src_ip"][0] = 0xC0A80101
+    k[0]["dst_ip"][0] = 0x08080808
+    k[0]["src_port"], k[0]["dst_port"], k[0]["protocol"], k[0]["family"] = 12345, 80, 6, 2
+    h1 = lib.fb_flow_hash(N.ptr(k))
+    h2 = lib.fb_flow_hash(N.ptr(k.copy()))
+    assert h1 == h2 and h1 != 0
+    k[0]["dst_port"] = 81
+    assert lib.fb_flow_hash(N.ptr(k)) != h1

@@ -1,0 +1,99 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, bit-exact.
+
+Every comparison is on whole records (all 56 bytes), DNS side records, per-frame classes and
+batch statistics.  Sizes: hand-built edge cases, seeded synthetic samples the oracle finishes
+in seconds, and BASELINE.json's full sizes through size-independent properties.
+"""
+import numpy as np
+import pytest
+
+import framegen as fg
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from flodbadd_amd.sessions import SessionFilter
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(gpu, ref):
+    g_out, g_dns, g_cls, g_st = gpu.records, gpu.dns, gpu.cls, gpu.stats
+    r_out, r_dns, r_cls, r_st = ref
+    assert np.array_equal(g_cls, r_cls), "per-frame class mismatch at %s" % np.nonzero(g_cls != r_cls)[0][:10]
+    assert g_out.tobytes() == r_out.tobytes(), "session records differ"
+    assert g_dns.tobytes() == r_dns.tobytes(), "dns records differ"
+    for k in N.STATS_FIELDS:
+        if k.startswith("reserved") or k in ("new_sessions", "updated_sessions", "error"):
+            continue
+        assert g_st[k] == int(r_st[0][k]), k
+
+
+@pytest.mark.parametrize("flt", [SessionFilter.All, SessionFilter.GlobalOnly, SessionFilter.LocalOnly])
+def test_edge_cases(gpu_capture, flt):
+    frames, offs = fg.pack([f for _, f in fg.edge_cases()])
+    lan = [("2001:db8:abcd:12::1", 64)]
+    own = ["192.168.1.1", "10.0.0.5", "2001:db8::1"]
+    gpu_capture.set_filter(flt)
+    gpu_capture.set_lan_v6(lan)
+    gpu_capture.set_own_ips(own)
+    try:
+        from flodbadd_amd.capture import lan_v6_table, own_ip_table
+        cfg = coracle.make_cfg(int(flt), lan_v6=lan_v6_table(lan), own_ips=own_ip_table(own))
+        _assert_same(gpu_capture.parse_classify(frames, offs), coracle.parse_classify(cfg, frames, offs))
+    finally:
+        gpu_capture.set_filter(SessionFilter.All)
+        gpu_capture.set_lan_v6([])
+        gpu_capture.set_own_ips([])
+
+
+@pytest.mark.parametrize("config_id,n", [(2, 5000), (3, 5000), (3, 70001), (4, 200000)])
+def test_synthetic_vs_oracle(gpu_capture, config_id, n):
+    frames, offs = synth.generate(config_id, n)
+    cfg = coracle.make_cfg(2)
+    _assert_same(gpu_capture.parse_classify(frames, offs), coracle.parse_classify(cfg, frames, offs))
+
+
+def test_empty_and_tiny_batches(gpu_capture):
+    cfg = coracle.make_cfg(2)
+    for frames in ([], [fg.tcp_frame("1.2.3.4", 1000, "5.6.7.8", 80, fg.SYN, 0)], [b""] * 3):
+        buf, offs = fg.pack(frames)
+        _assert_same(gpu_capture.parse_classify(buf, offs), coracle.parse_classify(cfg, buf, offs))
+
+
+def test_bad_offsets(gpu_capture):
+    buf, offs = fg.pack([fg.tcp_frame("1.2.3.4", 1000, "5.6.7.8", 80, fg.SYN, 0)] * 4)
+    offs = offs.copy()
+    offs[2] = offs[1] - 1          # decreasing
+    offs[4] = offs[4] + 1000       # past the end of the buffer
+    cfg = coracle.make_cfg(2)
+    g = gpu_capture.parse_classify(buf, offs)
+    _assert_same(g, coracle.parse_classify(cfg, buf, offs))
+    assert g.stats["bad_offsets"] == 2
+
+
+def test_flow_table_vs_oracle(gpu_capture):
+    gpu_capture.clear_all_sessions()
+    flows = coracle.Flows()
+    cfg = coracle.make_cfg(2)
+    for b in range(3):
+        frames, offs = synth.generate(4, 60000, first=b * 60000)
+        g = gpu_capture.process_frames(frames, offs)
+        r_out, r_dns, r_cls, r_st = coracle.parse_classify(cfg, frames, offs)
+        assert g.records.tobytes() == r_out.tobytes()
+        r_st = np.zeros(1, dtype=N.STATS_DTYPE)
+        flows.update(r_out, r_st)
+        assert g.stats["new_sessions"] == int(r_st[0]["new_sessions"])
+        assert g.stats["updated_sessions"] == int(r_st[0]["updated_sessions"])
+    gflows = gpu_capture.export_flows()
+    rflows = flows.export_sorted()
+    assert len(gflows) == len(rflows)
+    assert rows_sorted(gflows) == rows_sorted(rflows)
+    gpu_capture.clear_all_sessions()
+    assert gpu_capture.flow_count() == 0
+
+
+def rows_sorted(arr):
+    """Order-independent view of a record array: its rows as sorted byte strings."""
+    b = arr.tobytes()
+    w = arr.dtype.itemsize
+    return sorted(b[i:i + w] for i in range(0, len(b), w))
