@@ -86,20 +86,22 @@ static int upload_cfg(fb_ctx* c, hipStream_t s) {
     return FB_OK;
 }
 
+// Look-back scratch sized for `tiles`; (re)zeroed on growth and when the 8-bit epoch wraps.
 static int ensure_status(fb_ctx* c, uint64_t tiles, hipStream_t s) {
-    if (tiles <= c->status_tiles && c->epoch < 0xFFFFFFF0u) return FB_OK;
+    if (tiles <= c->status_tiles && c->epoch < kMaxEpoch) return FB_OK;
     HIP_TRY(hipStreamSynchronize(s));
     if (tiles > c->status_tiles) {
         if (c->d_status) HIP_TRY(hipFree(c->d_status));
         c->d_status = nullptr;
         uint64_t want = std::max<uint64_t>(tiles, 1024);
-        if (hipMalloc(&c->d_status, want * kStatusWords * 8ull) != hipSuccess) {
+        want = (want + kGroup - 1) / kGroup * kGroup;
+        if (hipMalloc(&c->d_status, scratch_words(want) * 8ull) != hipSuccess) {
             c->status_tiles = 0;
-            return set_err(FB_ERR_NOMEM, "status buffer (%llu tiles)", (unsigned long long)want);
+            return set_err(FB_ERR_NOMEM, "look-back scratch (%llu tiles)", (unsigned long long)want);
         }
         c->status_tiles = want;
     }
-    HIP_TRY(hipMemset(c->d_status, 0, c->status_tiles * kStatusWords * 8ull));
+    HIP_TRY(hipMemset(c->d_status, 0, scratch_words(c->status_tiles) * 8ull));
     c->epoch = 0;  // epoch 0 is never used by a launch
     return FB_OK;
 }
@@ -264,13 +266,20 @@ int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_by
     p.dns = d_dns;
     p.cls = d_class;
     p.stats = d_stats;
-    p.status = c->d_status;
+    const uint64_t max_groups = c->status_tiles / kGroup;
+    p.tagg = c->d_status;
+    p.ginc = p.tagg + c->status_tiles;
+    p.gpre = p.ginc + max_groups;
+    p.gacc = p.gpre + max_groups;
+    p.gstat = p.gacc + 2 * max_groups;
+    p.max_groups = (uint32_t)max_groups;
     p.cfg = c->d_cfg;
     p.frames_bytes = (uint32_t)frames_bytes;
     p.n = n;
     p.num_tiles = (uint32_t)tiles;
     p.epoch = ++c->epoch;
     p.error = c->d_error;
+    p.dbg = nullptr;
     HIP_TRY(launch_parse_classify(p, s));
     return FB_OK;
 }
@@ -308,7 +317,7 @@ static int check_error_word(fb_ctx* c, hipStream_t s) {
     if (e) {
         HIP_TRY(hipMemsetAsync(c->d_error, 0, 4, s));
         HIP_TRY(hipStreamSynchronize(s));
-        c->epoch = 0xFFFFFFFFu;  // force a scratch reset before the next launch
+        c->epoch = kMaxEpoch;  // force a scratch reset before the next launch
         if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full");
         return set_err(FB_ERR_INTERNAL, "kernel bounded spin expired (code %u)", e);
     }

@@ -10,14 +10,25 @@ namespace fbk {
 
 // Packets per tile = kThreads * kRounds; one wavefront lane per packet per round.
 constexpr int kThreads = 256;
-constexpr int kRounds = 2;
+constexpr int kRounds = 4;
 constexpr int kTile = kThreads * kRounds;
+// Tiles per look-back group (two-level decoupled look-back, fb_parse.hip lookback()).
+constexpr int kGroup = 32;
 
-// Decoupled look-back status: per tile two 4-word sets (aggregate, inclusive prefix).
-// Word 0 = (epoch << 32) | n_session; 1 = (n_dns << 32) | n_filtered;
-// 2 = (n_tcp << 32) | n_ipv4;         3 = (n_bad_offsets << 32).
-// A set is valid when word 0's epoch equals the launch epoch (no per-launch zeroing).
-constexpr int kStatusWords = 8;
+// Look-back scratch (one allocation per context, zeroed when the 8-bit epoch wraps):
+//   tagg[tiles]          tile aggregate          [epoch:8 | n_dns:28 | n_session:28]
+//   ginc[groups]         group inclusive prefix  [epoch:8 | n_dns:28 | n_session:28]
+//   gpre[groups]         group exclusive prefix  [epoch:8 | n_dns:28 | n_session:28]
+//   gacc[2][groups]      group accumulator       [arrivals:8 | n_dns:28 | n_session:28]
+//   gstat[2][groups][2]  group stats             [arrivals:8 | n_tcp:28 | n_filtered:28],
+//                                                [arrivals:8 | n_bad:28 | n_ipv4:28]
+// Epoch-tagged words need no per-launch zeroing; the two accumulator parities alternate
+// between launches and each launch zeroes the parity the next one uses.
+constexpr uint32_t kMaxEpoch = 255;
+inline uint64_t scratch_words(uint64_t tiles) {
+    const uint64_t groups = (tiles + kGroup - 1) / kGroup;
+    return tiles + groups + groups + 2 * groups + 4 * groups;
+}
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
@@ -41,13 +52,19 @@ struct ParseParams {
     fb_dns_out* dns;
     uint8_t* cls;
     fb_batch_stats* stats;
-    unsigned long long* status;  // kStatusWords * num_tiles
+    unsigned long long* tagg;
+    unsigned long long* ginc;
+    unsigned long long* gpre;
+    unsigned long long* gacc;   // [2][max_groups]
+    unsigned long long* gstat;  // [2][max_groups][2]
+    uint32_t max_groups;
     const DevConfig* cfg;
     uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
     uint32_t n;
     uint32_t num_tiles;
     uint32_t epoch;
     uint32_t* error;  // set nonzero when a bounded spin expires
+    unsigned long long* dbg;  // diagnostic timestamps (ablation builds only; nullptr in product)
 };
 
 // Flow table: 128-byte slots (one L2 line).  tag: 0 empty, 1 being inserted, else

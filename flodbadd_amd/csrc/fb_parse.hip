@@ -8,16 +8,15 @@
 //   PACKET_STATS pre-filter counters  src/packets.rs:211-227
 //   map_tcp_flags (history char)      src/packets.rs:561-601
 //
-// Memory plan (HBM-bound integer/byte work, no MFMA):
-//   * offsets: one coalesced u32 per lane (+ next lane's via DPP shuffle).
-//   * frame header: four unaligned 16-B buffer loads per lane at frame offsets 10, 26, 42, 58
-//     (gfx950 runs in unaligned-access mode).  Offsets are chosen so every field the decoder
-//     needs sits at a fixed dword/byte position:  A=f[10..25] B=f[26..41] C=f[42..57]
-//     D=f[58..73].  Only an IPv4 header with options needs a fifth (dependent) load.
-//     Buffer loads are range-checked against frames_bytes: no read past the batch.
-//   * records: compacted in packet order by wave ballot + mbcnt, a per-block prefix over
-//     (round, wave) and a decoupled look-back across tiles (blockIdx order); one 56-B record
-//     per emitted packet.  No same-address atomics anywhere (they serialise at ~12 ns each).
+// Structure of one tile (kThreads * R frames, R rounds of one frame per lane):
+//   1. phased loads: the 8 KB service-port bitmap -> LDS, every round's offsets, then every
+//      round's four unaligned 16-B header loads (frame offsets 10, 26, 42, 58 -- chosen so every
+//      decoder field sits at a fixed dword/byte position; gfx950 runs in unaligned-access mode).
+//      All loads of a tile are in flight before the first use.  Buffer loads are range-checked
+//      against frames_bytes, so nothing reads past the batch.
+//   2. decode + classify in registers; wave ballots give per-(round, wave) counts.
+//   3. two-level decoupled look-back for the tile's global output offset (see lookback()).
+//   4. records staged through LDS per round and written with fully coalesced 16-B stores.
 #include "fb_internal.h"
 
 namespace fbk {
@@ -33,9 +32,7 @@ __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) <<
 __device__ __forceinline__ uint32_t be16_hi(uint32_t w) { return ((w >> 8) & 0xff00u) | (w >> 24); }
 __device__ __forceinline__ uint32_t bswap(uint32_t w) { return __builtin_bswap32(w); }
 
-__device__ __forceinline__ uint32_t svc(const DevConfig* c, uint32_t p) {
-    return (c->service_bitmap[p >> 5] >> (p & 31)) & 1u;
-}
+__device__ __forceinline__ uint32_t svc(const uint32_t* bm, uint32_t p) { return (bm[p >> 5] >> (p & 31)) & 1u; }
 
 // is_lan_ip, src/ip.rs:55-156, 199-242.
 __device__ __forceinline__ bool lan_v4(uint32_t v) {
@@ -83,25 +80,28 @@ __device__ __forceinline__ uint32_t hist_char(uint32_t fl, uint32_t plen, bool o
     return orig ? c : c + 32u;  // lower-case for the responder
 }
 
+struct Hdr {
+    u32x4 A, B, C, D;  // f[10..25] f[26..41] f[42..57] f[58..73]
+};
+
 struct Pkt {
     uint32_t cls;         // fb_class after filtering
     uint32_t w[14];       // the fb_pkt_out record (SESSION) / dns fields (DNS)
     bool tcp, v4, bad;    // stats bits (valid when session or filtered)
 };
 
-// Decode + classify one frame.  All byte reads come from the four header vectors; a field is
-// only used when the pnet length rules guarantee it lies inside the frame's caplen.
+// Decode + classify one frame from its header vectors; a field is only used when the pnet
+// length rules guarantee it lies inside the frame's caplen.
 __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const DevConfig* cfg,
-                                              uint32_t o0, uint32_t o1, uint32_t fbytes,
-                                              uint32_t idx, Pkt& k) {
+                                              const uint32_t* bm, const Hdr& h, uint32_t o0, uint32_t o1,
+                                              uint32_t fbytes, uint32_t idx, Pkt& k) {
     k.cls = FB_CLASS_DROP;
     k.tcp = false;
     k.v4 = false;
     const bool okoff = o1 >= o0 && o1 <= fbytes;
     k.bad = !okoff;
     const uint32_t L = okoff ? o1 - o0 : 0u;
-    const u32x4 A = ld16(r, o0 + 10u), B = ld16(r, o0 + 26u), C = ld16(r, o0 + 42u),
-                D = ld16(r, o0 + 58u);
+    const u32x4 A = h.A, B = h.B, C = h.C, D = h.D;
     if (L < 14u) return;                       // EthernetPacket::new -> None
     const uint32_t et = be16_hi(A.x);          // f[12..13]
     const uint32_t n = L - 14u;
@@ -182,7 +182,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     // ---- process_parsed_packet, src/packets.rs:202-327 -------------------------------------
     k.tcp = proto == 6u;
     k.v4 = fam == 2u;
-    const uint32_t S = svc(cfg, sport), Dsv = svc(cfg, dport);
+    const uint32_t S = svc(bm, sport), Dsv = svc(bm, dport);
     bool swap;
     if (S && !Dsv) {
         swap = true;
@@ -212,7 +212,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     meta |= lan_d ? FB_META_LOCAL_DST : 0u;
     meta |= own_ip(cfg, fam, ks) ? FB_META_SELF_SRC : 0u;
     meta |= own_ip(cfg, fam, kd) ? FB_META_SELF_DST : 0u;
-    meta |= svc(cfg, kport_d) ? FB_META_DST_SERVICE : 0u;
+    meta |= svc(bm, kport_d) ? FB_META_DST_SERVICE : 0u;
     const uint32_t hc = hasf ? hist_char(flags, plen, orig) : 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -231,145 +231,306 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     k.cls = drop ? FB_CLASS_FILTERED : FB_CLASS_SESSION;
 }
 
-__device__ __forceinline__ unsigned long long ld_status(const unsigned long long* p) {
+__device__ __forceinline__ unsigned long long ald(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_status(unsigned long long* p, unsigned long long v) {
+__device__ __forceinline__ void ast(unsigned long long* p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Publish one 4-word status set: payload words first, drained, then the epoch-tagged word 0
-// (MI355X_MICROARCH.md "Valid forms": 8-B agent atomics on both sides + vmcnt(0) before flag).
-__device__ __forceinline__ void publish(unsigned long long* s, const unsigned long long v[4],
-                                        uint32_t epoch) {
-    st_status(s + 1, v[1]);
-    st_status(s + 2, v[2]);
-    st_status(s + 3, v[3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_status(s + 0, ((unsigned long long)epoch << 32) | (v[0] & 0xffffffffull));
-}
+
+constexpr unsigned long long kCountMask = (1ull << 56) - 1ull;  // [dns:28 | session:28]
+__device__ __forceinline__ uint32_t tag_of(unsigned long long w) { return (uint32_t)(w >> 56); }
 
 __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
 
+// Ablation switches (tools/ubench_parse.hip); the product instantiates kFlagsProduct.
+constexpr uint32_t kFlagsProduct = 0u;
+constexpr uint32_t kNoLookback = 1u;  // base offsets = tile start (wrong output, timing only)
+constexpr uint32_t kNoStore = 2u;     // no record / dns stores (timing only)
+constexpr uint32_t kLoadsOnly = 4u;   // header loads only, no decode (timing only)
+constexpr uint32_t kCoalesced = 8u;   // with kLoadsOnly: wave-contiguous 1-KiB loads instead
+constexpr uint32_t kStamps = 16u;     // diagnostic per-tile s_memrealtime stamps into P.dbg
+#define FB_STAMP(k)                                                                            \
+    do {                                                                                       \
+        if constexpr ((FLAGS & kStamps) != 0u)                                                 \
+            if (threadIdx.x == 0u) P.dbg[blockIdx.x * 8u + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// ---- two-level decoupled look-back --------------------------------------------------------
+// Tiles form groups of kGroup consecutive tiles.  Every tile publishes, without ordering
+// constraints, (a) its epoch-tagged aggregate tagg[t] and (b) arrival-counted adds into its
+// group's accumulator gacc[g] and stats words.  A tile's exclusive prefix is
+//     gpre[g]  (the group's exclusive prefix)  +  sum of tagg over the group's earlier tiles.
+// Only the group's first tile (the leader) walks back over earlier groups to compute gpre[g]:
+// a group contributes its inclusive prefix ginc[] when published (the walk stops there) or
+// its accumulator once all kGroup arrivals are in.  The leader publishes gpre[g]; the group's
+// last tile publishes ginc[g].  Every dependency points to lower tile indices.
+//
+// Waiting discipline: coherent polls travel to the memory side and queue behind the frame
+// stream, and hundreds of spinning threads per tile flood it (measured: a look-back with every
+// walker spinning cost more than all record stores).  So each wait below reads every word
+// ONCE per wave, then ONE lane polls the nearest word that is not ready, with a back-off sleep.
+template <typename F>
+__device__ __forceinline__ void poll_until(F ready, uint32_t* err) {
+    uint32_t spins = 0u;
+    while (!ready()) {
+        __builtin_amdgcn_s_sleep(8);
+        if (++spins > (1u << 21)) { atomicOr(err, 1u); return; }
+    }
+}
+
+// Wave-level: lane l < m owns one word; `probe(l, v)` loads it, returns readiness and the value.
+// Returns once every owned word is ready (or a bounded spin expired).
+template <typename Probe>
+__device__ __forceinline__ void wave_wait(uint32_t m, Probe probe, unsigned long long& v, bool& ok,
+                                          uint32_t* err) {
+    const uint32_t lane = threadIdx.x & 63u;
+    ok = lane >= m;
+    v = 0ull;
+    if (!ok) ok = probe(v);
+    for (;;) {
+        const unsigned long long nr = __ballot(!ok);
+        if (nr == 0ull) return;
+        const uint32_t first = (uint32_t)(__ffsll((long long)nr) - 1);
+        if (lane == first) poll_until([&] { return probe(v); }, err), ok = true;
+        if (!ok) ok = probe(v);  // one re-read by the others
+    }
+}
+
+constexpr uint32_t kNoInc = 1u << 30;
+
+// Exclusive prefix of group g: walk back from group g-1 in windows of 64 groups (wave-level).
+__device__ unsigned long long group_prefix(const ParseParams& P, uint32_t g) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t ep = P.epoch;
+    const unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
+    unsigned long long pre = 0ull;
+    long hi = (long)g - 1;
+    while (hi >= 0) {
+        const uint32_t m = (uint32_t)min(hi + 1, 64L);
+        const long gg = hi - (long)lane;  // lane 0 = nearest group
+        bool inc = false;
+        unsigned long long v;
+        bool ok;
+        wave_wait(m, [&](unsigned long long& out) {
+            const unsigned long long vi = ald(P.ginc + gg);
+            if (tag_of(vi) == ep) { out = vi & kCountMask; inc = true; return true; }
+            const unsigned long long va = ald(acc + gg);
+            out = va & kCountMask;
+            return tag_of(va) == (uint32_t)kGroup;
+        }, v, ok, P.error);
+        const unsigned long long im = __ballot(lane < m && inc);
+        const uint32_t near = im ? (uint32_t)(__ffsll((long long)im) - 1) : kNoInc;
+        pre += wave_sum64(lane < m && lane <= near ? v : 0ull);
+        if (im) break;
+        hi -= 64;
+    }
+    return pre;
+}
+
+__device__ unsigned long long lookback(const ParseParams& P, uint32_t t, unsigned long long* s_sum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t ep = P.epoch;
+    const uint32_t g = t / kGroup, leader = g * kGroup;
+    if (wave == 0u) {  // group prefix
+        unsigned long long pre = 0ull;
+        if (t == leader) {
+            pre = group_prefix(P, g);
+            if (lane == 0u) ast(P.gpre + g, ((unsigned long long)ep << 56) | pre);
+        } else {
+            if (lane == 0u) {
+                poll_until([&] {
+                    const unsigned long long v = ald(P.gpre + g);
+                    pre = v & kCountMask;
+                    return tag_of(v) == ep;
+                }, P.error);
+            }
+        }
+        if (lane == 0u) s_sum[0] = pre;
+    } else if (wave == 1u) {  // earlier tiles of the same group
+        unsigned long long v;
+        bool ok;
+        wave_wait(t - leader, [&](unsigned long long& out) {
+            const unsigned long long x = ald(P.tagg + leader + lane);
+            out = x & kCountMask;
+            return tag_of(x) == ep;
+        }, v, ok, P.error);
+        v = wave_sum64(lane < t - leader ? v : 0ull);
+        if (lane == 0u) s_sum[1] = v;
+    }
+    __syncthreads();
+    const unsigned long long excl = s_sum[0] + s_sum[1];
+    __syncthreads();
+    return excl;
+}
+template <int R, uint32_t FLAGS>
 __global__ __launch_bounds__(kThreads) void k_parse_classify(const ParseParams P) {
+    constexpr int TILE = kThreads * R;
     const uint32_t tile = blockIdx.x;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const DevConfig* cfg = P.cfg;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
+    FB_STAMP(0);
 
-    __shared__ uint32_t s_cnt[kRounds][4][2];   // per (round, wave): sessions, dns
-    __shared__ uint32_t s_aux[kRounds][4][4];   // filtered, tcp, ipv4, bad
-    __shared__ unsigned long long s_excl[4];
+    __shared__ uint32_t s_bm[FB_SERVICE_BITMAP_BYTES / 4];
+    __shared__ unsigned long long s_stage[kThreads * 7];  // one round of 56-B records
+    __shared__ uint32_t s_cnt[R][4][2];                   // per (round, wave): sessions, dns
+    __shared__ uint32_t s_aux[4][4];                      // per wave: filtered, tcp, ipv4, bad
+    __shared__ unsigned long long s_sum[4];
+    __shared__ unsigned long long s_excl;
 
-    Pkt k[kRounds];
-    unsigned long long m_sess[kRounds], m_dns[kRounds];
+    // ---- 1. phased loads --------------------------------------------------------------------
+    const uint4* bmg = reinterpret_cast<const uint4*>(cfg->service_bitmap);
+    const uint4 bm0 = bmg[tid], bm1 = bmg[tid + kThreads];
+    uint32_t o0[R], o1[R];
 #pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd) {
-        const uint32_t i = tile * kTile + rd * kThreads + tid;
+    for (int rd = 0; rd < R; ++rd) {
+        const uint32_t i = tile * TILE + rd * kThreads + tid;
+        o0[rd] = P.offsets[min(i, P.n)];       // offsets has n+1 entries
+        o1[rd] = P.offsets[min(i + 1u, P.n)];
+    }
+    Hdr h[R];
+#pragma unroll
+    for (int rd = 0; rd < R; ++rd) {
+        if constexpr ((FLAGS & kCoalesced) != 0u) {
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(o0[rd]) & ~15u;
+            h[rd].A = ld16(rs, wb + 16u * lane);
+            h[rd].B = ld16(rs, wb + 1024u + 16u * lane);
+            h[rd].C = ld16(rs, wb + 2048u + 16u * lane);
+            h[rd].D = ld16(rs, wb + 3072u + 16u * lane);
+        } else {
+            h[rd].A = ld16(rs, o0[rd] + 10u);
+            h[rd].B = ld16(rs, o0[rd] + 26u);
+            h[rd].C = ld16(rs, o0[rd] + 42u);
+            h[rd].D = ld16(rs, o0[rd] + 58u);
+        }
+    }
+    if constexpr ((FLAGS & kLoadsOnly) != 0u) {
+        uint32_t x = 0u;
+#pragma unroll
+        for (int rd = 0; rd < R; ++rd) {
+            const u32x4 v = h[rd].A ^ h[rd].B ^ h[rd].C ^ h[rd].D;
+            x ^= v.x ^ v.y ^ v.z ^ v.w ^ o1[rd];
+        }
+        if (x == 0x9E3779B9u && P.cls) P.cls[0] = (uint8_t)x;
+        return;
+    }
+    reinterpret_cast<uint4*>(s_bm)[tid] = bm0;
+    reinterpret_cast<uint4*>(s_bm)[tid + kThreads] = bm1;
+    __syncthreads();
+
+    // ---- 2. decode + classify ---------------------------------------------------------------
+    Pkt k[R];
+    unsigned long long m_sess[R], m_dns[R];
+    uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;
+#pragma unroll
+    for (int rd = 0; rd < R; ++rd) {
+        const uint32_t i = tile * TILE + rd * kThreads + tid;
         const bool valid = i < P.n;
-        // offsets has n+1 entries: lane i reads offsets[min(i, n)], so the last frame's end
-        // offset arrives from the next lane; lane 63 reads its own.
-        uint32_t o0 = P.offsets[min(i, P.n)];
-        uint32_t o1 = __shfl_down(o0, 1, 64);
-        if (lane == 63u && valid) o1 = P.offsets[i + 1];
-        if (!valid) { o0 = 1u; o1 = 0u; }   // forces DROP, no stats (masked below)
-        process_frame(rs, cfg, o0, o1, P.frames_bytes, i, k[rd]);
+        process_frame(rs, cfg, s_bm, h[rd], valid ? o0[rd] : 1u, valid ? o1[rd] : 0u, P.frames_bytes, i, k[rd]);
         const bool is_s = valid && k[rd].cls == FB_CLASS_SESSION;
         const bool is_d = valid && k[rd].cls == FB_CLASS_DNS;
         const bool is_f = valid && k[rd].cls == FB_CLASS_FILTERED;
         const bool counted = is_s || is_f;
         m_sess[rd] = __ballot(is_s);
         m_dns[rd] = __ballot(is_d);
-        const unsigned long long m_f = __ballot(is_f);
-        const unsigned long long m_t = __ballot(counted && k[rd].tcp);
-        const unsigned long long m_4 = __ballot(counted && k[rd].v4);
-        const unsigned long long m_b = __ballot(valid && k[rd].bad);
+        a_f += __popcll(__ballot(is_f));
+        a_t += __popcll(__ballot(counted && k[rd].tcp));
+        a_4 += __popcll(__ballot(counted && k[rd].v4));
+        a_b += __popcll(__ballot(valid && k[rd].bad));
         if (lane == 0u) {
             s_cnt[rd][wave][0] = __popcll(m_sess[rd]);
             s_cnt[rd][wave][1] = __popcll(m_dns[rd]);
-            s_aux[rd][wave][0] = __popcll(m_f);
-            s_aux[rd][wave][1] = __popcll(m_t);
-            s_aux[rd][wave][2] = __popcll(m_4);
-            s_aux[rd][wave][3] = __popcll(m_b);
         }
         if (valid && P.cls) P.cls[i] = (uint8_t)k[rd].cls;
     }
+    if (lane == 0u) {
+        s_aux[wave][0] = a_f;
+        s_aux[wave][1] = a_t;
+        s_aux[wave][2] = a_4;
+        s_aux[wave][3] = a_b;
+    }
     __syncthreads();
 
-    // ---- tile aggregate + decoupled look-back (wave 0) ----------------------------------
-    if (wave == 0u) {
-        unsigned long long agg[4] = {0ull, 0ull, 0ull, 0ull};
+    FB_STAMP(1);
+    // ---- 3. tile aggregate, look-back, batch totals -----------------------------------------
+    unsigned long long agg = 0ull;
 #pragma unroll
-        for (int rd = 0; rd < kRounds; ++rd)
+    for (int rd = 0; rd < R; ++rd)
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                agg[0] += s_cnt[rd][w][0];
-                agg[1] += ((unsigned long long)s_cnt[rd][w][1] << 32) | s_aux[rd][w][0];
-                agg[2] += ((unsigned long long)s_aux[rd][w][1] << 32) | s_aux[rd][w][2];
-                agg[3] += (unsigned long long)s_aux[rd][w][3] << 32;
-            }
-        unsigned long long* st_agg = P.status + (size_t)tile * kStatusWords;
-        unsigned long long* st_inc = st_agg + 4;
-        unsigned long long ex[4] = {0ull, 0ull, 0ull, 0ull};
-        const unsigned long long ep = (unsigned long long)P.epoch << 32;
-        if (tile != 0u) {
-            if (lane == 0u) publish(st_agg, agg, P.epoch);
-            long pred = (long)tile - 1;
-            bool spin_fail = false;
-            for (;;) {
-                const long t = pred - (long)lane;  // lane 0 = nearest predecessor
-                bool virt = t < 0;                 // before tile 0: an empty inclusive prefix
-                unsigned long long vi = 0ull, va = 0ull;
-                bool inc_ok = virt, agg_ok = false;
-                uint32_t spins = 0u;
-                for (;;) {
-                    if (!virt && !inc_ok && !agg_ok) {
-                        const unsigned long long* s = P.status + (size_t)t * kStatusWords;
-                        vi = ld_status(s + 4);
-                        inc_ok = (vi & 0xffffffff00000000ull) == ep;
-                        if (!inc_ok) {
-                            va = ld_status(s);
-                            agg_ok = (va & 0xffffffff00000000ull) == ep;
-                        }
-                    }
-                    if (__all(inc_ok || agg_ok)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 24)) { spin_fail = true; break; }
-                }
-                if (spin_fail) break;
-                const unsigned long long pm = __ballot(inc_ok);
-                const uint32_t first = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 64u;
-                unsigned long long c[4] = {0ull, 0ull, 0ull, 0ull};
-                if (lane <= first && !virt) {
-                    const unsigned long long* s = P.status + (size_t)t * kStatusWords + (lane == first ? 4 : 0);
-                    c[0] = (lane == first ? vi : va) & 0xffffffffull;
-                    c[1] = ld_status(s + 1);
-                    c[2] = ld_status(s + 2);
-                    c[3] = ld_status(s + 3);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) ex[j] += wave_sum64(c[j]);
-                if (pm) break;
-                pred -= 64;
-            }
-            if (spin_fail && lane == 0u) atomicOr(P.error, 1u);
+        for (int w = 0; w < 4; ++w) agg += s_cnt[rd][w][0] | ((unsigned long long)s_cnt[rd][w][1] << 28);
+    const uint32_t ep = P.epoch;
+    const uint32_t g = tile / kGroup;
+    unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
+    unsigned long long* gst = P.gstat + (size_t)(ep & 1u) * P.max_groups * 2;
+    if (!(FLAGS & kNoLookback)) {
+        if (tid == 0u) {
+            const unsigned long long f = s_aux[0][0] + s_aux[1][0] + s_aux[2][0] + s_aux[3][0];
+            const unsigned long long tc = s_aux[0][1] + s_aux[1][1] + s_aux[2][1] + s_aux[3][1];
+            const unsigned long long v4 = s_aux[0][2] + s_aux[1][2] + s_aux[2][2] + s_aux[3][2];
+            const unsigned long long b = s_aux[0][3] + s_aux[1][3] + s_aux[2][3] + s_aux[3][3];
+            // Every published word carries its own arrival count or epoch, so the four writes
+            // need no ordering among themselves (no vmcnt waits on the publish path).
+            atomicAdd(acc + g, (1ull << 56) | agg);
+            atomicAdd(gst + 2 * g, (1ull << 56) | f | (tc << 28));
+            atomicAdd(gst + 2 * g + 1, (1ull << 56) | v4 | (b << 28));
+            ast(P.tagg + tile, ((unsigned long long)ep << 56) | agg);
         }
-        unsigned long long inc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) inc[j] = ex[j] + agg[j];
-        if (lane == 0u) {
-            publish(st_inc, inc, P.epoch);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s_excl[j] = ex[j];
-            if (tile == P.num_tiles - 1u && P.stats) {   // totals of the whole batch
+        // Zero the other parity's group words for the next launch (the previous launch, which
+        // used them, has completed: launches on one context are stream-ordered).
+        {
+            unsigned long long* nacc = P.gacc + (size_t)((ep & 1u) ^ 1u) * P.max_groups;
+            unsigned long long* nst = P.gstat + (size_t)((ep & 1u) ^ 1u) * P.max_groups * 2;
+            for (uint32_t q = tile * kThreads + tid; q < P.max_groups; q += P.num_tiles * kThreads) {
+                nacc[q] = 0ull;
+                nst[2 * q] = 0ull;
+                nst[2 * q + 1] = 0ull;
+            }
+        }
+        FB_STAMP(2);
+        const unsigned long long excl = lookback(P, tile, s_sum);
+        FB_STAMP(3);
+        const uint32_t g_last = min(g * kGroup + kGroup, P.num_tiles) - 1u;
+        if (tid == 0u) {
+            s_excl = excl;
+            if (tile == g_last) ast(P.ginc + g, ((unsigned long long)ep << 56) | (excl + agg));
+        }
+        if (tile == P.num_tiles - 1u && P.stats) {
+            // Sum every group's stats words once each has all its tiles' arrivals.
+            unsigned long long sf = 0ull, sb = 0ull;
+            for (uint32_t q = tid; q <= g; q += kThreads) {
+                const uint32_t want = q == g ? P.num_tiles - g * kGroup : (uint32_t)kGroup;
+                unsigned long long a = 0ull, b = 0ull;
+                poll_until([&] { a = ald(gst + 2 * q); return tag_of(a) == want; }, P.error);
+                poll_until([&] { b = ald(gst + 2 * q + 1); return tag_of(b) == want; }, P.error);
+                sf += a & kCountMask;
+                sb += b & kCountMask;
+            }
+            sf = wave_sum64(sf);
+            sb = wave_sum64(sb);
+            if (lane == 0u) s_sum[wave] = sf;
+            __syncthreads();
+            const unsigned long long SF = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+            __syncthreads();
+            if (lane == 0u) s_sum[wave] = sb;
+            __syncthreads();
+            const unsigned long long SB = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+            if (tid == 0u) {
                 fb_batch_stats* S = P.stats;
-                const unsigned long long ns = inc[0] & 0xffffffffull, nd = inc[1] >> 32,
-                                         nf = inc[1] & 0xffffffffull, nt = inc[2] >> 32,
-                                         n4 = inc[2] & 0xffffffffull, nb = inc[3] >> 32;
+                const unsigned long long tot_c = excl + agg;
+                const unsigned long long ns = tot_c & ((1ull << 28) - 1ull), nd = tot_c >> 28;
+                const unsigned long long nf = SF & ((1ull << 28) - 1ull), nt = SF >> 28;
+                const unsigned long long n4 = SB & ((1ull << 28) - 1ull), nb = SB >> 28;
                 const unsigned long long tot = ns + nf;
                 S->total_processed = tot;
                 S->tcp_processed = nt;
@@ -383,45 +544,65 @@ __global__ __launch_bounds__(kThreads) void k_parse_classify(const ParseParams P
                 S->n_drop = (unsigned long long)P.n - tot - nd;
                 S->n_filtered = nf;
                 S->bad_offsets = nb;
-                S->error = 0ull;
+                S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
             }
         }
+    } else if (tid == 0u) {
+        s_excl = (unsigned long long)tile * TILE;
     }
     __syncthreads();
+    if (FLAGS & kNoStore) return;
 
-    // ---- scatter records in packet order ---------------------------------------------------
-    uint32_t base_s = (uint32_t)(s_excl[0] & 0xffffffffull);
-    uint32_t base_d = (uint32_t)(s_excl[1] >> 32);
+    // ---- 4. records: stage one round in LDS, then coalesced 16-B stores ---------------------
+    uint32_t base_s = (uint32_t)(s_excl & ((1ull << 28) - 1ull));
+    uint32_t base_d = (FLAGS & kNoLookback) ? base_s : (uint32_t)(s_excl >> 28);
     const unsigned long long lmask = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd) {
-        uint32_t ps = base_s, pd = base_d;
-        for (uint32_t w = 0; w < wave; ++w) {
-            ps += s_cnt[rd][w][0];
-            pd += s_cnt[rd][w][1];
-        }
-        if (P.out && ((m_sess[rd] >> lane) & 1ull)) {
-            const uint32_t pos = ps + __popcll(m_sess[rd] & lmask);
-            uint32_t* o = reinterpret_cast<uint32_t*>(P.out + pos);
+    for (int rd = 0; rd < R; ++rd) {
+        uint32_t ls = 0u, ld = 0u, cs = 0u;
 #pragma unroll
-            for (int j = 0; j < 14; j += 2)
-                *reinterpret_cast<uint2*>(o + j) = make_uint2(k[rd].w[j], k[rd].w[j + 1]);
+        for (int w = 0; w < 4; ++w) {
+            if ((uint32_t)w < wave) { ls += s_cnt[rd][w][0]; ld += s_cnt[rd][w][1]; }
+            cs += s_cnt[rd][w][0];
+        }
+        if ((m_sess[rd] >> lane) & 1ull) {
+            unsigned long long* d = s_stage + (size_t)(ls + __popcll(m_sess[rd] & lmask)) * 7;
+#pragma unroll
+            for (int j = 0; j < 7; ++j)
+                d[j] = (unsigned long long)k[rd].w[2 * j] | ((unsigned long long)k[rd].w[2 * j + 1] << 32);
         }
         if (P.dns && ((m_dns[rd] >> lane) & 1ull)) {
-            const uint32_t pos = pd + __popcll(m_dns[rd] & lmask);
+            const uint32_t pos = base_d + ld + __popcll(m_dns[rd] & lmask);
             *reinterpret_cast<uint4*>(P.dns + pos) = make_uint4(k[rd].w[0], k[rd].w[1], k[rd].w[2], k[rd].w[3]);
         }
+        __syncthreads();
+        if (P.out && cs) {
+            // [base_s*56, (base_s+cs)*56) is 8-B aligned; 16-B aligned body + 8-B head/tail.
+            unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)base_s * 7;
+            const uint32_t units = cs * 7;                     // 8-B units
+            const uint32_t head = (base_s & 1u) ? 1u : 0u;     // base_s*56 % 16 == 8 when odd
+            const uint32_t body = (units - head) >> 1;         // 16-B units
+            if (head && tid == 0u) g8[0] = s_stage[0];
+            uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
+            for (uint32_t q = tid; q < body; q += kThreads) {
+                const unsigned long long x = s_stage[head + 2 * q], y = s_stage[head + 2 * q + 1];
+                g16[q] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+            }
+            if (tid == 0u && head + 2 * body < units) g8[units - 1] = s_stage[units - 1];
+        }
+        __syncthreads();
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             base_s += s_cnt[rd][w][0];
             base_d += s_cnt[rd][w][1];
         }
     }
+    FB_STAMP(4);
 }
 
 hipError_t launch_parse_classify(const ParseParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_parse_classify, dim3(p.num_tiles), dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((k_parse_classify<kRounds, kFlagsProduct>), dim3(p.num_tiles), dim3(kThreads), 0, s, p);
     return hipGetLastError();
 }
 
