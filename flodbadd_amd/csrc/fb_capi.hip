@@ -7,6 +7,7 @@
 // nothing aborts.  No CPU fallback exists: without a gfx950 device fb_create fails.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -58,6 +59,9 @@ struct fb_ctx {
     unsigned long long* d_status = nullptr;
     uint64_t status_tiles = 0;
     uint32_t epoch = 0;
+    // persistent parse kernel: grid = co-resident blocks; disabled after a protocol failure
+    uint32_t persist_grid = 0;
+    bool use_persistent = true;
     uint32_t* d_error = nullptr;
     // flow table
     FlowSlot* d_table = nullptr;
@@ -157,6 +161,16 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
     fb_ctx* c = new (std::nothrow) fb_ctx();
     if (!c) { set_err(FB_ERR_NOMEM, "fb_ctx"); return nullptr; }
     c->device = device;
+    {
+        // One block per CU fewer than the occupancy API reports: the API can over-report by
+        // one block for SGPR-heavy kernels (MI355X_MICROARCH.md "Residency"), and the persistent
+        // kernel needs every block resident.
+        int bpc = 0;
+        if (occupancy_parse_persistent(&bpc) != hipSuccess || bpc < 1) bpc = 1;
+        const int use = bpc > 1 ? bpc - 1 : 1;
+        c->persist_grid = (uint32_t)(use * prop.multiProcessorCount);
+        if (getenv("FB_NO_PERSISTENT")) c->use_persistent = false;
+    }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
     if (ok) {
@@ -280,7 +294,11 @@ int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_by
     p.epoch = ++c->epoch;
     p.error = c->d_error;
     p.dbg = nullptr;
-    HIP_TRY(launch_parse_classify(p, s));
+    if (c->use_persistent && c->persist_grid) {
+        HIP_TRY(launch_parse_persistent(p, std::min<uint32_t>(p.num_tiles, c->persist_grid), s));
+    } else {
+        HIP_TRY(launch_parse_classify(p, s));
+    }
     return FB_OK;
 }
 
@@ -318,6 +336,7 @@ static int check_error_word(fb_ctx* c, hipStream_t s) {
         HIP_TRY(hipMemsetAsync(c->d_error, 0, 4, s));
         HIP_TRY(hipStreamSynchronize(s));
         c->epoch = kMaxEpoch;  // force a scratch reset before the next launch
+        c->use_persistent = false;  // fall back to one tile per block (in-order dispatch only)
         if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full");
         return set_err(FB_ERR_INTERNAL, "kernel bounded spin expired (code %u)", e);
     }

@@ -10,7 +10,8 @@ namespace fbk {
 
 // Packets per tile = kThreads * kRounds; one wavefront lane per packet per round.
 constexpr int kThreads = 256;
-constexpr int kRounds = 4;
+constexpr int kRounds = 2;
+constexpr int kPRounds = kRounds;  // persistent kernel (same tile size)
 constexpr int kTile = kThreads * kRounds;
 // Tiles per look-back group (two-level decoupled look-back, fb_parse.hip lookback()).
 constexpr int kGroup = 32;
@@ -90,6 +91,8 @@ struct FlowParams {
 
 // Launchers (fb_parse.hip / fb_flow.hip).
 hipError_t launch_parse_classify(const ParseParams& p, hipStream_t s);
+hipError_t launch_parse_persistent(const ParseParams& p, uint32_t grid, hipStream_t s);
+hipError_t occupancy_parse_persistent(int* blocks_per_cu);
 hipError_t launch_flow_update(const FlowParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);

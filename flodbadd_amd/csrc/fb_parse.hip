@@ -81,7 +81,8 @@ __device__ __forceinline__ uint32_t hist_char(uint32_t fl, uint32_t plen, bool o
 }
 
 struct Hdr {
-    u32x4 A, B, C, D;  // f[10..25] f[26..41] f[42..57] f[58..73]
+    u32x4 A, B, C;  // f[10..25] f[26..41] f[42..57]
+    uint32_t Dz;    // f[66..69] (IPv6 TCP data offset + flags)
 };
 
 struct Pkt {
@@ -101,7 +102,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     const bool okoff = o1 >= o0 && o1 <= fbytes;
     k.bad = !okoff;
     const uint32_t L = okoff ? o1 - o0 : 0u;
-    const u32x4 A = h.A, B = h.B, C = h.C, D = h.D;
+    const u32x4 A = h.A, B = h.B, C = h.C;
     if (L < 14u) return;                       // EthernetPacket::new -> None
     const uint32_t et = be16_hi(A.x);          // f[12..13]
     const uint32_t n = L - 14u;
@@ -139,7 +140,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
         iplen = plen6 + 40u;
         fam = 10u;
         d0 = C.w;                                            // f[54..57]
-        d3 = D.z;                                            // f[66..69]
+        d3 = h.Dz;                                           // f[66..69]
     } else {
         return;                                              // VLAN, ARP, ... -> None
     }
@@ -288,13 +289,13 @@ __device__ __forceinline__ void poll_until(F ready, uint32_t* err) {
     }
 }
 
-// Wave-level: lane l < m owns one word; `probe(l, v)` loads it, returns readiness and the value.
-// Returns once every owned word is ready (or a bounded spin expired).
+// Wave-level: a lane with `own` set owns one word; `probe(v)` loads it and returns readiness
+// (v = the value).  Returns once every owned word is ready (or a bounded spin expired).
 template <typename Probe>
-__device__ __forceinline__ void wave_wait(uint32_t m, Probe probe, unsigned long long& v, bool& ok,
+__device__ __forceinline__ void wave_wait(bool own, Probe probe, unsigned long long& v, bool& ok,
                                           uint32_t* err) {
     const uint32_t lane = threadIdx.x & 63u;
-    ok = lane >= m;
+    ok = !own;
     v = 0ull;
     if (!ok) ok = probe(v);
     for (;;) {
@@ -321,7 +322,7 @@ __device__ unsigned long long group_prefix(const ParseParams& P, uint32_t g) {
         bool inc = false;
         unsigned long long v;
         bool ok;
-        wave_wait(m, [&](unsigned long long& out) {
+        wave_wait(lane < m, [&](unsigned long long& out) {
             const unsigned long long vi = ald(P.ginc + gg);
             if (tag_of(vi) == ep) { out = vi & kCountMask; inc = true; return true; }
             const unsigned long long va = ald(acc + gg);
@@ -335,6 +336,31 @@ __device__ unsigned long long group_prefix(const ParseParams& P, uint32_t g) {
         hi -= 64;
     }
     return pre;
+}
+
+// Single-wave look-back (the persistent kernel's control wave): lanes 0..m-1 read the earlier
+// tiles of the group, lane 63 the group's exclusive prefix (or the leader walks for it).
+__device__ unsigned long long lookback_wave(const ParseParams& P, uint32_t t) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t ep = P.epoch;
+    const uint32_t g = t / kGroup, leader = g * kGroup, m = t - leader;
+    const bool is_leader = t == leader;
+    unsigned long long v;
+    bool ok;
+    wave_wait(lane < m || (lane == 63u && !is_leader), [&](unsigned long long& out) {
+        const unsigned long long x = ald(lane == 63u ? P.gpre + g : P.tagg + leader + lane);
+        out = x & kCountMask;
+        return tag_of(x) == ep;
+    }, v, ok, P.error);
+    const unsigned long long within = wave_sum64(lane < m ? v : 0ull);
+    unsigned long long pre;
+    if (is_leader) {
+        pre = group_prefix(P, g);
+        if (lane == 0u) ast(P.gpre + g, ((unsigned long long)ep << 56) | pre);
+    } else {
+        pre = __shfl(v, 63, 64);
+    }
+    return pre + within;
 }
 
 __device__ unsigned long long lookback(const ParseParams& P, uint32_t t, unsigned long long* s_sum) {
@@ -359,7 +385,7 @@ __device__ unsigned long long lookback(const ParseParams& P, uint32_t t, unsigne
     } else if (wave == 1u) {  // earlier tiles of the same group
         unsigned long long v;
         bool ok;
-        wave_wait(t - leader, [&](unsigned long long& out) {
+        wave_wait(lane < t - leader, [&](unsigned long long& out) {
             const unsigned long long x = ald(P.tagg + leader + lane);
             out = x & kCountMask;
             return tag_of(x) == ep;
@@ -407,20 +433,20 @@ __global__ __launch_bounds__(kThreads) void k_parse_classify(const ParseParams P
             h[rd].A = ld16(rs, wb + 16u * lane);
             h[rd].B = ld16(rs, wb + 1024u + 16u * lane);
             h[rd].C = ld16(rs, wb + 2048u + 16u * lane);
-            h[rd].D = ld16(rs, wb + 3072u + 16u * lane);
+            h[rd].Dz = ld16(rs, wb + 3072u + 16u * lane).x;
         } else {
             h[rd].A = ld16(rs, o0[rd] + 10u);
             h[rd].B = ld16(rs, o0[rd] + 26u);
             h[rd].C = ld16(rs, o0[rd] + 42u);
-            h[rd].D = ld16(rs, o0[rd] + 58u);
+            h[rd].Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o0[rd] + 66u, 0, 0);
         }
     }
     if constexpr ((FLAGS & kLoadsOnly) != 0u) {
         uint32_t x = 0u;
 #pragma unroll
         for (int rd = 0; rd < R; ++rd) {
-            const u32x4 v = h[rd].A ^ h[rd].B ^ h[rd].C ^ h[rd].D;
-            x ^= v.x ^ v.y ^ v.z ^ v.w ^ o1[rd];
+            const u32x4 v = h[rd].A ^ h[rd].B ^ h[rd].C;
+            x ^= v.x ^ v.y ^ v.z ^ v.w ^ o1[rd] ^ h[rd].Dz;
         }
         if (x == 0x9E3779B9u && P.cls) P.cls[0] = (uint8_t)x;
         return;
@@ -599,6 +625,255 @@ __global__ __launch_bounds__(kThreads) void k_parse_classify(const ParseParams P
         }
     }
     FB_STAMP(4);
+}
+
+// ============================================================================================
+// Persistent, software-pipelined variant (the product kernel).
+//
+// Block b of G walks tiles b, b+G, b+2G, ... (a tile = kThreads * R frames).  Four worker
+// waves parse; a fifth, control wave owns the look-back.  Per tile:
+//   workers : classify tile t (its headers were prefetched)      -> counts      | B1
+//   control : publish t's aggregate, look back, publish prefixes  -> excl        |
+//   workers : stage t's records in LDS; issue tile t+G's header loads and tile
+//             t+2G's offset loads                                                 | B2
+//   workers : coalesced record stores of tile t                                   | B3
+// The control wave's coherent polls never enter the workers' vmcnt queue, so the next tile's
+// header loads stay in flight across the whole look-back: HBM keeps streaming while a tile
+// waits for its predecessors.  Requires the grid to be co-resident (G <= resident blocks);
+// every dependency points to lower tile indices and every spin is bounded.
+// ============================================================================================
+constexpr int kPThreads = kThreads + 64;
+
+template <int R>
+__device__ __forceinline__ void load_offsets(const ParseParams& P, uint32_t t, uint32_t (&a)[R], uint32_t (&b)[R]) {
+    constexpr int TILE = kThreads * R;
+#pragma unroll
+    for (int rd = 0; rd < R; ++rd) {
+        const uint32_t i = t * TILE + rd * kThreads + threadIdx.x;
+        a[rd] = P.offsets[min(i, P.n)];
+        b[rd] = P.offsets[min(i + 1u, P.n)];
+    }
+}
+template <int R>
+__device__ __forceinline__ void load_headers(__amdgpu_buffer_rsrc_t rs, const uint32_t (&o)[R], Hdr (&h)[R]) {
+#pragma unroll
+    for (int rd = 0; rd < R; ++rd) {
+        h[rd].A = ld16(rs, o[rd] + 10u);
+        h[rd].B = ld16(rs, o[rd] + 26u);
+        h[rd].C = ld16(rs, o[rd] + 42u);
+        h[rd].Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o[rd] + 66u, 0, 0);
+    }
+}
+
+template <int R, uint32_t FLAGS>
+__global__ __launch_bounds__(kPThreads, 4) void k_parse_persistent(const ParseParams P) {
+    constexpr int TILE = kThreads * R;
+    const uint32_t G = gridDim.x, T = P.num_tiles;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const bool control = wave == 4u;
+    const DevConfig* cfg = P.cfg;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
+
+    __shared__ uint32_t s_bm[FB_SERVICE_BITMAP_BYTES / 4];
+    __shared__ unsigned long long s_stage[R * kThreads * 7];  // one tile of 56-B records
+    __shared__ uint32_t s_cnt[R][4][2];                       // per (round, wave): sessions, dns
+    __shared__ uint32_t s_aux[4][4];                          // per wave: filtered, tcp, ipv4, bad
+    __shared__ unsigned long long s_excl;
+
+    const uint32_t ep = P.epoch;
+    unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
+    unsigned long long* gst = P.gstat + (size_t)(ep & 1u) * P.max_groups * 2;
+
+    uint32_t o0[R], o1[R], n0[R], n1[R];
+    Hdr h[R];
+    uint32_t t = blockIdx.x;
+    if (!control) {
+        const uint4* bmg = reinterpret_cast<const uint4*>(cfg->service_bitmap);
+        const uint4 bm0 = bmg[tid], bm1 = bmg[tid + kThreads];
+        load_offsets<R>(P, t, o0, o1);
+        load_headers<R>(rs, o0, h);
+        load_offsets<R>(P, min(t + G, T - 1u), n0, n1);
+        reinterpret_cast<uint4*>(s_bm)[tid] = bm0;
+        reinterpret_cast<uint4*>(s_bm)[tid + kThreads] = bm1;
+    } else {
+        // zero the other parity's group words for the next launch (see fb_internal.h)
+        unsigned long long* nacc = P.gacc + (size_t)((ep & 1u) ^ 1u) * P.max_groups;
+        unsigned long long* nst = P.gstat + (size_t)((ep & 1u) ^ 1u) * P.max_groups * 2;
+        for (uint32_t q = blockIdx.x * 64u + lane; q < P.max_groups; q += G * 64u) {
+            nacc[q] = 0ull;
+            nst[2 * q] = 0ull;
+            nst[2 * q + 1] = 0ull;
+        }
+    }
+    __syncthreads();
+
+    uint4 dnsw[R];  // DNS side records stay in registers (rare); session records go to LDS
+    unsigned long long m_sess[R], m_dns[R];
+    const unsigned long long lmask = (1ull << lane) - 1ull;
+    for (; t < T; t += G) {
+        if (!control) {
+            uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;
+#pragma unroll
+            for (int rd = 0; rd < R; ++rd) {
+                const uint32_t i = t * TILE + rd * kThreads + tid;
+                const bool valid = i < P.n;
+                Pkt k;
+                process_frame(rs, cfg, s_bm, h[rd], valid ? o0[rd] : 1u, valid ? o1[rd] : 0u, P.frames_bytes, i, k);
+                const bool is_s = valid && k.cls == FB_CLASS_SESSION;
+                const bool is_d = valid && k.cls == FB_CLASS_DNS;
+                const bool is_f = valid && k.cls == FB_CLASS_FILTERED;
+                const bool counted = is_s || is_f;
+                m_sess[rd] = __ballot(is_s);
+                m_dns[rd] = __ballot(is_d);
+                a_f += __popcll(__ballot(is_f));
+                a_t += __popcll(__ballot(counted && k.tcp));
+                a_4 += __popcll(__ballot(counted && k.v4));
+                a_b += __popcll(__ballot(valid && k.bad));
+                if (lane == 0u) {
+                    s_cnt[rd][wave][0] = __popcll(m_sess[rd]);
+                    s_cnt[rd][wave][1] = __popcll(m_dns[rd]);
+                }
+                if (valid && P.cls) P.cls[i] = (uint8_t)k.cls;
+                // wave-compacted staging: region (round, wave), record at popc(earlier lanes)
+                if (is_s) {
+                    unsigned long long* d = s_stage + ((size_t)(rd * 4 + wave) * 64 + __popcll(m_sess[rd] & lmask)) * 7;
+#pragma unroll
+                    for (int j = 0; j < 7; ++j)
+                        d[j] = (unsigned long long)k.w[2 * j] | ((unsigned long long)k.w[2 * j + 1] << 32);
+                }
+                dnsw[rd] = make_uint4(k.w[0], k.w[1], k.w[2], k.w[3]);
+            }
+            if (lane == 0u) {
+                s_aux[wave][0] = a_f;
+                s_aux[wave][1] = a_t;
+                s_aux[wave][2] = a_4;
+                s_aux[wave][3] = a_b;
+            }
+        }
+        __syncthreads();  // B1
+        if (control) {
+            unsigned long long agg = 0ull;
+#pragma unroll
+            for (int rd = 0; rd < R; ++rd)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) agg += s_cnt[rd][w][0] | ((unsigned long long)s_cnt[rd][w][1] << 28);
+            const uint32_t g = t / kGroup;
+            if (lane == 0u) {
+                const unsigned long long f = s_aux[0][0] + s_aux[1][0] + s_aux[2][0] + s_aux[3][0];
+                const unsigned long long tc = s_aux[0][1] + s_aux[1][1] + s_aux[2][1] + s_aux[3][1];
+                const unsigned long long v4 = s_aux[0][2] + s_aux[1][2] + s_aux[2][2] + s_aux[3][2];
+                const unsigned long long b = s_aux[0][3] + s_aux[1][3] + s_aux[2][3] + s_aux[3][3];
+                atomicAdd(acc + g, (1ull << 56) | agg);
+                atomicAdd(gst + 2 * g, (1ull << 56) | f | (tc << 28));
+                atomicAdd(gst + 2 * g + 1, (1ull << 56) | v4 | (b << 28));
+                ast(P.tagg + t, ((unsigned long long)ep << 56) | agg);
+            }
+            const unsigned long long excl = lookback_wave(P, t);
+            if (lane == 0u) {
+                s_excl = excl;
+                if (t == min(g * kGroup + kGroup, T) - 1u) ast(P.ginc + g, ((unsigned long long)ep << 56) | (excl + agg));
+            }
+            if (t == T - 1u && P.stats) {
+                // batch totals: every group's stats words, once all their arrivals are in
+                unsigned long long sf = 0ull, sb = 0ull;
+                for (uint32_t q0 = 0; q0 <= g; q0 += 64u) {
+                    const uint32_t q = q0 + lane;
+                    const uint32_t want = q == g ? T - g * kGroup : (uint32_t)kGroup;
+                    unsigned long long a, b;
+                    bool ok;
+                    wave_wait(q <= g, [&](unsigned long long& out) {
+                        const unsigned long long x = ald(gst + 2 * q);
+                        out = x;
+                        return tag_of(x) == want;
+                    }, a, ok, P.error);
+                    wave_wait(q <= g, [&](unsigned long long& out) {
+                        const unsigned long long x = ald(gst + 2 * q + 1);
+                        out = x;
+                        return tag_of(x) == want;
+                    }, b, ok, P.error);
+                    sf += q <= g ? (a & kCountMask) : 0ull;
+                    sb += q <= g ? (b & kCountMask) : 0ull;
+                }
+                sf = wave_sum64(sf);
+                sb = wave_sum64(sb);
+                if (lane == 0u) {
+                    fb_batch_stats* S = P.stats;
+                    const unsigned long long tot_c = excl + agg;
+                    const unsigned long long ns = tot_c & ((1ull << 28) - 1ull), nd = tot_c >> 28;
+                    const unsigned long long nf = sf & ((1ull << 28) - 1ull), nt = sf >> 28;
+                    const unsigned long long n4 = sb & ((1ull << 28) - 1ull), nb = sb >> 28;
+                    const unsigned long long tot = ns + nf;
+                    S->total_processed = tot;
+                    S->tcp_processed = nt;
+                    S->udp_processed = tot - nt;
+                    S->ipv4_processed = n4;
+                    S->ipv6_processed = tot - n4;
+                    S->new_sessions = 0ull;
+                    S->updated_sessions = 0ull;
+                    S->n_session = ns;
+                    S->n_dns = nd;
+                    S->n_drop = (unsigned long long)P.n - tot - nd;
+                    S->n_filtered = nf;
+                    S->bad_offsets = nb;
+                    S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
+                }
+            }
+        } else if (t + G < T) {
+            // prefetch: headers of tile t+G (offsets already here), offsets of tile t+2G
+#pragma unroll
+            for (int rd = 0; rd < R; ++rd) { o0[rd] = n0[rd]; o1[rd] = n1[rd]; }
+            load_headers<R>(rs, o0, h);
+            load_offsets<R>(P, min(t + 2u * G, T - 1u), n0, n1);
+        }
+        __syncthreads();  // B2
+        if (!control) {
+            // Each wave writes its (round, wave) segments: packet order = (round, wave, lane).
+            uint32_t exs = (uint32_t)(s_excl & ((1ull << 28) - 1ull));
+            uint32_t exd = (uint32_t)(s_excl >> 28);
+#pragma unroll
+            for (int rd = 0; rd < R; ++rd) {
+                uint32_t ls = 0u, ld = 0u, ts = 0u, td = 0u;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    if ((uint32_t)w < wave) { ls += s_cnt[rd][w][0]; ld += s_cnt[rd][w][1]; }
+                    ts += s_cnt[rd][w][0];
+                    td += s_cnt[rd][w][1];
+                }
+                if (P.dns && ((m_dns[rd] >> lane) & 1ull))
+                    P.dns[exd + ld + __popcll(m_dns[rd] & lmask)] = *reinterpret_cast<const fb_dns_out*>(&dnsw[rd]);
+                const uint32_t c = s_cnt[rd][wave][0];
+                if (P.out && c) {
+                    // [pos*56, (pos+c)*56) is 8-B aligned: 16-B body + 8-B head/tail
+                    const uint32_t pos = exs + ls;
+                    const unsigned long long* st = s_stage + (size_t)(rd * 4 + wave) * 64 * 7;
+                    unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)pos * 7;
+                    const uint32_t units = c * 7, head = pos & 1u, body = (units - head) >> 1;
+                    if (head && lane == 0u) g8[0] = st[0];
+                    uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
+                    for (uint32_t q = lane; q < body; q += 64u) {
+                        const unsigned long long x = st[head + 2 * q], y = st[head + 2 * q + 1];
+                        g16[q] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+                    }
+                    if (lane == 0u && head + 2 * body < units) g8[units - 1] = st[units - 1];
+                }
+                exs += ts;
+                exd += td;
+            }
+        }
+        __syncthreads();  // B3: stage and counts free for the next tile
+    }
+}
+
+hipError_t launch_parse_persistent(const ParseParams& p, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_parse_persistent<kPRounds, kFlagsProduct>), dim3(grid), dim3(kPThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t occupancy_parse_persistent(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_persistent<kPRounds, kFlagsProduct>),
+                                                        kPThreads, 0);
 }
 
 hipError_t launch_parse_classify(const ParseParams& p, hipStream_t s) {

@@ -125,8 +125,14 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;  // upper bound: all emitted
     const char* names[] = {"product", "no_lookback", "no_store", "loads_classify_only", "read_frames", "copy_frames_to_out",
-                           "header_loads_only", "coalesced_loads_only"};
-    const int NV = 8;
+                           "header_loads_only", "coalesced_loads_only", "persistent"};
+    const int NV = 9;
+    int bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_persistent<UB_R, 0>), fbk::kPThreads, 0));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const uint32_t pgrid = std::min<uint32_t>(tiles, (uint32_t)(std::max(bpc - 1, 1) * prop.multiProcessorCount));
+    printf("{\"persistent_blocks_per_cu_api\": %d, \"grid\": %u, \"cus\": %d}\n", bpc, pgrid, prop.multiProcessorCount);
     std::vector<double> best(NV, 1e30), sum(NV, 0.0);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -145,6 +151,7 @@ int main(int argc, char** argv) {
                 case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
                 case 6: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kLoadsOnly>), dim3(tiles), dim3(256), 0, s, params(r, false)); break;
                 case 7: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kLoadsOnly | fbk::kCoalesced>), dim3(tiles), dim3(256), 0, s, params(r, false)); break;
+                case 8: hipLaunchKernelGGL((fbk::k_parse_persistent<UB_R, 0>), dim3(pgrid), dim3(fbk::kPThreads), 0, s, params(r, true)); break;
                 case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
                 }
             }
