@@ -13,7 +13,7 @@ GPU_LIB_PATH = os.path.join(PKG, "libflodbadd_gpu.so")
 SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
 
 FB_ABI_VERSION = 1
-FB_MAX_BATCH_PACKETS = (1 << 28) - 1
+FB_MAX_BATCH_PACKETS = (1 << 27) - 1
 FB_MAX_LAN_V6 = 64
 FB_MAX_OWN_IPS = 64
 

@@ -59,10 +59,9 @@ struct fb_ctx {
     unsigned long long* d_status = nullptr;
     uint64_t status_tiles = 0;
     uint32_t epoch = 0;
-    // persistent parse kernel: grid = co-resident blocks; disabled after a protocol failure
-    uint32_t persist_grid = 0;
-    bool use_persistent = true;
-    uint32_t* d_error = nullptr;
+    // persistent parse kernel: grid = co-resident blocks (halved after a protocol failure)
+    uint32_t grid = 0;
+    uint32_t* d_error = nullptr;  // [2] error words, indexed by epoch parity
     // flow table
     FlowSlot* d_table = nullptr;
     uint64_t table_cap = 0;
@@ -98,14 +97,16 @@ static int ensure_status(fb_ctx* c, uint64_t tiles, hipStream_t s) {
         if (c->d_status) HIP_TRY(hipFree(c->d_status));
         c->d_status = nullptr;
         uint64_t want = std::max<uint64_t>(tiles, 1024);
-        want = (want + kGroup - 1) / kGroup * kGroup;
         if (hipMalloc(&c->d_status, scratch_words(want) * 8ull) != hipSuccess) {
             c->status_tiles = 0;
             return set_err(FB_ERR_NOMEM, "look-back scratch (%llu tiles)", (unsigned long long)want);
         }
         c->status_tiles = want;
     }
-    HIP_TRY(hipMemset(c->d_status, 0, scratch_words(c->status_tiles) * 8ull));
+    // Stream-ordered: the launches run on `s`, which may be a non-blocking stream that does not
+    // synchronise with the null stream (a plain hipMemset here raced the next launch).
+    HIP_TRY(hipMemsetAsync(c->d_status, 0, scratch_words(c->status_tiles) * 8ull, s));
+    HIP_TRY(hipMemsetAsync(c->d_error, 0, 16, s));
     c->epoch = 0;  // epoch 0 is never used by a launch
     return FB_OK;
 }
@@ -162,14 +163,17 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
     if (!c) { set_err(FB_ERR_NOMEM, "fb_ctx"); return nullptr; }
     c->device = device;
     {
-        // One block per CU fewer than the occupancy API reports: the API can over-report by
-        // one block for SGPR-heavy kernels (MI355X_MICROARCH.md "Residency"), and the persistent
-        // kernel needs every block resident.
+        // Residency: the occupancy API, capped by the SGPR rule of MI355X_MICROARCH.md
+        // ("Residency"): at most floor(800 / (sgpr_alloc + 16)) waves per SIMD, i.e. 6 at the
+        // 106-SGPR worst case, 24 per CU.  The kernel needs every block resident (look-back).
         int bpc = 0;
-        if (occupancy_parse_persistent(&bpc) != hipSuccess || bpc < 1) bpc = 1;
-        const int use = bpc > 1 ? bpc - 1 : 1;
-        c->persist_grid = (uint32_t)(use * prop.multiProcessorCount);
-        if (getenv("FB_NO_PERSISTENT")) c->use_persistent = false;
+        if (occupancy_parse(&bpc) != hipSuccess || bpc < 1) bpc = 1;
+        int use = std::min(bpc, std::max(1, 24 / (kThreads / 64)));
+        if (const char* e = getenv("FB_BLOCKS_PER_CU")) {
+            const int want = atoi(e);
+            if (want >= 1 && want < use) use = want;
+        }
+        c->grid = std::min<uint32_t>((uint32_t)(use * prop.multiProcessorCount), kMaxBlocks);  // FB_BLOCKS_PER_CU: tuning cap
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -280,25 +284,17 @@ int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_by
     p.dns = d_dns;
     p.cls = d_class;
     p.stats = d_stats;
-    const uint64_t max_groups = c->status_tiles / kGroup;
     p.tagg = c->d_status;
-    p.ginc = p.tagg + c->status_tiles;
-    p.gpre = p.ginc + max_groups;
-    p.gacc = p.gpre + max_groups;
-    p.gstat = p.gacc + 2 * max_groups;
-    p.max_groups = (uint32_t)max_groups;
+    p.wstat = p.tagg + c->status_tiles;
     p.cfg = c->d_cfg;
     p.frames_bytes = (uint32_t)frames_bytes;
     p.n = n;
     p.num_tiles = (uint32_t)tiles;
     p.epoch = ++c->epoch;
-    p.error = c->d_error;
+    p.error = c->d_error + (p.epoch & 1u);
+    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
     p.dbg = nullptr;
-    if (c->use_persistent && c->persist_grid) {
-        HIP_TRY(launch_parse_persistent(p, std::min<uint32_t>(p.num_tiles, c->persist_grid), s));
-    } else {
-        HIP_TRY(launch_parse_classify(p, s));
-    }
+    HIP_TRY(launch_parse_classify(p, std::min<uint32_t>(p.num_tiles, c->grid), s));
     return FB_OK;
 }
 
@@ -330,13 +326,11 @@ static int ensure_staging(fb_ctx* c, uint64_t n, uint64_t bytes) {
 
 static int check_error_word(fb_ctx* c, hipStream_t s) {
     uint32_t e = 0;
-    HIP_TRY(hipMemcpyAsync(&e, c->d_error, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&e, c->d_error + (c->epoch & 1u), 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (e) {
-        HIP_TRY(hipMemsetAsync(c->d_error, 0, 4, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        c->epoch = kMaxEpoch;  // force a scratch reset before the next launch
-        c->use_persistent = false;  // fall back to one tile per block (in-order dispatch only)
+        c->epoch = kMaxEpoch;  // force a scratch + error-word reset before the next launch
+        if (e & 1u) c->grid = std::max<uint32_t>(c->grid / 2u, 1u);  // look-back starved: shrink
         if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full");
         return set_err(FB_ERR_INTERNAL, "kernel bounded spin expired (code %u)", e);
     }
@@ -386,10 +380,10 @@ int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_st
     p.table = c->d_table;
     p.mask = c->table_cap - 1;
     p.partials = c->d_partials;
-    p.error = c->d_error;
+    p.error = c->d_error + (c->epoch & 1u);
     p.max_recs = 0xFFFFFFFFu;
     HIP_TRY(launch_flow_update(p, kFlowGrid, s));
-    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, kFlowGrid, c->d_error, s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, kFlowGrid, c->d_error + (c->epoch & 1u), s));
     return FB_OK;
 }
 

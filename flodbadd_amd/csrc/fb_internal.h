@@ -8,28 +8,28 @@
 
 namespace fbk {
 
-// Packets per tile = kThreads * kRounds; one wavefront lane per packet per round.
-constexpr int kThreads = 256;
-constexpr int kRounds = 2;
-constexpr int kPRounds = kRounds;  // persistent kernel (same tile size)
-constexpr int kTile = kThreads * kRounds;
-// Tiles per look-back group (two-level decoupled look-back, fb_parse.hip lookback()).
-constexpr int kGroup = 32;
+// Parse kernel (fb_parse.hip): a look-back unit = one block-round = kThreads/64 waves x
+// kUnitTiles wave-tiles x 64 frames (one lane per frame per wave-tile).
+#ifndef FB_BLOCK_THREADS
+#define FB_BLOCK_THREADS 512
+#endif
+constexpr int kThreads = FB_BLOCK_THREADS;
+#ifndef FB_UNIT_TILES
+#define FB_UNIT_TILES 2
+#endif
+constexpr int kUnitTiles = FB_UNIT_TILES;
+constexpr int kTile = (kThreads / 64) * 64 * kUnitTiles;  // frames per look-back unit
+
+// Upper bound on parse blocks per launch (per-block stats slots).
+constexpr uint32_t kMaxBlocks = 4096;
 
 // Look-back scratch (one allocation per context, zeroed when the 8-bit epoch wraps):
-//   tagg[tiles]          tile aggregate          [epoch:8 | n_dns:28 | n_session:28]
-//   ginc[groups]         group inclusive prefix  [epoch:8 | n_dns:28 | n_session:28]
-//   gpre[groups]         group exclusive prefix  [epoch:8 | n_dns:28 | n_session:28]
-//   gacc[2][groups]      group accumulator       [arrivals:8 | n_dns:28 | n_session:28]
-//   gstat[2][groups][2]  group stats             [arrivals:8 | n_tcp:28 | n_filtered:28],
-//                                                [arrivals:8 | n_bad:28 | n_ipv4:28]
-// Epoch-tagged words need no per-launch zeroing; the two accumulator parities alternate
-// between launches and each launch zeroes the parity the next one uses.
+//   tagg[units]           unit status   [epoch:8 | INC:1 | n_dns:27 | n_session:28]
+//   wstat[kMaxBlocks][2]  per-block pre-filter counters [epoch:8 | n_tcp:28 | n_filtered:28],
+//                                                      [epoch:8 | n_bad:28 | n_ipv4:28]
+// Epoch-tagged words need no per-launch zeroing.
 constexpr uint32_t kMaxEpoch = 255;
-inline uint64_t scratch_words(uint64_t tiles) {
-    const uint64_t groups = (tiles + kGroup - 1) / kGroup;
-    return tiles + groups + groups + 2 * groups + 4 * groups;
-}
+inline uint64_t scratch_words(uint64_t units) { return units + 2ull * kMaxBlocks; }
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
@@ -53,19 +53,16 @@ struct ParseParams {
     fb_dns_out* dns;
     uint8_t* cls;
     fb_batch_stats* stats;
-    unsigned long long* tagg;
-    unsigned long long* ginc;
-    unsigned long long* gpre;
-    unsigned long long* gacc;   // [2][max_groups]
-    unsigned long long* gstat;  // [2][max_groups][2]
-    uint32_t max_groups;
+    unsigned long long* tagg;   // [units]
+    unsigned long long* wstat;  // [kMaxBlocks][2]
     const DevConfig* cfg;
     uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
     uint32_t n;
     uint32_t num_tiles;
     uint32_t epoch;
-    uint32_t* error;  // set nonzero when a bounded spin expires
-    unsigned long long* dbg;  // diagnostic timestamps (ablation builds only; nullptr in product)
+    uint32_t* error;       // this launch's error word (epoch parity); nonzero: a bounded spin expired
+    uint32_t* error_next;  // the other parity's word, zeroed by this launch for the next one
+    unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
 };
 
 // Flow table: 128-byte slots (one L2 line).  tag: 0 empty, 1 being inserted, else
@@ -90,9 +87,8 @@ struct FlowParams {
 };
 
 // Launchers (fb_parse.hip / fb_flow.hip).
-hipError_t launch_parse_classify(const ParseParams& p, hipStream_t s);
-hipError_t launch_parse_persistent(const ParseParams& p, uint32_t grid, hipStream_t s);
-hipError_t occupancy_parse_persistent(int* blocks_per_cu);
+hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
+hipError_t occupancy_parse(int* blocks_per_cu);
 hipError_t launch_flow_update(const FlowParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);

@@ -1,4 +1,4 @@
-// fb_parse.hip -- gfx950 parse + classify kernel.
+// fb_parse.hip -- gfx950 parse + classify kernel (persistent, wave-level lag-1 pipeline).
 //
 // One wavefront lane per frame.  Replaces, per frame:
 //   parse_packet_pcap                 src/packets.rs:603-802 (pnet_packet 0.35.0 decode)
@@ -8,15 +8,27 @@
 //   PACKET_STATS pre-filter counters  src/packets.rs:211-227
 //   map_tcp_flags (history char)      src/packets.rs:561-601
 //
-// Structure of one tile (kThreads * R frames, R rounds of one frame per lane):
-//   1. phased loads: the 8 KB service-port bitmap -> LDS, every round's offsets, then every
-//      round's four unaligned 16-B header loads (frame offsets 10, 26, 42, 58 -- chosen so every
-//      decoder field sits at a fixed dword/byte position; gfx950 runs in unaligned-access mode).
-//      All loads of a tile are in flight before the first use.  Buffer loads are range-checked
-//      against frames_bytes, so nothing reads past the batch.
-//   2. decode + classify in registers; wave ballots give per-(round, wave) counts.
-//   3. two-level decoupled look-back for the tile's global output offset (see lookback()).
-//   4. records staged through LDS per round and written with fully coalesced 16-B stores.
+// Output is stream-compacted in packet order (SESSION records, DNS side records), so each tile
+// needs the global count of records emitted before it: a decoupled look-back.  Measured on a
+// one-tile-per-block kernel (C2, 1M x 64 B): 45 us, 14 us of it look-back waits, because all
+// resident blocks load, then all wait, then all store, with HBM idle during the wait.
+//
+// Here every WAVE is an independent agent with no block barrier in its loop:
+//   grid = co-resident blocks of 4 waves; wave w (of W) owns wave-tiles w, w+W, w+2W, ...
+//   (a wave-tile = 64*R frames; static ownership, no ticket atomics: every tile a look-back
+//   waits on belongs to a running wave because the grid never exceeds residency).
+//   iteration: wait headers(cur) -> decode/classify into registers -> publish cur's count
+//              -> probe the look-back words of PREV (the wave's previous tile, classified one
+//                 iteration ago, so its predecessors are normally published by now)
+//              -> issue header loads of next and offset loads of the tile after (younger than
+//                 the probes, so the probes do not wait for them)
+//              -> finish the look-back (all not-ready lanes re-poll together) -> store prev's
+//                 records with coalesced 16-B stores from the wave's LDS stage -> stage cur.
+//   HBM sees one tile of header loads per wave in flight across the look-back and the stores.
+//
+// Loads: four unaligned 16-B header loads per frame at frame offsets 10, 26, 42 (+ one dword at
+// 66 for IPv6/TCP) so every decoder field sits at a fixed dword/byte position; buffer loads are
+// range-checked against frames_bytes, so nothing reads past the batch.
 #include "fb_internal.h"
 
 namespace fbk {
@@ -232,6 +244,17 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     k.cls = drop ? FB_CLASS_FILTERED : FB_CLASS_SESSION;
 }
 
+__device__ __forceinline__ fb_dns_out make_fb_dns(const Pkt& k) {
+    fb_dns_out d;
+    d.pkt_index = k.w[0];
+    d.payload_offset = k.w[1];
+    d.payload_length = k.w[2];
+    d.protocol = (uint8_t)(k.w[3] & 0xffu);
+    d.family = (uint8_t)(k.w[3] >> 8);
+    d.reserved = 0;
+    return d;
+}
+
 __device__ __forceinline__ unsigned long long ald(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -247,638 +270,327 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
 // Ablation switches (tools/ubench_parse.hip); the product instantiates kFlagsProduct.
 constexpr uint32_t kFlagsProduct = 0u;
 constexpr uint32_t kNoLookback = 1u;  // base offsets = tile start (wrong output, timing only)
 constexpr uint32_t kNoStore = 2u;     // no record / dns stores (timing only)
-constexpr uint32_t kLoadsOnly = 4u;   // header loads only, no decode (timing only)
-constexpr uint32_t kCoalesced = 8u;   // with kLoadsOnly: wave-contiguous 1-KiB loads instead
-constexpr uint32_t kStamps = 16u;     // diagnostic per-tile s_memrealtime stamps into P.dbg
-#define FB_STAMP(k)                                                                            \
-    do {                                                                                       \
-        if constexpr ((FLAGS & kStamps) != 0u)                                                 \
-            if (threadIdx.x == 0u) P.dbg[blockIdx.x * 8u + (k)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
+constexpr uint32_t kStamps = 4u;      // per-tile s_memrealtime stamps + poll counts into P.dbg
+// dbg layout per tile t: [0] classified, [1] look-back issued, [2] look-back done, [3] spins
 
-// ---- two-level decoupled look-back --------------------------------------------------------
-// Tiles form groups of kGroup consecutive tiles.  Every tile publishes, without ordering
-// constraints, (a) its epoch-tagged aggregate tagg[t] and (b) arrival-counted adds into its
-// group's accumulator gacc[g] and stats words.  A tile's exclusive prefix is
-//     gpre[g]  (the group's exclusive prefix)  +  sum of tagg over the group's earlier tiles.
-// Only the group's first tile (the leader) walks back over earlier groups to compute gpre[g]:
-// a group contributes its inclusive prefix ginc[] when published (the walk stops there) or
-// its accumulator once all kGroup arrivals are in.  The leader publishes gpre[g]; the group's
-// last tile publishes ginc[g].  Every dependency points to lower tile indices.
-//
-// Waiting discipline: coherent polls travel to the memory side and queue behind the frame
-// stream, and hundreds of spinning threads per tile flood it (measured: a look-back with every
-// walker spinning cost more than all record stores).  So each wait below reads every word
-// ONCE per wave, then ONE lane polls the nearest word that is not ready, with a back-off sleep.
-template <typename F>
-__device__ __forceinline__ void poll_until(F ready, uint32_t* err) {
-    uint32_t spins = 0u;
-    while (!ready()) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++spins > (1u << 21)) { atomicOr(err, 1u); return; }
-    }
+// ---- look-back ----------------------------------------------------------------------------
+// One status word per unit, epoch-tagged: [epoch:8 | INC:1 | n_dns:27 | n_session:28].
+//   published twice by the unit's look-back wave with plain sc1 stores (no atomics, no shared
+//   accumulator line that every block hammers): AGG (its own count) right after classification,
+//   INC (its inclusive prefix) once its look-back is done.
+// Look-back of unit u: read predecessors u-1, u-2, ... in windows of 256 (4 words per lane, one
+// memory round trip), stop at the nearest INC; every word up to it must be published (AGG or
+// INC of this epoch).  Not-ready words are re-polled by their lanes together with exponential
+// back-off, so a wait costs one round trip per readiness event, not one per word.
+constexpr unsigned long long kIncBit = 1ull << 55;
+constexpr unsigned long long kCnt28 = (1ull << 28) - 1ull;
+__device__ __forceinline__ unsigned long long st_counts(unsigned long long w) {
+    return (w & kCnt28) | (((w >> 28) & ((1ull << 27) - 1ull)) << 28);
+}
+__device__ __forceinline__ unsigned long long st_pack(uint32_t ep, bool inc, unsigned long long c) {
+    return ((unsigned long long)ep << 56) | (inc ? kIncBit : 0ull) | (c & kCnt28) |
+           (((c >> 28) & ((1ull << 27) - 1ull)) << 28);
 }
 
-// Wave-level: a lane with `own` set owns one word; `probe(v)` loads it and returns readiness
-// (v = the value).  Returns once every owned word is ready (or a bounded spin expired).
-template <typename Probe>
-__device__ __forceinline__ void wave_wait(bool own, Probe probe, unsigned long long& v, bool& ok,
-                                          uint32_t* err) {
-    const uint32_t lane = threadIdx.x & 63u;
-    ok = !own;
-    v = 0ull;
-    if (!ok) ok = probe(v);
-    for (;;) {
-        const unsigned long long nr = __ballot(!ok);
-        if (nr == 0ull) return;
-        const uint32_t first = (uint32_t)(__ffsll((long long)nr) - 1);
-        if (lane == first) poll_until([&] { return probe(v); }, err), ok = true;
-        if (!ok) ok = probe(v);  // one re-read by the others
-    }
-}
-
-constexpr uint32_t kNoInc = 1u << 30;
-
-// Exclusive prefix of group g: walk back from group g-1 in windows of 64 groups (wave-level).
-__device__ unsigned long long group_prefix(const ParseParams& P, uint32_t g) {
+template <uint32_t FLAGS>
+__device__ unsigned long long lookback_unit(const ParseParams& P, uint32_t u, uint32_t& spins) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t ep = P.epoch;
-    const unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
     unsigned long long pre = 0ull;
-    long hi = (long)g - 1;
+    long hi = (long)u - 1;  // nearest predecessor not yet accounted for
+    spins = 0u;
     while (hi >= 0) {
-        const uint32_t m = (uint32_t)min(hi + 1, 64L);
-        const long gg = hi - (long)lane;  // lane 0 = nearest group
-        bool inc = false;
-        unsigned long long v;
-        bool ok;
-        wave_wait(lane < m, [&](unsigned long long& out) {
-            const unsigned long long vi = ald(P.ginc + gg);
-            if (tag_of(vi) == ep) { out = vi & kCountMask; inc = true; return true; }
-            const unsigned long long va = ald(acc + gg);
-            out = va & kCountMask;
-            return tag_of(va) == (uint32_t)kGroup;
-        }, v, ok, P.error);
-        const unsigned long long im = __ballot(lane < m && inc);
-        const uint32_t near = im ? (uint32_t)(__ffsll((long long)im) - 1) : kNoInc;
-        pre += wave_sum64(lane < m && lane <= near ? v : 0ull);
-        if (im) break;
-        hi -= 64;
+        unsigned long long v[4];
+        bool own[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long idx = hi - (long)(k * 64 + lane);  // distance k*64+lane from hi
+            own[k] = idx >= 0;
+            v[k] = own[k] ? ald(P.tagg + idx) : 0ull;
+        }
+        for (;;) {
+            // nearest INC in the window (smallest distance)
+            uint32_t near = 256u;
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {
+                const unsigned long long im = __ballot(own[k] && tag_of(v[k]) == ep && (v[k] & kIncBit));
+                if (im) near = (uint32_t)k * 64u + (uint32_t)(__ffsll((long long)im) - 1);
+            }
+            bool ready = true;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool need = own[k] && (uint32_t)(k * 64) + lane <= near;
+                ready &= !need || tag_of(v[k]) == ep;
+            }
+            if (__ballot(!ready) == 0ull) {
+                unsigned long long s = 0ull;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    s += (own[k] && (uint32_t)(k * 64) + lane <= near) ? st_counts(v[k]) : 0ull;
+                pre += wave_sum64(s);
+                if (near < 256u) return pre;
+                break;
+            }
+            if (++spins > (1u << 16)) { if (lane == 0u) atomicOr(P.error, 1u); return pre; }
+            // exponential back-off: every poll is a memory-side read
+            for (uint32_t z = 0; z < min(spins, 6u); ++z) __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long idx = hi - (long)(k * 64 + lane);
+                if (own[k] && tag_of(v[k]) != ep) v[k] = ald(P.tagg + idx);
+            }
+        }
+        hi -= 256;
     }
     return pre;
 }
 
-// Single-wave look-back (the persistent kernel's control wave): lanes 0..m-1 read the earlier
-// tiles of the group, lane 63 the group's exclusive prefix (or the leader walks for it).
-__device__ unsigned long long lookback_wave(const ParseParams& P, uint32_t t) {
+// Batch totals (the wave owning the last tile): `tot_c` = inclusive [dns|session] count
+// through the last tile; the pre-filter counters come from every wave's epoch-tagged slot.
+__device__ void write_batch_stats(const ParseParams& P, unsigned long long tot_c, uint32_t W) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t ep = P.epoch;
-    const uint32_t g = t / kGroup, leader = g * kGroup, m = t - leader;
-    const bool is_leader = t == leader;
-    unsigned long long v;
-    bool ok;
-    wave_wait(lane < m || (lane == 63u && !is_leader), [&](unsigned long long& out) {
-        const unsigned long long x = ald(lane == 63u ? P.gpre + g : P.tagg + leader + lane);
-        out = x & kCountMask;
-        return tag_of(x) == ep;
-    }, v, ok, P.error);
-    const unsigned long long within = wave_sum64(lane < m ? v : 0ull);
-    unsigned long long pre;
-    if (is_leader) {
-        pre = group_prefix(P, g);
-        if (lane == 0u) ast(P.gpre + g, ((unsigned long long)ep << 56) | pre);
-    } else {
-        pre = __shfl(v, 63, 64);
-    }
-    return pre + within;
-}
-
-__device__ unsigned long long lookback(const ParseParams& P, uint32_t t, unsigned long long* s_sum) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t ep = P.epoch;
-    const uint32_t g = t / kGroup, leader = g * kGroup;
-    if (wave == 0u) {  // group prefix
-        unsigned long long pre = 0ull;
-        if (t == leader) {
-            pre = group_prefix(P, g);
-            if (lane == 0u) ast(P.gpre + g, ((unsigned long long)ep << 56) | pre);
-        } else {
-            if (lane == 0u) {
-                poll_until([&] {
-                    const unsigned long long v = ald(P.gpre + g);
-                    pre = v & kCountMask;
-                    return tag_of(v) == ep;
-                }, P.error);
-            }
+    unsigned long long sf = 0ull, sb = 0ull;
+    uint32_t spins = 0u;
+    for (uint32_t q0 = 0; q0 < W; q0 += 64u) {
+        const uint32_t q = q0 + lane;
+        const bool own = q < W;
+        unsigned long long a = own ? ald(P.wstat + 2 * q) : 0ull, b = own ? ald(P.wstat + 2 * q + 1) : 0ull;
+        for (;;) {
+            const bool ok = !own || (tag_of(a) == ep && tag_of(b) == ep);
+            if (__ballot(!ok) == 0ull) break;
+            if (++spins > (1u << 20)) { if (lane == 0u) atomicOr(P.error, 1u); break; }
+            __builtin_amdgcn_s_sleep(8);
+            if (!ok) { a = ald(P.wstat + 2 * q); b = ald(P.wstat + 2 * q + 1); }
         }
-        if (lane == 0u) s_sum[0] = pre;
-    } else if (wave == 1u) {  // earlier tiles of the same group
-        unsigned long long v;
-        bool ok;
-        wave_wait(lane < t - leader, [&](unsigned long long& out) {
-            const unsigned long long x = ald(P.tagg + leader + lane);
-            out = x & kCountMask;
-            return tag_of(x) == ep;
-        }, v, ok, P.error);
-        v = wave_sum64(lane < t - leader ? v : 0ull);
-        if (lane == 0u) s_sum[1] = v;
+        sf += own ? (a & kCountMask) : 0ull;
+        sb += own ? (b & kCountMask) : 0ull;
     }
-    __syncthreads();
-    const unsigned long long excl = s_sum[0] + s_sum[1];
-    __syncthreads();
-    return excl;
-}
-template <int R, uint32_t FLAGS>
-__global__ __launch_bounds__(kThreads) void k_parse_classify(const ParseParams P) {
-    constexpr int TILE = kThreads * R;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const DevConfig* cfg = P.cfg;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
-    FB_STAMP(0);
-
-    __shared__ uint32_t s_bm[FB_SERVICE_BITMAP_BYTES / 4];
-    __shared__ unsigned long long s_stage[kThreads * 7];  // one round of 56-B records
-    __shared__ uint32_t s_cnt[R][4][2];                   // per (round, wave): sessions, dns
-    __shared__ uint32_t s_aux[4][4];                      // per wave: filtered, tcp, ipv4, bad
-    __shared__ unsigned long long s_sum[4];
-    __shared__ unsigned long long s_excl;
-
-    // ---- 1. phased loads --------------------------------------------------------------------
-    const uint4* bmg = reinterpret_cast<const uint4*>(cfg->service_bitmap);
-    const uint4 bm0 = bmg[tid], bm1 = bmg[tid + kThreads];
-    uint32_t o0[R], o1[R];
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        const uint32_t i = tile * TILE + rd * kThreads + tid;
-        o0[rd] = P.offsets[min(i, P.n)];       // offsets has n+1 entries
-        o1[rd] = P.offsets[min(i + 1u, P.n)];
-    }
-    Hdr h[R];
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        if constexpr ((FLAGS & kCoalesced) != 0u) {
-            const uint32_t wb = __builtin_amdgcn_readfirstlane(o0[rd]) & ~15u;
-            h[rd].A = ld16(rs, wb + 16u * lane);
-            h[rd].B = ld16(rs, wb + 1024u + 16u * lane);
-            h[rd].C = ld16(rs, wb + 2048u + 16u * lane);
-            h[rd].Dz = ld16(rs, wb + 3072u + 16u * lane).x;
-        } else {
-            h[rd].A = ld16(rs, o0[rd] + 10u);
-            h[rd].B = ld16(rs, o0[rd] + 26u);
-            h[rd].C = ld16(rs, o0[rd] + 42u);
-            h[rd].Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o0[rd] + 66u, 0, 0);
-        }
-    }
-    if constexpr ((FLAGS & kLoadsOnly) != 0u) {
-        uint32_t x = 0u;
-#pragma unroll
-        for (int rd = 0; rd < R; ++rd) {
-            const u32x4 v = h[rd].A ^ h[rd].B ^ h[rd].C;
-            x ^= v.x ^ v.y ^ v.z ^ v.w ^ o1[rd] ^ h[rd].Dz;
-        }
-        if (x == 0x9E3779B9u && P.cls) P.cls[0] = (uint8_t)x;
-        return;
-    }
-    reinterpret_cast<uint4*>(s_bm)[tid] = bm0;
-    reinterpret_cast<uint4*>(s_bm)[tid + kThreads] = bm1;
-    __syncthreads();
-
-    // ---- 2. decode + classify ---------------------------------------------------------------
-    Pkt k[R];
-    unsigned long long m_sess[R], m_dns[R];
-    uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        const uint32_t i = tile * TILE + rd * kThreads + tid;
-        const bool valid = i < P.n;
-        process_frame(rs, cfg, s_bm, h[rd], valid ? o0[rd] : 1u, valid ? o1[rd] : 0u, P.frames_bytes, i, k[rd]);
-        const bool is_s = valid && k[rd].cls == FB_CLASS_SESSION;
-        const bool is_d = valid && k[rd].cls == FB_CLASS_DNS;
-        const bool is_f = valid && k[rd].cls == FB_CLASS_FILTERED;
-        const bool counted = is_s || is_f;
-        m_sess[rd] = __ballot(is_s);
-        m_dns[rd] = __ballot(is_d);
-        a_f += __popcll(__ballot(is_f));
-        a_t += __popcll(__ballot(counted && k[rd].tcp));
-        a_4 += __popcll(__ballot(counted && k[rd].v4));
-        a_b += __popcll(__ballot(valid && k[rd].bad));
-        if (lane == 0u) {
-            s_cnt[rd][wave][0] = __popcll(m_sess[rd]);
-            s_cnt[rd][wave][1] = __popcll(m_dns[rd]);
-        }
-        if (valid && P.cls) P.cls[i] = (uint8_t)k[rd].cls;
-    }
+    sf = wave_sum64(sf);
+    sb = wave_sum64(sb);
     if (lane == 0u) {
-        s_aux[wave][0] = a_f;
-        s_aux[wave][1] = a_t;
-        s_aux[wave][2] = a_4;
-        s_aux[wave][3] = a_b;
-    }
-    __syncthreads();
-
-    FB_STAMP(1);
-    // ---- 3. tile aggregate, look-back, batch totals -----------------------------------------
-    unsigned long long agg = 0ull;
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) agg += s_cnt[rd][w][0] | ((unsigned long long)s_cnt[rd][w][1] << 28);
-    const uint32_t ep = P.epoch;
-    const uint32_t g = tile / kGroup;
-    unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
-    unsigned long long* gst = P.gstat + (size_t)(ep & 1u) * P.max_groups * 2;
-    if (!(FLAGS & kNoLookback)) {
-        if (tid == 0u) {
-            const unsigned long long f = s_aux[0][0] + s_aux[1][0] + s_aux[2][0] + s_aux[3][0];
-            const unsigned long long tc = s_aux[0][1] + s_aux[1][1] + s_aux[2][1] + s_aux[3][1];
-            const unsigned long long v4 = s_aux[0][2] + s_aux[1][2] + s_aux[2][2] + s_aux[3][2];
-            const unsigned long long b = s_aux[0][3] + s_aux[1][3] + s_aux[2][3] + s_aux[3][3];
-            // Every published word carries its own arrival count or epoch, so the four writes
-            // need no ordering among themselves (no vmcnt waits on the publish path).
-            atomicAdd(acc + g, (1ull << 56) | agg);
-            atomicAdd(gst + 2 * g, (1ull << 56) | f | (tc << 28));
-            atomicAdd(gst + 2 * g + 1, (1ull << 56) | v4 | (b << 28));
-            ast(P.tagg + tile, ((unsigned long long)ep << 56) | agg);
-        }
-        // Zero the other parity's group words for the next launch (the previous launch, which
-        // used them, has completed: launches on one context are stream-ordered).
-        {
-            unsigned long long* nacc = P.gacc + (size_t)((ep & 1u) ^ 1u) * P.max_groups;
-            unsigned long long* nst = P.gstat + (size_t)((ep & 1u) ^ 1u) * P.max_groups * 2;
-            for (uint32_t q = tile * kThreads + tid; q < P.max_groups; q += P.num_tiles * kThreads) {
-                nacc[q] = 0ull;
-                nst[2 * q] = 0ull;
-                nst[2 * q + 1] = 0ull;
-            }
-        }
-        FB_STAMP(2);
-        const unsigned long long excl = lookback(P, tile, s_sum);
-        FB_STAMP(3);
-        const uint32_t g_last = min(g * kGroup + kGroup, P.num_tiles) - 1u;
-        if (tid == 0u) {
-            s_excl = excl;
-            if (tile == g_last) ast(P.ginc + g, ((unsigned long long)ep << 56) | (excl + agg));
-        }
-        if (tile == P.num_tiles - 1u && P.stats) {
-            // Sum every group's stats words once each has all its tiles' arrivals.
-            unsigned long long sf = 0ull, sb = 0ull;
-            for (uint32_t q = tid; q <= g; q += kThreads) {
-                const uint32_t want = q == g ? P.num_tiles - g * kGroup : (uint32_t)kGroup;
-                unsigned long long a = 0ull, b = 0ull;
-                poll_until([&] { a = ald(gst + 2 * q); return tag_of(a) == want; }, P.error);
-                poll_until([&] { b = ald(gst + 2 * q + 1); return tag_of(b) == want; }, P.error);
-                sf += a & kCountMask;
-                sb += b & kCountMask;
-            }
-            sf = wave_sum64(sf);
-            sb = wave_sum64(sb);
-            if (lane == 0u) s_sum[wave] = sf;
-            __syncthreads();
-            const unsigned long long SF = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-            __syncthreads();
-            if (lane == 0u) s_sum[wave] = sb;
-            __syncthreads();
-            const unsigned long long SB = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-            if (tid == 0u) {
-                fb_batch_stats* S = P.stats;
-                const unsigned long long tot_c = excl + agg;
-                const unsigned long long ns = tot_c & ((1ull << 28) - 1ull), nd = tot_c >> 28;
-                const unsigned long long nf = SF & ((1ull << 28) - 1ull), nt = SF >> 28;
-                const unsigned long long n4 = SB & ((1ull << 28) - 1ull), nb = SB >> 28;
-                const unsigned long long tot = ns + nf;
-                S->total_processed = tot;
-                S->tcp_processed = nt;
-                S->udp_processed = tot - nt;
-                S->ipv4_processed = n4;
-                S->ipv6_processed = tot - n4;
-                S->new_sessions = 0ull;
-                S->updated_sessions = 0ull;
-                S->n_session = ns;
-                S->n_dns = nd;
-                S->n_drop = (unsigned long long)P.n - tot - nd;
-                S->n_filtered = nf;
-                S->bad_offsets = nb;
-                S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
-            }
-        }
-    } else if (tid == 0u) {
-        s_excl = (unsigned long long)tile * TILE;
-    }
-    __syncthreads();
-    if (FLAGS & kNoStore) return;
-
-    // ---- 4. records: stage one round in LDS, then coalesced 16-B stores ---------------------
-    uint32_t base_s = (uint32_t)(s_excl & ((1ull << 28) - 1ull));
-    uint32_t base_d = (FLAGS & kNoLookback) ? base_s : (uint32_t)(s_excl >> 28);
-    const unsigned long long lmask = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        uint32_t ls = 0u, ld = 0u, cs = 0u;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            if ((uint32_t)w < wave) { ls += s_cnt[rd][w][0]; ld += s_cnt[rd][w][1]; }
-            cs += s_cnt[rd][w][0];
-        }
-        if ((m_sess[rd] >> lane) & 1ull) {
-            unsigned long long* d = s_stage + (size_t)(ls + __popcll(m_sess[rd] & lmask)) * 7;
-#pragma unroll
-            for (int j = 0; j < 7; ++j)
-                d[j] = (unsigned long long)k[rd].w[2 * j] | ((unsigned long long)k[rd].w[2 * j + 1] << 32);
-        }
-        if (P.dns && ((m_dns[rd] >> lane) & 1ull)) {
-            const uint32_t pos = base_d + ld + __popcll(m_dns[rd] & lmask);
-            *reinterpret_cast<uint4*>(P.dns + pos) = make_uint4(k[rd].w[0], k[rd].w[1], k[rd].w[2], k[rd].w[3]);
-        }
-        __syncthreads();
-        if (P.out && cs) {
-            // [base_s*56, (base_s+cs)*56) is 8-B aligned; 16-B aligned body + 8-B head/tail.
-            unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)base_s * 7;
-            const uint32_t units = cs * 7;                     // 8-B units
-            const uint32_t head = (base_s & 1u) ? 1u : 0u;     // base_s*56 % 16 == 8 when odd
-            const uint32_t body = (units - head) >> 1;         // 16-B units
-            if (head && tid == 0u) g8[0] = s_stage[0];
-            uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
-            for (uint32_t q = tid; q < body; q += kThreads) {
-                const unsigned long long x = s_stage[head + 2 * q], y = s_stage[head + 2 * q + 1];
-                g16[q] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
-            }
-            if (tid == 0u && head + 2 * body < units) g8[units - 1] = s_stage[units - 1];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            base_s += s_cnt[rd][w][0];
-            base_d += s_cnt[rd][w][1];
-        }
-    }
-    FB_STAMP(4);
-}
-
-// ============================================================================================
-// Persistent, software-pipelined variant (the product kernel).
-//
-// Block b of G walks tiles b, b+G, b+2G, ... (a tile = kThreads * R frames).  Four worker
-// waves parse; a fifth, control wave owns the look-back.  Per tile:
-//   workers : classify tile t (its headers were prefetched)      -> counts      | B1
-//   control : publish t's aggregate, look back, publish prefixes  -> excl        |
-//   workers : stage t's records in LDS; issue tile t+G's header loads and tile
-//             t+2G's offset loads                                                 | B2
-//   workers : coalesced record stores of tile t                                   | B3
-// The control wave's coherent polls never enter the workers' vmcnt queue, so the next tile's
-// header loads stay in flight across the whole look-back: HBM keeps streaming while a tile
-// waits for its predecessors.  Requires the grid to be co-resident (G <= resident blocks);
-// every dependency points to lower tile indices and every spin is bounded.
-// ============================================================================================
-constexpr int kPThreads = kThreads + 64;
-
-template <int R>
-__device__ __forceinline__ void load_offsets(const ParseParams& P, uint32_t t, uint32_t (&a)[R], uint32_t (&b)[R]) {
-    constexpr int TILE = kThreads * R;
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        const uint32_t i = t * TILE + rd * kThreads + threadIdx.x;
-        a[rd] = P.offsets[min(i, P.n)];
-        b[rd] = P.offsets[min(i + 1u, P.n)];
-    }
-}
-template <int R>
-__device__ __forceinline__ void load_headers(__amdgpu_buffer_rsrc_t rs, const uint32_t (&o)[R], Hdr (&h)[R]) {
-#pragma unroll
-    for (int rd = 0; rd < R; ++rd) {
-        h[rd].A = ld16(rs, o[rd] + 10u);
-        h[rd].B = ld16(rs, o[rd] + 26u);
-        h[rd].C = ld16(rs, o[rd] + 42u);
-        h[rd].Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o[rd] + 66u, 0, 0);
+        fb_batch_stats* S = P.stats;
+        const unsigned long long ns = tot_c & ((1ull << 28) - 1ull), nd = tot_c >> 28;
+        const unsigned long long nf = sf & ((1ull << 28) - 1ull), nt = sf >> 28;
+        const unsigned long long n4 = sb & ((1ull << 28) - 1ull), nb = sb >> 28;
+        const unsigned long long tot = ns + nf;
+        S->total_processed = tot;
+        S->tcp_processed = nt;
+        S->udp_processed = tot - nt;
+        S->ipv4_processed = n4;
+        S->ipv6_processed = tot - n4;
+        S->new_sessions = 0ull;
+        S->updated_sessions = 0ull;
+        S->n_session = ns;
+        S->n_dns = nd;
+        S->n_drop = (unsigned long long)P.n - tot - nd;
+        S->n_filtered = nf;
+        S->bad_offsets = nb;
+        S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
     }
 }
 
-template <int R, uint32_t FLAGS>
-__global__ __launch_bounds__(kPThreads, 4) void k_parse_persistent(const ParseParams P) {
-    constexpr int TILE = kThreads * R;
-    const uint32_t G = gridDim.x, T = P.num_tiles;
+__device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_t o, Hdr& h) {
+    h.A = ld16(rs, o + 10u);
+    h.B = ld16(rs, o + 26u);
+    h.C = ld16(rs, o + 42u);
+    h.Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 66u, 0, 0);
+}
+
+// One look-back unit = one block-round: kWaves waves x U wave-tiles x 64 frames.  Block b
+// (of G co-resident blocks) owns units b, b+G, b+2G, ...; inside a unit, wave w owns the
+// contiguous frames [w*U*64, (w+1)*U*64), so packet order = (wave, tile, lane).  Per unit:
+//   1. every wave issues the offsets of its U tiles, then all 4U header loads (U*64 frames of
+//      loads in flight per wave)
+//   2. every wave classifies and stages its SESSION records, compacted, in its own LDS region
+//      (records do not stay live in VGPRs across the look-back); counts -> LDS     | barrier
+//   3. wave 0 publishes the unit's count and runs the look-back: ONE participant per block
+//      (a few hundred per launch) keeps the polled words cold; lanes poll together with
+//      exponential back-off                                                          | barrier
+//   4. every wave copies its LDS region to its place in the output with coalesced 16-B
+//      stores; DNS records straight from registers
+template <int U, uint32_t FLAGS>
+__global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
+    constexpr uint32_t kWaves = kThreads / 64;
+    constexpr uint32_t WF = 64u * U;          // frames per wave per unit
+    constexpr uint32_t UF = WF * kWaves;      // frames per unit
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const bool control = wave == 4u;
-    const DevConfig* cfg = P.cfg;
+    const uint32_t G = gridDim.x, T = P.num_tiles;  // T = units
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
-
-    __shared__ uint32_t s_bm[FB_SERVICE_BITMAP_BYTES / 4];
-    __shared__ unsigned long long s_stage[R * kThreads * 7];  // one tile of 56-B records
-    __shared__ uint32_t s_cnt[R][4][2];                       // per (round, wave): sessions, dns
-    __shared__ uint32_t s_aux[4][4];                          // per wave: filtered, tcp, ipv4, bad
-    __shared__ unsigned long long s_excl;
-
     const uint32_t ep = P.epoch;
-    unsigned long long* acc = P.gacc + (size_t)(ep & 1u) * P.max_groups;
-    unsigned long long* gst = P.gstat + (size_t)(ep & 1u) * P.max_groups * 2;
 
-    uint32_t o0[R], o1[R], n0[R], n1[R];
-    Hdr h[R];
-    uint32_t t = blockIdx.x;
-    if (!control) {
-        const uint4* bmg = reinterpret_cast<const uint4*>(cfg->service_bitmap);
-        const uint4 bm0 = bmg[tid], bm1 = bmg[tid + kThreads];
-        load_offsets<R>(P, t, o0, o1);
-        load_headers<R>(rs, o0, h);
-        load_offsets<R>(P, min(t + G, T - 1u), n0, n1);
-        reinterpret_cast<uint4*>(s_bm)[tid] = bm0;
-        reinterpret_cast<uint4*>(s_bm)[tid + kThreads] = bm1;
-    } else {
-        // zero the other parity's group words for the next launch (see fb_internal.h)
-        unsigned long long* nacc = P.gacc + (size_t)((ep & 1u) ^ 1u) * P.max_groups;
-        unsigned long long* nst = P.gstat + (size_t)((ep & 1u) ^ 1u) * P.max_groups * 2;
-        for (uint32_t q = blockIdx.x * 64u + lane; q < P.max_groups; q += G * 64u) {
-            nacc[q] = 0ull;
-            nst[2 * q] = 0ull;
-            nst[2 * q + 1] = 0ull;
-        }
+    __shared__ DevConfig s_cfg;                                  // service bitmap + tables
+    __shared__ unsigned long long s_stage_all[kWaves][WF * 7];  // per-wave compacted records
+    __shared__ uint32_t s_cnt[kWaves][4];                        // sessions, dns, filtered|tcp, v4|bad
+    __shared__ unsigned long long s_excl;
+    unsigned long long* s_stage = s_stage_all[wave];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
+        uint4* dst = reinterpret_cast<uint4*>(&s_cfg);
+        for (uint32_t q = tid; q < sizeof(DevConfig) / 16; q += kThreads) dst[q] = src[q];
+        // Zero the other parity's error word for the next launch (the previous launch, which
+        // used it, has completed: launches on one context are stream-ordered).
+        if (blockIdx.x == 0u && tid == 0u) *P.error_next = 0u;
     }
     __syncthreads();
+    const DevConfig* cfg = &s_cfg;
 
-    uint4 dnsw[R];  // DNS side records stay in registers (rare); session records go to LDS
-    unsigned long long m_sess[R], m_dns[R];
     const unsigned long long lmask = (1ull << lane) - 1ull;
-    for (; t < T; t += G) {
-        if (!control) {
-            uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;
+    uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;  // pre-filter counters (block, wave 0 keeps them)
+
+    for (uint32_t u = blockIdx.x; u < T; u += G) {
+        const uint32_t f0 = u * UF + wave * WF;  // first frame of this wave
+        // ---- 1. loads -----------------------------------------------------------------------
+        uint2 o[U];
+        Hdr h[U];
 #pragma unroll
-            for (int rd = 0; rd < R; ++rd) {
-                const uint32_t i = t * TILE + rd * kThreads + tid;
-                const bool valid = i < P.n;
-                Pkt k;
-                process_frame(rs, cfg, s_bm, h[rd], valid ? o0[rd] : 1u, valid ? o1[rd] : 0u, P.frames_bytes, i, k);
-                const bool is_s = valid && k.cls == FB_CLASS_SESSION;
-                const bool is_d = valid && k.cls == FB_CLASS_DNS;
-                const bool is_f = valid && k.cls == FB_CLASS_FILTERED;
-                const bool counted = is_s || is_f;
-                m_sess[rd] = __ballot(is_s);
-                m_dns[rd] = __ballot(is_d);
-                a_f += __popcll(__ballot(is_f));
-                a_t += __popcll(__ballot(counted && k.tcp));
-                a_4 += __popcll(__ballot(counted && k.v4));
-                a_b += __popcll(__ballot(valid && k.bad));
-                if (lane == 0u) {
-                    s_cnt[rd][wave][0] = __popcll(m_sess[rd]);
-                    s_cnt[rd][wave][1] = __popcll(m_dns[rd]);
-                }
-                if (valid && P.cls) P.cls[i] = (uint8_t)k.cls;
-                // wave-compacted staging: region (round, wave), record at popc(earlier lanes)
-                if (is_s) {
-                    unsigned long long* d = s_stage + ((size_t)(rd * 4 + wave) * 64 + __popcll(m_sess[rd] & lmask)) * 7;
-#pragma unroll
-                    for (int j = 0; j < 7; ++j)
-                        d[j] = (unsigned long long)k.w[2 * j] | ((unsigned long long)k.w[2 * j + 1] << 32);
-                }
-                dnsw[rd] = make_uint4(k.w[0], k.w[1], k.w[2], k.w[3]);
-            }
-            if (lane == 0u) {
-                s_aux[wave][0] = a_f;
-                s_aux[wave][1] = a_t;
-                s_aux[wave][2] = a_4;
-                s_aux[wave][3] = a_b;
-            }
+        for (int r = 0; r < U; ++r) {
+            const uint32_t i = f0 + r * 64u + lane;
+            o[r] = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);  // n+1 entries
         }
-        __syncthreads();  // B1
-        if (control) {
-            unsigned long long agg = 0ull;
 #pragma unroll
-            for (int rd = 0; rd < R; ++rd)
+        for (int r = 0; r < U; ++r) load_headers1(rs, o[r].x, h[r]);
+        // ---- 2. classify + stage ----------------------------------------------------------------
+        unsigned long long m_dns[U];
+        uint4 dnsw[U];
+        uint32_t cs = 0u, cd = 0u, wf = 0u, wt = 0u, w4 = 0u, wb = 0u;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) agg += s_cnt[rd][w][0] | ((unsigned long long)s_cnt[rd][w][1] << 28);
-            const uint32_t g = t / kGroup;
-            if (lane == 0u) {
-                const unsigned long long f = s_aux[0][0] + s_aux[1][0] + s_aux[2][0] + s_aux[3][0];
-                const unsigned long long tc = s_aux[0][1] + s_aux[1][1] + s_aux[2][1] + s_aux[3][1];
-                const unsigned long long v4 = s_aux[0][2] + s_aux[1][2] + s_aux[2][2] + s_aux[3][2];
-                const unsigned long long b = s_aux[0][3] + s_aux[1][3] + s_aux[2][3] + s_aux[3][3];
-                atomicAdd(acc + g, (1ull << 56) | agg);
-                atomicAdd(gst + 2 * g, (1ull << 56) | f | (tc << 28));
-                atomicAdd(gst + 2 * g + 1, (1ull << 56) | v4 | (b << 28));
-                ast(P.tagg + t, ((unsigned long long)ep << 56) | agg);
-            }
-            const unsigned long long excl = lookback_wave(P, t);
-            if (lane == 0u) {
-                s_excl = excl;
-                if (t == min(g * kGroup + kGroup, T) - 1u) ast(P.ginc + g, ((unsigned long long)ep << 56) | (excl + agg));
-            }
-            if (t == T - 1u && P.stats) {
-                // batch totals: every group's stats words, once all their arrivals are in
-                unsigned long long sf = 0ull, sb = 0ull;
-                for (uint32_t q0 = 0; q0 <= g; q0 += 64u) {
-                    const uint32_t q = q0 + lane;
-                    const uint32_t want = q == g ? T - g * kGroup : (uint32_t)kGroup;
-                    unsigned long long a, b;
-                    bool ok;
-                    wave_wait(q <= g, [&](unsigned long long& out) {
-                        const unsigned long long x = ald(gst + 2 * q);
-                        out = x;
-                        return tag_of(x) == want;
-                    }, a, ok, P.error);
-                    wave_wait(q <= g, [&](unsigned long long& out) {
-                        const unsigned long long x = ald(gst + 2 * q + 1);
-                        out = x;
-                        return tag_of(x) == want;
-                    }, b, ok, P.error);
-                    sf += q <= g ? (a & kCountMask) : 0ull;
-                    sb += q <= g ? (b & kCountMask) : 0ull;
-                }
-                sf = wave_sum64(sf);
-                sb = wave_sum64(sb);
-                if (lane == 0u) {
-                    fb_batch_stats* S = P.stats;
-                    const unsigned long long tot_c = excl + agg;
-                    const unsigned long long ns = tot_c & ((1ull << 28) - 1ull), nd = tot_c >> 28;
-                    const unsigned long long nf = sf & ((1ull << 28) - 1ull), nt = sf >> 28;
-                    const unsigned long long n4 = sb & ((1ull << 28) - 1ull), nb = sb >> 28;
-                    const unsigned long long tot = ns + nf;
-                    S->total_processed = tot;
-                    S->tcp_processed = nt;
-                    S->udp_processed = tot - nt;
-                    S->ipv4_processed = n4;
-                    S->ipv6_processed = tot - n4;
-                    S->new_sessions = 0ull;
-                    S->updated_sessions = 0ull;
-                    S->n_session = ns;
-                    S->n_dns = nd;
-                    S->n_drop = (unsigned long long)P.n - tot - nd;
-                    S->n_filtered = nf;
-                    S->bad_offsets = nb;
-                    S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
-                }
-            }
-        } else if (t + G < T) {
-            // prefetch: headers of tile t+G (offsets already here), offsets of tile t+2G
+        for (int r = 0; r < U; ++r) {
+            const uint32_t i = f0 + r * 64u + lane;
+            const bool valid = i < P.n;
+            Pkt k;
+            process_frame(rs, cfg, cfg->service_bitmap, h[r], valid ? o[r].x : 1u, valid ? o[r].y : 0u,
+                          P.frames_bytes, i, k);
+            const bool is_s = valid && k.cls == FB_CLASS_SESSION;
+            const bool is_d = valid && k.cls == FB_CLASS_DNS;
+            const bool is_f = valid && k.cls == FB_CLASS_FILTERED;
+            const bool counted = is_s || is_f;
+            const unsigned long long m_sess = __ballot(is_s);
+            m_dns[r] = __ballot(is_d);
+            dnsw[r] = make_uint4(k.w[0], k.w[1], k.w[2], k.w[3]);
+            if (is_s) {
+                unsigned long long* d = s_stage + (size_t)(cs + __popcll(m_sess & lmask)) * 7;
 #pragma unroll
-            for (int rd = 0; rd < R; ++rd) { o0[rd] = n0[rd]; o1[rd] = n1[rd]; }
-            load_headers<R>(rs, o0, h);
-            load_offsets<R>(P, min(t + 2u * G, T - 1u), n0, n1);
+                for (int w = 0; w < 7; ++w)
+                    d[w] = (unsigned long long)k.w[2 * w] | ((unsigned long long)k.w[2 * w + 1] << 32);
+            }
+            cs += (uint32_t)__popcll(m_sess);
+            cd += (uint32_t)__popcll(m_dns[r]);
+            wf += __popcll(__ballot(is_f));
+            wt += __popcll(__ballot(counted && k.tcp));
+            w4 += __popcll(__ballot(counted && k.v4));
+            wb += __popcll(__ballot(valid && k.bad));
+            if (valid && P.cls) P.cls[i] = (uint8_t)k.cls;
         }
-        __syncthreads();  // B2
-        if (!control) {
-            // Each wave writes its (round, wave) segments: packet order = (round, wave, lane).
-            uint32_t exs = (uint32_t)(s_excl & ((1ull << 28) - 1ull));
-            uint32_t exd = (uint32_t)(s_excl >> 28);
+        if (lane == 0u) {
+            s_cnt[wave][0] = cs;
+            s_cnt[wave][1] = cd;
+            s_cnt[wave][2] = wf | (wt << 16);
+            s_cnt[wave][3] = w4 | (wb << 16);
+        }
+        __syncthreads();  // counts of every wave
+        // ---- 3. publish + look-back (wave 0) --------------------------------------------------
+        if (wave == 0u) {
+            uint32_t bs = 0u, bd = 0u;
 #pragma unroll
-            for (int rd = 0; rd < R; ++rd) {
-                uint32_t ls = 0u, ld = 0u, ts = 0u, td = 0u;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    if ((uint32_t)w < wave) { ls += s_cnt[rd][w][0]; ld += s_cnt[rd][w][1]; }
-                    ts += s_cnt[rd][w][0];
-                    td += s_cnt[rd][w][1];
-                }
-                if (P.dns && ((m_dns[rd] >> lane) & 1ull))
-                    P.dns[exd + ld + __popcll(m_dns[rd] & lmask)] = *reinterpret_cast<const fb_dns_out*>(&dnsw[rd]);
-                const uint32_t c = s_cnt[rd][wave][0];
-                if (P.out && c) {
-                    // [pos*56, (pos+c)*56) is 8-B aligned: 16-B body + 8-B head/tail
-                    const uint32_t pos = exs + ls;
-                    const unsigned long long* st = s_stage + (size_t)(rd * 4 + wave) * 64 * 7;
-                    unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)pos * 7;
-                    const uint32_t units = c * 7, head = pos & 1u, body = (units - head) >> 1;
-                    if (head && lane == 0u) g8[0] = st[0];
-                    uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
-                    for (uint32_t q = lane; q < body; q += 64u) {
-                        const unsigned long long x = st[head + 2 * q], y = st[head + 2 * q + 1];
-                        g16[q] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+            for (uint32_t w = 0; w < kWaves; ++w) {
+                bs += s_cnt[w][0];
+                bd += s_cnt[w][1];
+                a_f += s_cnt[w][2] & 0xFFFFu;
+                a_t += s_cnt[w][2] >> 16;
+                a_4 += s_cnt[w][3] & 0xFFFFu;
+                a_b += s_cnt[w][3] >> 16;
+            }
+            const unsigned long long agg = (unsigned long long)bs | ((unsigned long long)bd << 28);
+            if constexpr ((FLAGS & kStamps) != 0u)
+                if (lane == 0u) P.dbg[4ull * u] = __builtin_amdgcn_s_memrealtime();
+            unsigned long long excl;
+            if (FLAGS & kNoLookback) {
+                excl = (unsigned long long)u * UF;
+            } else {
+                if (lane == 0u) ast(P.tagg + u, st_pack(ep, false, agg));
+                uint32_t spins;
+                excl = lookback_unit<FLAGS>(P, u, spins);
+                if (lane == 0u) ast(P.tagg + u, st_pack(ep, true, excl + agg));
+                if constexpr ((FLAGS & kStamps) != 0u)
+                    if (lane == 0u) {
+                        P.dbg[4ull * u + 2] = __builtin_amdgcn_s_memrealtime();
+                        P.dbg[4ull * u + 3] = spins;
                     }
-                    if (lane == 0u && head + 2 * body < units) g8[units - 1] = st[units - 1];
+            }
+            if (lane == 0u) s_excl = excl;
+            if (u == T - 1u && P.stats && !(FLAGS & kNoLookback)) {
+                // the last unit's owner: own counters first (this is the block's last unit)
+                if (lane == 0u) {
+                    ast(P.wstat + 2 * blockIdx.x, ((unsigned long long)ep << 56) | a_f | ((unsigned long long)a_t << 28));
+                    ast(P.wstat + 2 * blockIdx.x + 1, ((unsigned long long)ep << 56) | a_4 | ((unsigned long long)a_b << 28));
                 }
-                exs += ts;
-                exd += td;
+                write_batch_stats(P, excl + agg, G);
             }
         }
-        __syncthreads();  // B3: stage and counts free for the next tile
+        __syncthreads();  // s_excl
+        // ---- 4. stores ---------------------------------------------------------------------------
+        if (!(FLAGS & kNoStore)) {
+            const unsigned long long bex = s_excl;
+            uint32_t base_s = (uint32_t)(bex & ((1ull << 28) - 1ull));
+            uint32_t base_d = (uint32_t)(bex >> 28);
+            for (uint32_t w = 0; w < wave; ++w) {
+                base_s += s_cnt[w][0];
+                base_d += s_cnt[w][1];
+            }
+            if (P.out && cs) {
+                // [base_s*56, (base_s+cs)*56) is 8-B aligned: 16-B aligned body + 8-B head/tail
+                unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)base_s * 7;
+                const uint32_t units = cs * 7, head = base_s & 1u, body = (units - head) >> 1;
+                if (head && lane == 0u) g8[0] = s_stage[0];
+                uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
+                for (uint32_t c = lane; c < body; c += 64u) {
+                    const unsigned long long x = s_stage[head + 2 * c], y = s_stage[head + 2 * c + 1];
+                    g16[c] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+                }
+                if (lane == 0u && head + 2 * body < units) g8[units - 1] = s_stage[units - 1];
+            }
+            if (P.dns) {
+#pragma unroll
+                for (int r = 0; r < U; ++r) {
+                    if ((m_dns[r] >> lane) & 1ull) {
+                        fb_dns_out d;
+                        d.pkt_index = dnsw[r].x;
+                        d.payload_offset = dnsw[r].y;
+                        d.payload_length = dnsw[r].z;
+                        d.protocol = (uint8_t)(dnsw[r].w & 0xffu);
+                        d.family = (uint8_t)(dnsw[r].w >> 8);
+                        d.reserved = 0;
+                        P.dns[base_d + __popcll(m_dns[r] & lmask)] = d;
+                    }
+                    base_d += (uint32_t)__popcll(m_dns[r]);
+                }
+            }
+        }
+        __syncthreads();  // s_cnt / s_excl / stage reuse by the next unit
+    }
+    // every block publishes its pre-filter counters (the last unit's owner did so above)
+    const bool owner_last = T > 0u && (T - 1u) % G == blockIdx.x;
+    if (!owner_last && tid == 0u && !(FLAGS & kNoLookback)) {
+        ast(P.wstat + 2 * blockIdx.x, ((unsigned long long)ep << 56) | a_f | ((unsigned long long)a_t << 28));
+        ast(P.wstat + 2 * blockIdx.x + 1, ((unsigned long long)ep << 56) | a_4 | ((unsigned long long)a_b << 28));
     }
 }
 
-hipError_t launch_parse_persistent(const ParseParams& p, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_parse_persistent<kPRounds, kFlagsProduct>), dim3(grid), dim3(kPThreads), 0, s, p);
+hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_parse_block<kUnitTiles, kFlagsProduct>), dim3(grid), dim3(kThreads), 0, s, p);
     return hipGetLastError();
 }
 
-hipError_t occupancy_parse_persistent(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_persistent<kPRounds, kFlagsProduct>),
-                                                        kPThreads, 0);
-}
-
-hipError_t launch_parse_classify(const ParseParams& p, hipStream_t s) {
-    hipLaunchKernelGGL((k_parse_classify<kRounds, kFlagsProduct>), dim3(p.num_tiles), dim3(kThreads), 0, s, p);
-    return hipGetLastError();
+hipError_t occupancy_parse(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_block<kUnitTiles, kFlagsProduct>),
+                                                        kThreads, 0);
 }
 
 }  // namespace fbk

@@ -38,7 +38,7 @@ extern "C" {
 #endif
 
 #define FB_ABI_VERSION 1u
-#define FB_MAX_BATCH_PACKETS ((1u << 28) - 1u)
+#define FB_MAX_BATCH_PACKETS ((1u << 27) - 1u)
 #define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
 #define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
 #define FB_SERVICE_BITMAP_BYTES 8192u

@@ -4,10 +4,15 @@
 // interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 //   build: tools/build_ubench.sh ; run: tools/ubench_parse [config_id] [n] [rotate] [iters]
 #include "../flodbadd_amd/csrc/fb_parse.hip"
-#ifndef UB_R
-#define UB_R fbk::kRounds
+#ifndef FB_FRAME_WAVES
+#define FB_FRAME_WAVES 7
 #endif
-#define UB_TILE (fbk::kThreads * UB_R)
+namespace fbk { constexpr int kExpFrameWaves = FB_FRAME_WAVES; }
+#include "parse_experiments.hip"
+#ifndef UB_R
+#define UB_R fbk::kUnitTiles
+#endif
+#define UB_TILE (fbk::kTile)
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -52,6 +57,17 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
     }
 }
 
+__global__ __launch_bounds__(256) void k_hdr_loads(const uint8_t* fr, const uint32_t* off, uint32_t n, uint32_t bytes,
+                                                   unsigned* sink) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)fr, (short)0, (int)bytes, 0x00020000);
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t o = off[min(i, n)], o1 = off[min(i + 1u, n)];
+    const fbk::u32x4 A = fbk::ld16(rs, o + 10u), B = fbk::ld16(rs, o + 26u), C = fbk::ld16(rs, o + 42u);
+    const uint32_t D = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 66u, 0, 0);
+    const fbk::u32x4 v = A ^ B ^ C;
+    if ((v.x ^ v.y ^ v.z ^ v.w ^ D ^ o1) == 0x9E3779B9u) sink[0] = 1;
+}
+
 int main(int argc, char** argv) {
     int cfg_id = argc > 1 ? atoi(argv[1]) : 2;
     uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : (1u << 20);
@@ -83,7 +99,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dcfg, &hc, sizeof(hc), hipMemcpyHostToDevice));
 
     const uint32_t tiles = (n + UB_TILE - 1) / UB_TILE;
-    const uint32_t stiles = (tiles + fbk::kGroup - 1) / fbk::kGroup * fbk::kGroup;
+    const uint32_t stiles = tiles;
     const size_t swords = fbk::scratch_words(stiles);
     unsigned long long* status;
     CK(hipMalloc(&status, swords * 8));
@@ -92,8 +108,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&err, 16));
     CK(hipMemset(err, 0, 16));
     unsigned long long* dbg;
-    CK(hipMalloc(&dbg, (size_t)tiles * 64));
-    CK(hipMemset(dbg, 0, (size_t)tiles * 64));
+    CK(hipMalloc(&dbg, (size_t)tiles * 32));
+    CK(hipMemset(dbg, 0, (size_t)tiles * 32));
     unsigned* sink;
     CK(hipMalloc(&sink, 16));
     struct Buf { uint8_t* fr; uint32_t* off; fb_pkt_out* out; fb_dns_out* dns; fb_batch_stats* st; };
@@ -114,86 +130,104 @@ int main(int argc, char** argv) {
         fbk::ParseParams p;
         p.frames = bufs[r].fr; p.offsets = bufs[r].off; p.out = bufs[r].out; p.dns = bufs[r].dns;
         p.cls = nullptr; p.stats = bufs[r].st; p.cfg = dcfg;
-        p.tagg = status; p.ginc = status + stiles; p.gpre = p.ginc + stiles / fbk::kGroup; p.gacc = p.gpre + stiles / fbk::kGroup;
-        p.gstat = p.gacc + 2 * (stiles / fbk::kGroup); p.max_groups = stiles / fbk::kGroup;
-        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = tiles; p.error = err; p.dbg = dbg;
-        if (lb && ++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); epoch = 1; }
+        p.tagg = status; p.wstat = status + stiles;
+        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = tiles;
+        if (lb && ++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); CK(hipMemset(err, 0, 16)); epoch = 1; }
         p.epoch = epoch;
+        p.error = err + (epoch & 1u); p.error_next = err + ((epoch & 1u) ^ 1u); p.dbg = dbg;
         return p;
     };
     uint64_t caps = 0;
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;  // upper bound: all emitted
-    const char* names[] = {"product", "no_lookback", "no_store", "loads_classify_only", "read_frames", "copy_frames_to_out",
-                           "header_loads_only", "coalesced_loads_only", "persistent"};
-    const int NV = 9;
+    const char* names[] = {"product", "no_lookback", "no_store", "no_lookback_no_store", "read_frames",
+                           "copy_frames_to_out", "header_loads_only"};
+    const int NV = 7;
     int bpc = 0;
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_persistent<UB_R, 0>), fbk::kPThreads, 0));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_block<UB_R, 0>), fbk::kThreads, 0));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
-    const uint32_t pgrid = std::min<uint32_t>(tiles, (uint32_t)(std::max(bpc - 1, 1) * prop.multiProcessorCount));
-    printf("{\"persistent_blocks_per_cu_api\": %d, \"grid\": %u, \"cus\": %d}\n", bpc, pgrid, prop.multiProcessorCount);
-    std::vector<double> best(NV, 1e30), sum(NV, 0.0);
+    printf("{\"blocks_per_cu_api\": %d, \"cus\": %d, \"tiles\": %u}\n", bpc, prop.multiProcessorCount, tiles);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int rounds = 5;
-    for (int round = 0; round < rounds; ++round) {
-        for (int v = 0; v < NV; ++v) {
-            for (int warm = -10; warm < iters; ++warm) {
-                if (warm == 0) CK(hipEventRecord(e0, s));
-                int r = (warm + 100) % R;
-                switch (v) {
-                case 0: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, 0>), dim3(tiles), dim3(256), 0, s, params(r, true)); break;
-                case 1: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kNoLookback>), dim3(tiles), dim3(256), 0, s, params(r, false)); break;
-                case 2: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kNoStore>), dim3(tiles), dim3(256), 0, s, params(r, true)); break;
-                case 3: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kNoLookback | fbk::kNoStore>), dim3(tiles), dim3(256), 0, s, params(r, true)); break;
-                case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
-                case 6: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kLoadsOnly>), dim3(tiles), dim3(256), 0, s, params(r, false)); break;
-                case 7: hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kLoadsOnly | fbk::kCoalesced>), dim3(tiles), dim3(256), 0, s, params(r, false)); break;
-                case 8: hipLaunchKernelGGL((fbk::k_parse_persistent<UB_R, 0>), dim3(pgrid), dim3(fbk::kPThreads), 0, s, params(r, true)); break;
-                case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+    const int rounds = 3;
+    const int maxb = std::min(bpc, std::max(1, 24 / (fbk::kThreads / 64)));
+    for (int bpcu = 1; bpcu <= maxb; ++bpcu) {
+        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(bpcu * prop.multiProcessorCount));
+        std::vector<double> best(NV, 1e30), sum(NV, 0.0);
+        for (int round = 0; round < rounds; ++round) {
+            for (int v = 0; v < NV; ++v) {
+                if (v >= 4 && bpcu > 1) continue;
+                for (int warm = -10; warm < iters; ++warm) {
+                    if (warm == 0) CK(hipEventRecord(e0, s));
+                    int r = (warm + 100) % R;
+                    switch (v) {
+                    case 0: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, 0>), dim3(grid), dim3(fbk::kThreads), 0, s, params(r, true)); break;
+                    case 1: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kNoLookback>), dim3(grid), dim3(fbk::kThreads), 0, s, params(r, true)); break;
+                    case 2: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kNoStore>), dim3(grid), dim3(fbk::kThreads), 0, s, params(r, true)); break;
+                    case 3: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kNoLookback | fbk::kNoStore>), dim3(grid), dim3(fbk::kThreads), 0, s, params(r, true)); break;
+                    case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
+                    case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+                    case 6: hipLaunchKernelGGL(k_hdr_loads, dim3((n + 255) / 256), dim3(256), 0, s, bufs[r].fr, bufs[r].off, n, (uint32_t)bytes, sink); break;
+                    }
                 }
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                double us = ms * 1e3 / iters;
+                best[v] = std::min(best[v], us);
+                sum[v] += us;
             }
-            CK(hipEventRecord(e1, s));
-            CK(hipEventSynchronize(e1));
-            float ms;
-            CK(hipEventElapsedTime(&ms, e0, e1));
-            double us = ms * 1e3 / iters;
-            best[v] = std::min(best[v], us);
-            sum[v] += us;
         }
+        for (int v = 0; v < NV; ++v) {
+            if (v >= 4 && bpcu > 1) continue;
+            double us = sum[v] / rounds;
+            double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
+            printf("{\"variant\": \"%s\", \"blocks_per_cu\": %d, \"grid\": %u, \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n",
+                   names[v], bpcu, grid, us, best[v], n / (best[v] * 1e3), gbs);
+        }
+        fflush(stdout);
     }
-    // ---- timeline of one stamped launch (after warm-up) ----
-    for (int w = 0; w < 5; ++w)
-        hipLaunchKernelGGL((fbk::k_parse_classify<UB_R, fbk::kStamps>), dim3(tiles), dim3(256), 0, s, params(w % R, true));
-    CK(hipStreamSynchronize(s));
     {
-        std::vector<unsigned long long> st(tiles * 8ull);
+        // stamped run (diagnostic build of the same kernel)
+        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(maxb * prop.multiProcessorCount));
+        for (int w = 0; w < 5; ++w)
+            hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kStamps>), dim3(grid), dim3(fbk::kThreads), 0, s, params(w % R, true));
+        CK(hipStreamSynchronize(s));
+        std::vector<unsigned long long> st(tiles * 4ull);
         CK(hipMemcpy(st.data(), dbg, st.size() * 8, hipMemcpyDeviceToHost));
         unsigned long long t0 = ~0ull;
-        for (uint32_t t = 0; t < tiles; ++t) t0 = std::min(t0, st[t * 8]);
-        const char* ph[] = {"entry", "classified", "published", "lookback_done", "end"};
-        for (int k = 0; k < 5; ++k) {
-            std::vector<double> v;
-            for (uint32_t t = 0; t < tiles; ++t) v.push_back((st[t * 8 + k] - t0) * 0.01);  // 100 MHz -> us
-            std::vector<double> sv = v;
-            std::sort(sv.begin(), sv.end());
-            printf("{\"stamp\": \"%s\", \"us_min\": %.2f, \"us_p10\": %.2f, \"us_med\": %.2f, \"us_p90\": %.2f, \"us_max\": %.2f, \"first_tiles\": [%.2f, %.2f, %.2f], \"last_tile\": %.2f}\n",
-                   ph[k], sv[0], sv[sv.size() / 10], sv[sv.size() / 2], sv[sv.size() * 9 / 10], sv.back(), v[0], v[1], v[2], v.back());
+        for (uint32_t t = 0; t < tiles; ++t) t0 = std::min(t0, st[t * 4]);
+        const uint32_t W = grid;
+        const uint32_t nround = (tiles + W - 1) / W;
+        for (uint32_t r = 0; r < nround; ++r) {
+            std::vector<double> cl, li, ld, wait, sp;
+            for (uint32_t t = r * W; t < std::min(tiles, (r + 1) * W); ++t) {
+                cl.push_back((st[t * 4] - t0) * 0.01);
+                li.push_back((st[t * 4 + 1] - t0) * 0.01);
+                ld.push_back((st[t * 4 + 2] - t0) * 0.01);
+                wait.push_back((st[t * 4 + 2] - st[t * 4]) * 0.01);
+                sp.push_back((double)st[t * 4 + 3]);
+            }
+            auto q = [](std::vector<double> v, double f) { std::sort(v.begin(), v.end()); return v[(size_t)(f * (v.size() - 1))]; };
+            printf("{\"round\": %u, \"classified_us\": [%.2f, %.2f, %.2f], \"lb_issue_us\": [%.2f, %.2f, %.2f], \"lb_done_us\": [%.2f, %.2f, %.2f], \"lb_wait_us\": [%.2f, %.2f, %.2f], \"spins\": [%.0f, %.0f, %.0f]}\n",
+                   r, q(cl, 0.0), q(cl, 0.5), q(cl, 1.0), q(li, 0.0), q(li, 0.5), q(li, 1.0), q(ld, 0.0), q(ld, 0.5), q(ld, 1.0),
+                   q(wait, 0.0), q(wait, 0.5), q(wait, 1.0), q(sp, 0.0), q(sp, 0.5), q(sp, 1.0));
         }
     }
-    unsigned e = 0;
-    CK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    {
+        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(maxb * prop.multiProcessorCount));
+        hipLaunchKernelGGL((fbk::k_parse_block<UB_R, 0>), dim3(grid), dim3(fbk::kThreads), 0, s, params(0, true));
+        CK(hipStreamSynchronize(s));
+    }
+    unsigned errw[2] = {0, 0};
+    CK(hipMemcpy(errw, err, 8, hipMemcpyDeviceToHost));
     fb_batch_stats st;
     CK(hipMemcpy(&st, bufs[0].st, sizeof(st), hipMemcpyDeviceToHost));
-    printf("{\"config\": %d, \"n\": %u, \"bytes\": %llu, \"rotate\": %d, \"err\": %u, \"n_session\": %llu, \"n_dns\": %llu}\n",
-           cfg_id, n, (unsigned long long)bytes, R, e, (unsigned long long)st.n_session, (unsigned long long)st.n_dns);
-    for (int v = 0; v < NV; ++v) {
-        double us = sum[v] / rounds;
-        double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
-        printf("{\"variant\": \"%s\", \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n", names[v], us,
-               best[v], n / (best[v] * 1e3), gbs);
-    }
+    printf("{\"config\": %d, \"n\": %u, \"bytes\": %llu, \"rotate\": %d, \"err\": [%u, %u], \"n_session\": %llu, \"n_dns\": %llu, \"stats_error\": %llu}\n",
+           cfg_id, n, (unsigned long long)bytes, R, errw[0], errw[1], (unsigned long long)st.n_session, (unsigned long long)st.n_dns,
+           (unsigned long long)st.error);
     return 0;
 }
