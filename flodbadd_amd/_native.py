@@ -32,6 +32,9 @@ KEY_FIELDS = [("src_ip", "<u4", (4,)), ("dst_ip", "<u4", (4,)), ("src_port", "<u
 PKT_OUT_DTYPE = np.dtype(KEY_FIELDS + [
     ("packet_length", "<u4"), ("ip_packet_length", "<u4"), ("tcp_flags", "u1"), ("meta", "u1"),
     ("hist_char", "u1"), ("reserved", "u1"), ("pkt_index", "<u4")])
+PARSED_DTYPE = np.dtype(KEY_FIELDS + [
+    ("packet_length", "<u4"), ("ip_packet_length", "<u4"), ("tcp_flags", "u1"), ("has_flags", "u1"),
+    ("reserved", "<u2"), ("pkt_index", "<u4")])
 DNS_OUT_DTYPE = np.dtype([("pkt_index", "<u4"), ("payload_offset", "<u4"), ("payload_length", "<u4"),
                           ("protocol", "u1"), ("family", "u1"), ("reserved", "<u2")])
 STATS_FIELDS = ["total_processed", "tcp_processed", "udp_processed", "ipv4_processed", "ipv6_processed",
@@ -44,7 +47,7 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
 LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
 FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
 
-assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16
+assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 56
 assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 88
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
 
@@ -80,6 +83,8 @@ GPU_SYMBOLS = [
     ("fb_set_own_ips", _I, [_P, _P, _U32]),
     ("fb_parse_classify_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_parse_classify", _I, [_P, _P, _U64, _P, _U32, _P, _PU32, _P, _PU32, _P, _P, _P]),
+    ("fb_process_parsed_dev", _I, [_P, _P, _U32, _P, _P, _P, _P]),
+    ("fb_process_parsed", _I, [_P, _P, _U32, _P, _PU32, _P, _P, _P]),
     ("fb_flow_update_dev", _I, [_P, _P, _P, _P]),
     ("fb_process_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_count", _I, [_P, _PU64, _P]),

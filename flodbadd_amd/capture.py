@@ -116,6 +116,22 @@ class FlodbaddGpuCapture:
                                               N.ptr(cls), N.ptr(st), None))
         return BatchResult(out[: n_out.value], dns[: n_dns.value], cls[:n], stats_dict(st))
 
+    def process_parsed(self, packets):
+        """process_parsed_packet (src/packets.rs:202-537) for a batch of SessionPacketData (list)
+        or PARSED_DTYPE records: canonical keys + filter on the GPU, then the session-table upsert
+        when the capture has a flow table.  Returns a BatchResult (records, cls, stats)."""
+        from .sessions import packets_to_parsed
+        arr = packets if isinstance(packets, np.ndarray) else packets_to_parsed(list(packets))
+        arr = np.ascontiguousarray(arr, dtype=N.PARSED_DTYPE)
+        n = arr.size
+        out = np.zeros(max(n, 1), dtype=N.PKT_OUT_DTYPE)
+        cls = np.zeros(max(n, 1), dtype=np.uint8)
+        st = np.zeros(1, dtype=N.STATS_DTYPE)
+        n_out = C.c_uint32(0)
+        N.check(N.gpu_lib().fb_process_parsed(self.ctx, N.ptr(arr) if n else None, n, N.ptr(out), C.byref(n_out),
+                                              N.ptr(cls), N.ptr(st), None))
+        return BatchResult(out[: n_out.value], np.zeros(0, dtype=N.DNS_OUT_DTYPE), cls[:n], stats_dict(st))
+
     def process_frames(self, frames, offsets):
         """parse + classify + flow-table upsert (the whole process_parsed_packet per frame)."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)

@@ -258,6 +258,28 @@ int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
     return FB_OK;
 }
 
+// Shared launch of the parse/classify kernel (frames) or its parsed-packet instantiation.
+static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipStream_t s) {
+    const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
+    int rc = ensure_status(c, tiles, s);
+    if (rc) return rc;
+    rc = upload_cfg(c, s);
+    if (rc) return rc;
+    p.tagg = c->d_status;
+    p.wstat = p.tagg + c->status_tiles;
+    p.cfg = c->d_cfg;
+    p.n = n;
+    p.num_tiles = (uint32_t)tiles;
+    p.epoch = ++c->epoch;
+    p.error = c->d_error + (p.epoch & 1u);
+    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
+    p.dbg = nullptr;
+    const uint32_t grid = std::min<uint32_t>(p.num_tiles, c->grid);
+    if (parsed) HIP_TRY(launch_process_parsed(p, grid, s));
+    else HIP_TRY(launch_parse_classify(p, grid, s));
+    return FB_OK;
+}
+
 int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes,
                           const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns,
                           uint8_t* d_class, fb_batch_stats* d_stats, void* stream) {
@@ -272,30 +294,39 @@ int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_by
         HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
         return FB_OK;
     }
-    const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
-    int rc = ensure_status(c, tiles, s);
-    if (rc) return rc;
-    rc = upload_cfg(c, s);
-    if (rc) return rc;
     ParseParams p;
+    p.parsed = nullptr;
     p.frames = d_frames;
     p.offsets = d_offsets;
     p.out = d_out;
     p.dns = d_dns;
     p.cls = d_class;
     p.stats = d_stats;
-    p.tagg = c->d_status;
-    p.wstat = p.tagg + c->status_tiles;
-    p.cfg = c->d_cfg;
     p.frames_bytes = (uint32_t)frames_bytes;
-    p.n = n;
-    p.num_tiles = (uint32_t)tiles;
-    p.epoch = ++c->epoch;
-    p.error = c->d_error + (p.epoch & 1u);
-    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
-    p.dbg = nullptr;
-    HIP_TRY(launch_parse_classify(p, std::min<uint32_t>(p.num_tiles, c->grid), s));
-    return FB_OK;
+    return launch_batch(c, p, n, false, s);
+}
+
+int fb_process_parsed_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out,
+                          uint8_t* d_class, fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_stats) return set_err(FB_ERR_INVAL, "ctx and d_stats are required");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (n && !d_in) return set_err(FB_ERR_INVAL, "d_in is NULL");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
+        return FB_OK;
+    }
+    ParseParams p;
+    p.parsed = d_in;
+    p.frames = nullptr;
+    p.offsets = nullptr;
+    p.out = d_out;
+    p.dns = nullptr;
+    p.cls = d_class;
+    p.stats = d_stats;
+    p.frames_bytes = 0;
+    return launch_batch(c, p, n, true, s);
 }
 
 static int ensure_staging(fb_ctx* c, uint64_t n, uint64_t bytes) {
@@ -365,6 +396,36 @@ int fb_parse_classify(fb_ctx* c, const uint8_t* frames, uint64_t frames_bytes, c
     HIP_TRY(hipStreamSynchronize(s));
     if (n_out) *n_out = (uint32_t)st.n_session;
     if (n_dns) *n_dns = (uint32_t)st.n_dns;
+    if (stats) *stats = st;
+    return FB_OK;
+}
+
+int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out* out, uint32_t* n_out,
+                      uint8_t* cls, fb_batch_stats* stats, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n too large");
+    if (n && !in) return set_err(FB_ERR_INVAL, "NULL input");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_staging(c, n, (uint64_t)n * sizeof(fb_parsed_pkt));
+    if (rc) return rc;
+    const fb_parsed_pkt* d_in = reinterpret_cast<const fb_parsed_pkt*>(c->s_frames);
+    if (n) HIP_TRY(hipMemcpyAsync(c->s_frames, in, (uint64_t)n * sizeof(fb_parsed_pkt), hipMemcpyHostToDevice, s));
+    rc = fb_process_parsed_dev(c, d_in, n, c->s_out, cls ? c->s_cls : nullptr, c->s_stats, s);
+    if (rc) return rc;
+    if (n && c->d_table) {
+        rc = fb_flow_update_dev(c, c->s_out, c->s_stats, s);
+        if (rc) return rc;
+    }
+    fb_batch_stats st;
+    HIP_TRY(hipMemcpyAsync(&st, c->s_stats, sizeof(st), hipMemcpyDeviceToHost, s));
+    rc = check_error_word(c, s);  // synchronises the stream
+    if (rc) return rc;
+    if (out && st.n_session)
+        HIP_TRY(hipMemcpyAsync(out, c->s_out, st.n_session * sizeof(fb_pkt_out), hipMemcpyDeviceToHost, s));
+    if (cls && n) HIP_TRY(hipMemcpyAsync(cls, c->s_cls, n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n_out) *n_out = (uint32_t)st.n_session;
     if (stats) *stats = st;
     return FB_OK;
 }

@@ -47,6 +47,7 @@ struct DevConfig {
 };
 
 struct ParseParams {
+    const fb_parsed_pkt* parsed;  // parsed-packet path (fb_process_parsed*) instead of frames
     const uint8_t* frames;
     const uint32_t* offsets;
     fb_pkt_out* out;
@@ -88,6 +89,7 @@ struct FlowParams {
 
 // Launchers (fb_parse.hip / fb_flow.hip).
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse(int* blocks_per_cu);
 hipError_t launch_flow_update(const FlowParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,

@@ -103,6 +103,67 @@ struct Pkt {
     bool tcp, v4, bad;    // stats bits (valid when session or filtered)
 };
 
+// ---- process_parsed_packet, src/packets.rs:202-327, for one SessionPacketData -------------
+// (raw 5-tuple src/dst/ports as parsed, L4 payload length, IP length, TCP flags if any) ->
+// canonical session key, originator, local/global filter, history char; k.cls = SESSION or
+// FILTERED.  Shared by the frame path (process_frame) and the parsed-packet path.
+__device__ __forceinline__ void classify_session(const DevConfig* cfg, const uint32_t* bm, uint32_t proto,
+                                                 uint32_t fam, const uint32_t (&src)[4], const uint32_t (&dst)[4],
+                                                 uint32_t sport, uint32_t dport, uint32_t hasf, uint32_t flags,
+                                                 uint32_t plen, uint32_t iplen, uint32_t idx, Pkt& k) {
+    k.tcp = proto == 6u;
+    k.v4 = fam == 2u;
+    const uint32_t S = svc(bm, sport), Dsv = svc(bm, dport);
+    bool swap;
+    if (S && !Dsv) {
+        swap = true;
+    } else if (S && Dsv) {
+        // flags only count for TCP (src/packets.rs:257-275); otherwise the port tiebreak
+        const bool tf = hasf && proto == 6u && (flags & 0x02u);
+        if (tf && !(flags & 0x10u)) swap = false;       // SYN
+        else if (tf && (flags & 0x10u)) swap = true;    // SYN+ACK
+        else swap = sport < dport;                      // port tiebreak (smaller port = server)
+    } else {
+        swap = false;
+    }
+    // is_originator: raw == key field-wise; with a swap that holds only for src==dst & sport==dport.
+    const bool orig = !swap || (src[0] == dst[0] && src[1] == dst[1] && src[2] == dst[2] &&
+                                src[3] == dst[3] && sport == dport);
+    uint32_t ks[4], kd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ks[j] = swap ? dst[j] : src[j];
+        kd[j] = swap ? src[j] : dst[j];
+    }
+    const uint32_t kport_s = swap ? dport : sport, kport_d = swap ? sport : dport;
+    const bool lan_s = fam == 2u ? lan_v4(ks[0]) : lan_v6(cfg, ks);
+    const bool lan_d = fam == 2u ? lan_v4(kd[0]) : lan_v6(cfg, kd);
+    uint32_t meta = hasf;
+    meta |= swap ? FB_META_SWAP : 0u;
+    meta |= orig ? FB_META_ORIGINATOR : 0u;
+    meta |= lan_s ? FB_META_LOCAL_SRC : 0u;
+    meta |= lan_d ? FB_META_LOCAL_DST : 0u;
+    meta |= own_ip(cfg, fam, ks) ? FB_META_SELF_SRC : 0u;
+    meta |= own_ip(cfg, fam, kd) ? FB_META_SELF_DST : 0u;
+    meta |= svc(bm, kport_d) ? FB_META_DST_SERVICE : 0u;
+    const uint32_t hc = hasf ? hist_char(flags, plen, orig) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        k.w[j] = ks[j];
+        k.w[4 + j] = kd[j];
+    }
+    k.w[8] = kport_s | (kport_d << 16);
+    k.w[9] = proto | (fam << 8);
+    k.w[10] = plen;
+    k.w[11] = iplen;
+    k.w[12] = flags | (meta << 8) | (hc << 16);
+    k.w[13] = idx;
+    const bool local = lan_s && lan_d;  // is_local_session! (symmetric in src/dst)
+    const uint32_t f = cfg->filter;
+    const bool drop = (f == FB_FILTER_LOCAL_ONLY && !local) || (f == FB_FILTER_GLOBAL_ONLY && local);
+    k.cls = drop ? FB_CLASS_FILTERED : FB_CLASS_SESSION;
+}
+
 // Decode + classify one frame from its header vectors; a field is only used when the pnet
 // length rules guarantee it lies inside the frame's caplen.
 __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const DevConfig* cfg,
@@ -192,56 +253,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
         return;
     }
 
-    // ---- process_parsed_packet, src/packets.rs:202-327 -------------------------------------
-    k.tcp = proto == 6u;
-    k.v4 = fam == 2u;
-    const uint32_t S = svc(bm, sport), Dsv = svc(bm, dport);
-    bool swap;
-    if (S && !Dsv) {
-        swap = true;
-    } else if (S && Dsv) {
-        if (hasf && (flags & 0x02u) && !(flags & 0x10u)) swap = false;       // SYN
-        else if (hasf && (flags & 0x02u) && (flags & 0x10u)) swap = true;    // SYN+ACK
-        else swap = sport < dport;                                          // port tiebreak
-    } else {
-        swap = false;
-    }
-    // is_originator: raw == key field-wise; with a swap that holds only for src==dst & sport==dport.
-    const bool orig = !swap || (src[0] == dst[0] && src[1] == dst[1] && src[2] == dst[2] &&
-                                src[3] == dst[3] && sport == dport);
-    uint32_t ks[4], kd[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        ks[j] = swap ? dst[j] : src[j];
-        kd[j] = swap ? src[j] : dst[j];
-    }
-    const uint32_t kport_s = swap ? dport : sport, kport_d = swap ? sport : dport;
-    const bool lan_s = fam == 2u ? lan_v4(ks[0]) : lan_v6(cfg, ks);
-    const bool lan_d = fam == 2u ? lan_v4(kd[0]) : lan_v6(cfg, kd);
-    uint32_t meta = hasf;
-    meta |= swap ? FB_META_SWAP : 0u;
-    meta |= orig ? FB_META_ORIGINATOR : 0u;
-    meta |= lan_s ? FB_META_LOCAL_SRC : 0u;
-    meta |= lan_d ? FB_META_LOCAL_DST : 0u;
-    meta |= own_ip(cfg, fam, ks) ? FB_META_SELF_SRC : 0u;
-    meta |= own_ip(cfg, fam, kd) ? FB_META_SELF_DST : 0u;
-    meta |= svc(bm, kport_d) ? FB_META_DST_SERVICE : 0u;
-    const uint32_t hc = hasf ? hist_char(flags, plen, orig) : 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        k.w[j] = ks[j];
-        k.w[4 + j] = kd[j];
-    }
-    k.w[8] = kport_s | (kport_d << 16);
-    k.w[9] = proto | (fam << 8);
-    k.w[10] = plen;
-    k.w[11] = iplen;
-    k.w[12] = flags | (meta << 8) | (hc << 16);
-    k.w[13] = idx;
-    const bool local = lan_s && lan_d;  // is_local_session! (symmetric in src/dst)
-    const uint32_t f = cfg->filter;
-    const bool drop = (f == FB_FILTER_LOCAL_ONLY && !local) || (f == FB_FILTER_GLOBAL_ONLY && local);
-    k.cls = drop ? FB_CLASS_FILTERED : FB_CLASS_SESSION;
+    classify_session(cfg, bm, proto, fam, src, dst, sport, dport, hasf, flags, plen, iplen, idx, k);
 }
 
 __device__ __forceinline__ fb_dns_out make_fb_dns(const Pkt& k) {
@@ -414,7 +426,7 @@ __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_
 //      exponential back-off                                                          | barrier
 //   4. every wave copies its LDS region to its place in the output with coalesced 16-B
 //      stores; DNS records straight from registers
-template <int U, uint32_t FLAGS>
+template <int U, uint32_t FLAGS, bool PARSED = false>
 __global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
     constexpr uint32_t kWaves = kThreads / 64;
     constexpr uint32_t WF = 64u * U;          // frames per wave per unit
@@ -449,13 +461,27 @@ __global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
         // ---- 1. loads -----------------------------------------------------------------------
         uint2 o[U];
         Hdr h[U];
+        uint4 pin[U][4];  // PARSED: one fb_parsed_pkt (56 B) per lane
+        if constexpr (!PARSED) {
 #pragma unroll
-        for (int r = 0; r < U; ++r) {
-            const uint32_t i = f0 + r * 64u + lane;
-            o[r] = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);  // n+1 entries
+            for (int r = 0; r < U; ++r) {
+                const uint32_t i = f0 + r * 64u + lane;
+                o[r] = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);  // n+1 entries
+            }
+#pragma unroll
+            for (int r = 0; r < U; ++r) load_headers1(rs, o[r].x, h[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const uint32_t i = min(f0 + r * 64u + lane, P.n - 1u);  // n >= 1 here
+                const uint4* q = reinterpret_cast<const uint4*>(P.parsed + i);
+                pin[r][0] = q[0];
+                pin[r][1] = q[1];
+                pin[r][2] = q[2];
+                const uint2 t = *reinterpret_cast<const uint2*>(q + 3);
+                pin[r][3] = make_uint4(t.x, t.y, 0u, 0u);
+            }
         }
-#pragma unroll
-        for (int r = 0; r < U; ++r) load_headers1(rs, o[r].x, h[r]);
         // ---- 2. classify + stage ----------------------------------------------------------------
         unsigned long long m_dns[U];
         uint4 dnsw[U];
@@ -465,8 +491,21 @@ __global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
             const uint32_t i = f0 + r * 64u + lane;
             const bool valid = i < P.n;
             Pkt k;
-            process_frame(rs, cfg, cfg->service_bitmap, h[r], valid ? o[r].x : 1u, valid ? o[r].y : 0u,
-                          P.frames_bytes, i, k);
+            if constexpr (!PARSED) {
+                process_frame(rs, cfg, cfg->service_bitmap, h[r], valid ? o[r].x : 1u, valid ? o[r].y : 0u,
+                              P.frames_bytes, i, k);
+            } else {
+                // fb_parsed_pkt: session_key words 0..9, then lengths, flags, pkt_index
+                const uint4 a = pin[r][0], b = pin[r][1], c = pin[r][2], d = pin[r][3];
+                const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {b.x, b.y, b.z, b.w};
+                const uint32_t proto = c.y & 0xffu, fam = (c.y >> 8) & 0xffu;
+                k.bad = false;
+                k.cls = FB_CLASS_DROP;
+                k.tcp = k.v4 = false;
+                if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
+                    classify_session(cfg, cfg->service_bitmap, proto, fam, src, dst, c.x & 0xffffu, c.x >> 16,
+                                     (d.x >> 8) & 1u, d.x & 0xffu, c.z, c.w, d.y, k);
+            }
             const bool is_s = valid && k.cls == FB_CLASS_SESSION;
             const bool is_d = valid && k.cls == FB_CLASS_DNS;
             const bool is_f = valid && k.cls == FB_CLASS_FILTERED;
@@ -585,6 +624,11 @@ __global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
 
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s) {
     hipLaunchKernelGGL((k_parse_block<kUnitTiles, kFlagsProduct>), dim3(grid), dim3(kThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_parse_block<kUnitTiles, kFlagsProduct, true>), dim3(grid), dim3(kThreads), 0, s, p);
     return hipGetLastError();
 }
 

@@ -7,12 +7,14 @@ query over the session list, not per packet.  Per-packet work never runs here.
 """
 import enum
 import ipaddress
+
+import numpy as np
 from dataclasses import dataclass, field
 from typing import List, Optional
 
 from ._native import (FB_FILTER_ALL, FB_FILTER_GLOBAL_ONLY, FB_FILTER_LOCAL_ONLY, FLOW_REC_DTYPE,
                       META_DST_SERVICE, META_HAS_FLAGS, META_LOCAL_DST, META_LOCAL_SRC, META_ORIGINATOR,
-                      META_SELF_DST, META_SELF_SRC, META_SWAP, PKT_OUT_DTYPE)
+                      META_SELF_DST, META_SELF_SRC, META_SWAP, PARSED_DTYPE, PKT_OUT_DTYPE)
 
 
 class Protocol(enum.IntEnum):
@@ -131,6 +133,54 @@ def records_to_packets(recs):
     return out
 
 
+def packets_to_parsed(packets):
+    """SessionPacketData list -> PARSED_DTYPE array (fb_parsed_pkt), pkt_index = list position."""
+    a = np.zeros(len(packets), dtype=PARSED_DTYPE)
+    for i, p in enumerate(packets):
+        s, d, fam = p.session.key_fields()
+        a[i]["src_ip"], a[i]["dst_ip"] = s, d
+        a[i]["src_port"], a[i]["dst_port"] = p.session.src_port, p.session.dst_port
+        a[i]["protocol"], a[i]["family"] = int(p.session.protocol), fam
+        a[i]["packet_length"], a[i]["ip_packet_length"] = p.packet_length, p.ip_packet_length
+        a[i]["tcp_flags"] = p.flags or 0
+        a[i]["has_flags"] = 0 if p.flags is None else 1
+        a[i]["pkt_index"] = i
+    return a
+
+
+def determine_conn_state(history):
+    """src/packets.rs:539-559."""
+    h = set(history)
+    if {"S", "H", "F", "f"} <= h:
+        return "SF"
+    if "S" in h and "h" not in h and "r" not in h:
+        return "S0"
+    if "R" in h or "r" in h:
+        return "REJ"
+    if "S" in h and "H" in h and "F" not in h and "f" not in h:
+        return "S1"
+    return "-"
+
+
+def histories_from_records(recs):
+    """Per-flow history strings + conn_state from packet-ordered fb_pkt_out records.
+
+    The GPU emits each packet's map_tcp_flags char (src/packets.rs:561-601) in its record; the
+    ordered per-flow string (src/packets.rs:187-198, 410-426) is the concatenation in packet order,
+    and conn_state is fixed at the first FIN/RST.  Returns {Session: (history, conn_state)}."""
+    assert recs.dtype == PKT_OUT_DTYPE
+    hist, state = {}, {}
+    for r in recs[np.argsort(recs["pkt_index"], kind="stable")]:
+        if not int(r["meta"]) & META_HAS_FLAGS:
+            continue
+        k = Session.from_key(r)
+        h = hist.get(k, "") + chr(int(r["hist_char"]))
+        hist[k] = h
+        if int(r["tcp_flags"]) & 0x05 and k not in state:  # FIN | RST
+            state[k] = determine_conn_state(h)
+    return {k: (h, state.get(k)) for k, h in hist.items()}
+
+
 def flows_to_sessions(flows, is_lan=None):
     """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session."""
     assert flows.dtype == FLOW_REC_DTYPE
@@ -158,5 +208,6 @@ def filter_sessions(sessions: List[SessionInfo], flt: SessionFilter) -> List[Ses
 
 __all__ = ["Protocol", "SessionFilter", "Session", "SessionPacketData", "SessionStats", "SessionInfo",
            "ip_to_words", "words_to_ip", "records_to_packets", "flows_to_sessions", "filter_sessions",
+           "packets_to_parsed", "determine_conn_state", "histories_from_records",
            "META_HAS_FLAGS", "META_SWAP", "META_ORIGINATOR", "META_LOCAL_SRC", "META_LOCAL_DST",
            "META_SELF_SRC", "META_SELF_DST", "META_DST_SERVICE"]

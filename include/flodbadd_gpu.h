@@ -112,6 +112,22 @@ typedef struct fb_pkt_out {
     uint32_t pkt_index;        /* 52: index of the frame in the batch                          */
 } fb_pkt_out;                  /* 56 bytes */
 
+/*
+ * One SessionPacketData (src/packets.rs:92-98) -- the input of process_parsed_packet
+ * (src/packets.rs:202) -- for hosts that keep their own decode and batch only the
+ * classification + session-table part.  `session` is the Session AS PARSED (src = sender,
+ * not canonicalised), in session_key layout; has_flags = flags.is_some().
+ */
+typedef struct fb_parsed_pkt {
+    fb_session_key session;    /*  0 */
+    uint32_t packet_length;    /* 40: L4 payload bytes                                        */
+    uint32_t ip_packet_length; /* 44                                                          */
+    uint8_t tcp_flags;         /* 48                                                          */
+    uint8_t has_flags;         /* 49: 1 = Some(flags)                                          */
+    uint16_t reserved;         /* 50: 0                                                        */
+    uint32_t pkt_index;        /* 52: copied to fb_pkt_out.pkt_index                           */
+} fb_parsed_pkt;               /* 56 bytes */
+
 /* One DNS-diverted packet: payload = frames[payload_offset .. +payload_length). */
 typedef struct fb_dns_out {
     uint32_t pkt_index;
@@ -230,6 +246,20 @@ int fb_parse_classify(fb_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes,
  */
 int fb_flow_update_dev(fb_ctx* ctx, const fb_pkt_out* d_recs, fb_batch_stats* d_stats,
                        void* stream);
+
+/*
+ * Batched process_parsed_packet (src/packets.rs:202-537) without the decode: canonical key,
+ * originator, Local/Global filter, history char for each fb_parsed_pkt, stream-compacted into
+ * d_out (class SESSION, input order).  A record with a protocol other than 6/17 or a family other
+ * than 2/10 is classified DROP.  DEVICE pointers, asynchronous; follow with fb_flow_update_dev
+ * for the session-table upsert.  d_class (n bytes) may be NULL; d_stats is required.
+ */
+int fb_process_parsed_dev(fb_ctx* ctx, const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out,
+                          uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+/* Host-memory variant of fb_process_parsed_dev followed by the session-table upsert when the
+ * context has a flow table (new_sessions / updated_sessions filled).  Synchronous. */
+int fb_process_parsed(fb_ctx* ctx, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out* out,
+                      uint32_t* n_out, uint8_t* cls, fb_batch_stats* stats, void* stream);
 
 /* Fused device-resident parse + classify + flow upsert (no record round trip through HBM).
  * Same outputs as fb_parse_classify_dev (d_out may be NULL) followed by fb_flow_update_dev. */

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 BITMAP_PATH = os.path.join(ROOT, "flodbadd_amd", "data", "service_ports.bin")
 
 # Record layouts are defined once, in the product's binding of include/flodbadd_gpu.h.
-from flodbadd_amd._native import (DNS_OUT_DTYPE, FB_IP_DTYPE, FLOW_REC_DTYPE, LAN_V6_DTYPE,  # noqa: E402
+from flodbadd_amd._native import (DNS_OUT_DTYPE, FB_IP_DTYPE, FLOW_REC_DTYPE, LAN_V6_DTYPE, PARSED_DTYPE,  # noqa: E402
                                   PKT_OUT_DTYPE, STATS_DTYPE)
 
 
@@ -41,6 +41,8 @@ def lib():
         P, U32, U64 = C.c_void_p, C.c_uint32, C.c_uint64
         L.orc_parse_classify.restype = C.c_int
         L.orc_parse_classify.argtypes = [P, P, U64, P, U32, P, C.POINTER(U32), P, C.POINTER(U32), P, P]
+        L.orc_process_parsed.restype = C.c_int
+        L.orc_process_parsed.argtypes = [P, P, U32, P, C.POINTER(U32), P, P]
         L.orc_flows_new.restype = P
         L.orc_flows_free.argtypes = [P]
         L.orc_flows_clear.argtypes = [P]
@@ -95,6 +97,19 @@ def parse_classify(cfg, frames, offsets):
                              out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), cls.ctypes.data,
                              st.ctypes.data)
     return out[: no.value], dns[: nd.value], cls[:n], st
+
+
+def process_parsed(cfg, parsed):
+    """Batched process_parsed_packet over PARSED_DTYPE records -> (records, cls, stats)."""
+    parsed = np.ascontiguousarray(parsed, dtype=PARSED_DTYPE)
+    n = parsed.size
+    out = np.zeros(max(n, 1), dtype=PKT_OUT_DTYPE)
+    cls = np.zeros(max(n, 1), dtype=np.uint8)
+    st = np.zeros(1, dtype=STATS_DTYPE)
+    no = C.c_uint32()
+    lib().orc_process_parsed(C.byref(cfg), parsed.ctypes.data if n else None, n, out.ctypes.data, C.byref(no),
+                             cls.ctypes.data, st.ctypes.data)
+    return out[: no.value], cls[:n], st
 
 
 class Flows:

@@ -308,6 +308,49 @@ int orc_parse_classify(const orc_cfg* c, const uint8_t* frames, uint64_t frames_
     return 0;
 }
 
+int orc_process_parsed(const orc_cfg* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out* out,
+                       uint32_t* n_out, uint8_t* cls, fb_batch_stats* st) {
+    fb_batch_stats s;
+    memset(&s, 0, sizeof(s));
+    uint32_t no = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const fb_parsed_pkt* q = &in[i];
+        uint32_t k = FB_CLASS_DROP;
+        if ((q->session.protocol == 6 || q->session.protocol == 17) &&
+            (q->session.family == 2 || q->session.family == 10)) {
+            orc_parsed p;
+            memset(&p, 0, sizeof(p));
+            p.kind = ORC_SESSION;
+            p.protocol = q->session.protocol;
+            p.family = q->session.family;
+            p.has_flags = q->has_flags ? 1 : 0;
+            p.flags = q->tcp_flags;
+            memcpy(p.src_ip, q->session.src_ip, 16);
+            memcpy(p.dst_ip, q->session.dst_ip, 16);
+            p.src_port = q->session.src_port;
+            p.dst_port = q->session.dst_port;
+            p.packet_length = q->packet_length;
+            p.ip_packet_length = q->ip_packet_length;
+            s.total_processed++; /* PACKET_STATS, src/packets.rs:211-227 */
+            if (p.protocol == 6) s.tcp_processed++; else s.udp_processed++;
+            if (p.family == 2) s.ipv4_processed++; else s.ipv6_processed++;
+            fb_pkt_out rec;
+            k = orc_classify(c, &p, q->pkt_index, &rec);
+            if (k == FB_CLASS_SESSION) {
+                if (out) out[no] = rec;
+                no++;
+            }
+        }
+        if (k == FB_CLASS_DROP) s.n_drop++;
+        if (k == FB_CLASS_FILTERED) s.n_filtered++;
+        if (cls) cls[i] = (uint8_t)k;
+    }
+    s.n_session = no;
+    if (n_out) *n_out = no;
+    if (st) *st = s;
+    return 0;
+}
+
 /* ---------------------------------------------------------------------------------------
  * Session table: a restatement of the DashMap<Session, SessionInfo> upsert
  * (src/packets.rs:329-535) keeping the integer counters (src/packets.rs:111-120, 383-391),

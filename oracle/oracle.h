@@ -71,6 +71,12 @@ int orc_parse_classify(const orc_cfg* cfg, const uint8_t* frames, uint64_t frame
                        const uint32_t* offsets, uint32_t n, fb_pkt_out* out, uint32_t* n_out,
                        fb_dns_out* dns, uint32_t* n_dns, uint8_t* cls, fb_batch_stats* stats);
 
+/* Batched process_parsed_packet (src/packets.rs:202-327) over fb_parsed_pkt records, same
+ * contract as fb_process_parsed_dev: PACKET_STATS before the filter, SESSION records compacted
+ * in input order, protocol not 6/17 or family not 2/10 -> DROP. */
+int orc_process_parsed(const orc_cfg* cfg, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out* out,
+                       uint32_t* n_out, uint8_t* cls, fb_batch_stats* stats);
+
 /* ---- session table (DashMap<Session, SessionInfo> restated; integer part + history) ---- */
 typedef struct orc_flows orc_flows;
 orc_flows* orc_flows_new(void);

@@ -1,0 +1,72 @@
+"""Runner for tests/golden/reference_kats.json (known-answer tests transcribed from the
+reference's own tests).  A `processor(case_cfg, packets)` returns (records, flows) where
+records are the packet-ordered fb_pkt_out SESSION records and flows the fb_flow_rec table."""
+import ipaddress
+import json
+import os
+
+from flodbadd_amd.sessions import (META_DST_SERVICE, Protocol, Session, SessionFilter, SessionPacketData,
+                                   flows_to_sessions, histories_from_records)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAT_PATH = os.path.join(HERE, "golden", "reference_kats.json")
+FLAGS = {"FIN": 0x01, "SYN": 0x02, "RST": 0x04, "PSH": 0x08, "ACK": 0x10}
+
+
+def load():
+    with open(KAT_PATH) as f:
+        return json.load(f)
+
+
+def packets_of(case):
+    out = []
+    for p in case["packets"]:
+        s = Session(Protocol[p["proto"]], ipaddress.ip_address(p["src"]), p["sport"],
+                    ipaddress.ip_address(p["dst"]), p["dport"])
+        fl = None if p["flags"] is None else sum(FLAGS[x] for x in p["flags"])
+        out.append(SessionPacketData(s, p["len"], p["ip_len"], fl))
+    return out
+
+
+def key_of(k):
+    return Session(Protocol[k[0]], ipaddress.ip_address(k[1]), k[2], ipaddress.ip_address(k[3]), k[4])
+
+
+def check_case(case, records, flows):
+    """Assert everything the reference asserts for this case."""
+    sess = {i.session: i for i in flows_to_sessions(flows)}
+    hist = histories_from_records(records)
+    exp = case["expect"]
+    name = case["name"]
+    if "n_sessions" in exp:
+        assert len(sess) == exp["n_sessions"], (name, sorted(sess, key=lambda s: s.sort_key()))
+    tol = 1e-9
+    for e in exp["sessions"]:
+        k = key_of(e["key"])
+        assert k in sess, (name, "missing session", k, list(sess))
+        st = sess[k].stats
+        tol = e.get("tolerance", 1e-9)
+        for f in ("outbound_bytes", "inbound_bytes", "orig_pkts", "resp_pkts"):
+            if f in e:
+                assert getattr(st, f) == e[f], (name, f, getattr(st, f), e[f])
+        for f in ("average_packet_size", "inbound_outbound_ratio"):
+            if f in e:
+                assert abs(getattr(st, f) - e[f]) <= tol, (name, f, getattr(st, f), e[f])
+        h, cs = hist.get(k, ("", None))
+        if "history" in e:
+            assert h == e["history"], (name, h)
+        for c in e.get("history_contains", []):
+            assert c in h, (name, h, c)
+        if "history_order" in e:
+            a, b = e["history_order"]
+            assert h.index(a) < h.index(b), (name, h)
+        if e.get("conn_state_set"):
+            assert cs is not None, (name, h)
+        if "dst_service" in e:
+            # dst_service is set at session creation from the first packet (src/packets.rs:441-464)
+            first = next(r for r in records if Session.from_key(r) == k)
+            assert bool(int(first["meta"]) & META_DST_SERVICE) == e["dst_service"], (name, k.dst_port)
+
+
+def filter_of(case):
+    return SessionFilter[case["filter"]]
