@@ -143,3 +143,48 @@ def test_parsed_path_matches_frame_path(gpu_capture):
     g2 = gpu_capture.process_parsed(parsed)
     assert g2.records.tobytes() == g.records.tobytes()
     gpu_capture.clear_all_sessions()
+
+
+# ---- committed golden fixtures through the GPU frame path --------------------------------------
+import os  # noqa: E402
+
+_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _golden(name):
+    return np.load(os.path.join(_GOLDEN, name), allow_pickle=False)
+
+
+@pytest.mark.parametrize("tag,flt", [("all", SessionFilter.All), ("global", SessionFilter.GlobalOnly),
+                                     ("local", SessionFilter.LocalOnly)])
+def test_golden_edge_frames_on_gpu(gpu_capture, tag, flt):
+    from flodbadd_amd.sessions import words_to_ip
+    g = _golden("edge_frames.npz")
+    gpu_capture.set_filter(flt)
+    gpu_capture.set_lan_v6([(str(words_to_ip(r["net"], 10)), int(r["prefix"])) for r in g["lan_v6"]])
+    gpu_capture.set_own_ips([str(words_to_ip(r["addr"], int(r["family"]))) for r in g["own_ips"]])
+    try:
+        r = gpu_capture.parse_classify(g["frames"], g["offsets"])
+        assert r.records.tobytes() == g["records_" + tag].tobytes()
+        assert r.dns.tobytes() == g["dns_" + tag].tobytes()
+        assert np.array_equal(r.cls, g["cls_" + tag])
+        st = g["stats_" + tag][0]
+        for k in ("total_processed", "tcp_processed", "udp_processed", "ipv4_processed", "ipv6_processed",
+                  "n_session", "n_dns", "n_drop", "n_filtered", "bad_offsets"):
+            assert r.stats[k] == int(st[k]), k
+    finally:
+        gpu_capture.set_filter(SessionFilter.All)
+        gpu_capture.set_lan_v6([])
+        gpu_capture.set_own_ips([])
+
+
+@pytest.mark.parametrize("cid", [2, 3])
+def test_golden_samples_on_gpu(gpu_capture, cid):
+    g = _golden("c%d_sample.npz" % cid)
+    gpu_capture.clear_all_sessions()
+    r = gpu_capture.process_frames(g["frames"], g["offsets"])
+    assert r.records.tobytes() == g["records_all"].tobytes()
+    assert r.dns.tobytes() == g["dns_all"].tobytes()
+    assert rows_sorted(gpu_capture.export_flows()) == rows_sorted(g["flows_all"])
+    assert r.stats["new_sessions"] == int(g["flow_stats_all"][0]["new_sessions"])
+    gpu_capture.clear_all_sessions()
