@@ -97,6 +97,67 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
                 stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
+def host_inclusive(N, lib, ctx, frames, offs, calls=20):
+    """fb_parse_classify from PINNED host buffers to pinned host outputs: H2D of frames+offsets,
+    the kernel, D2H of records/DNS/stats (the path that starts and ends in host memory, as
+    pcap buffers do).  Reported in DESIGN.md; never the headline value."""
+    n = len(offs) - 1
+    pin_fr = N.PinnedBuffer(frames.nbytes)
+    pin_fr.array[:] = frames
+    pin_off = N.PinnedBuffer(offs.nbytes)
+    pin_off.array[:] = offs.view(np.uint8)
+    pin_out = N.PinnedBuffer(n * N.PKT_OUT_DTYPE.itemsize)
+    pin_dns = N.PinnedBuffer(n * N.DNS_OUT_DTYPE.itemsize)
+    st = np.zeros(1, dtype=N.STATS_DTYPE)
+    no, nd = C.c_uint32(), C.c_uint32()
+
+    def call():
+        N.check(lib.fb_parse_classify(ctx, pin_fr.ptr, frames.nbytes, pin_off.ptr, n, pin_out.ptr, C.byref(no),
+                                      pin_dns.ptr, C.byref(nd), None, st.ctypes.data, None))
+    call()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    el = time.perf_counter() - t0
+    moved = frames.nbytes + offs.nbytes + no.value * N.PKT_OUT_DTYPE.itemsize + nd.value * N.DNS_OUT_DTYPE.itemsize
+    for b in (pin_fr, pin_off, pin_out, pin_dns):
+        b.free()
+    return dict(value=round(calls * n / el / 1e6, 2), unit="Mpackets/s", ms_per_call=round(el * 1e3 / calls, 3),
+                pcie_bytes_per_call=int(moved), pcie_GBs=round(moved * calls / el / 1e9, 2),
+                note="synchronous fb_parse_classify on pinned host buffers (H2D + kernel + D2H, no overlap)")
+
+
+def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device):
+    """BASELINE config C5's exchange after the timed region: this rank's shard through the fused
+    parse + classify + flow-table kernel, then the global per-flow counter merge
+    (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce SUM over RCCL)."""
+    from flodbadd_amd.distributed import global_flow_table
+    n = len(offs) - 1
+    N.check(lib.fb_flow_clear(ctx, None))
+    d_fr = N.DeviceBuffer(frames.nbytes).upload(frames)
+    d_off = N.DeviceBuffer(offs.nbytes).upload(offs)
+    d_out = N.DeviceBuffer(n * N.PKT_OUT_DTYPE.itemsize)
+    d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+    ev0, ev1 = N.Event(), N.Event()
+    ev0.record(None)
+    N.check(lib.fb_process_dev(ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, None, None, d_st.ptr, None))
+    ev1.record(None)
+    flow_ms = ev0.elapsed_ms(ev1)
+    cnt = C.c_uint64()
+    N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
+    flows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
+    got = C.c_uint64()
+    t0 = time.perf_counter()
+    N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
+    merged = global_flow_table(dist_nccl, flows[: got.value], device=device)
+    el = time.perf_counter() - t0
+    for b in (d_fr, d_off, d_out, d_st):
+        b.free()
+    return dict(local_flows=int(got.value), global_flows=int(len(merged)), flow_update_ms=round(flow_ms, 3),
+                export_merge_ms=round(el * 1e3, 3),
+                note="per-rank fused parse+flow upsert of the rank's shard, then export + RCCL all-gather/all-reduce")
+
+
 def cpu_baseline(frames, offs, seconds):
     """The oracle (C restatement of src/packets.rs parse + classify, 1 thread) on the same batch,
     repeated until `seconds` of CPU work: a bounded sample of the same workload."""
@@ -143,6 +204,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C3) measurement")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (pinned H2D/D2H) measurement")
+    ap.add_argument("--no-flow-reduce", action="store_true", help="N>1: skip the C5 global flow-counter exchange")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,6 +227,7 @@ def main():
     cfg.abi_version = N.FB_ABI_VERSION
     cfg.filter = N.FB_FILTER_GLOBAL_ONLY  # FlodbaddCapture::new() default (src/capture.rs:108)
     cfg.max_batch_packets = 1 << 24
+    cfg.flow_capacity = 1 << 21  # C5 exchange: the rank's shard flows (<= 2^20 in the C4/C5 pool)
     N.check(lib.fb_set_device(device))
     ctx = lib.fb_create(device, C.byref(cfg))
     if not ctx:
@@ -187,6 +251,26 @@ def main():
                                 roofline_achieved_GBs=round(r3["algo_bytes"] / pl3 / 1e9, 1),
                                 roofline_frac=round(r3["algo_bytes"] / pl3 / 1e9 / HBM_PEAK_GBS, 4),
                                 algo_bytes_per_launch=r3["algo_bytes"])
+
+    if not args.no_host and rank == 0 and args.config == 2:
+        extra["host_inclusive_c2"] = host_inclusive(N, lib, ctx, main_r["frames"], main_r["offs"])
+
+    if world > 1 and not args.no_flow_reduce:
+        try:
+            import torch
+            import torch.distributed as tdist
+            dev = torch.device("cuda", device)
+            torch.cuda.set_device(dev)
+            g = tdist.new_group(backend="nccl")
+
+            class _D:  # torch.distributed bound to the RCCL group
+                ReduceOp = tdist.ReduceOp
+                get_world_size = staticmethod(lambda group=None: tdist.get_world_size(g))
+                all_gather = staticmethod(lambda a, b, group=None: tdist.all_gather(a, b, group=g))
+                all_reduce = staticmethod(lambda t, op, group=None: tdist.all_reduce(t, op=op, group=g))
+            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], _D, dev)
+        except Exception as e:  # the exchange is reported, never allowed to break the bench line
+            extra["c5_flow_reduce"] = {"error": repr(e)[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
