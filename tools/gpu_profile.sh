@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 CFG=${CFG:-2}
 STEPS=${STEPS:-200}
-step() { echo "== $*"; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+step() { echo "== $*" >&2; "$@"; rc=$?; echo "rc=$rc" >&2; [ $rc -eq 0 ] || exit $rc; }
 step timeout -k 10 400 python3 bench.py --config $CFG --steps $STEPS --warmup 20 > "$OUT/bench_c$CFG.json" 2> "$OUT/bench_c$CFG.err"
 cat "$OUT/bench_c$CFG.json"
 cd /tmp
