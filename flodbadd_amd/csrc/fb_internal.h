@@ -20,16 +20,30 @@ constexpr int kThreads = FB_BLOCK_THREADS;
 constexpr int kUnitTiles = FB_UNIT_TILES;
 constexpr int kTile = (kThreads / 64) * 64 * kUnitTiles;  // frames per look-back unit
 
+// k_parse_ctl: kCtlFW frame waves + 1 control wave per block; kCtlU wave-tiles per frame wave.
+#ifndef FB_CTL_FW
+#define FB_CTL_FW 7
+#endif
+#ifndef FB_CTL_U
+#define FB_CTL_U 2
+#endif
+constexpr int kCtlFW = FB_CTL_FW;
+constexpr int kCtlU = FB_CTL_U;
+constexpr int kCtlThreads = 64 * (kCtlFW + 1);
+constexpr int kCtlTile = kCtlFW * 64 * kCtlU;  // frames per unit of k_parse_ctl
+
 // Upper bound on parse blocks per launch (per-block stats slots).
 constexpr uint32_t kMaxBlocks = 4096;
 
 // Look-back scratch (one allocation per context, zeroed when the 8-bit epoch wraps):
 //   tagg[units]           unit status   [epoch:8 | INC:1 | n_dns:27 | n_session:28]
-//   wstat[kMaxBlocks][2]  per-block pre-filter counters [epoch:8 | n_tcp:28 | n_filtered:28],
+//   wstat[slots][2]       per-block pre-filter counters (slots = stat_slots(units)) [epoch:8 | n_tcp:28 | n_filtered:28],
 //                                                      [epoch:8 | n_bad:28 | n_ipv4:28]
 // Epoch-tagged words need no per-launch zeroing.
 constexpr uint32_t kMaxEpoch = 255;
-inline uint64_t scratch_words(uint64_t units) { return units + 2ull * kMaxBlocks; }
+// Stats slots: one pair per block, and a grid never exceeds max(kMaxBlocks, units).
+inline uint64_t stat_slots(uint64_t units) { return units > kMaxBlocks ? units : kMaxBlocks; }
+inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units); }
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {

@@ -308,57 +308,65 @@ __device__ __forceinline__ unsigned long long st_pack(uint32_t ep, bool inc, uns
            (((c >> 28) & ((1ull << 27) - 1ull)) << 28);
 }
 
-template <uint32_t FLAGS>
+template <uint32_t FLAGS, int NW = 4>
 __device__ unsigned long long lookback_unit(const ParseParams& P, uint32_t u, uint32_t& spins) {
+    constexpr int WIN = 64 * NW;  // predecessors probed per round trip
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t ep = P.epoch;
+    // sc1 buffer loads (aux 16): L1-bypassing like the agent-scope atomic loads, 32-bit offsets,
+    // and out-of-range offsets (negative indices) read as 0 = "not published".
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.tagg, (short)0, (int)(u * 8u), 0x00020000);
+    auto word = [&](int idx) {
+        const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rt, (uint32_t)idx * 8u, 0, 16);
+        return (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+    };
     unsigned long long pre = 0ull;
-    long hi = (long)u - 1;  // nearest predecessor not yet accounted for
+    int lo = (int)u - WIN;  // window = [lo, lo + WIN), lane l of chunk k reads lo + 64k + l
     spins = 0u;
-    while (hi >= 0) {
-        unsigned long long v[4];
-        bool own[4];
+    for (;;) {
+        unsigned long long v[NW];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const long idx = hi - (long)(k * 64 + lane);  // distance k*64+lane from hi
-            own[k] = idx >= 0;
-            v[k] = own[k] ? ald(P.tagg + idx) : 0ull;
-        }
+        for (int k = 0; k < NW; ++k) v[k] = word(lo + 64 * k + (int)lane);
         for (;;) {
-            // nearest INC in the window (smallest distance)
-            uint32_t near = 256u;
+            // nearest published inclusive prefix = the highest index carrying INC
+            int near = -1;
 #pragma unroll
-            for (int k = 3; k >= 0; --k) {
-                const unsigned long long im = __ballot(own[k] && tag_of(v[k]) == ep && (v[k] & kIncBit));
-                if (im) near = (uint32_t)k * 64u + (uint32_t)(__ffsll((long long)im) - 1);
+            for (int k = 0; k < NW; ++k) {
+                const int idx = lo + 64 * k + (int)lane;
+                const unsigned long long im = __ballot(idx >= 0 && tag_of(v[k]) == ep && (v[k] & kIncBit));
+                if (im) near = lo + 64 * k + (63 - __clzll((long long)im));
             }
+            const int floor_idx = near >= 0 ? near : (lo > 0 ? lo : 0);  // words below are not needed
             bool ready = true;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool need = own[k] && (uint32_t)(k * 64) + lane <= near;
-                ready &= !need || tag_of(v[k]) == ep;
+            for (int k = 0; k < NW; ++k) {
+                const int idx = lo + 64 * k + (int)lane;
+                ready &= idx < floor_idx || tag_of(v[k]) == ep;
             }
             if (__ballot(!ready) == 0ull) {
-                unsigned long long s = 0ull;
+                unsigned long long sum = 0ull;
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    s += (own[k] && (uint32_t)(k * 64) + lane <= near) ? st_counts(v[k]) : 0ull;
-                pre += wave_sum64(s);
-                if (near < 256u) return pre;
+                for (int k = 0; k < NW; ++k) {
+                    const int idx = lo + 64 * k + (int)lane;
+                    sum += idx >= floor_idx ? st_counts(v[k]) : 0ull;
+                }
+                pre += wave_sum64(sum);
+                if (near >= 0 || lo <= 0) return pre;
                 break;
             }
             if (++spins > (1u << 16)) { if (lane == 0u) atomicOr(P.error, 1u); return pre; }
             // exponential back-off: every poll is a memory-side read
             for (uint32_t z = 0; z < min(spins, 6u); ++z) __builtin_amdgcn_s_sleep(8);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const long idx = hi - (long)(k * 64 + lane);
-                if (own[k] && tag_of(v[k]) != ep) v[k] = ald(P.tagg + idx);
+            for (int k = 0; k < NW; ++k) {
+                const int idx = lo + 64 * k + (int)lane;
+                if (idx >= floor_idx && tag_of(v[k]) != ep) v[k] = word(idx);
             }
         }
-        hi -= 256;
+        lo -= WIN;  // no INC in this window: every word was an aggregate, continue below it
     }
-    return pre;
 }
 
 // Batch totals (the wave owning the last tile): `tot_c` = inclusive [dns|session] count
@@ -406,6 +414,11 @@ __device__ void write_batch_stats(const ParseParams& P, unsigned long long tot_c
         S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
     }
 }
+
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
 
 __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_t o, Hdr& h) {
     h.A = ld16(rs, o + 10u);

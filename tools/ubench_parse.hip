@@ -99,7 +99,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dcfg, &hc, sizeof(hc), hipMemcpyHostToDevice));
 
     const uint32_t tiles = (n + UB_TILE - 1) / UB_TILE;
-    const uint32_t stiles = tiles;
+    const uint32_t ctiles = (n + fbk::kCtlTile - 1) / fbk::kCtlTile;
+    const uint32_t t4 = (n + (fbk::kThreads / 64) * 256 - 1) / ((fbk::kThreads / 64) * 256);
+    const uint32_t t2 = (n + (fbk::kThreads / 64) * 128 - 1) / ((fbk::kThreads / 64) * 128);
+    // look-back scratch sized for the larger unit count of the kernels (a smaller one let
+    // the status words of one kernel overlap its stats slots -> garbage prefixes -> OOB stores)
+    const uint32_t stiles = std::max(std::max(tiles, ctiles), std::max(t4, t2));
     const size_t swords = fbk::scratch_words(stiles);
     unsigned long long* status;
     CK(hipMalloc(&status, swords * 8));
@@ -126,12 +131,13 @@ int main(int argc, char** argv) {
     hipStream_t s;
     CK(hipStreamCreate(&s));
     uint32_t epoch = 0;
-    auto params = [&](int r, bool lb) {
+    auto params = [&](int r, bool lb, uint32_t nt = 0) {
+        if ((nt ? nt : tiles) > stiles) { fprintf(stderr, "scratch too small\n"); exit(2); }
         fbk::ParseParams p;
         p.frames = bufs[r].fr; p.offsets = bufs[r].off; p.out = bufs[r].out; p.dns = bufs[r].dns;
         p.cls = nullptr; p.stats = bufs[r].st; p.cfg = dcfg;
         p.tagg = status; p.wstat = status + stiles;
-        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = tiles;
+        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = nt ? nt : tiles; p.parsed = nullptr;
         if (lb && ++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); CK(hipMemset(err, 0, 16)); epoch = 1; }
         p.epoch = epoch;
         p.error = err + (epoch & 1u); p.error_next = err + ((epoch & 1u) ^ 1u); p.dbg = dbg;
@@ -140,11 +146,21 @@ int main(int argc, char** argv) {
     uint64_t caps = 0;
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;  // upper bound: all emitted
-    const char* names[] = {"product", "no_lookback", "no_store", "no_lookback_no_store", "read_frames",
-                           "copy_frames_to_out", "header_loads_only"};
-    const int NV = 7;
+    const char* names[] = {"block", "block_no_lookback", "block_no_store", "block_no_lookback_no_store", "read_frames",
+                           "copy_frames_to_out", "header_loads_only", "ctl", "ctl_no_lookback", "ctl_no_store",
+                           "ctl_no_lookback_no_store", "block_nonpersistent", "ctl1", "ctl1_no_lookback", "ctl1_no_store",
+                           "ctl1_no_lookback_no_store", "2p_u4", "2p_u4_no_lookback", "2p_u4_no_store",
+                           "2p_u4_no_lookback_no_store", "2p_u2", "2p_u2_no_lookback"};
+    const int NV = 22;
     int bpc = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_block<UB_R, 0>), fbk::kThreads, 0));
+    int cbpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&cbpc, (fbk::k_parse_ctl<fbk::kCtlU, 0>), fbk::kCtlThreads, 0));
+    cbpc = std::min(cbpc, std::max(1, 24 / (fbk::kCtlThreads / 64)));
+    int c1bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1bpc, (fbk::k_parse_ctl1<fbk::kCtlU, 0, false, 2>), fbk::kCtlThreads, 0));
+    c1bpc = std::min(c1bpc, std::max(1, 24 / (fbk::kCtlThreads / 64)));
+    printf("{\"ctl_blocks_per_cu\": %d, \"ctl1_blocks_per_cu\": %d, \"ctl_units\": %u}\n", cbpc, c1bpc, ctiles);
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     printf("{\"blocks_per_cu_api\": %d, \"cus\": %d, \"tiles\": %u}\n", bpc, prop.multiProcessorCount, tiles);
@@ -152,13 +168,28 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const int rounds = 3;
-    const int maxb = std::min(bpc, std::max(1, 24 / (fbk::kThreads / 64)));
+    const int blimit = std::min(bpc, std::max(1, 24 / (fbk::kThreads / 64)));
+    int pbpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pbpc, (fbk::k_parse_2p<4, 0>), fbk::kThreads, 0));
+    pbpc = std::min(pbpc, std::max(1, 24 / (fbk::kThreads / 64)));
+    const int maxb = std::max(std::max(std::max(blimit, cbpc), c1bpc), pbpc);
     for (int bpcu = 1; bpcu <= maxb; ++bpcu) {
         const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(bpcu * prop.multiProcessorCount));
+        const uint32_t cgrid = std::min<uint32_t>(ctiles, (uint32_t)(std::min(bpcu, cbpc) * prop.multiProcessorCount));
+        const uint32_t p4grid = std::min<uint32_t>(t4, (uint32_t)(std::min(bpcu, pbpc) * prop.multiProcessorCount));
+        const uint32_t p2grid = std::min<uint32_t>(t2, (uint32_t)(std::min(bpcu, pbpc) * prop.multiProcessorCount));
+        const uint32_t c1grid = std::min<uint32_t>(ctiles, (uint32_t)(std::min(bpcu, c1bpc) * prop.multiProcessorCount));
         std::vector<double> best(NV, 1e30), sum(NV, 0.0);
         for (int round = 0; round < rounds; ++round) {
             for (int v = 0; v < NV; ++v) {
-                if (v >= 4 && bpcu > 1) continue;
+                if (((v >= 4 && v <= 6) || v == 11) && bpcu > 1) continue;
+                if (v >= 7 && v <= 10 && bpcu > cbpc) continue;
+            if (v >= 12 && v <= 15 && bpcu > c1bpc) continue;
+            if (v >= 16 && bpcu > pbpc) continue;
+                if (v >= 12 && v <= 15 && bpcu > c1bpc) continue;
+                if (v >= 16 && bpcu > pbpc) continue;
+            if (v <= 3 && bpcu > blimit) continue;
+                if (v <= 3 && bpcu > blimit) continue;
                 for (int warm = -10; warm < iters; ++warm) {
                     if (warm == 0) CK(hipEventRecord(e0, s));
                     int r = (warm + 100) % R;
@@ -169,6 +200,21 @@ int main(int argc, char** argv) {
                     case 3: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kNoLookback | fbk::kNoStore>), dim3(grid), dim3(fbk::kThreads), 0, s, params(r, true)); break;
                     case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
                     case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+                    case 7: hipLaunchKernelGGL((fbk::k_parse_ctl<fbk::kCtlU, 0>), dim3(cgrid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 8: hipLaunchKernelGGL((fbk::k_parse_ctl<fbk::kCtlU, fbk::kNoLookback>), dim3(cgrid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 9: hipLaunchKernelGGL((fbk::k_parse_ctl<fbk::kCtlU, fbk::kNoStore>), dim3(cgrid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 10: hipLaunchKernelGGL((fbk::k_parse_ctl<fbk::kCtlU, fbk::kNoLookback | fbk::kNoStore>), dim3(cgrid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 12: hipLaunchKernelGGL((fbk::k_parse_ctl1<fbk::kCtlU, 0, false, 2>), dim3(c1grid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 13: hipLaunchKernelGGL((fbk::k_parse_ctl1<fbk::kCtlU, fbk::kNoLookback, false, 2>), dim3(c1grid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 14: hipLaunchKernelGGL((fbk::k_parse_ctl1<fbk::kCtlU, fbk::kNoStore, false, 2>), dim3(c1grid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 15: hipLaunchKernelGGL((fbk::k_parse_ctl1<fbk::kCtlU, fbk::kNoLookback | fbk::kNoStore, false, 2>), dim3(c1grid), dim3(fbk::kCtlThreads), 0, s, params(r, true, ctiles)); break;
+                    case 16: hipLaunchKernelGGL((fbk::k_parse_2p<4, 0>), dim3(p4grid), dim3(fbk::kThreads), 0, s, params(r, true, t4)); break;
+                    case 17: hipLaunchKernelGGL((fbk::k_parse_2p<4, fbk::kNoLookback>), dim3(p4grid), dim3(fbk::kThreads), 0, s, params(r, true, t4)); break;
+                    case 18: hipLaunchKernelGGL((fbk::k_parse_2p<4, fbk::kNoStore>), dim3(p4grid), dim3(fbk::kThreads), 0, s, params(r, true, t4)); break;
+                    case 19: hipLaunchKernelGGL((fbk::k_parse_2p<4, fbk::kNoLookback | fbk::kNoStore>), dim3(p4grid), dim3(fbk::kThreads), 0, s, params(r, true, t4)); break;
+                    case 20: hipLaunchKernelGGL((fbk::k_parse_2p<2, 0>), dim3(p2grid), dim3(fbk::kThreads), 0, s, params(r, true, t2)); break;
+                    case 21: hipLaunchKernelGGL((fbk::k_parse_2p<2, fbk::kNoLookback>), dim3(p2grid), dim3(fbk::kThreads), 0, s, params(r, true, t2)); break;
+                    case 11: hipLaunchKernelGGL((fbk::k_parse_block<UB_R, 0>), dim3(tiles), dim3(fbk::kThreads), 0, s, params(r, true)); break;
                     case 6: hipLaunchKernelGGL(k_hdr_loads, dim3((n + 255) / 256), dim3(256), 0, s, bufs[r].fr, bufs[r].off, n, (uint32_t)bytes, sink); break;
                     }
                 }
@@ -182,7 +228,11 @@ int main(int argc, char** argv) {
             }
         }
         for (int v = 0; v < NV; ++v) {
-            if (v >= 4 && bpcu > 1) continue;
+            if (((v >= 4 && v <= 6) || v == 11) && bpcu > 1) continue;
+            if (v >= 7 && v <= 10 && bpcu > cbpc) continue;
+            if (v >= 12 && v <= 15 && bpcu > c1bpc) continue;
+            if (v >= 16 && bpcu > pbpc) continue;
+            if (v <= 3 && bpcu > blimit) continue;
             double us = sum[v] / rounds;
             double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
             printf("{\"variant\": \"%s\", \"blocks_per_cu\": %d, \"grid\": %u, \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n",
@@ -192,7 +242,7 @@ int main(int argc, char** argv) {
     }
     {
         // stamped run (diagnostic build of the same kernel)
-        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(maxb * prop.multiProcessorCount));
+        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(blimit * prop.multiProcessorCount));
         for (int w = 0; w < 5; ++w)
             hipLaunchKernelGGL((fbk::k_parse_block<UB_R, fbk::kStamps>), dim3(grid), dim3(fbk::kThreads), 0, s, params(w % R, true));
         CK(hipStreamSynchronize(s));
@@ -218,7 +268,7 @@ int main(int argc, char** argv) {
         }
     }
     {
-        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(maxb * prop.multiProcessorCount));
+        const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)(blimit * prop.multiProcessorCount));
         hipLaunchKernelGGL((fbk::k_parse_block<UB_R, 0>), dim3(grid), dim3(fbk::kThreads), 0, s, params(0, true));
         CK(hipStreamSynchronize(s));
     }
