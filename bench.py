@@ -28,7 +28,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 WORKLOADS = {
     2: "C2: 1,048,576 x 64-B IPv4/TCP frames per GPU, device-resident (BASELINE configs[1])",
     3: "C3: 1,048,576-frame IMIX 64/576/1500 (7:4:1), IPv4+IPv6, TCP+UDP per GPU, device-resident",
-    4: "C4: 10,485,760-frame IMIX batch per GPU, device-resident",
+    4: "C4: 10,485,760-frame IMIX batch per GPU, device-resident, + session-table upsert with per-flow counters (pool 2^20)",
 }
 
 
@@ -39,7 +39,10 @@ def algorithmic_bytes(offsets, n_session, n_dns):
     return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
 
 
-def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist):
+def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False):
+    """Time `steps` launches of the hot path.  flow=False: fb_parse_classify_dev.  flow=True (C4):
+    fb_process_dev's two stages -- parse + classify, then the session-table upsert with per-flow
+    counters (fb_flow_update_dev) -- with an event between them so each stage is timed."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n)
     nbytes = frames.nbytes
@@ -53,27 +56,43 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
         bufs.append((d_fr, d_off, d_out, d_dns, d_st))
 
-    def step(i):
+    mid = []
+
+    def step(i, ev=None):
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
         rc = lib.fb_parse_classify_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
                                        d_st.ptr, stream.ptr)
+        if rc == 0 and flow:
+            if ev is not None:
+                ev.record(stream)
+            rc = lib.fb_flow_update_dev(ctx, d_out.ptr, d_st.ptr, stream.ptr)
         if rc != 0:
             raise RuntimeError(lib.fb_last_error().decode())
 
+    if flow:
+        N.check(lib.fb_flow_clear(ctx, stream.ptr))
     for i in range(warmup):
         step(i)
     stream.sync()
     st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
     if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
         raise RuntimeError("bad batch stats: %s" % st)
+    if flow and int(st[0]["new_sessions"]) + int(st[0]["updated_sessions"]) != int(st[0]["n_session"]):
+        raise RuntimeError("flow upsert lost records: %s" % st)
     ev0, ev1 = N.Event(), N.Event()
+    evs = [(N.Event(), N.Event(), N.Event()) for _ in range(steps)] if flow else None
     if dist:
         dist.barrier()
     stream.sync()
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(steps):
-        step(i)
+        if flow:
+            evs[i][0].record(stream)
+            step(i, evs[i][1])
+            evs[i][2].record(stream)
+        else:
+            step(i)
     ev1.record(stream)
     stream.sync()
     t1 = time.perf_counter()
@@ -89,11 +108,24 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     algo = algorithmic_bytes(offs, st[0]["n_session"], st[0]["n_dns"])
     # make sure the last step's results are sane too
     st2 = bufs[(steps - 1) % rotate][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
-    assert st2.tobytes() == st.tobytes()
+    stage = None
+    if flow:
+        # after warmup every session exists: the timed steps are all updates
+        same = [k for k in st.dtype.names if k not in ("new_sessions", "updated_sessions")]
+        assert all(int(st2[0][k]) == int(st[0][k]) for k in same), (st, st2)
+        assert int(st2[0]["updated_sessions"]) + int(st2[0]["new_sessions"]) == int(st2[0]["n_session"])
+        parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps
+        flow_ms = sum(b.elapsed_ms(c) for _, b, c in evs) / steps
+        stage = dict(parse_ms=parse_ms, flow_ms=flow_ms)
+        cnt = C.c_uint64()
+        N.check(lib.fb_flow_count(ctx, C.byref(cnt), stream.ptr))
+        stage["flows"] = int(cnt.value)
+    else:
+        assert st2.tobytes() == st.tobytes()
     for b in bufs:
         for x in b:
             x.free()
-    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo,
+    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage,
                 stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
@@ -236,12 +268,19 @@ def main():
 
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
     rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
-    main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist)
+    main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
+                        flow=args.config == 4)
     per_launch_s = main_r["ev_ms"] / 1e3 / args.steps
     achieved = main_r["algo_bytes"] / per_launch_s / 1e9
     value = world * n * args.steps / main_r["elapsed"] / 1e6
 
     extra = {}
+    if main_r["stage"]:
+        sg = main_r["stage"]
+        extra["c4_stages"] = dict(parse_ms=round(sg["parse_ms"], 4), flow_update_ms=round(sg["flow_ms"], 4),
+                                  flows_in_table=sg["flows"],
+                                  parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
+                                  flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
     if not args.no_imix and args.config == 2:
         steps3 = max(args.steps // 2, 10)
         r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist)

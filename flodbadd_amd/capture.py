@@ -154,7 +154,9 @@ class FlodbaddGpuCapture:
                              sd["n_dns"] * N.DNS_OUT_DTYPE.itemsize)[: sd["n_dns"]]
         cls = d_cls.download(np.zeros(max(n, 1), dtype=np.uint8), n)[:n]
         if sd["error"]:
-            raise N.FbError(N.FB_ERR_INTERNAL, "device error word %d" % sd["error"])
+            e = sd["error"]
+            code = N.FB_ERR_TABLE_FULL if e & 4 else N.FB_ERR_INTERNAL
+            raise N.FbError(code, "device error word %d" % e)
         return BatchResult(out, dns, cls, sd)
 
     # ---- session table -----------------------------------------------------------------------

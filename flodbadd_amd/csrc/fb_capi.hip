@@ -65,6 +65,13 @@ struct fb_ctx {
     // flow table
     FlowSlot* d_table = nullptr;
     uint64_t table_cap = 0;
+    uint32_t flow_parts = 0;        // partitions of kFlowSlots slots
+    uint32_t flow_shift = 64;       // 64 - log2(flow_parts)
+    FlowEntry* d_entries = nullptr; // update scratch, flow_recs entries
+    uint32_t* d_rows = nullptr;     // [flow_chunks][flow_parts]
+    uint32_t* d_cols = nullptr;     // [flow_parts][flow_chunks]
+    uint64_t flow_recs = 0;         // scratch capacity (multiple of kFlowChunk)
+    uint32_t last_n = 0;            // packets of the last parse launch (bounds its records)
     unsigned long long* d_partials = nullptr;
     unsigned long long* d_n = nullptr;
     // host-mode staging
@@ -78,7 +85,27 @@ struct fb_ctx {
     fb_batch_stats* s_stats = nullptr;
 };
 
-static constexpr uint32_t kFlowGrid = 1024;
+// Session-table update scratch for batches of up to `recs` records (grown, never shrunk).
+static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
+    if (!c->d_table) return FB_OK;
+    recs = std::max<uint64_t>(recs, kFlowChunk);
+    recs = (recs + kFlowChunk - 1) / kFlowChunk * kFlowChunk;
+    if (recs <= c->flow_recs) return FB_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(c->d_entries);
+    hipFree(c->d_rows);
+    hipFree(c->d_cols);
+    c->d_entries = nullptr;
+    c->d_rows = c->d_cols = nullptr;
+    c->flow_recs = 0;
+    const uint64_t chunks = recs / kFlowChunk;
+    if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
+        hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
+    c->flow_recs = recs;
+    return FB_OK;
+}
 
 static int upload_cfg(fb_ctx* c, hipStream_t s) {
     if (!c->cfg_dirty) return FB_OK;
@@ -188,14 +215,24 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
     }
     ok = ok && hipMalloc(&c->d_cfg, sizeof(DevConfig)) == hipSuccess;
     ok = ok && hipMalloc(&c->d_error, 16) == hipSuccess && hipMemset(c->d_error, 0, 16) == hipSuccess;
-    ok = ok && hipMalloc(&c->d_partials, 2ull * kFlowGrid * 8ull) == hipSuccess;
     ok = ok && hipMalloc(&c->d_n, 16) == hipSuccess;
+    if (ok && cfg->flow_capacity > kFlowMaxCapacity) {
+        set_err(FB_ERR_INVAL, "flow_capacity %llu > %llu slots", (unsigned long long)cfg->flow_capacity,
+                (unsigned long long)kFlowMaxCapacity);
+        ok = false;
+    }
     if (ok && cfg->flow_capacity) {
-        uint64_t cap = 1;
+        uint64_t cap = kFlowSlots;
         while (cap < cfg->flow_capacity) cap <<= 1;
         c->table_cap = cap;
+        c->flow_parts = (uint32_t)(cap / kFlowSlots);
+        uint32_t lg = 0;
+        while ((1u << lg) < c->flow_parts) ++lg;
+        c->flow_shift = 64u - lg;
         ok = hipMalloc(&c->d_table, cap * sizeof(FlowSlot)) == hipSuccess &&
-             hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess;
+             hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess &&
+             hipMalloc(&c->d_partials, 2ull * c->flow_parts * 8ull) == hipSuccess;
+        ok = ok && ensure_flow_scratch(c, cfg->max_batch_packets, nullptr) == FB_OK;
     }
     if (ok) {
         uint64_t tiles = ((uint64_t)cfg->max_batch_packets + kTile - 1) / kTile;
@@ -217,6 +254,9 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_status);
     hipFree(c->d_error);
     hipFree(c->d_table);
+    hipFree(c->d_entries);
+    hipFree(c->d_rows);
+    hipFree(c->d_cols);
     hipFree(c->d_partials);
     hipFree(c->d_n);
     hipFree(c->s_frames);
@@ -265,6 +305,9 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
     if (rc) return rc;
     rc = upload_cfg(c, s);
     if (rc) return rc;
+    rc = ensure_flow_scratch(c, n, s);
+    if (rc) return rc;
+    c->last_n = n;
     p.tagg = c->d_status;
     p.wstat = p.tagg + c->status_tiles;
     p.cfg = c->d_cfg;
@@ -435,16 +478,25 @@ int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_st
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_flow_scratch(c, c->last_n, s);
+    if (rc) return rc;
+    // the records of the context's last parse launch: at most last_n of them
+    const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)c->last_n + kFlowChunk - 1) / kFlowChunk);
     FlowParams p;
     p.recs = d_recs;
     p.stats = d_stats;
     p.table = c->d_table;
-    p.mask = c->table_cap - 1;
+    p.entries = c->d_entries;
+    p.rows = c->d_rows;
+    p.cols = c->d_cols;
     p.partials = c->d_partials;
     p.error = c->d_error + (c->epoch & 1u);
-    p.max_recs = 0xFFFFFFFFu;
-    HIP_TRY(launch_flow_update(p, kFlowGrid, s));
-    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, kFlowGrid, c->d_error + (c->epoch & 1u), s));
+    p.max_recs = (uint32_t)std::min<uint64_t>((uint64_t)chunks * kFlowChunk, c->flow_recs);
+    p.parts = c->flow_parts;
+    p.part_shift = c->flow_shift;
+    p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
+    HIP_TRY(launch_flow_update(p, chunks, s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
     return FB_OK;
 }
 

@@ -5,14 +5,25 @@
 // new SessionInfo with the first packet's counters (src/packets.rs:383-391), and the
 // PACKET_STATS new/updated counters (src/packets.rs:334-347).
 //
-// Table: open addressing, linear probing, 128-B slots (one line: tag + key + 6 u64 counters).
+// Design (owner-computes, no global atomics on the data path).  A per-packet global atomic
+// design is bound by the memory-side atomic rate: 3 counter adds per packet ran at ~17 G
+// atomics/s = 1.73 ms per 10M-record batch on MI355X (profiles/r01_c4_kernel_stats.csv).
+// Instead the table is split into P partitions of kFlowSlots slots (fb_internal.h) and a batch
+// is applied in three launches:
+//   K1 k_flow_bucket    one workgroup per chunk of kFlowChunk records: LDS histogram of the
+//                       records' partitions, exclusive scan, then a counting-sort scatter of
+//                       48-B FlowEntry items into the chunk's region of `entries` (partition-
+//                       major inside the chunk); row b of `rows` = (start, count) per partition.
+//   K1t k_flow_transpose rows[chunk][part] -> cols[part][chunk] (so K2 reads its column
+//                       contiguously).
+//   K2 k_flow_apply     one workgroup per partition: loads the partition's 48-KiB slice into
+//                       LDS, gathers its entries from every chunk, finds/inserts each key in
+//                       the slice and adds the counters with LDS atomics, writes the slice back.
+// Counters are integer sums, so results are bit-exact whatever the order; new_sessions counts
+// the keys inserted (each key is inserted once), updated_sessions the remaining records.
 // The reference hashes Session with SipHash under a random per-process key (dashmap 6.1.0
-// RandomState), so no hash value is a parity target; this table uses fb_flow_hash (below),
-// a deterministic 64-bit mix of the 40-B session_key, identical on host and device.
-// Cross-workgroup visibility (MI355X_MICROARCH.md "Valid forms"): every shared word is read
-// and written with agent-scope atomics (sc1), key words are drained (vmcnt(0)) before the tag
-// that publishes them; counters are device-scope atomic adds (order-independent integer sums,
-// so results are bit-exact whatever the interleaving).
+// RandomState), so no hash value is a parity target; this table uses fb_flow_hash (below), a
+// deterministic 64-bit mix of the 40-B session_key, identical on host and device.
 #include "fb_internal.h"
 
 namespace fbk {
@@ -31,64 +42,30 @@ __host__ __device__ inline unsigned long long flow_hash_words(const uint32_t k[1
     return h;
 }
 
-__device__ __forceinline__ unsigned long long ald(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ast(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint32_t part_of(unsigned long long h, uint32_t shift) {
+    return shift >= 64u ? 0u : (uint32_t)(h >> shift);
 }
 
-// Find-or-insert `key` (10 words).  Returns the slot or nullptr (table full / spin expired).
-__device__ __forceinline__ FlowSlot* upsert(FlowSlot* table, unsigned long long mask,
-                                            const uint32_t key[10], bool& inserted, uint32_t* err) {
-    const unsigned long long h = flow_hash_words(key);
-    const unsigned long long want = h | 2ull;  // 0 = empty, 1 = being inserted
-    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
-    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
-    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
-    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
-    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
-    unsigned long long idx = h & mask;
-    inserted = false;
-    for (unsigned long long probe = 0; probe <= mask; ++probe) {
-        FlowSlot* s = table + idx;
-        unsigned long long* kp = reinterpret_cast<unsigned long long*>(s->key);
-        unsigned long long t = ald(&s->tag);
-        if (t == 0ull) {
-            const unsigned long long old = atomicCAS(&s->tag, 0ull, 1ull);
-            if (old == 0ull) {
-                ast(kp + 0, kw0);
-                ast(kp + 1, kw1);
-                ast(kp + 2, kw2);
-                ast(kp + 3, kw3);
-                ast(kp + 4, kw4);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                ast(&s->tag, want);
-                inserted = true;
-                return s;
-            }
-            t = old;
-        }
-        uint32_t spins = 0u;
-        while (t == 1ull) {  // another lane is publishing this slot's key
-            __builtin_amdgcn_s_sleep(1);
-            t = ald(&s->tag);
-            if (++spins > (1u << 24)) { atomicOr(err, 2u); return nullptr; }
-        }
-        if (t == want && ald(kp + 0) == kw0 && ald(kp + 1) == kw1 && ald(kp + 2) == kw2 &&
-            ald(kp + 3) == kw3 && ald(kp + 4) == kw4)
-            return s;
-        idx = (idx + 1ull) & mask;
+// Inclusive wave scan + block exclusive scan of one u32 per thread (blockDim multiple of 64).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
     }
-    atomicOr(err, 4u);  // table full
-    return nullptr;
-}
-
-__device__ __forceinline__ void count_packet(FlowSlot* s, uint32_t plen, uint32_t iplen, bool orig) {
-    // originator -> outbound_bytes/orig_pkts/orig_ip_bytes, else inbound/resp (packets.rs:111-120)
-    atomicAdd(&s->cnt[orig ? 0 : 1], (unsigned long long)plen);
-    atomicAdd(&s->cnt[orig ? 2 : 3], 1ull);
-    atomicAdd(&s->cnt[orig ? 4 : 5], (unsigned long long)iplen);
+    if (lane == 63u) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0u, tot = 0u;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t s = wsum[w];
+        before += w < wave ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return before + x - v;
 }
 
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* sh) {
@@ -103,32 +80,214 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
     return t;
 }
 
-__global__ __launch_bounds__(256) void k_flow_update(const FlowParams P) {
-    __shared__ unsigned long long sh[4];
+__device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
     const unsigned long long n = P.stats->n_session;  // written by the parse kernel
-    const uint32_t lim = (uint32_t)min(n, (unsigned long long)P.max_recs);
-    unsigned long long n_new = 0ull, n_upd = 0ull;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
-        const uint32_t* r = reinterpret_cast<const uint32_t*>(P.recs + i);
+    return (uint32_t)min(n, (unsigned long long)P.max_recs);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1: bucket one chunk of records by partition (counting sort in LDS).
+__global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams P) {
+    extern __shared__ uint32_t hist[];  // [P.parts]
+    __shared__ uint32_t wsum[kFlowK1Threads / 64];
+    const uint32_t n = batch_records(P);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && P.stats->n_session > (unsigned long long)P.max_recs)
+        atomicOr(P.error, 8u);  // more records than the update scratch holds: the rest is dropped
+    const uint32_t base = blockIdx.x * kFlowChunk;
+    if (base >= n) return;
+    const uint32_t cnt = min(kFlowChunk, n - base);
+    const fb_pkt_out* R = P.recs + base;
+    for (uint32_t j = threadIdx.x; j < P.parts; j += kFlowK1Threads) hist[j] = 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
         const uint4 a = *reinterpret_cast<const uint4*>(r);
         const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
         const uint2 c = *reinterpret_cast<const uint2*>(r + 8);
-        const uint2 d = *reinterpret_cast<const uint2*>(r + 10);
+        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+        atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of hist[0..parts): each thread owns E consecutive partitions
+    const uint32_t E = (P.parts + kFlowK1Threads - 1u) / kFlowK1Threads;
+    const uint32_t j0 = threadIdx.x * E;
+    uint32_t local = 0u;
+    for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) local += hist[j];
+    uint32_t total;
+    uint32_t run = block_excl_scan(local, wsum, total);
+    uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
+    for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
+        const uint32_t c = hist[j];
+        row[j] = run | (c << 16);
+        hist[j] = run;  // becomes the scatter cursor
+        run += c;
+    }
+    __syncthreads();
+    FlowEntry* out = P.entries + base;
+    for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
+        const uint4 a = *reinterpret_cast<const uint4*>(r);
+        const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
+        const uint4 c = *reinterpret_cast<const uint4*>(r + 8);  // key 8,9 | packet_length | ip_packet_length
         const uint32_t m = r[12];
-        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y};
-        bool ins;
-        FlowSlot* s = upsert(P.table, P.mask, key, ins, P.error);
-        if (s) {
-            count_packet(s, d.x, d.y, (m >> 8) & FB_META_ORIGINATOR);
-            n_new += ins;
-            n_upd += !ins;
+        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+        const uint32_t d = atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+        const uint32_t orig = ((m >> 8) & FB_META_ORIGINATOR) ? 1u : 0u;
+        uint4* e = reinterpret_cast<uint4*>(out + d);
+        e[0] = a;
+        e[1] = b;
+        e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1t: rows[chunk][part] -> cols[part][chunk_stride]
+__global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint32_t chunks) {
+    __shared__ uint32_t tile[64][65];
+    const uint32_t p0 = blockIdx.x * 64u, c0 = blockIdx.y * 64u;
+    const uint32_t tx = threadIdx.x & 63u, ty = threadIdx.x >> 6;
+    for (uint32_t y = ty; y < 64u; y += 4u) {
+        const uint32_t c = c0 + y, p = p0 + tx;
+        tile[y][tx] = (c < chunks && p < P.parts) ? P.rows[(size_t)c * P.parts + p] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t y = ty; y < 64u; y += 4u) {
+        const uint32_t p = p0 + y, c = c0 + tx;
+        if (p < P.parts && c < chunks) P.cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: apply one partition's entries to its LDS-resident slice.
+constexpr uint32_t kSlotWords = sizeof(FlowSlot) / 8;  // 12 u64 words per slot
+
+__device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
+__device__ __forceinline__ int apply_entry(unsigned long long* slice, const uint4 e0, const uint4 e1,
+                                           const uint4 e2, uint32_t* err) {
+    const uint32_t orig = (e2.y >> 16) & 1u;
+    const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
+    const unsigned long long h = flow_hash_words(key);
+    const unsigned long long want = h | 2ull;
+    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
+    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
+    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
+    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
+    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
+    uint32_t i = (uint32_t)h & (kFlowSlots - 1u);
+    int result = -1;
+    unsigned long long* s = nullptr;
+    for (uint32_t probe = 0; probe < kFlowSlots; ++probe) {
+        s = slice + (size_t)i * kSlotWords;
+        unsigned long long t = lds_ld(s);
+        if (t == 0ull) {
+            const unsigned long long old = atomicCAS(s, 0ull, 1ull);
+            if (old == 0ull) {
+                s[1] = kw0;
+                s[2] = kw1;
+                s[3] = kw2;
+                s[4] = kw3;
+                s[5] = kw4;
+                __hip_atomic_store(s, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                result = 1;
+                break;
+            }
+            t = old;
         }
+        uint32_t spins = 0u;
+        while (t == 1ull) {  // another lane of this workgroup is publishing the slot's key
+            __builtin_amdgcn_s_sleep(1);
+            t = lds_ld(s);
+            if (++spins > (1u << 22)) { atomicOr(err, 2u); return -1; }
+        }
+        if (t == want && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) {
+            result = 0;
+            break;
+        }
+        i = (i + 1u) & (kFlowSlots - 1u);
+    }
+    if (result < 0) {
+        atomicOr(err, 4u);  // partition full
+        return -1;
+    }
+    // originator -> outbound_bytes/orig_pkts/orig_ip_bytes, else inbound/resp (packets.rs:111-120)
+    atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
+    atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
+    atomicAdd(s + 10 + (orig ? 0 : 1), (unsigned long long)e2.w);
+    return result;
+}
+
+__global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams P) {
+    extern __shared__ uint4 slice4[];  // kFlowSlots * 96 B
+    __shared__ uint32_t sp[kFlowK2Threads];
+    __shared__ uint32_t ss[kFlowK2Threads];
+    __shared__ uint32_t wsum[kFlowK2Threads / 64];
+    __shared__ unsigned long long sh[kFlowK2Threads / 64];
+    unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
+    const uint32_t part = blockIdx.x;
+    const uint32_t n = batch_records(P);
+    const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
+    const uint32_t* col = P.cols + (size_t)part * P.chunk_stride;
+
+    uint32_t mine = 0u;
+    for (uint32_t b = threadIdx.x; b < chunks; b += kFlowK2Threads) mine += col[b] >> 16;
+    const unsigned long long total = block_sum(mine, sh);
+    unsigned long long n_new = 0ull, n_upd = 0ull;
+    if (total != 0ull) {
+        constexpr uint32_t kSlice16 = kFlowSlots * sizeof(FlowSlot) / 16u;
+        const uint4* g = reinterpret_cast<const uint4*>(P.table + (size_t)part * kFlowSlots);
+        for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) slice4[j] = g[j];
+        __syncthreads();
+        const uint4* E = reinterpret_cast<const uint4*>(P.entries);
+        for (uint32_t g0 = 0; g0 < chunks; g0 += kFlowK2Threads) {
+            const uint32_t b = g0 + threadIdx.x;
+            const uint32_t v = b < chunks ? col[b] : 0u;
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan(v >> 16, wsum, tot);
+            sp[threadIdx.x] = pre;
+            ss[threadIdx.x] = b * kFlowChunk + (v & 0xFFFFu);
+            __syncthreads();
+            for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 4u * kFlowK2Threads) {
+                uint4 q[4][3];
+                uint32_t ne = 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; ++u) {
+                    const uint32_t e = e0 + u * kFlowK2Threads;
+                    if (e < tot) {
+                        uint32_t lo = 0u, hi = kFlowK2Threads - 1u;  // largest j with sp[j] <= e
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi + 1u) >> 1;
+                            if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
+                        }
+                        const size_t idx = (size_t)ss[lo] + (e - sp[lo]);
+                        q[u][0] = E[idx * 3u];
+                        q[u][1] = E[idx * 3u + 1u];
+                        q[u][2] = E[idx * 3u + 2u];
+                        ne = u + 1u;
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; ++u) {
+                    if (u < ne) {
+                        const int r = apply_entry(slice, q[u][0], q[u][1], q[u][2], P.error);
+                        n_new += r == 1;
+                        n_upd += r == 0;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        uint4* gw = reinterpret_cast<uint4*>(P.table + (size_t)part * kFlowSlots);
+        for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) gw[j] = slice4[j];
     }
     n_new = block_sum(n_new, sh);
     n_upd = block_sum(n_upd, sh);
     if (threadIdx.x == 0) {
-        P.partials[2 * blockIdx.x] = n_new;
-        P.partials[2 * blockIdx.x + 1] = n_upd;
+        P.partials[2 * part] = n_new;
+        P.partials[2 * part + 1] = n_upd;
     }
 }
 
@@ -195,8 +354,16 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
     if (threadIdx.x == 0 && c) atomicAdd(d_n, c);
 }
 
-hipError_t launch_flow_update(const FlowParams& p, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_flow_update, dim3(grid), dim3(256), 0, s, p);
+hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s) {
+    if (chunks == 0u) chunks = 1u;
+    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), p.parts * sizeof(uint32_t), s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_flow_transpose, dim3((p.parts + 63u) / 64u, (chunks + 63u) / 64u), dim3(256), 0, s, p,
+                       chunks);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_flow_apply, dim3(p.parts), dim3(kFlowK2Threads), kFlowSlots * sizeof(FlowSlot), s, p);
     return hipGetLastError();
 }
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials, uint32_t nblk,
@@ -226,5 +393,6 @@ hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap, unsi
 extern "C" uint64_t fb_flow_hash(const fb_session_key* key) {
     uint32_t w[10];
     __builtin_memcpy(w, key, 40);
+    w[9] &= 0xFFFFu;  // the key's padding is not part of the key
     return fbk::flow_hash_words(w);
 }

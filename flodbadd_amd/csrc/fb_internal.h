@@ -80,32 +80,55 @@ struct ParseParams {
     unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
 };
 
-// Flow table: 128-byte slots (one L2 line).  tag: 0 empty, 1 being inserted, else
-// (hash | 2).  Key words 8..47, counters 48..95 (fb_flow_rec order).
+// Flow (session) table, partitioned for owner-computes updates (fb_flow.hip):
+//   capacity = P partitions x kFlowSlots slots; a key's partition is the top log2(P) bits of its
+//   64-bit hash, its home slot inside the partition the low bits (linear probing wraps inside
+//   the partition).  One workgroup owns one partition per batch and updates it in LDS, so the
+//   upsert needs no global atomics.
+//   Slot (96 B): tag (0 empty, 1 being inserted [LDS only], else hash | 2), 40-B key,
+//   6 counters in fb_flow_rec order.
+constexpr uint32_t kFlowSlots = 512;             // slots per partition: 48 KiB LDS slice
+constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
+constexpr uint32_t kFlowChunk = 16384;           // records per bucketing workgroup (K1)
+constexpr uint32_t kFlowK1Threads = 1024;
+constexpr uint32_t kFlowK2Threads = 256;
+constexpr uint64_t kFlowMaxCapacity = (uint64_t)kFlowSlots * kFlowMaxParts;
 struct FlowSlot {
     unsigned long long tag;
     uint32_t key[10];
     unsigned long long cnt[6];  // outbound_bytes, inbound_bytes, orig_pkts, resp_pkts,
                                 // orig_ip_bytes, resp_ip_bytes
-    unsigned long long pad[4];
 };
-static_assert(sizeof(FlowSlot) == 128, "flow slot must be one 128-B line");
+static_assert(sizeof(FlowSlot) == 96, "flow slot is 96 B");
+// Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
+// word 9 (the key's padding), L4 payload bytes, IP bytes.
+struct FlowEntry {
+    uint32_t key[10];
+    uint32_t packet_length;
+    uint32_t ip_packet_length;
+};
+static_assert(sizeof(FlowEntry) == 48, "flow entry is 48 B");
 
 struct FlowParams {
     const fb_pkt_out* recs;
-    fb_batch_stats* stats;  // n_session read from here; new/updated accumulated
+    fb_batch_stats* stats;      // n_session read from here; new/updated accumulated
     FlowSlot* table;
-    unsigned long long mask;  // capacity - 1
-    unsigned long long* partials;  // 2 per block: new, updated
+    FlowEntry* entries;         // [max_recs]
+    uint32_t* rows;             // [chunks][parts]  start | count << 16, per bucketing chunk
+    uint32_t* cols;             // [parts][chunk_stride] the same, transposed
+    unsigned long long* partials;  // 2 per partition: new, updated
     uint32_t* error;
-    uint32_t max_recs;
+    uint32_t max_recs;          // scratch capacity in records
+    uint32_t parts;             // P (power of two)
+    uint32_t part_shift;        // 64 - log2(P) (64 when P == 1)
+    uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
 };
 
 // Launchers (fb_parse.hip / fb_flow.hip).
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse(int* blocks_per_cu);
-hipError_t launch_flow_update(const FlowParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,

@@ -153,7 +153,9 @@ typedef struct fb_batch_stats {
     uint64_t n_drop;           /* parse_packet_pcap -> None                                   */
     uint64_t n_filtered;       /* rejected by the session filter                              */
     uint64_t bad_offsets;      /* frames with invalid offsets (counted in n_drop too)         */
-    uint64_t error;            /* nonzero: kernel protocol failure (see FB_ERR_INTERNAL)      */
+    uint64_t error;            /* nonzero = failure bits: 1|2 bounded spin expired (FB_ERR_INTERNAL),
+                                  4 flow-table partition full (FB_ERR_TABLE_FULL), 8 more records
+                                  than the update scratch of the last parse launch holds     */
     uint64_t reserved[3];
 } fb_batch_stats; /* 128 bytes */
 
@@ -180,7 +182,10 @@ typedef struct fb_config {
     uint32_t n_lan_v6;             /* <= FB_MAX_LAN_V6                                        */
     uint32_t n_own_ips;            /* <= FB_MAX_OWN_IPS                                       */
     const fb_ip* own_ips;          /* may be NULL when n_own_ips == 0                         */
-    uint64_t flow_capacity;        /* flow-table slots (rounded up to a power of two, 0 = none)*/
+    uint64_t flow_capacity;        /* flow-table slots: rounded up to a power of two >= 512,
+                                      at most 2^22; 0 = no table. Stored as partitions of 512
+                                      slots chosen by the key hash: a partition fills (error
+                                      bit 4) when more than 512 of its keys exist            */
     uint32_t max_batch_packets;    /* host-mode staging capacity (packets per call)           */
     uint32_t reserved0;
     uint64_t max_batch_bytes;      /* host-mode staging capacity (frame bytes per call)       */
@@ -261,8 +266,8 @@ int fb_process_parsed_dev(fb_ctx* ctx, const fb_parsed_pkt* d_in, uint32_t n, fb
 int fb_process_parsed(fb_ctx* ctx, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out* out,
                       uint32_t* n_out, uint8_t* cls, fb_batch_stats* stats, void* stream);
 
-/* Fused device-resident parse + classify + flow upsert (no record round trip through HBM).
- * Same outputs as fb_parse_classify_dev (d_out may be NULL) followed by fb_flow_update_dev. */
+/* Device-resident parse + classify + flow upsert: fb_parse_classify_dev followed by
+ * fb_flow_update_dev on the same stream (d_out is required: the update reads the records). */
 int fb_process_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                    const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns,
                    uint8_t* d_class, fb_batch_stats* d_stats, void* stream);

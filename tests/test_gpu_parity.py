@@ -92,6 +92,51 @@ def test_flow_table_vs_oracle(gpu_capture):
     assert gpu_capture.flow_count() == 0
 
 
+def _flows_vs_oracle(cap, batches):
+    cap.clear_all_sessions()
+    flows = coracle.Flows()
+    for frames, offs in batches:
+        g = cap.process_frames(frames, offs)
+        r_st = np.zeros(1, dtype=N.STATS_DTYPE)
+        flows.update(g.records, r_st)  # records are checked against the oracle elsewhere
+        assert g.stats["new_sessions"] == int(r_st[0]["new_sessions"])
+        assert g.stats["updated_sessions"] == int(r_st[0]["updated_sessions"])
+        assert g.stats["error"] == 0
+    gflows = cap.export_flows()
+    rflows = flows.export_sorted()
+    assert len(gflows) == len(rflows)
+    assert rows_sorted(gflows) == rows_sorted(rflows)
+
+
+def test_flow_table_zipf_many_chunks(gpu_capture):
+    """One 600k-record batch (37 bucketing chunks) with Zipf(1.1) flow popularity: hot flows put
+    thousands of records into one partition; counters must still be exact."""
+    _flows_vs_oracle(gpu_capture, [synth.generate(4, 600000, first=0, zipf=1, zipf_s=1.1),
+                                   synth.generate(4, 100000, first=600000, zipf=1, zipf_s=1.1)])
+
+
+def test_flow_table_single_flow_batch(gpu_capture):
+    """Every record of the batch on ONE flow (one partition, one slot, all LDS adds collide)."""
+    buf, offs = fg.pack([fg.tcp_frame("10.0.0.1", 40000, "8.8.8.8", 443, fg.ACK, 100)] * 50000 +
+                        [fg.tcp_frame("8.8.8.8", 443, "10.0.0.1", 40000, fg.ACK, 7)] * 30000)
+    _flows_vs_oracle(gpu_capture, [(buf, offs), (buf, offs)])
+
+
+def test_flow_table_small_capacity_and_full():
+    """flow_capacity 512 = one partition: 300 flows fit; 600 distinct flows report TABLE_FULL."""
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.sessions import SessionFilter
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512)
+    try:
+        mk = lambda k: fg.tcp_frame("10.1.%d.%d" % (k >> 8, k & 255), 40000, "8.8.8.8", 443, fg.ACK, 10)
+        _flows_vs_oracle(cap, [fg.pack([mk(k) for k in range(300)] * 3)])
+        with pytest.raises(N.FbError) as ei:
+            cap.process_frames(*fg.pack([mk(k) for k in range(600)]))
+        assert ei.value.code == N.FB_ERR_TABLE_FULL
+    finally:
+        cap.close()
+
+
 def rows_sorted(arr):
     """Order-independent view of a record array: its rows as sorted byte strings."""
     b = arr.tobytes()
