@@ -195,7 +195,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         // 106-SGPR worst case, 24 per CU.  The kernel needs every block resident (look-back).
         int bpc = 0;
         if (occupancy_parse(&bpc) != hipSuccess || bpc < 1) bpc = 1;
-        int use = std::min(bpc, std::max(1, 24 / (kThreads / 64)));
+        int use = std::min(bpc, std::max(1, 24 / (int)parse_block_waves()));
         if (const char* e = getenv("FB_BLOCKS_PER_CU")) {
             const int want = atoi(e);
             if (want >= 1 && want < use) use = want;
@@ -235,7 +235,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         ok = ok && ensure_flow_scratch(c, cfg->max_batch_packets, nullptr) == FB_OK;
     }
     if (ok) {
-        uint64_t tiles = ((uint64_t)cfg->max_batch_packets + kTile - 1) / kTile;
+        uint64_t tiles = ((uint64_t)cfg->max_batch_packets + parse_unit_frames() - 1) / parse_unit_frames();
         ok = ensure_status(c, tiles, nullptr) == FB_OK && upload_cfg(c, nullptr) == FB_OK;
     }
     if (!ok) {
@@ -300,7 +300,7 @@ int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
 
 // Shared launch of the parse/classify kernel (frames) or its parsed-packet instantiation.
 static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipStream_t s) {
-    const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
+    const uint64_t tiles = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
     int rc = ensure_status(c, tiles, s);
     if (rc) return rc;
     rc = upload_cfg(c, s);
@@ -310,6 +310,7 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
     c->last_n = n;
     p.tagg = c->d_status;
     p.wstat = p.tagg + c->status_tiles;
+    p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
     p.cfg = c->d_cfg;
     p.n = n;
     p.num_tiles = (uint32_t)tiles;

@@ -8,30 +8,6 @@
 
 namespace fbk {
 
-// Parse kernel (fb_parse.hip): a look-back unit = one block-round = kThreads/64 waves x
-// kUnitTiles wave-tiles x 64 frames (one lane per frame per wave-tile).
-#ifndef FB_BLOCK_THREADS
-#define FB_BLOCK_THREADS 512
-#endif
-constexpr int kThreads = FB_BLOCK_THREADS;
-#ifndef FB_UNIT_TILES
-#define FB_UNIT_TILES 2
-#endif
-constexpr int kUnitTiles = FB_UNIT_TILES;
-constexpr int kTile = (kThreads / 64) * 64 * kUnitTiles;  // frames per look-back unit
-
-// k_parse_ctl: kCtlFW frame waves + 1 control wave per block; kCtlU wave-tiles per frame wave.
-#ifndef FB_CTL_FW
-#define FB_CTL_FW 7
-#endif
-#ifndef FB_CTL_U
-#define FB_CTL_U 2
-#endif
-constexpr int kCtlFW = FB_CTL_FW;
-constexpr int kCtlU = FB_CTL_U;
-constexpr int kCtlThreads = 64 * (kCtlFW + 1);
-constexpr int kCtlTile = kCtlFW * 64 * kCtlU;  // frames per unit of k_parse_ctl
-
 // Upper bound on parse blocks per launch (per-block stats slots).
 constexpr uint32_t kMaxBlocks = 4096;
 
@@ -43,22 +19,26 @@ constexpr uint32_t kMaxBlocks = 4096;
 constexpr uint32_t kMaxEpoch = 255;
 // Stats slots: one pair per block, and a grid never exceeds max(kMaxBlocks, units).
 inline uint64_t stat_slots(uint64_t units) { return units > kMaxBlocks ? units : kMaxBlocks; }
-inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units); }
+//   rsum[units]           per-round sums of unit aggregates (round r = units [r*G, (r+1)*G))  [epoch:8 | 0 | n_dns:27 | n_session:28]
+inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + units; }
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
     uint32_t net[4];
     uint32_t mask[4];
 };
+// The parse kernel copies the first kCfgLdsBytes (header + service bitmap) into LDS; the
+// tables behind them are read from global memory by uniform loops (only when non-empty).
 struct DevConfig {
-    uint32_t service_bitmap[FB_SERVICE_BITMAP_BYTES / 4];  // bit p <=> name(p) != ""
     uint32_t filter;
     uint32_t n_lan_v6;
     uint32_t n_own;
     uint32_t pad;
+    uint32_t service_bitmap[FB_SERVICE_BITMAP_BYTES / 4];  // bit p <=> name(p) != ""
     LanV6 lan_v6[FB_MAX_LAN_V6];
     fb_ip own[FB_MAX_OWN_IPS];
 };
+constexpr uint32_t kCfgLdsBytes = 16u + FB_SERVICE_BITMAP_BYTES;
 
 struct ParseParams {
     const fb_parsed_pkt* parsed;  // parsed-packet path (fb_process_parsed*) instead of frames
@@ -70,6 +50,7 @@ struct ParseParams {
     fb_batch_stats* stats;
     unsigned long long* tagg;   // [units]
     unsigned long long* wstat;  // [kMaxBlocks][2]
+    unsigned long long* rsum;   // [rounds] round sums (k_parse_ws look-back)
     const DevConfig* cfg;
     uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
     uint32_t n;
@@ -128,6 +109,8 @@ struct FlowParams {
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse(int* blocks_per_cu);
+uint32_t parse_unit_frames();  // frames per look-back unit of the product parse kernel
+uint32_t parse_block_waves();  // waves per block of the product parse kernel
 hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);

@@ -52,7 +52,7 @@ __device__ __forceinline__ bool lan_v4(uint32_t v) {
     return v == 0u || v == 0xffffffffu || a == 127u || (v >> 28) == 0xEu || (v >> 16) == 0xA9FEu ||
            a == 10u || (a == 172u && b >= 16u && b <= 31u) || (v >> 16) == 0xC0A8u;
 }
-__device__ __forceinline__ bool lan_v6(const DevConfig* c, const uint32_t w[4]) {
+__device__ __forceinline__ bool lan_v6(const DevConfig* c, const DevConfig* g, const uint32_t w[4]) {
     uint32_t s0 = w[0] >> 16;
     if ((w[0] | w[1] | w[2] | w[3]) == 0u) return true;                       // ::
     if ((w[0] | w[1] | w[2]) == 0u && w[3] == 1u) return true;                // ::1
@@ -60,18 +60,18 @@ __device__ __forceinline__ bool lan_v6(const DevConfig* c, const uint32_t w[4]) 
         return true;                                                          // fe80::/10 ff00::/8 fc00::/7
     const uint32_t nl = c->n_lan_v6;                                          // uniform loop
     for (uint32_t i = 0; i < nl; ++i) {
-        const LanV6& e = c->lan_v6[i];
+        const LanV6& e = g->lan_v6[i];
         if ((w[0] & e.mask[0]) == e.net[0] && (w[1] & e.mask[1]) == e.net[1] &&
             (w[2] & e.mask[2]) == e.net[2] && (w[3] & e.mask[3]) == e.net[3])
             return true;
     }
     return false;
 }
-__device__ __forceinline__ bool own_ip(const DevConfig* c, uint32_t fam, const uint32_t w[4]) {
+__device__ __forceinline__ bool own_ip(const DevConfig* c, const DevConfig* g, uint32_t fam, const uint32_t w[4]) {
     const uint32_t no = c->n_own;
     bool hit = false;
     for (uint32_t i = 0; i < no; ++i) {
-        const fb_ip& o = c->own[i];
+        const fb_ip& o = g->own[i];
         hit |= o.family == fam && o.addr[0] == w[0] && o.addr[1] == w[1] && o.addr[2] == w[2] &&
                o.addr[3] == w[3];
     }
@@ -107,10 +107,11 @@ struct Pkt {
 // (raw 5-tuple src/dst/ports as parsed, L4 payload length, IP length, TCP flags if any) ->
 // canonical session key, originator, local/global filter, history char; k.cls = SESSION or
 // FILTERED.  Shared by the frame path (process_frame) and the parsed-packet path.
-__device__ __forceinline__ void classify_session(const DevConfig* cfg, const uint32_t* bm, uint32_t proto,
+__device__ __forceinline__ void classify_session(const DevConfig* cfg, const DevConfig* gcfg, uint32_t proto,
                                                  uint32_t fam, const uint32_t (&src)[4], const uint32_t (&dst)[4],
                                                  uint32_t sport, uint32_t dport, uint32_t hasf, uint32_t flags,
                                                  uint32_t plen, uint32_t iplen, uint32_t idx, Pkt& k) {
+    const uint32_t* bm = cfg->service_bitmap;
     k.tcp = proto == 6u;
     k.v4 = fam == 2u;
     const uint32_t S = svc(bm, sport), Dsv = svc(bm, dport);
@@ -136,16 +137,16 @@ __device__ __forceinline__ void classify_session(const DevConfig* cfg, const uin
         kd[j] = swap ? src[j] : dst[j];
     }
     const uint32_t kport_s = swap ? dport : sport, kport_d = swap ? sport : dport;
-    const bool lan_s = fam == 2u ? lan_v4(ks[0]) : lan_v6(cfg, ks);
-    const bool lan_d = fam == 2u ? lan_v4(kd[0]) : lan_v6(cfg, kd);
+    const bool lan_s = fam == 2u ? lan_v4(ks[0]) : lan_v6(cfg, gcfg, ks);
+    const bool lan_d = fam == 2u ? lan_v4(kd[0]) : lan_v6(cfg, gcfg, kd);
     uint32_t meta = hasf;
     meta |= swap ? FB_META_SWAP : 0u;
     meta |= orig ? FB_META_ORIGINATOR : 0u;
     meta |= lan_s ? FB_META_LOCAL_SRC : 0u;
     meta |= lan_d ? FB_META_LOCAL_DST : 0u;
-    meta |= own_ip(cfg, fam, ks) ? FB_META_SELF_SRC : 0u;
-    meta |= own_ip(cfg, fam, kd) ? FB_META_SELF_DST : 0u;
-    meta |= svc(bm, kport_d) ? FB_META_DST_SERVICE : 0u;
+    meta |= own_ip(cfg, gcfg, fam, ks) ? FB_META_SELF_SRC : 0u;
+    meta |= own_ip(cfg, gcfg, fam, kd) ? FB_META_SELF_DST : 0u;
+    meta |= (swap ? S : Dsv) ? FB_META_DST_SERVICE : 0u;  // service(key dst port)
     const uint32_t hc = hasf ? hist_char(flags, plen, orig) : 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -167,7 +168,7 @@ __device__ __forceinline__ void classify_session(const DevConfig* cfg, const uin
 // Decode + classify one frame from its header vectors; a field is only used when the pnet
 // length rules guarantee it lies inside the frame's caplen.
 __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const DevConfig* cfg,
-                                              const uint32_t* bm, const Hdr& h, uint32_t o0, uint32_t o1,
+                                              const DevConfig* gcfg, const Hdr& h, uint32_t o0, uint32_t o1,
                                               uint32_t fbytes, uint32_t idx, Pkt& k) {
     k.cls = FB_CLASS_DROP;
     k.tcp = false;
@@ -253,7 +254,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
         return;
     }
 
-    classify_session(cfg, bm, proto, fam, src, dst, sport, dport, hasf, flags, plen, iplen, idx, k);
+    classify_session(cfg, gcfg, proto, fam, src, dst, sport, dport, hasf, flags, plen, iplen, idx, k);
 }
 
 __device__ __forceinline__ fb_dns_out make_fb_dns(const Pkt& k) {
@@ -282,22 +283,12 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-// Ablation switches (tools/ubench_parse.hip); the product instantiates kFlagsProduct.
+// Ablation switches (tools/ubench_ws.hip); the product instantiates kFlagsProduct.
 constexpr uint32_t kFlagsProduct = 0u;
 constexpr uint32_t kNoLookback = 1u;  // base offsets = tile start (wrong output, timing only)
 constexpr uint32_t kNoStore = 2u;     // no record / dns stores (timing only)
-constexpr uint32_t kStamps = 4u;      // per-tile s_memrealtime stamps + poll counts into P.dbg
-// dbg layout per tile t: [0] classified, [1] look-back issued, [2] look-back done, [3] spins
+constexpr uint32_t kStamps = 4u;      // per-unit s_memrealtime stamps into P.dbg
 
-// ---- look-back ----------------------------------------------------------------------------
-// One status word per unit, epoch-tagged: [epoch:8 | INC:1 | n_dns:27 | n_session:28].
-//   published twice by the unit's look-back wave with plain sc1 stores (no atomics, no shared
-//   accumulator line that every block hammers): AGG (its own count) right after classification,
-//   INC (its inclusive prefix) once its look-back is done.
-// Look-back of unit u: read predecessors u-1, u-2, ... in windows of 256 (4 words per lane, one
-// memory round trip), stop at the nearest INC; every word up to it must be published (AGG or
-// INC of this epoch).  Not-ready words are re-polled by their lanes together with exponential
-// back-off, so a wait costs one round trip per readiness event, not one per word.
 constexpr unsigned long long kIncBit = 1ull << 55;
 constexpr unsigned long long kCnt28 = (1ull << 28) - 1ull;
 __device__ __forceinline__ unsigned long long st_counts(unsigned long long w) {
@@ -306,67 +297,6 @@ __device__ __forceinline__ unsigned long long st_counts(unsigned long long w) {
 __device__ __forceinline__ unsigned long long st_pack(uint32_t ep, bool inc, unsigned long long c) {
     return ((unsigned long long)ep << 56) | (inc ? kIncBit : 0ull) | (c & kCnt28) |
            (((c >> 28) & ((1ull << 27) - 1ull)) << 28);
-}
-
-template <uint32_t FLAGS, int NW = 4>
-__device__ unsigned long long lookback_unit(const ParseParams& P, uint32_t u, uint32_t& spins) {
-    constexpr int WIN = 64 * NW;  // predecessors probed per round trip
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t ep = P.epoch;
-    // sc1 buffer loads (aux 16): L1-bypassing like the agent-scope atomic loads, 32-bit offsets,
-    // and out-of-range offsets (negative indices) read as 0 = "not published".
-    const __amdgpu_buffer_rsrc_t rt =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.tagg, (short)0, (int)(u * 8u), 0x00020000);
-    auto word = [&](int idx) {
-        const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rt, (uint32_t)idx * 8u, 0, 16);
-        return (unsigned long long)x.x | ((unsigned long long)x.y << 32);
-    };
-    unsigned long long pre = 0ull;
-    int lo = (int)u - WIN;  // window = [lo, lo + WIN), lane l of chunk k reads lo + 64k + l
-    spins = 0u;
-    for (;;) {
-        unsigned long long v[NW];
-#pragma unroll
-        for (int k = 0; k < NW; ++k) v[k] = word(lo + 64 * k + (int)lane);
-        for (;;) {
-            // nearest published inclusive prefix = the highest index carrying INC
-            int near = -1;
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                const int idx = lo + 64 * k + (int)lane;
-                const unsigned long long im = __ballot(idx >= 0 && tag_of(v[k]) == ep && (v[k] & kIncBit));
-                if (im) near = lo + 64 * k + (63 - __clzll((long long)im));
-            }
-            const int floor_idx = near >= 0 ? near : (lo > 0 ? lo : 0);  // words below are not needed
-            bool ready = true;
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                const int idx = lo + 64 * k + (int)lane;
-                ready &= idx < floor_idx || tag_of(v[k]) == ep;
-            }
-            if (__ballot(!ready) == 0ull) {
-                unsigned long long sum = 0ull;
-#pragma unroll
-                for (int k = 0; k < NW; ++k) {
-                    const int idx = lo + 64 * k + (int)lane;
-                    sum += idx >= floor_idx ? st_counts(v[k]) : 0ull;
-                }
-                pre += wave_sum64(sum);
-                if (near >= 0 || lo <= 0) return pre;
-                break;
-            }
-            if (++spins > (1u << 16)) { if (lane == 0u) atomicOr(P.error, 1u); return pre; }
-            // exponential back-off: every poll is a memory-side read
-            for (uint32_t z = 0; z < min(spins, 6u); ++z) __builtin_amdgcn_s_sleep(8);
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                const int idx = lo + 64 * k + (int)lane;
-                if (idx >= floor_idx && tag_of(v[k]) != ep) v[k] = word(idx);
-            }
-        }
-        lo -= WIN;  // no INC in this window: every word was an aggregate, continue below it
-    }
 }
 
 // Batch totals (the wave owning the last tile): `tot_c` = inclusive [dns|session] count
@@ -415,11 +345,6 @@ __device__ void write_batch_stats(const ParseParams& P, unsigned long long tot_c
     }
 }
 
-template <int V>
-struct IC {
-    static constexpr int value = V;
-};
-
 __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_t o, Hdr& h) {
     h.A = ld16(rs, o + 10u);
     h.B = ld16(rs, o + 26u);
@@ -427,227 +352,457 @@ __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_
     h.Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 66u, 0, 0);
 }
 
-// One look-back unit = one block-round: kWaves waves x U wave-tiles x 64 frames.  Block b
-// (of G co-resident blocks) owns units b, b+G, b+2G, ...; inside a unit, wave w owns the
-// contiguous frames [w*U*64, (w+1)*U*64), so packet order = (wave, tile, lane).  Per unit:
-//   1. every wave issues the offsets of its U tiles, then all 4U header loads (U*64 frames of
-//      loads in flight per wave)
-//   2. every wave classifies and stages its SESSION records, compacted, in its own LDS region
-//      (records do not stay live in VGPRs across the look-back); counts -> LDS     | barrier
-//   3. wave 0 publishes the unit's count and runs the look-back: ONE participant per block
-//      (a few hundred per launch) keeps the polled words cold; lanes poll together with
-//      exponential back-off                                                          | barrier
-//   4. every wave copies its LDS region to its place in the output with coalesced 16-B
-//      stores; DNS records straight from registers
-template <int U, uint32_t FLAGS, bool PARSED = false>
-__global__ __launch_bounds__(kThreads) void k_parse_block(const ParseParams P) {
-    constexpr uint32_t kWaves = kThreads / 64;
-    constexpr uint32_t WF = 64u * U;          // frames per wave per unit
-    constexpr uint32_t UF = WF * kWaves;      // frames per unit
+// ---- round look-back (k_parse_ws) -----------------------------------------------------------
+// Units are dealt round-robin: round r = units [r*G, (r+1)*G), unit r*G + b belongs to block b.
+// The exclusive prefix of unit u = r*G + b is  sum(RSUM[0..r-1]) + sum(AGG[r*G .. u-1]):  one
+// probe of b + r epoch-tagged words, with no chain of inclusive prefixes from round to round
+// (each link of such a chain costs a memory round trip, ~2-3 us on a CU that streams, and the
+// chain grows with the round count).  RSUM[r] is published by the look-back of the round's last
+// unit (b = G-1), which reads every other AGG of the round anyway.  Not-ready words are
+// re-polled by their lanes together with exponential back-off.
+template <uint32_t FLAGS>
+__device__ unsigned long long lookback_round(const ParseParams& P, uint32_t r, uint32_t b, uint32_t G,
+                                             unsigned long long agg, uint32_t& spins) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t ep = P.epoch;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(P.tagg + (size_t)r * G), (short)0, (int)(b * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)P.rsum, (short)0, (int)(r * 8u), 0x00020000);
+    auto word = [&](uint32_t idx) {  // idx < b: AGG of round-mate idx; else RSUM[idx - b]
+        const u32x2 x = idx < b ? __builtin_amdgcn_raw_buffer_load_b64(ra, idx * 8u, 0, 16)
+                                : __builtin_amdgcn_raw_buffer_load_b64(rr, (idx - b) * 8u, 0, 16);
+        return (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+    };
+    const uint32_t m = b + r;
+    unsigned long long sa = 0ull, sr = 0ull;  // AGG part, RSUM part
+    spins = 0u;
+    for (uint32_t c0 = 0; c0 < m; c0 += 256u) {
+        unsigned long long v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t idx = c0 + 64u * q + lane;
+            v[q] = idx < m ? word(idx) : ((unsigned long long)ep << 56);
+        }
+        for (;;) {
+            bool ready = true;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ready &= tag_of(v[q]) == ep;
+            if (__ballot(!ready) == 0ull) break;
+            if (++spins > (1u << 16)) { if (lane == 0u) atomicOr(P.error, 1u); return 0ull; }
+            for (uint32_t z = 0; z < min(spins, 4u); ++z) __builtin_amdgcn_s_sleep(4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t idx = c0 + 64u * q + lane;
+                if (tag_of(v[q]) != ep) v[q] = word(idx);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t idx = c0 + 64u * q + lane;
+            if (idx < b) sa += st_counts(v[q]);
+            else sr += st_counts(v[q]);
+        }
+    }
+    sa = wave_sum64(sa);
+    sr = wave_sum64(sr);
+    // the round's last unit: round r is complete, publish its sum (round-mates' AGGs + own)
+    if (b == G - 1u && lane == 0u) ast(P.rsum + r, st_pack(ep, false, sa + agg));
+    return sa + sr;
+}
+
+// ============================================================================================
+// k_parse_ws -- role-specialised block pipeline (the product kernel).
+//
+// A block (one per CU) = kWsLoad loader waves + kWsLb look-back waves + kWsStore storer waves.
+// A unit = kWsLoad x kWsU wave-tiles x 64 frames (loader wave w owns frames [w*64U, (w+1)*64U)
+// of the unit, so packet order = (wave, tile, lane)); block b owns units b, b+G, b+2G, ...
+// (k-th unit of the block = b + k*G, staged in LDS slot k % kWsSlots).  The roles run
+// decoupled, each at its own pace, handing units over through monotonic LDS counters (no
+// block barrier in the loop, so a slow look-back stalls nobody until the slots run out):
+//   loader waves   : wait until slot k%S is free -> classify unit k (its headers were issued two
+//                    units earlier) -> stage SESSION / DNS records, compacted per wave, + counts
+//                    -> signal STAGED -> issue the offset loads of unit k+3 and the header loads
+//                    of unit k+2
+//   look-back wave : (unit k = j mod kWsLb for wave j) wait STAGED -> publish AGG, decoupled
+//                    look-back, publish INC -> prefix to the slot -> signal READY
+//   storer waves   : wait READY -> copy the slot's records to the output with coalesced 16-B
+//                    stores -> signal FREE
+// Loader waves issue only loads and storer waves only stores, so no wave's vmcnt wait covers
+// the other role's traffic: two units of header loads stay in flight per loader wave.
+// ============================================================================================
+#ifndef FB_WS_LOAD
+#define FB_WS_LOAD 8
+#endif
+#ifndef FB_WS_U
+#define FB_WS_U 1
+#endif
+#ifndef FB_WS_STORE
+#define FB_WS_STORE 4
+#endif
+#ifndef FB_WS_LB
+#define FB_WS_LB 2
+#endif
+#ifndef FB_WS_SLOTS
+#define FB_WS_SLOTS 5
+#endif
+#ifndef FB_WS_DEPTH
+#define FB_WS_DEPTH 3
+#endif
+constexpr int kWsLoad = FB_WS_LOAD;
+constexpr int kWsU = FB_WS_U;
+constexpr int kWsStore = FB_WS_STORE;
+constexpr int kWsLb = FB_WS_LB;
+constexpr int kWsSlots = FB_WS_SLOTS;
+constexpr int kWsDepth = FB_WS_DEPTH;  // units of header loads in flight per loader wave
+constexpr int kWsThreads = 64 * (kWsLoad + 1 + kWsLb + kWsStore);  // + 1 AGG publisher wave
+#ifndef FB_WS_LBWIN
+#define FB_WS_LBWIN 8
+#endif
+constexpr int kWsLbWin = FB_WS_LBWIN;  // look-back probe window, x64 units
+constexpr uint32_t kWsWF = 64u * kWsU;         // frames per loader wave per unit
+constexpr uint32_t kWsUnit = kWsWF * kWsLoad;  // frames per unit
+
+// Per loader wave, one 64U x 56-B region: SESSION records compacted from the front, DNS records
+// (16 B) from the back -- a frame is one or the other, so they never overlap.
+struct WsSlot {
+    unsigned long long rec[kWsLoad][kWsWF * 7];
+    uint32_t cnt[kWsLoad][4];  // sessions, dns, filtered|tcp<<16, v4|bad<<16
+    unsigned long long agg;    // [dns:28 | session:28] of the unit
+    unsigned long long excl;   // [dns:28 | session:28] prefix of the unit
+};
+struct WsSync {               // monotonic hand-off counters per slot
+    uint32_t cfg;               // + 1 per copying wave once the configuration is in LDS
+    uint32_t staged[kWsSlots];  // + 1 per loader wave per unit
+    uint32_t agged[kWsSlots];   // = generation + 1 once the AGG is published and in the slot
+    uint32_t ready[kWsSlots];   // = generation + 1 once the prefix is in the slot
+    uint32_t freed[kWsSlots];   // + 1 per storer wave per unit
+};
+__device__ __forceinline__ uint4* ws_dns(WsSlot& S, uint32_t w, uint32_t j) {
+    return reinterpret_cast<uint4*>(&S.rec[w][kWsWF * 7]) - 1 - j;
+}
+__device__ __forceinline__ const uint4* ws_dns(const WsSlot& S, uint32_t w, uint32_t j) {
+    return reinterpret_cast<const uint4*>(&S.rec[w][kWsWF * 7]) - 1 - j;
+}
+// s_barrier that drains this wave's LDS traffic only (never vector memory).
+__device__ __forceinline__ void ws_tick() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Signal after this wave's LDS writes / reads of a slot: drain LDS (not vector memory), then add.
+__device__ __forceinline__ void lds_signal(uint32_t* p, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63u) == 0u) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t target) {
+    while (lds_ld(p) < target) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+// kStamps (ablation builds): P.dbg[(b * kWsDbgUnits + k) * 4 + role] = s_memrealtime at
+// role 3: loader wave 0 starts unit k, 0: loader wave 0 staged it, 1: its INC published,
+// 2: storer wave 0 done with it.
+constexpr uint32_t kWsDbgUnits = 64;
+template <bool PARSED, uint32_t FLAGS = kFlagsProduct>
+__global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
+    constexpr int U = kWsU;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t G = gridDim.x, T = P.num_tiles;  // T = units
+    const uint32_t G = gridDim.x, T = P.num_tiles, b = blockIdx.x;
+    const uint32_t K = (T - b + G - 1u) / G;  // units of this block (grid <= T, so K >= 1)
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
     const uint32_t ep = P.epoch;
+    auto stamp = [&](uint32_t k, int role) {
+        if constexpr ((FLAGS & kStamps) != 0u)
+            if (lane == 0u && k < kWsDbgUnits - 1u) P.dbg[(b * kWsDbgUnits + k) * 4 + role] = __builtin_amdgcn_s_memrealtime();
+    };
+    // block-level stamps in the last debug unit: 3 entry, 0 loader exit, 1 look-back exit, 2 storer exit
+    auto bstamp = [&](int role) {
+        if constexpr ((FLAGS & kStamps) != 0u)
+            if (lane == 0u) P.dbg[(b * kWsDbgUnits + kWsDbgUnits - 1u) * 4 + role] = __builtin_amdgcn_s_memrealtime();
+    };
+    if (tid == 0u) bstamp(3);
 
-    __shared__ DevConfig s_cfg;                                  // service bitmap + tables
-    __shared__ unsigned long long s_stage_all[kWaves][WF * 7];  // per-wave compacted records
-    __shared__ uint32_t s_cnt[kWaves][4];                        // sessions, dns, filtered|tcp, v4|bad
-    __shared__ unsigned long long s_excl;
-    unsigned long long* s_stage = s_stage_all[wave];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
-        uint4* dst = reinterpret_cast<uint4*>(&s_cfg);
-        for (uint32_t q = tid; q < sizeof(DevConfig) / 16; q += kThreads) dst[q] = src[q];
-        // Zero the other parity's error word for the next launch (the previous launch, which
-        // used it, has completed: launches on one context are stream-ordered).
-        if (blockIdx.x == 0u && tid == 0u) *P.error_next = 0u;
-    }
-    __syncthreads();
-    const DevConfig* cfg = &s_cfg;
-
+    __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];  // header + bitmap + the used table entries
+    __shared__ WsSlot s_slot[kWsSlots];
+    __shared__ WsSync s_sync;
+    const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
+    const DevConfig* gcfg = cfg;  // tables read from LDS too (a global read here would wait for
+                                  // every in-flight header load)
+    constexpr uint32_t kCopyWaves = (uint32_t)(kWsThreads / 64 - kWsLoad);
+    if (tid < sizeof(WsSync) / 4) reinterpret_cast<uint32_t*>(&s_sync)[tid] = 0u;
+    ws_tick();  // counters zeroed (LDS-only barrier; nothing is in flight yet)
+    const bool is_loader = wave < (uint32_t)kWsLoad;
     const unsigned long long lmask = (1ull << lane) - 1ull;
-    uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;  // pre-filter counters (block, wave 0 keeps them)
 
-    for (uint32_t u = blockIdx.x; u < T; u += G) {
-        const uint32_t f0 = u * UF + wave * WF;  // first frame of this wave
-        // ---- 1. loads -----------------------------------------------------------------------
-        uint2 o[U];
-        Hdr h[U];
-        uint4 pin[U][4];  // PARSED: one fb_parsed_pkt (56 B) per lane
+    if (is_loader) {
+        // ================================ loader waves ================================
+        // kWsDepth units of header loads in flight per wave.  Register set d (headers h, the
+        // unit's offsets c, and q = the offsets of the unit it fetches next) serves units
+        // k = d mod D; the loop is unrolled by D, so no set is indexed at run time.  After
+        // classifying unit k with set X:  X.h <- headers(k+D) from X.q (waited for with the
+        // younger loads of D-1 other units in flight) ; X.c <- X.q (explicit v_mov: the
+        // allocator cannot rename q across the loop, so no back-edge copy waits on a pending
+        // load) ; X.q <- offsets(k+2D).  The prefetch is unconditional (past the last unit the
+        // offsets clamp to offsets[n] and the header loads fall outside the buffer), so every
+        // path issues the same VMEM sequence and the compiler's vmcnt bookkeeping stays exact.
+        constexpr int D = kWsDepth;
+        struct Set {
+            Hdr h[U];
+            uint2 c[U];
+            uint2 q[U];
+        };
+        Set SS[D];
+        uint4 pin[U][4];
+        auto vmov = [](uint32_t x) {
+            uint32_t y;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+            return y;
+        };
+        auto frame0 = [&](uint32_t k) { return (b + k * G) * kWsUnit + wave * kWsWF; };
+        auto load_offs = [&](uint32_t k, uint2 (&dst)[U]) {
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const uint32_t i = frame0(k) + r * 64u + lane;
+                dst[r] = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);
+            }
+        };
+        auto load_parsed = [&](uint32_t k) {
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const uint32_t i = min(frame0(k) + r * 64u + lane, P.n - 1u);
+                const uint4* qq = reinterpret_cast<const uint4*>(P.parsed + i);
+                pin[r][0] = qq[0];
+                pin[r][1] = qq[1];
+                pin[r][2] = qq[2];
+                const uint2 t = *reinterpret_cast<const uint2*>(qq + 3);
+                pin[r][3] = make_uint4(t.x, t.y, 0u, 0u);
+            }
+        };
+        auto fetch = [&](Set& X, uint32_t k_next_q) {  // headers from X.q, then X.q <- offs(k_next_q)
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                load_headers1(rs, X.q[r].x, X.h[r]);
+                X.c[r] = make_uint2(vmov(X.q[r].x), vmov(X.q[r].y));
+            }
+            load_offs(k_next_q, X.q);
+        };
         if constexpr (!PARSED) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) load_offs((uint32_t)d, SS[d].q);
+#pragma unroll
+            for (int d = 0; d < D; ++d) fetch(SS[d], (uint32_t)(d + D));
+        } else {
+            load_parsed(0);
+        }
+        auto step = [&](uint32_t k, Set& X) {
+            const uint32_t sl = k % kWsSlots, g = k / kWsSlots;
+            stamp(k, 3);
+            lds_wait_ge(&s_sync.cfg, kCopyWaves);           // configuration in LDS (first unit)
+            lds_wait_ge(&s_sync.freed[sl], g * kWsStore);  // unit k - S fully copied out
+            WsSlot& S = s_slot[sl];
+            unsigned long long* stage = S.rec[wave];
+            const uint32_t f0 = frame0(k);
+            uint32_t cs = 0u, cd = 0u, wf = 0u, wt = 0u, w4 = 0u, wb = 0u;
 #pragma unroll
             for (int r = 0; r < U; ++r) {
                 const uint32_t i = f0 + r * 64u + lane;
-                o[r] = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);  // n+1 entries
-            }
+                const bool valid = i < P.n;
+                Pkt kk;
+                if constexpr (!PARSED) {
+                    process_frame(rs, cfg, gcfg, X.h[r], valid ? X.c[r].x : 1u, valid ? X.c[r].y : 0u,
+                                  P.frames_bytes, i, kk);
+                } else {
+                    const uint4 a = pin[r][0], bb = pin[r][1], c = pin[r][2], d = pin[r][3];
+                    const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {bb.x, bb.y, bb.z, bb.w};
+                    const uint32_t proto = c.y & 0xffu, fam = (c.y >> 8) & 0xffu;
+                    kk.bad = false;
+                    kk.cls = FB_CLASS_DROP;
+                    kk.tcp = kk.v4 = false;
+                    if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
+                        classify_session(cfg, gcfg, proto, fam, src, dst, c.x & 0xffffu, c.x >> 16, (d.x >> 8) & 1u,
+                                         d.x & 0xffu, c.z, c.w, d.y, kk);
+                }
+                const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
+                const bool is_d = valid && kk.cls == FB_CLASS_DNS;
+                const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
+                const bool counted = is_s || is_f;
+                const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+                if (is_s) {
+                    unsigned long long* dd = stage + (size_t)(cs + __popcll(m_sess & lmask)) * 7;
 #pragma unroll
-            for (int r = 0; r < U; ++r) load_headers1(rs, o[r].x, h[r]);
-        } else {
-#pragma unroll
-            for (int r = 0; r < U; ++r) {
-                const uint32_t i = min(f0 + r * 64u + lane, P.n - 1u);  // n >= 1 here
-                const uint4* q = reinterpret_cast<const uint4*>(P.parsed + i);
-                pin[r][0] = q[0];
-                pin[r][1] = q[1];
-                pin[r][2] = q[2];
-                const uint2 t = *reinterpret_cast<const uint2*>(q + 3);
-                pin[r][3] = make_uint4(t.x, t.y, 0u, 0u);
+                    for (int w = 0; w < 7; ++w)
+                        dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
+                }
+                if (is_d) *ws_dns(S, wave, cd + __popcll(m_dns & lmask)) = make_uint4(kk.w[0], kk.w[1], kk.w[2], kk.w[3]);
+                cs += (uint32_t)__popcll(m_sess);
+                cd += (uint32_t)__popcll(m_dns);
+                wf += __popcll(__ballot(is_f));
+                wt += __popcll(__ballot(counted && kk.tcp));
+                w4 += __popcll(__ballot(counted && kk.v4));
+                wb += __popcll(__ballot(valid && kk.bad));
+                if (valid && P.cls) P.cls[i] = (uint8_t)kk.cls;
             }
+            if (lane == 0u) {
+                S.cnt[wave][0] = cs;
+                S.cnt[wave][1] = cd;
+                S.cnt[wave][2] = wf | (wt << 16);
+                S.cnt[wave][3] = w4 | (wb << 16);
+            }
+            lds_signal(&s_sync.staged[sl], 1u);
+            stamp(k, 0);
+            if constexpr (!PARSED) fetch(X, k + 2u * D);
+            else load_parsed(k + 1u);
+        };
+        uint32_t k = 0;
+        for (; k + D <= K; k += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) step(k + d, SS[d]);
         }
-        // ---- 2. classify + stage ----------------------------------------------------------------
-        unsigned long long m_dns[U];
-        uint4 dnsw[U];
-        uint32_t cs = 0u, cd = 0u, wf = 0u, wt = 0u, w4 = 0u, wb = 0u;
 #pragma unroll
-        for (int r = 0; r < U; ++r) {
-            const uint32_t i = f0 + r * 64u + lane;
-            const bool valid = i < P.n;
-            Pkt k;
-            if constexpr (!PARSED) {
-                process_frame(rs, cfg, cfg->service_bitmap, h[r], valid ? o[r].x : 1u, valid ? o[r].y : 0u,
-                              P.frames_bytes, i, k);
-            } else {
-                // fb_parsed_pkt: session_key words 0..9, then lengths, flags, pkt_index
-                const uint4 a = pin[r][0], b = pin[r][1], c = pin[r][2], d = pin[r][3];
-                const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {b.x, b.y, b.z, b.w};
-                const uint32_t proto = c.y & 0xffu, fam = (c.y >> 8) & 0xffu;
-                k.bad = false;
-                k.cls = FB_CLASS_DROP;
-                k.tcp = k.v4 = false;
-                if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
-                    classify_session(cfg, cfg->service_bitmap, proto, fam, src, dst, c.x & 0xffffu, c.x >> 16,
-                                     (d.x >> 8) & 1u, d.x & 0xffu, c.z, c.w, d.y, k);
-            }
-            const bool is_s = valid && k.cls == FB_CLASS_SESSION;
-            const bool is_d = valid && k.cls == FB_CLASS_DNS;
-            const bool is_f = valid && k.cls == FB_CLASS_FILTERED;
-            const bool counted = is_s || is_f;
-            const unsigned long long m_sess = __ballot(is_s);
-            m_dns[r] = __ballot(is_d);
-            dnsw[r] = make_uint4(k.w[0], k.w[1], k.w[2], k.w[3]);
-            if (is_s) {
-                unsigned long long* d = s_stage + (size_t)(cs + __popcll(m_sess & lmask)) * 7;
-#pragma unroll
-                for (int w = 0; w < 7; ++w)
-                    d[w] = (unsigned long long)k.w[2 * w] | ((unsigned long long)k.w[2 * w + 1] << 32);
-            }
-            cs += (uint32_t)__popcll(m_sess);
-            cd += (uint32_t)__popcll(m_dns[r]);
-            wf += __popcll(__ballot(is_f));
-            wt += __popcll(__ballot(counted && k.tcp));
-            w4 += __popcll(__ballot(counted && k.v4));
-            wb += __popcll(__ballot(valid && k.bad));
-            if (valid && P.cls) P.cls[i] = (uint8_t)k.cls;
-        }
-        if (lane == 0u) {
-            s_cnt[wave][0] = cs;
-            s_cnt[wave][1] = cd;
-            s_cnt[wave][2] = wf | (wt << 16);
-            s_cnt[wave][3] = w4 | (wb << 16);
-        }
-        __syncthreads();  // counts of every wave
-        // ---- 3. publish + look-back (wave 0) --------------------------------------------------
-        if (wave == 0u) {
+        for (int d = 0; d < D - 1; ++d)
+            if (k + d < K) step(k + d, SS[d]);
+        if (wave == 0u) bstamp(0);
+    } else {
+        // non-loader waves copy the configuration header + service bitmap into LDS while the
+        // loaders' first header loads are in flight
+        const uint32_t t2 = tid - 64u * kWsLoad;
+        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
+        for (uint32_t q = t2; q < kCfgLdsBytes / 16; q += 64u * kCopyWaves) s_cfg4[q] = src[q];
+        // table entries in use only (sizes are uniform: scalar loads of the header)
+        constexpr uint32_t kLanOff = offsetof(DevConfig, lan_v6) / 16, kOwnOff = offsetof(DevConfig, own) / 16;
+        const uint32_t nl = P.cfg->n_lan_v6 * (sizeof(LanV6) / 16), no = P.cfg->n_own * (sizeof(fb_ip) / 16);
+        for (uint32_t q = t2; q < nl; q += 64u * kCopyWaves) s_cfg4[kLanOff + q] = src[kLanOff + q];
+        for (uint32_t q = t2; q < no; q += 64u * kCopyWaves) s_cfg4[kOwnOff + q] = src[kOwnOff + q];
+        if (b == 0u && t2 == 0u) *P.error_next = 0u;  // other parity's word, for the next launch
+        lds_signal(&s_sync.cfg, 1u);
+    }
+    if (is_loader) {
+    } else if (wave == (uint32_t)kWsLoad) {
+        // ============================== AGG publisher wave ==============================
+        // Publishes every unit's aggregate as soon as it is staged (a look-back of another
+        // block may be waiting for it), and sums the block's pre-filter counters.
+        uint32_t a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u;
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t sl = k % kWsSlots, g = k / kWsSlots;
+            WsSlot& S = s_slot[sl];
+            lds_wait_ge(&s_sync.staged[sl], (g + 1u) * kWsLoad);
             uint32_t bs = 0u, bd = 0u;
 #pragma unroll
-            for (uint32_t w = 0; w < kWaves; ++w) {
-                bs += s_cnt[w][0];
-                bd += s_cnt[w][1];
-                a_f += s_cnt[w][2] & 0xFFFFu;
-                a_t += s_cnt[w][2] >> 16;
-                a_4 += s_cnt[w][3] & 0xFFFFu;
-                a_b += s_cnt[w][3] >> 16;
+            for (int w = 0; w < kWsLoad; ++w) {
+                bs += S.cnt[w][0];
+                bd += S.cnt[w][1];
+                a_f += S.cnt[w][2] & 0xFFFFu;
+                a_t += S.cnt[w][2] >> 16;
+                a_4 += S.cnt[w][3] & 0xFFFFu;
+                a_b += S.cnt[w][3] >> 16;
             }
             const unsigned long long agg = (unsigned long long)bs | ((unsigned long long)bd << 28);
-            if constexpr ((FLAGS & kStamps) != 0u)
-                if (lane == 0u) P.dbg[4ull * u] = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0u) {
+                if (!(FLAGS & kNoLookback)) ast(P.tagg + b + k * G, st_pack(ep, false, agg));
+                S.agg = agg;
+                __hip_atomic_store(&s_sync.agged[sl], g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        if (lane == 0u && !(FLAGS & kNoLookback)) {
+            ast(P.wstat + 2 * b, ((unsigned long long)ep << 56) | a_f | ((unsigned long long)a_t << 28));
+            ast(P.wstat + 2 * b + 1, ((unsigned long long)ep << 56) | a_4 | ((unsigned long long)a_b << 28));
+        }
+    } else if (wave < (uint32_t)(kWsLoad + 1 + kWsLb)) {
+        // ================================ look-back waves ================================
+        const uint32_t j = wave - (uint32_t)kWsLoad - 1u;
+        unsigned long long tot_c = 0ull;
+        for (uint32_t k = j; k < K; k += kWsLb) {
+            const uint32_t sl = k % kWsSlots, g = k / kWsSlots;
+            WsSlot& S = s_slot[sl];
+            const uint32_t u = b + k * G;
+            lds_wait_ge(&s_sync.agged[sl], g + 1u);
+            const unsigned long long agg = S.agg;
             unsigned long long excl;
-            if (FLAGS & kNoLookback) {
-                excl = (unsigned long long)u * UF;
+            if constexpr ((FLAGS & kNoLookback) != 0u) {
+                excl = (unsigned long long)u * kWsUnit;
             } else {
-                if (lane == 0u) ast(P.tagg + u, st_pack(ep, false, agg));
                 uint32_t spins;
-                excl = lookback_unit<FLAGS>(P, u, spins);
-                if (lane == 0u) ast(P.tagg + u, st_pack(ep, true, excl + agg));
-                if constexpr ((FLAGS & kStamps) != 0u)
-                    if (lane == 0u) {
-                        P.dbg[4ull * u + 2] = __builtin_amdgcn_s_memrealtime();
-                        P.dbg[4ull * u + 3] = spins;
-                    }
+                excl = lookback_round<kFlagsProduct>(P, k, b, G, agg, spins);
             }
-            if (lane == 0u) s_excl = excl;
-            if (u == T - 1u && P.stats && !(FLAGS & kNoLookback)) {
-                // the last unit's owner: own counters first (this is the block's last unit)
-                if (lane == 0u) {
-                    ast(P.wstat + 2 * blockIdx.x, ((unsigned long long)ep << 56) | a_f | ((unsigned long long)a_t << 28));
-                    ast(P.wstat + 2 * blockIdx.x + 1, ((unsigned long long)ep << 56) | a_4 | ((unsigned long long)a_b << 28));
-                }
-                write_batch_stats(P, excl + agg, G);
+            if (lane == 0u) {
+                S.excl = excl;
+                __hip_atomic_store(&s_sync.ready[sl], g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            stamp(k, 1);
+            if (u == T - 1u) tot_c = excl + agg;  // the batch's last unit: inclusive totals
         }
-        __syncthreads();  // s_excl
-        // ---- 4. stores ---------------------------------------------------------------------------
-        if (!(FLAGS & kNoStore)) {
-            const unsigned long long bex = s_excl;
-            uint32_t base_s = (uint32_t)(bex & ((1ull << 28) - 1ull));
-            uint32_t base_d = (uint32_t)(bex >> 28);
-            for (uint32_t w = 0; w < wave; ++w) {
-                base_s += s_cnt[w][0];
-                base_d += s_cnt[w][1];
-            }
-            if (P.out && cs) {
-                // [base_s*56, (base_s+cs)*56) is 8-B aligned: 16-B aligned body + 8-B head/tail
-                unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)base_s * 7;
-                const uint32_t units = cs * 7, head = base_s & 1u, body = (units - head) >> 1;
-                if (head && lane == 0u) g8[0] = s_stage[0];
-                uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
-                for (uint32_t c = lane; c < body; c += 64u) {
-                    const unsigned long long x = s_stage[head + 2 * c], y = s_stage[head + 2 * c + 1];
-                    g16[c] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
-                }
-                if (lane == 0u && head + 2 * body < units) g8[units - 1] = s_stage[units - 1];
-            }
-            if (P.dns) {
-#pragma unroll
-                for (int r = 0; r < U; ++r) {
-                    if ((m_dns[r] >> lane) & 1ull) {
-                        fb_dns_out d;
-                        d.pkt_index = dnsw[r].x;
-                        d.payload_offset = dnsw[r].y;
-                        d.payload_length = dnsw[r].z;
-                        d.protocol = (uint8_t)(dnsw[r].w & 0xffu);
-                        d.family = (uint8_t)(dnsw[r].w >> 8);
-                        d.reserved = 0;
-                        P.dns[base_d + __popcll(m_dns[r] & lmask)] = d;
+        // the wave that owns the batch's last unit sums every block's pre-filter counters
+        if ((T - 1u) % G == b && (K - 1u) % kWsLb == j && P.stats && !(FLAGS & kNoLookback))
+            write_batch_stats(P, tot_c, G);
+        if (j == 0u) bstamp(1);
+    } else {
+        // ================================ storer waves ================================
+        // Storer wave v copies loader regions v, v+SW, ...: region w's records go to output
+        // records [base + ps[w], +cs_w) with 16-B stores (8-B head/tail where the 56-B record
+        // boundary is not 16-B aligned); its DNS records likewise, 16 B each.
+        const uint32_t sw = wave - (uint32_t)(kWsLoad + 1 + kWsLb);
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t sl = k % kWsSlots, g = k / kWsSlots;
+            lds_wait_ge(&s_sync.ready[sl], g + 1u);
+            const WsSlot& S = s_slot[sl];
+            if (!(FLAGS & kNoStore)) {
+                const unsigned long long ex = S.excl;
+                uint32_t base_s = (uint32_t)(ex & kCnt28), base_d = (uint32_t)(ex >> 28);
+                for (uint32_t w = 0; w < (uint32_t)kWsLoad; ++w) {
+                    const uint32_t cs = S.cnt[w][0], cd = S.cnt[w][1];
+                    if ((w % kWsStore) == sw) {
+                        const unsigned long long* src = S.rec[w];
+                        if (P.out && cs) {
+                            unsigned long long* g8 = reinterpret_cast<unsigned long long*>(P.out) + (size_t)base_s * 7u;
+                            const uint32_t words = cs * 7u, head = base_s & 1u, body = (words - head) >> 1;
+                            if (head && lane == 0u) g8[0] = src[0];
+                            uint4* g16 = reinterpret_cast<uint4*>(g8 + head);
+                            for (uint32_t c = lane; c < body; c += 64u) {
+                                const unsigned long long x = src[head + 2u * c], y = src[head + 2u * c + 1u];
+                                g16[c] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+                            }
+                            if (lane == 0u && head + 2u * body < words) g8[words - 1u] = src[words - 1u];
+                        }
+                        if (P.dns) {
+                            for (uint32_t jd = lane; jd < cd; jd += 64u) {
+                                const uint4 v = *ws_dns(S, w, jd);
+                                fb_dns_out d;
+                                d.pkt_index = v.x;
+                                d.payload_offset = v.y;
+                                d.payload_length = v.z;
+                                d.protocol = (uint8_t)(v.w & 0xffu);
+                                d.family = (uint8_t)(v.w >> 8);
+                                d.reserved = 0;
+                                P.dns[base_d + jd] = d;
+                            }
+                        }
                     }
-                    base_d += (uint32_t)__popcll(m_dns[r]);
+                    base_s += cs;
+                    base_d += cd;
                 }
             }
+            lds_signal(&s_sync.freed[sl], 1u);
+            if (sw == 0u) stamp(k, 2);
         }
-        __syncthreads();  // s_cnt / s_excl / stage reuse by the next unit
-    }
-    // every block publishes its pre-filter counters (the last unit's owner did so above)
-    const bool owner_last = T > 0u && (T - 1u) % G == blockIdx.x;
-    if (!owner_last && tid == 0u && !(FLAGS & kNoLookback)) {
-        ast(P.wstat + 2 * blockIdx.x, ((unsigned long long)ep << 56) | a_f | ((unsigned long long)a_t << 28));
-        ast(P.wstat + 2 * blockIdx.x + 1, ((unsigned long long)ep << 56) | a_4 | ((unsigned long long)a_b << 28));
+        if (sw == 0u) bstamp(2);
     }
 }
 
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_parse_block<kUnitTiles, kFlagsProduct>), dim3(grid), dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((k_parse_ws<false>), dim3(grid), dim3(kWsThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_parse_block<kUnitTiles, kFlagsProduct, true>), dim3(grid), dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((k_parse_ws<true>), dim3(grid), dim3(kWsThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t occupancy_parse(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_block<kUnitTiles, kFlagsProduct>),
-                                                        kThreads, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_ws<false>), kWsThreads, 0);
 }
+uint32_t parse_unit_frames() { return kWsUnit; }
+uint32_t parse_block_waves() { return kWsThreads / 64; }
 
 }  // namespace fbk

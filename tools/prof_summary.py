@@ -17,7 +17,7 @@ import sqlite3
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PARSE_KERNEL = "k_parse_block"
+PARSE_KERNEL = "k_parse_ws"
 
 
 def db_of(d):

@@ -1,0 +1,222 @@
+// ubench_ws.hip -- timing + per-tick stamps of the role-specialised parse kernel (tooling, not
+// product).  Includes the product kernel source and times, interleaved in one process:
+//   ws            the product kernel (k_parse_ws<false>)
+//   ws_no_lb      look-back replaced by a fixed prefix (wrong output, timing only)
+//   ws_no_store   storer waves idle
+//   ws_no_lb_st   both
+//   read / copy   plain streaming read of the frame buffer / read frames + write 56 B per frame
+// then one stamped run: per tick, quantiles over blocks of the tick length and of each role's
+// busy time (loader: tick start -> classify + prefetch issued; look-back: -> prefix published;
+// storers: -> last store issued).
+//   build: tools/build_ubench_ws.sh ; run: tools/ubench_ws [config_id] [n] [rotate] [iters]
+#include "../flodbadd_amd/csrc/fb_parse.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+extern "C" {
+typedef struct fb_synth_cfg {
+    uint64_t seed;
+    uint32_t n_flows, mode, v6_permille, udp_permille, dns_permille, zipf;
+    double zipf_s;
+} fb_synth_cfg;
+uint64_t fb_synth_plan(const fb_synth_cfg* c, uint64_t first, uint32_t n, uint32_t* offsets);
+int fb_synth_fill(const fb_synth_cfg* c, uint64_t first, uint32_t n, const uint32_t* offsets, uint8_t* frames,
+                  int n_threads);
+}
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e = (x);                                                                    \
+        if (e != hipSuccess) {                                                                 \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));   \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+__global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ in, size_t n16, unsigned* sink) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256ull) {
+        uint4 v = in[i];
+        acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;
+}
+__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n_in16,
+                                              size_t n_out16) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n_in16; i += (size_t)gridDim.x * 256ull) {
+        uint4 v = in[i];
+        if (i < n_out16) out[i] = v;
+    }
+}
+
+int main(int argc, char** argv) {
+    const int cfg_id = argc > 1 ? atoi(argv[1]) : 2;
+    const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : (1u << 20);
+    const int R = argc > 3 ? atoi(argv[3]) : 8;
+    const int iters = argc > 4 ? atoi(argv[4]) : 200;
+    fb_synth_cfg sc;
+    memset(&sc, 0, sizeof(sc));
+    sc.seed = 0xF10DBADDull ^ (uint64_t)cfg_id;
+    sc.n_flows = cfg_id >= 4 ? (1u << 20) : (1u << 16);
+    sc.mode = cfg_id == 2 ? 0 : 1;
+    sc.v6_permille = cfg_id == 2 ? 0 : 200;
+    sc.udp_permille = cfg_id == 2 ? 0 : 300;
+    sc.dns_permille = 5;
+    sc.zipf_s = 1.1;
+    std::vector<uint32_t> offs(n + 1);
+    const uint64_t bytes = fb_synth_plan(&sc, 0, n, offs.data());
+    std::vector<uint8_t> frames(bytes);
+    fb_synth_fill(&sc, 0, n, offs.data(), frames.data(), 16);
+
+    fbk::DevConfig hc;
+    memset(&hc, 0, sizeof(hc));
+    FILE* f = fopen("flodbadd_amd/data/service_ports.bin", "rb");
+    if (!f || fread(hc.service_bitmap, 1, 8192, f) != 8192) { fprintf(stderr, "bitmap\n"); return 1; }
+    fclose(f);
+    hc.filter = FB_FILTER_GLOBAL_ONLY;
+    fbk::DevConfig* dcfg;
+    CK(hipMalloc(&dcfg, sizeof(hc)));
+    CK(hipMemcpy(dcfg, &hc, sizeof(hc), hipMemcpyHostToDevice));
+
+    const uint32_t units = (n + fbk::kWsUnit - 1) / fbk::kWsUnit;
+    const size_t swords = fbk::scratch_words(units);
+    unsigned long long* status;
+    CK(hipMalloc(&status, swords * 8));
+    CK(hipMemset(status, 0, swords * 8));
+    uint32_t* err;
+    CK(hipMalloc(&err, 16));
+    CK(hipMemset(err, 0, 16));
+    int bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_ws<false>), fbk::kWsThreads, 0));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const uint32_t grid = std::min<uint32_t>(units, (uint32_t)(std::max(bpc, 1) * prop.multiProcessorCount));
+    unsigned long long* dbg;
+    const size_t dbg_words = (size_t)grid * fbk::kWsDbgUnits * 4;
+    CK(hipMalloc(&dbg, dbg_words * 8));
+    CK(hipMemset(dbg, 0, dbg_words * 8));
+    unsigned* sink;
+    CK(hipMalloc(&sink, 16));
+    struct Buf { uint8_t* fr; uint32_t* off; fb_pkt_out* out; fb_dns_out* dns; fb_batch_stats* st; };
+    std::vector<Buf> bufs(R);
+    for (int r = 0; r < R; ++r) {
+        CK(hipMalloc(&bufs[r].fr, bytes));
+        CK(hipMalloc(&bufs[r].off, (n + 1) * 4ull));
+        CK(hipMalloc(&bufs[r].out, n * 56ull));
+        CK(hipMalloc(&bufs[r].dns, n * 16ull));
+        CK(hipMalloc(&bufs[r].st, sizeof(fb_batch_stats)));
+        CK(hipMemcpy(bufs[r].fr, frames.data(), bytes, hipMemcpyHostToDevice));
+        CK(hipMemcpy(bufs[r].off, offs.data(), (n + 1) * 4ull, hipMemcpyHostToDevice));
+    }
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    uint32_t epoch = 0;
+    auto params = [&](int r) {
+        fbk::ParseParams p;
+        p.frames = bufs[r].fr; p.offsets = bufs[r].off; p.out = bufs[r].out; p.dns = bufs[r].dns;
+        p.cls = nullptr; p.stats = bufs[r].st; p.cfg = dcfg;
+        p.tagg = status; p.wstat = status + units; p.rsum = p.wstat + 2ull * fbk::stat_slots(units);
+        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = units; p.parsed = nullptr;
+        if (++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); CK(hipMemset(err, 0, 16)); epoch = 1; }
+        p.epoch = epoch;
+        p.error = err + (epoch & 1u); p.error_next = err + ((epoch & 1u) ^ 1u); p.dbg = dbg;
+        return p;
+    };
+    uint64_t caps = 0;
+    for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
+    const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;
+    printf("{\"blocks_per_cu_api\": %d, \"cus\": %d, \"units\": %u, \"grid\": %u, \"unit_frames\": %u, \"threads\": %d}\n", bpc,
+           prop.multiProcessorCount, units, grid, fbk::kWsUnit, fbk::kWsThreads);
+    const char* names[] = {"ws", "ws_no_lb", "ws_no_store", "ws_no_lb_st", "read", "copy"};
+    const int NV = 6;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<double> best(NV, 1e30), sum(NV, 0.0);
+    const int rounds = 3;
+    for (int round = 0; round < rounds; ++round) {
+        for (int v = 0; v < NV; ++v) {
+            for (int it = -10; it < iters; ++it) {
+                if (it == 0) CK(hipEventRecord(e0, s));
+                const int r = (it + 100) % R;
+                switch (v) {
+                case 0: hipLaunchKernelGGL((fbk::k_parse_ws<false, 0>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
+                case 1: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoLookback>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
+                case 2: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
+                case 3: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoLookback | fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
+                case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
+                case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+                }
+            }
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = ms * 1e3 / iters;
+            best[v] = std::min(best[v], us);
+            sum[v] += us;
+        }
+    }
+    for (int v = 0; v < NV; ++v) {
+        const double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
+        printf("{\"variant\": \"%s\", \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n", names[v],
+               sum[v] / rounds, best[v], n / (best[v] * 1e3), gbs);
+    }
+    // stamped run
+    CK(hipMemset(dbg, 0, dbg_words * 8));
+    for (int w = 0; w < 3; ++w)
+        hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kStamps>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(w % R));
+    CK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> st(dbg_words);
+    CK(hipMemcpy(st.data(), dbg, dbg_words * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull;
+    for (uint32_t b = 0; b < grid; ++b) t0 = std::min(t0, st[(b * fbk::kWsDbgUnits + fbk::kWsDbgUnits - 1) * 4 + 3]);
+    const uint32_t Kmax = (units + grid - 1) / grid;
+    auto q = [](std::vector<double> v, double fr) {
+        if (v.empty()) return 0.0;
+        std::sort(v.begin(), v.end());
+        return v[(size_t)(fr * (v.size() - 1))];
+    };
+    // per unit k of a block: start (loader wave 0 begins it), staged, INC published, stored
+    {
+        std::vector<double> en, lx, bx, sx;
+        for (uint32_t b = 0; b < grid; ++b) {
+            const unsigned long long* r0 = &st[(b * fbk::kWsDbgUnits + fbk::kWsDbgUnits - 1) * 4];
+            en.push_back((r0[3] - t0) * 0.01); lx.push_back((r0[0] - t0) * 0.01);
+            bx.push_back((r0[1] - t0) * 0.01); sx.push_back((r0[2] - t0) * 0.01);
+        }
+        printf("{\"block\": 1, \"entry_us\": [%.2f, %.2f, %.2f], \"loader_exit\": [%.2f, %.2f, %.2f], \"lb_exit\": [%.2f, %.2f, %.2f], \"storer_exit\": [%.2f, %.2f, %.2f]}\n",
+               q(en, 0), q(en, .5), q(en, 1), q(lx, 0), q(lx, .5), q(lx, 1), q(bx, 0), q(bx, .5), q(bx, 1), q(sx, 0), q(sx, .5), q(sx, 1));
+    }
+    for (uint32_t k = 0; k < std::min<uint32_t>(Kmax, fbk::kWsDbgUnits - 1); ++k) {
+        std::vector<double> start, ld, lb, sto, done;
+        for (uint32_t b = 0; b < grid; ++b) {
+            const unsigned long long* r0 = &st[(b * fbk::kWsDbgUnits + k) * 4];
+            if (!r0[3] || !r0[0] || !r0[1] || !r0[2]) continue;
+            start.push_back((r0[3] - t0) * 0.01);
+            ld.push_back(((double)r0[0] - (double)r0[3]) * 0.01);
+            lb.push_back(((double)r0[1] - (double)r0[0]) * 0.01);
+            sto.push_back(((double)r0[2] - (double)r0[1]) * 0.01);
+            done.push_back((r0[2] - t0) * 0.01);
+        }
+        printf("{\"unit\": %u, \"start_us\": [%.2f, %.2f, %.2f], \"staged_after\": [%.2f, %.2f, %.2f], "
+               "\"inc_after_staged\": [%.2f, %.2f, %.2f], \"stored_after_inc\": [%.2f, %.2f, %.2f], \"stored_at\": [%.2f, %.2f, %.2f]}\n",
+               k, q(start, 0), q(start, .5), q(start, 1), q(ld, 0), q(ld, .5), q(ld, 1), q(lb, 0), q(lb, .5), q(lb, 1),
+               q(sto, 0), q(sto, .5), q(sto, 1), q(done, 0), q(done, .5), q(done, 1));
+    }
+    hipLaunchKernelGGL((fbk::k_parse_ws<false, 0>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(0));
+    CK(hipStreamSynchronize(s));
+    unsigned errw[2] = {0, 0};
+    CK(hipMemcpy(errw, err, 8, hipMemcpyDeviceToHost));
+    fb_batch_stats bs;
+    CK(hipMemcpy(&bs, bufs[0].st, sizeof(bs), hipMemcpyDeviceToHost));
+    printf("{\"config\": %d, \"n\": %u, \"bytes\": %llu, \"rotate\": %d, \"err\": [%u, %u], \"n_session\": %llu, \"n_dns\": %llu, \"stats_error\": %llu}\n",
+           cfg_id, n, (unsigned long long)bytes, R, errw[0], errw[1], (unsigned long long)bs.n_session,
+           (unsigned long long)bs.n_dns, (unsigned long long)bs.error);
+    return 0;
+}
