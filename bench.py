@@ -39,33 +39,46 @@ def algorithmic_bytes(offsets, n_session, n_dns):
     return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
 
 
-def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False):
-    """Time `steps` launches of the hot path.  flow=False: fb_parse_classify_dev.  flow=True (C4):
-    fb_process_dev's two stages -- parse + classify, then the session-table upsert with per-flow
-    counters (fb_flow_update_dev) -- with an event between them so each stage is timed."""
+def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg"):
+    """Time `steps` launches of the hot path.  mode "seg": fb_parse_classify_seg_dev (records
+    compacted per 64-frame wavefront segment, no cross-workgroup dependency); mode "dense":
+    fb_parse_classify_dev (one batch-wide compaction through a decoupled look-back).
+    flow=True (C4): the two stages of fb_process[_seg]_dev -- parse + classify, then the
+    session-table upsert with per-flow counters -- with an event between them so each stage is
+    timed."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n)
     nbytes = frames.nbytes
     stream = N.Stream()
+    nseg = (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES
     bufs = []
     for _ in range(rotate):
         d_fr = N.DeviceBuffer(nbytes).upload(frames)
         d_off = N.DeviceBuffer(offs.nbytes).upload(offs)
-        d_out = N.DeviceBuffer(n * N.PKT_OUT_DTYPE.itemsize)
-        d_dns = N.DeviceBuffer(n * N.DNS_OUT_DTYPE.itemsize)
+        if mode == "seg":
+            d_out = N.DeviceBuffer(nseg * N.SEG_BYTES)
+            d_dns = N.DeviceBuffer(nseg * 4)  # the segment counts
+        else:
+            d_out = N.DeviceBuffer(n * N.PKT_OUT_DTYPE.itemsize)
+            d_dns = N.DeviceBuffer(n * N.DNS_OUT_DTYPE.itemsize)
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
         bufs.append((d_fr, d_off, d_out, d_dns, d_st))
 
-    mid = []
-
     def step(i, ev=None):
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
-        rc = lib.fb_parse_classify_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
-                                       d_st.ptr, stream.ptr)
+        if mode == "seg":
+            rc = lib.fb_parse_classify_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
+                                               d_st.ptr, stream.ptr)
+        else:
+            rc = lib.fb_parse_classify_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
+                                           d_st.ptr, stream.ptr)
         if rc == 0 and flow:
             if ev is not None:
                 ev.record(stream)
-            rc = lib.fb_flow_update_dev(ctx, d_out.ptr, d_st.ptr, stream.ptr)
+            if mode == "seg":
+                rc = lib.fb_flow_update_seg_dev(ctx, d_out.ptr, d_dns.ptr, n, d_st.ptr, stream.ptr)
+            else:
+                rc = lib.fb_flow_update_dev(ctx, d_out.ptr, d_st.ptr, stream.ptr)
         if rc != 0:
             raise RuntimeError(lib.fb_last_error().decode())
 
@@ -238,6 +251,9 @@ def main():
     ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C3) measurement")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (pinned H2D/D2H) measurement")
     ap.add_argument("--no-flow-reduce", action="store_true", help="N>1: skip the C5 global flow-counter exchange")
+    ap.add_argument("--mode", choices=["seg", "dense"], default="seg",
+                    help="output layout: per-wavefront segments (default) or one batch-wide compaction")
+    ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,7 +285,7 @@ def main():
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
     rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
-                        flow=args.config == 4)
+                        flow=args.config == 4, mode=args.mode)
     per_launch_s = main_r["ev_ms"] / 1e3 / args.steps
     achieved = main_r["algo_bytes"] / per_launch_s / 1e9
     value = world * n * args.steps / main_r["elapsed"] / 1e6
@@ -281,9 +297,20 @@ def main():
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
+    if not args.no_other_mode:
+        other = "dense" if args.mode == "seg" else "seg"
+        st_o = max(args.steps // 2, 10)
+        ro = run_config(N, lib, ctx, args.config, n, st_o, max(args.warmup // 2, 2), rotate, rank, world, dist,
+                        flow=args.config == 4, mode=other)
+        plo = ro["ev_ms"] / 1e3 / st_o
+        extra["mode_" + other] = dict(value=round(world * n * st_o / ro["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                                      ms_per_step=round(ro["elapsed"] * 1e3 / st_o, 4),
+                                      roofline_achieved_GBs=round(ro["algo_bytes"] / plo / 1e9, 1),
+                                      roofline_frac=round(ro["algo_bytes"] / plo / 1e9 / HBM_PEAK_GBS, 4))
     if not args.no_imix and args.config == 2:
         steps3 = max(args.steps // 2, 10)
-        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist)
+        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist,
+                        mode=args.mode)
         pl3 = r3["ev_ms"] / 1e3 / steps3
         extra["imix_c3"] = dict(value=round(world * (1 << 20) * steps3 / r3["elapsed"] / 1e6, 2),
                                 unit="Mpackets/s", ms_per_step=round(r3["elapsed"] * 1e3 / steps3, 4),
@@ -332,6 +359,9 @@ def main():
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.config], "frames_per_gpu_per_step": n,
                        "rotated_batches": rotate, "filter": "GlobalOnly",
+                       "output": ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)"
+                                  if args.mode == "seg" else
+                                  "batch-wide compaction (fb_parse_classify_dev)"),
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),

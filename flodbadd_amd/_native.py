@@ -47,6 +47,29 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
 LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
 FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
 
+FB_SEG_FRAMES = 64
+SEG_BYTES = FB_SEG_FRAMES * 56
+
+
+def seg_unpack(out_bytes, seg):
+    """Densify a segmented batch (fb_parse_classify_seg_dev layout, include/flodbadd_gpu.h):
+    returns (SESSION records, DNS records) in packet order, as the dense call would."""
+    out_bytes = np.frombuffer(memoryview(out_bytes), dtype=np.uint8)
+    seg = np.asarray(seg, dtype=np.uint32)
+    recs, dns = [], []
+    for s, w in enumerate(seg.tolist()):
+        cs, cd = w & 0xFFFF, w >> 16
+        base = s * SEG_BYTES
+        if cs:
+            recs.append(out_bytes[base: base + cs * 56].view(PKT_OUT_DTYPE))
+        if cd:
+            tail = out_bytes[base + SEG_BYTES - 16 * cd: base + SEG_BYTES].view(DNS_OUT_DTYPE)
+            dns.append(tail[::-1])
+    r = np.concatenate(recs) if recs else np.zeros(0, dtype=PKT_OUT_DTYPE)
+    d = np.concatenate(dns) if dns else np.zeros(0, dtype=DNS_OUT_DTYPE)
+    return r, d
+
+
 assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 56
 assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 88
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
@@ -87,6 +110,10 @@ GPU_SYMBOLS = [
     ("fb_process_parsed", _I, [_P, _P, _U32, _P, _PU32, _P, _P, _P]),
     ("fb_flow_update_dev", _I, [_P, _P, _P, _P]),
     ("fb_process_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_parse_classify_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_process_parsed_seg_dev", _I, [_P, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
+    ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_count", _I, [_P, _PU64, _P]),
     ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),

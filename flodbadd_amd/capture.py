@@ -159,6 +159,33 @@ class FlodbaddGpuCapture:
             raise N.FbError(code, "device error word %d" % e)
         return BatchResult(out, dns, cls, sd)
 
+    def process_frames_seg(self, frames, offsets, flow=True):
+        """The segmented streaming path (fb_process_seg_dev / fb_parse_classify_seg_dev): same
+        classification and session-table update, records left in per-wavefront segments on the
+        device; returned here densified (packet order) for comparison with process_frames."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n = offsets.size - 1
+        nseg = max((n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES, 1)
+        lib = N.gpu_lib()
+        d_fr = N.DeviceBuffer(max(frames.nbytes, 1)).upload(frames) if frames.nbytes else N.DeviceBuffer(1)
+        d_off = N.DeviceBuffer(offsets.nbytes).upload(offsets)
+        d_out = N.DeviceBuffer(nseg * N.SEG_BYTES)
+        d_seg = N.DeviceBuffer(nseg * 4)
+        d_cls = N.DeviceBuffer(max(n, 1))
+        d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        fn = lib.fb_process_seg_dev if flow else lib.fb_parse_classify_seg_dev
+        N.check(fn(self.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, d_seg.ptr, d_cls.ptr, d_st.ptr, None))
+        sd = stats_dict(d_st.download(np.zeros(1, dtype=N.STATS_DTYPE)))
+        if sd["error"]:
+            e = sd["error"]
+            raise N.FbError(N.FB_ERR_TABLE_FULL if e & 4 else N.FB_ERR_INTERNAL, "device error word %d" % e)
+        seg = d_seg.download(np.zeros(nseg, dtype=np.uint32))
+        raw = d_out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8))
+        out, dns = N.seg_unpack(raw, seg[: (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES])
+        cls = d_cls.download(np.zeros(max(n, 1), dtype=np.uint8), n)[:n]
+        return BatchResult(out, dns, cls, sd)
+
     # ---- session table -----------------------------------------------------------------------
     def flow_count(self):
         n = C.c_uint64(0)

@@ -61,6 +61,7 @@ struct fb_ctx {
     uint32_t epoch = 0;
     // persistent parse kernel: grid = co-resident blocks (halved after a protocol failure)
     uint32_t grid = 0;
+    uint32_t seg_grid = 0;        // streaming segmented kernel: co-resident blocks
     uint32_t* d_error = nullptr;  // [2] error words, indexed by epoch parity
     // flow table
     FlowSlot* d_table = nullptr;
@@ -201,6 +202,9 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
             if (want >= 1 && want < use) use = want;
         }
         c->grid = std::min<uint32_t>((uint32_t)(use * prop.multiProcessorCount), kMaxBlocks);  // FB_BLOCKS_PER_CU: tuning cap
+        int sb = 0;
+        if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
+        c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -311,6 +315,8 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
     p.tagg = c->d_status;
     p.wstat = p.tagg + c->status_tiles;
     p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
+    p.tick = reinterpret_cast<uint32_t*>(p.rsum + rsum_words(c->status_tiles));
+    p.seg = nullptr;
     p.cfg = c->d_cfg;
     p.n = n;
     p.num_tiles = (uint32_t)tiles;
@@ -322,6 +328,85 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
     if (parsed) HIP_TRY(launch_process_parsed(p, grid, s));
     else HIP_TRY(launch_parse_classify(p, grid, s));
     return FB_OK;
+}
+
+// Shared launch of the segmented streaming kernel (frames or parsed packets).
+static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s) {
+    const uint64_t units = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
+    int rc = ensure_status(c, units, s);
+    if (rc) return rc;
+    rc = upload_cfg(c, s);
+    if (rc) return rc;
+    rc = ensure_flow_scratch(c, n, s);
+    if (rc) return rc;
+    c->last_n = n;
+    p.tagg = c->d_status;
+    p.wstat = p.tagg + c->status_tiles;
+    p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
+    p.tick = reinterpret_cast<uint32_t*>(p.rsum + rsum_words(c->status_tiles));
+    p.cfg = c->d_cfg;
+    p.n = n;
+    p.num_tiles = (uint32_t)units;
+    p.epoch = ++c->epoch;
+    p.error = c->d_error + (p.epoch & 1u);
+    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
+    p.dbg = nullptr;
+    const uint32_t waves = parse_seg_block_threads() / 64u;
+    const uint32_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (nseg + waves - 1) / waves));
+    HIP_TRY(launch_parse_seg(p, grid, s));
+    return FB_OK;
+}
+
+int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                              uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,
+                              fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_stats) return set_err(FB_ERR_INVAL, "ctx and d_stats are required");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "frames_bytes must be < 4 GiB");
+    if (n && (!d_offsets || !d_out || !d_seg)) return set_err(FB_ERR_INVAL, "d_offsets, d_out and d_seg are required");
+    if (n && frames_bytes && !d_frames) return set_err(FB_ERR_INVAL, "d_frames is NULL");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
+        return FB_OK;
+    }
+    ParseParams p;
+    p.parsed = nullptr;
+    p.frames = d_frames;
+    p.offsets = d_offsets;
+    p.out = d_out;
+    p.dns = nullptr;
+    p.cls = d_class;
+    p.stats = d_stats;
+    p.seg = d_seg;
+    p.frames_bytes = (uint32_t)frames_bytes;
+    return launch_seg(c, p, n, s);
+}
+
+int fb_process_parsed_seg_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
+                              uint8_t* d_class, fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_stats) return set_err(FB_ERR_INVAL, "ctx and d_stats are required");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (n && (!d_in || !d_out || !d_seg)) return set_err(FB_ERR_INVAL, "d_in, d_out and d_seg are required");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
+        return FB_OK;
+    }
+    ParseParams p;
+    p.parsed = d_in;
+    p.frames = nullptr;
+    p.offsets = nullptr;
+    p.out = d_out;
+    p.dns = nullptr;
+    p.cls = d_class;
+    p.stats = d_stats;
+    p.seg = d_seg;
+    p.frames_bytes = 0;
+    return launch_seg(c, p, n, s);
 }
 
 int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes,
@@ -474,17 +559,18 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
     return FB_OK;
 }
 
-int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_stats, void* stream) {
-    if (!c || !d_recs || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_recs and d_stats are required");
+static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_seg, uint32_t n_slots,
+                       fb_batch_stats* d_stats, hipStream_t s) {
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     DeviceGuard g(c->device);
-    hipStream_t s = (hipStream_t)stream;
-    int rc = ensure_flow_scratch(c, c->last_n, s);
+    int rc = ensure_flow_scratch(c, n_slots, s);
     if (rc) return rc;
-    // the records of the context's last parse launch: at most last_n of them
-    const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)c->last_n + kFlowChunk - 1) / kFlowChunk);
+    // record slots of the batch: at most last_n records (dense) / n_slots slots (segmented)
+    const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_slots + kFlowChunk - 1) / kFlowChunk);
     FlowParams p;
     p.recs = d_recs;
+    p.seg = d_seg;
+    p.n_slots = n_slots;
     p.stats = d_stats;
     p.table = c->d_table;
     p.entries = c->d_entries;
@@ -499,6 +585,30 @@ int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_st
     HIP_TRY(launch_flow_update(p, chunks, s));
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
     return FB_OK;
+}
+
+int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_recs || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_recs and d_stats are required");
+    return flow_update(c, d_recs, nullptr, c->last_n, d_stats, (hipStream_t)stream);
+}
+
+int fb_flow_update_seg_dev(fb_ctx* c, const fb_pkt_out* d_out, const uint32_t* d_seg, uint32_t n,
+                           fb_batch_stats* d_stats, void* stream) {
+    if (!c || !d_out || !d_seg || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_out, d_seg and d_stats are required");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (n == 0) return FB_OK;
+    const uint32_t slots = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES;
+    return flow_update(c, d_out, d_seg, slots, d_stats, (hipStream_t)stream);
+}
+
+int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                       uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class, fb_batch_stats* d_stats,
+                       void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    int rc = fb_parse_classify_seg_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream);
+    if (rc || n == 0) return rc;
+    return fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
 }
 
 int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,

@@ -80,9 +80,14 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
     return t;
 }
 
+// Record slots of the batch: dense -> n_session of the parse launch (read on the device);
+// segmented -> every slot of every segment (invalid slots are skipped by slot_valid).
 __device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
-    const unsigned long long n = P.stats->n_session;  // written by the parse kernel
+    const unsigned long long n = P.seg ? (unsigned long long)P.n_slots : P.stats->n_session;
     return (uint32_t)min(n, (unsigned long long)P.max_recs);
+}
+__device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
+    return !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     extern __shared__ uint32_t hist[];  // [P.parts]
     __shared__ uint32_t wsum[kFlowK1Threads / 64];
     const uint32_t n = batch_records(P);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && P.stats->n_session > (unsigned long long)P.max_recs)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !P.seg && P.stats->n_session > (unsigned long long)P.max_recs)
         atomicOr(P.error, 8u);  // more records than the update scratch holds: the rest is dropped
     const uint32_t base = blockIdx.x * kFlowChunk;
     if (base >= n) return;
@@ -100,6 +105,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     for (uint32_t j = threadIdx.x; j < P.parts; j += kFlowK1Threads) hist[j] = 0u;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
+        if (!slot_valid(P, base + k)) continue;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
         const uint4 a = *reinterpret_cast<const uint4*>(r);
         const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
@@ -125,6 +131,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     __syncthreads();
     FlowEntry* out = P.entries + base;
     for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
+        if (!slot_valid(P, base + k)) continue;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
         const uint4 a = *reinterpret_cast<const uint4*>(r);
         const uint4 b = *reinterpret_cast<const uint4*>(r + 4);

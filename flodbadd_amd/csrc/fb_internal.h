@@ -19,8 +19,12 @@ constexpr uint32_t kMaxBlocks = 4096;
 constexpr uint32_t kMaxEpoch = 255;
 // Stats slots: one pair per block, and a grid never exceeds max(kMaxBlocks, units).
 inline uint64_t stat_slots(uint64_t units) { return units > kMaxBlocks ? units : kMaxBlocks; }
-//   rsum[units]           per-round sums of unit aggregates (round r = units [r*G, (r+1)*G))  [epoch:8 | 0 | n_dns:27 | n_session:28]
-inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + units; }
+//   rsum[rsum_words(units)]  k_parse_ws: per-round sums of unit aggregates (round r = units
+//                          [r*G, (r+1)*G)) [epoch:8 | 0 | n_dns:27 | n_session:28];
+//                          k_parse_seg: 3 epoch-tagged partial-count words per block
+//   tick[64]              k_parse_seg arrival tickets (u32), two epoch-parity sets of 16
+inline uint64_t rsum_words(uint64_t units) { return units > 4ull * kMaxBlocks ? units : 4ull * kMaxBlocks; }
+inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + rsum_words(units) + 64ull; }
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
@@ -50,7 +54,9 @@ struct ParseParams {
     fb_batch_stats* stats;
     unsigned long long* tagg;   // [units]
     unsigned long long* wstat;  // [kMaxBlocks][2]
-    unsigned long long* rsum;   // [rounds] round sums (k_parse_ws look-back)
+    unsigned long long* rsum;   // [rounds] round sums (k_parse_ws look-back) / block partials (k_parse_seg)
+    uint32_t* tick;             // [2][16] arrival tickets (k_parse_seg)
+    uint32_t* seg;              // k_parse_seg: per 64-frame segment, n_session | n_dns << 16
     const DevConfig* cfg;
     uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
     uint32_t n;
@@ -92,6 +98,9 @@ static_assert(sizeof(FlowEntry) == 48, "flow entry is 48 B");
 
 struct FlowParams {
     const fb_pkt_out* recs;
+    const uint32_t* seg;        // non-null: recs are 64-record segments, record slot i valid iff
+                                // (i & 63) < (seg[i >> 6] & 0xFFFF); n_slots slots in all
+    uint32_t n_slots;
     fb_batch_stats* stats;      // n_session read from here; new/updated accumulated
     FlowSlot* table;
     FlowEntry* entries;         // [max_recs]
@@ -109,6 +118,9 @@ struct FlowParams {
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse(int* blocks_per_cu);
+hipError_t launch_parse_seg(const ParseParams& p, uint32_t grid, hipStream_t s);
+hipError_t occupancy_parse_seg(int* blocks_per_cu);
+uint32_t parse_seg_block_threads();
 uint32_t parse_unit_frames();  // frames per look-back unit of the product parse kernel
 uint32_t parse_block_waves();  // waves per block of the product parse kernel
 hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);

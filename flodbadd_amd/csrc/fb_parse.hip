@@ -447,7 +447,7 @@ __device__ unsigned long long lookback_round(const ParseParams& P, uint32_t r, u
 #define FB_WS_SLOTS 5
 #endif
 #ifndef FB_WS_DEPTH
-#define FB_WS_DEPTH 3
+#define FB_WS_DEPTH 2
 #endif
 constexpr int kWsLoad = FB_WS_LOAD;
 constexpr int kWsU = FB_WS_U;
@@ -506,7 +506,8 @@ constexpr uint32_t kWsDbgUnits = 64;
 template <bool PARSED, uint32_t FLAGS = kFlagsProduct>
 __global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
     constexpr int U = kWsU;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t G = gridDim.x, T = P.num_tiles, b = blockIdx.x;
     const uint32_t K = (T - b + G - 1u) / G;  // units of this block (grid <= T, so K >= 1)
     const __amdgpu_buffer_rsrc_t rs =
@@ -788,6 +789,280 @@ __global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
         if (sw == 0u) bstamp(2);
     }
 }
+
+// ============================================================================================
+// k_parse_seg -- streaming parse + classify with per-wavefront compaction (segmented output).
+//
+// The batch is cut into segments of 64 frames (one wavefront); segment sg owns output bytes
+// [sg*3584, (sg+1)*3584) of `out` = 64 record slots.  The wave classifies its 64 frames (one
+// lane per frame), compacts the SESSION records with a ballot prefix-sum into LDS and writes
+// them, in packet order, to the segment's first n_session slots with coalesced 16-B stores (the
+// segment base is 16-B aligned, so no head/tail splits); DNS records (16 B) go to the segment's
+// tail, the j-th at byte (sg+1)*3584 - 16*(j+1).  seg[sg] = n_session | n_dns << 16.  No wave
+// waits for any other: no look-back, no cross-block prefix -- the kernel streams at the rate of
+// its loads and stores.  Consumers (the session-table update, the host wrapper) read the
+// segments through seg[].  Batch stats: per-block partials (epoch-tagged) + arrival tickets
+// sharded by blockIdx % 8; the last arrival sums the partials.
+// ============================================================================================
+#ifndef FB_SEG_WAVES
+#define FB_SEG_WAVES 16
+#endif
+#ifndef FB_SEG_BPC
+#define FB_SEG_BPC 1
+#endif
+constexpr int kSegWaves = FB_SEG_WAVES;
+constexpr int kSegThreads = 64 * kSegWaves;
+constexpr uint32_t kSegBytes = 64u * 56u;  // one segment of output: 64 record slots
+
+// Ablations (tools/ubench_ws.hip): kNoStore drops every store, kNoLookback here means "no
+// classification" (each frame becomes a SESSION record of raw header words).
+template <bool PARSED, uint32_t FLAGS = kFlagsProduct>
+__global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_parse_seg(const ParseParams P) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: segment resources in SGPRs
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t nseg = (P.n + 63u) / 64u;
+    const uint32_t ep = P.epoch;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
+    __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
+    __shared__ unsigned long long s_stage[kSegWaves][64 * 7];
+    __shared__ uint32_t s_acc[11];  // block counters (see the stats section) + wave arrivals
+    const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
+    const unsigned long long lmask = (1ull << lane) - 1ull;
+    unsigned long long* stage = s_stage[wave];
+    // kStamps: P.dbg[(b * kSegWaves + wave) * 16 + slot]: 0 entry, 1 prologue done, 2.. end of
+    // iteration j (j < 12), 14 stats start, 15 exit
+    auto sstamp = [&](uint32_t slot) {
+        if constexpr ((FLAGS & kStamps) != 0u)
+            if (lane == 0u && slot < 16u)
+                P.dbg[((size_t)b * kSegWaves + wave) * 16u + slot] = __builtin_amdgcn_s_memrealtime();
+    };
+    sstamp(0);
+    uint32_t iter = 0;
+    uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
+    if (tid < 11u) s_acc[tid] = 0u;  // published by the prologue barrier
+
+    // One segment per iteration with the next segment's header loads in flight.  Every store of
+    // an iteration is an unconditional buffer store (lanes with nothing to write use an offset
+    // past the resource's end, which the hardware drops), so each iteration issues exactly the
+    // same VMEM sequence -- headers(next), offsets(next+1), 8 stores -- and the compiler's vmcnt
+    // bookkeeping lets the wait for the next headers pass over this iteration's stores.
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t kOob = 0x80000000u;
+    const uint32_t stride = G * kSegWaves;
+    const __amdgpu_buffer_rsrc_t r_seg = __builtin_amdgcn_make_buffer_rsrc(P.seg, (short)0, (int)(nseg * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_cls =
+        __builtin_amdgcn_make_buffer_rsrc(P.cls, (short)0, P.cls ? (int)P.n : 0, 0x00020000);
+    auto vmov = [](uint32_t x) {
+        uint32_t y;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+        return y;
+    };
+    Hdr h;
+    uint2 c = make_uint2(0u, 0u), q = make_uint2(0u, 0u);
+    uint4 pin[4];
+    auto load_q = [&](uint32_t sg) {
+        const uint32_t i = sg * 64u + lane;
+        q = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);
+    };
+    auto load_parsed = [&](uint32_t sg) {
+        const uint4* qq = reinterpret_cast<const uint4*>(P.parsed + min(sg * 64u + lane, P.n - 1u));
+        pin[0] = qq[0];
+        pin[1] = qq[1];
+        pin[2] = qq[2];
+        const uint2 t = *reinterpret_cast<const uint2*>(qq + 3);
+        pin[3] = make_uint4(t.x, t.y, 0u, 0u);
+    };
+    // Prologue: the configuration loads and the first offsets loads are issued together (the
+    // header loads then wait for one round trip, not two), the configuration goes to LDS, and
+    // an LDS-only barrier publishes it while the header loads stay in flight.
+    uint32_t sg = b * kSegWaves + wave;
+    constexpr uint32_t kCfg16 = kCfgLdsBytes / 16, kCfgIt = (kCfg16 + kSegThreads - 1) / kSegThreads;
+    uint4 cfgv[kCfgIt];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
+#pragma unroll
+        for (uint32_t it = 0; it < kCfgIt; ++it) cfgv[it] = src[min(tid + it * kSegThreads, kCfg16 - 1u)];
+    }
+    if constexpr (!PARSED) load_q(sg);
+    else load_parsed(sg);
+#pragma unroll
+    for (uint32_t it = 0; it < kCfgIt; ++it)
+        if (tid + it * kSegThreads < kCfg16) s_cfg4[tid + it * kSegThreads] = cfgv[it];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
+        constexpr uint32_t kLanOff = offsetof(DevConfig, lan_v6) / 16, kOwnOff = offsetof(DevConfig, own) / 16;
+        const uint32_t nl = P.cfg->n_lan_v6 * (sizeof(LanV6) / 16), no = P.cfg->n_own * (sizeof(fb_ip) / 16);
+        for (uint32_t k = tid; k < nl; k += kSegThreads) s_cfg4[kLanOff + k] = src[kLanOff + k];
+        for (uint32_t k = tid; k < no; k += kSegThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
+        if (b == 0u && tid == 0u) *P.error_next = 0u;  // other parity's word, for the next launch
+    }
+    if constexpr (!PARSED) {
+        load_headers1(rs, q.x, h);
+        c = make_uint2(vmov(q.x), vmov(q.y));
+        load_q(sg + stride);
+    }
+    // 8 dropped stores: the loop entry then has the same VMEM history as its back edge (the
+    // iteration's 8 stores behind the prefetch), so the compiler does not merge a shorter
+    // history into the loop and wait for the stores of the previous iteration.
+    if constexpr ((FLAGS & kNoStore) == 0u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_seg, kOob + 64u * j, 0, 0);
+    }
+    ws_tick();  // configuration in LDS (LDS-only barrier: the header loads stay in flight)
+    sstamp(1);
+    for (; sg < nseg; sg += stride) {
+        const uint32_t i = sg * 64u + lane;
+        const bool valid = i < P.n;
+        Pkt kk;
+        if constexpr ((FLAGS & kNoLookback) != 0u) {
+            kk.cls = FB_CLASS_SESSION;
+            kk.tcp = kk.v4 = true;
+            kk.bad = false;
+            const uint32_t hw[14] = {h.A.x, h.A.y, h.A.z, h.A.w, h.B.x, h.B.y, h.B.z, h.B.w, h.C.x, h.C.y, h.C.z, h.C.w, h.Dz, c.x};
+#pragma unroll
+            for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
+        } else if constexpr (!PARSED) {
+            process_frame(rs, cfg, cfg, h, valid ? c.x : 1u, valid ? c.y : 0u, P.frames_bytes, i, kk);
+        } else {
+            const uint4 a = pin[0], bb = pin[1], cc = pin[2], d = pin[3];
+            const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {bb.x, bb.y, bb.z, bb.w};
+            const uint32_t proto = cc.y & 0xffu, fam = (cc.y >> 8) & 0xffu;
+            kk.bad = false;
+            kk.cls = FB_CLASS_DROP;
+            kk.tcp = kk.v4 = false;
+            if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
+                classify_session(cfg, cfg, proto, fam, src, dst, cc.x & 0xffffu, cc.x >> 16, (d.x >> 8) & 1u,
+                                 d.x & 0xffu, cc.z, cc.w, d.y, kk);
+        }
+        const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
+        const bool is_d = valid && kk.cls == FB_CLASS_DNS;
+        const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
+        const bool counted = is_s || is_f;
+        const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+        const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
+        if (is_s) {
+            unsigned long long* dd = stage + (size_t)__popcll(m_sess & lmask) * 7;
+#pragma unroll
+            for (int w = 0; w < 7; ++w)
+                dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // prefetch: headers of the next segment (offsets already here), offsets of the one after
+        if constexpr (!PARSED) {
+            load_headers1(rs, q.x, h);
+            c = make_uint2(vmov(q.x), vmov(q.y));
+            load_q(sg + 2u * stride);
+        } else {
+            load_parsed(sg + stride);
+        }
+        if constexpr ((FLAGS & kNoStore) == 0u) {
+        // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
+            const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint8_t*>(P.out) + (size_t)sg * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
+            const uint32_t words = cs * 7u, body = words >> 1;
+    #pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t cc = lane + 64u * j;
+                const uint32_t src = min(cc, 223u);
+                const unsigned long long x = stage[2u * src], y = stage[2u * src + 1u];
+                const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? cc * 16u : kOob, 0, 0);
+            }
+            {
+                const bool tail = (words & 1u) && lane == 0u;
+                const unsigned long long x = stage[words ? words - 1u : 0u];
+                const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(v, r_out, tail ? (words - 1u) * 8u : kOob, 0, 0);
+            }
+            {
+                const u32x4 v = {kk.w[0], kk.w[1], kk.w[2], kk.w[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    v, r_out, is_d ? kSegBytes - 16u * (1u + (uint32_t)__popcll(m_dns & lmask)) : kOob, 0, 0);
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? sg * 4u : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
+        a_s += cs;
+        a_d += cd;
+        a_f += __popcll(__ballot(is_f));
+        a_t += __popcll(__ballot(counted && kk.tcp));
+        a_4 += __popcll(__ballot(counted && kk.v4));
+        a_b += __popcll(__ballot(valid && kk.bad));
+        a_n += __popcll(__ballot(valid));
+        sstamp(2u + min(iter++, 11u));
+    }
+    sstamp(14);
+    // ---- batch stats, no barrier and no partials read-back:
+    // every wave adds its counters into LDS; the block's last wave (LDS arrival count) adds the
+    // block's counters into 5 packed device words [ticket:10 | hi:27 | lo:27] (one atomic per
+    // word, lanes 0-4 in parallel); the block whose add brings a word's ticket to G owns that
+    // word's final totals (old + its own add), writes those two stats fields and zeroes the word
+    // for the next launch.  The derived counts (total, udp, ipv6, drop) are linear, so they are
+    // counted per wave and summed like the others.
+    {
+        const uint32_t a_tot = a_s + a_f;
+        const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
+        if (lane < 10u) {
+            uint32_t v = 0u;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
+            __hip_atomic_fetch_add(&s_acc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t arrived = 0u;
+        if (lane == 0u) arrived = __hip_atomic_fetch_add(&s_acc[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        arrived = __shfl(arrived, 0, 64);
+        if (arrived == (uint32_t)kSegWaves - 1u && lane < 5u) {
+            asm volatile("" ::: "memory");
+            const unsigned long long lo = s_acc[2u * lane], hi = s_acc[2u * lane + 1u];
+            unsigned long long* word = reinterpret_cast<unsigned long long*>(P.tick) + lane;
+            const unsigned long long add = (1ull << 54) | (hi << 27) | lo;
+            const unsigned long long old = __hip_atomic_fetch_add(word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((old >> 54) == (unsigned long long)G - 1u) {
+                const unsigned long long t = old + add, m27 = (1ull << 27) - 1ull;
+                const unsigned long long f_lo = t & m27, f_hi = (t >> 27) & m27;
+                __hip_atomic_store(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fb_batch_stats* S = P.stats;
+                if (S) {
+                    if (lane == 0u) {
+                        S->n_session = f_lo;
+                        S->n_filtered = f_hi;
+                        S->new_sessions = 0ull;
+                        S->updated_sessions = 0ull;
+                        S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
+                    } else if (lane == 1u) {
+                        S->n_dns = f_lo;
+                        S->bad_offsets = f_hi;
+                    } else if (lane == 2u) {
+                        S->tcp_processed = f_lo;
+                        S->udp_processed = f_hi;
+                    } else if (lane == 3u) {
+                        S->ipv4_processed = f_lo;
+                        S->ipv6_processed = f_hi;
+                    } else {
+                        S->total_processed = f_lo;
+                        S->n_drop = f_hi;
+                    }
+                }
+            }
+        }
+    }
+    sstamp(15);
+}
+
+hipError_t launch_parse_seg(const ParseParams& p, uint32_t grid, hipStream_t s) {
+    if (p.parsed) hipLaunchKernelGGL((k_parse_seg<true>), dim3(grid), dim3(kSegThreads), 0, s, p);
+    else hipLaunchKernelGGL((k_parse_seg<false>), dim3(grid), dim3(kSegThreads), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t occupancy_parse_seg(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (k_parse_seg<false>), kSegThreads, 0);
+}
+uint32_t parse_seg_block_threads() { return kSegThreads; }
 
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s) {
     hipLaunchKernelGGL((k_parse_ws<false>), dim3(grid), dim3(kWsThreads), 0, s, p);

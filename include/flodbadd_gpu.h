@@ -272,6 +272,36 @@ int fb_process_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                    const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns,
                    uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
 
+/*
+ * Segmented output (one wavefront-compacted segment per FB_SEG_FRAMES frames; no cross-segment
+ * compaction, so the kernel streams with no inter-workgroup dependency).  Segment s holds the
+ * frames [64s, 64s+64) and owns d_out records [64s, 64s+64) (3584 bytes):
+ *   - its SESSION records, packet order, in records [64s, 64s + n_session(s))
+ *   - its DNS side records (fb_dns_out, 16 B), packet order, the j-th at byte offset
+ *     (s+1)*3584 - 16*(j+1) of d_out (packed at the segment's tail)
+ *   - d_seg[s] = n_session(s) | n_dns(s) << 16; the other bytes are left unwritten.
+ * d_out needs room for ceil(n/64)*64 records, d_seg for ceil(n/64) words.  Same classification,
+ * record layout and stats as fb_parse_classify_dev (which compacts across the whole batch).
+ * DEVICE pointers, asynchronous.  d_class may be NULL; d_stats is required.
+ */
+#define FB_SEG_FRAMES 64u
+int fb_parse_classify_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
+                              const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out,
+                              uint32_t* d_seg, uint8_t* d_class, fb_batch_stats* d_stats,
+                              void* stream);
+/* fb_process_parsed_dev with segmented output (same segment layout; no DNS records). */
+int fb_process_parsed_seg_dev(fb_ctx* ctx, const fb_parsed_pkt* d_in, uint32_t n,
+                              fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,
+                              fb_batch_stats* d_stats, void* stream);
+/* Flow-table upsert of the SESSION records of a segmented batch of n frames (d_out / d_seg of
+ * fb_parse_classify_seg_dev or fb_process_parsed_seg_dev); new/updated ADDED into d_stats. */
+int fb_flow_update_seg_dev(fb_ctx* ctx, const fb_pkt_out* d_out, const uint32_t* d_seg, uint32_t n,
+                           fb_batch_stats* d_stats, void* stream);
+/* fb_parse_classify_seg_dev followed by fb_flow_update_seg_dev on the same stream. */
+int fb_process_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
+                       const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
+                       uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+
 int fb_flow_count(fb_ctx* ctx, uint64_t* n_flows, void* stream); /* synchronous */
 /* Copy every flow (slot order) to host memory; *n = flows written (<= cap). Synchronous. */
 int fb_flow_export(fb_ctx* ctx, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream);

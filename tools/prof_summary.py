@@ -17,7 +17,7 @@ import sqlite3
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PARSE_KERNEL = "k_parse_ws"
+PARSE_KERNEL = "k_parse_seg"
 
 
 def db_of(d):
@@ -58,8 +58,12 @@ def main():
     ap.add_argument("--trace")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--kernel", default=None, help="substring of the dominant kernel's name (default k_parse_seg)")
     ap.add_argument("--algo-bytes", type=float, default=None, help="algorithmic bytes per launch (bench line)")
     a = ap.parse_args()
+    global PARSE_KERNEL
+    if a.kernel:
+        PARSE_KERNEL = a.kernel
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     if a.trace:
         st = kernel_stats(a.trace)

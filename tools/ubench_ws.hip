@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < R; ++r) {
         CK(hipMalloc(&bufs[r].fr, bytes));
         CK(hipMalloc(&bufs[r].off, (n + 1) * 4ull));
-        CK(hipMalloc(&bufs[r].out, n * 56ull));
+        CK(hipMalloc(&bufs[r].out, ((n + 63) / 64) * 3584ull));
         CK(hipMalloc(&bufs[r].dns, n * 16ull));
         CK(hipMalloc(&bufs[r].st, sizeof(fb_batch_stats)));
         CK(hipMemcpy(bufs[r].fr, frames.data(), bytes, hipMemcpyHostToDevice));
@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
         fbk::ParseParams p;
         p.frames = bufs[r].fr; p.offsets = bufs[r].off; p.out = bufs[r].out; p.dns = bufs[r].dns;
         p.cls = nullptr; p.stats = bufs[r].st; p.cfg = dcfg;
-        p.tagg = status; p.wstat = status + units; p.rsum = p.wstat + 2ull * fbk::stat_slots(units);
+        p.tagg = status; p.wstat = status + units; p.rsum = p.wstat + 2ull * fbk::stat_slots(units); p.tick = reinterpret_cast<uint32_t*>(p.rsum + fbk::rsum_words(units)); p.seg = nullptr;
         p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = units; p.parsed = nullptr;
         if (++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); CK(hipMemset(err, 0, 16)); epoch = 1; }
         p.epoch = epoch;
@@ -132,8 +132,17 @@ int main(int argc, char** argv) {
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;
     printf("{\"blocks_per_cu_api\": %d, \"cus\": %d, \"units\": %u, \"grid\": %u, \"unit_frames\": %u, \"threads\": %d}\n", bpc,
            prop.multiProcessorCount, units, grid, fbk::kWsUnit, fbk::kWsThreads);
-    const char* names[] = {"ws", "ws_no_lb", "ws_no_store", "ws_no_lb_st", "read", "copy"};
-    const int NV = 6;
+    const char* names[] = {"ws", "ws_no_lb", "ws_no_store", "ws_no_lb_st", "read", "copy", "seg", "seg_no_store",
+                           "seg_no_classify", "seg_no_classify_no_store"};
+    const int NV = 10;
+    int sbpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&sbpc, (fbk::k_parse_seg<false>), fbk::kSegThreads, 0));
+    const uint32_t nseg = (n + 63) / 64;
+    const uint32_t sgrid = std::min<uint32_t>((uint32_t)(sbpc * prop.multiProcessorCount),
+                                              (nseg + fbk::kSegWaves - 1) / fbk::kSegWaves);
+    uint32_t* dseg;
+    CK(hipMalloc(&dseg, nseg * 4ull));
+    printf("{\"seg_blocks_per_cu\": %d, \"seg_grid\": %u}\n", sbpc, sgrid);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -150,6 +159,13 @@ int main(int argc, char** argv) {
                 case 2: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
                 case 3: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoLookback | fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
                 case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
+                case 6: case 7: case 8: case 9: {
+                    fbk::ParseParams pp = params(r); pp.seg = dseg; pp.dns = nullptr;
+                    if (v == 6) hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+                    if (v == 7) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+                    if (v == 8) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+                    if (v == 9) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+                } break;
                 case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
                 }
             }
@@ -166,6 +182,45 @@ int main(int argc, char** argv) {
         const double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
         printf("{\"variant\": \"%s\", \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n", names[v],
                sum[v] / rounds, best[v], n / (best[v] * 1e3), gbs);
+    }
+    {   // stamped seg run
+        unsigned long long* sd;
+        const size_t sw = (size_t)sgrid * fbk::kSegWaves * 16;
+        CK(hipMalloc(&sd, sw * 8));
+        CK(hipMemset(sd, 0, sw * 8));
+        for (int w = 0; w < 3; ++w) {
+            fbk::ParseParams pp = params(w % R); pp.seg = dseg; pp.dns = nullptr; pp.dbg = sd;
+            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+        }
+        CK(hipStreamSynchronize(s));
+        std::vector<unsigned long long> st2(sw);
+        CK(hipMemcpy(st2.data(), sd, sw * 8, hipMemcpyDeviceToHost));
+        unsigned long long z = ~0ull;
+        for (size_t w = 0; w < sw / 16; ++w) if (st2[w * 16]) z = std::min(z, st2[w * 16]);
+        auto qq = [](std::vector<double> v, double fr) { if (v.empty()) return 0.0; std::sort(v.begin(), v.end()); return v[(size_t)(fr * (v.size() - 1))]; };
+        for (int slot = 0; slot < 16; ++slot) {
+            std::vector<double> v;
+            for (size_t w = 0; w < sw / 16; ++w) if (st2[w * 16 + slot]) v.push_back((st2[w * 16 + slot] - z) * 0.01);
+            if (v.empty()) continue;
+            printf("{\"seg_slot\": %d, \"n\": %zu, \"us\": [%.2f, %.2f, %.2f, %.2f]}\n", slot, v.size(), qq(v, 0), qq(v, .5), qq(v, .9), qq(v, 1));
+        }
+        // slot-1 (prologue done) by XCD (b % 8) and by dispatch third (b * 3 / grid)
+        for (int key = 0; key < 2; ++key) {
+            const int nk = key == 0 ? 8 : 3;
+            for (int k = 0; k < nk; ++k) {
+                std::vector<double> v, e;
+                for (size_t w = 0; w < sw / 16; ++w) {
+                    const size_t b = w / fbk::kSegWaves;
+                    const int kk = key == 0 ? (int)(b % 8) : (int)(b * 3 / sgrid);
+                    if (kk != k || !st2[w * 16 + 1]) continue;
+                    v.push_back((st2[w * 16 + 1] - z) * 0.01);
+                    e.push_back((st2[w * 16 + 15] - z) * 0.01);
+                }
+                printf("{\"by\": \"%s\", \"k\": %d, \"prologue_us\": [%.2f, %.2f, %.2f], \"exit_us\": [%.2f, %.2f, %.2f]}\n",
+                       key == 0 ? "xcd" : "third", k, qq(v, 0), qq(v, .5), qq(v, 1), qq(e, 0), qq(e, .5), qq(e, 1));
+            }
+        }
+        CK(hipFree(sd));
     }
     // stamped run
     CK(hipMemset(dbg, 0, dbg_words * 8));
