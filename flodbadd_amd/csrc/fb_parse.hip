@@ -810,7 +810,11 @@ __global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
 #ifndef FB_SEG_BPC
 #define FB_SEG_BPC 1
 #endif
+#ifndef FB_SEG_DEPTH
+#define FB_SEG_DEPTH 1
+#endif
 constexpr int kSegWaves = FB_SEG_WAVES;
+constexpr int kSegDepth = FB_SEG_DEPTH;  // segments of header loads in flight per wave
 constexpr int kSegThreads = 64 * kSegWaves;
 constexpr uint32_t kSegBytes = 64u * 56u;  // one segment of output: 64 record slots
 
@@ -859,12 +863,34 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
         return y;
     };
-    Hdr h;
-    uint2 c = make_uint2(0u, 0u), q = make_uint2(0u, 0u);
+    // kSegDepth segments of header loads in flight per wave: set d (headers h, the segment's
+    // offsets c, and q = the offsets of the set's next segment) serves the wave's segments
+    // d, d+D, d+2D, ... (loop unrolled by D, so no set is indexed at run time).  After a
+    // segment: X.h <- headers of the set's next segment from X.q, X.c <- X.q (explicit v_mov:
+    // no back-edge copy of a pending load), X.q <- offsets of the one after.  Every step issues
+    // the same VMEM sequence (4 header loads, 2 offset loads, 8 stores) and the prologue mirrors
+    // it with dropped stores, so the compiler's vmcnt waits let D-1 younger steps' traffic pass.
+    constexpr int D = kSegDepth;
+    struct Set {
+        Hdr h;
+        uint2 c, q;
+    };
+    Set SS[D];
     uint4 pin[4];
-    auto load_q = [&](uint32_t sg) {
+    auto load_q = [&](uint32_t sg, uint2& q) {
         const uint32_t i = sg * 64u + lane;
         q = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);
+    };
+    auto fetch = [&](Set& X, uint32_t next_q) {
+        load_headers1(rs, X.q.x, X.h);
+        X.c = make_uint2(vmov(X.q.x), vmov(X.q.y));
+        load_q(next_q, X.q);
+    };
+    auto dropped_stores = [&]() {
+        if constexpr ((FLAGS & kNoStore) == 0u) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_seg, kOob + 64u * j, 0, 0);
+        }
     };
     auto load_parsed = [&](uint32_t sg) {
         const uint4* qq = reinterpret_cast<const uint4*>(P.parsed + min(sg * 64u + lane, P.n - 1u));
@@ -885,8 +911,12 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 #pragma unroll
         for (uint32_t it = 0; it < kCfgIt; ++it) cfgv[it] = src[min(tid + it * kSegThreads, kCfg16 - 1u)];
     }
-    if constexpr (!PARSED) load_q(sg);
-    else load_parsed(sg);
+    if constexpr (!PARSED) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) load_q(sg + d * stride, SS[d].q);
+    } else {
+        load_parsed(sg);
+    }
 #pragma unroll
     for (uint32_t it = 0; it < kCfgIt; ++it)
         if (tid + it * kSegThreads < kCfg16) s_cfg4[tid + it * kSegThreads] = cfgv[it];
@@ -899,101 +929,101 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         if (b == 0u && tid == 0u) *P.error_next = 0u;  // other parity's word, for the next launch
     }
     if constexpr (!PARSED) {
-        load_headers1(rs, q.x, h);
-        c = make_uint2(vmov(q.x), vmov(q.y));
-        load_q(sg + stride);
-    }
-    // 8 dropped stores: the loop entry then has the same VMEM history as its back edge (the
-    // iteration's 8 stores behind the prefetch), so the compiler does not merge a shorter
-    // history into the loop and wait for the stores of the previous iteration.
-    if constexpr ((FLAGS & kNoStore) == 0u) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_seg, kOob + 64u * j, 0, 0);
+        for (int d = 0; d < D; ++d) {
+            fetch(SS[d], sg + (uint32_t)(d + D) * stride);
+            dropped_stores();
+        }
+    } else {
+        dropped_stores();
     }
     ws_tick();  // configuration in LDS (LDS-only barrier: the header loads stay in flight)
     sstamp(1);
-    for (; sg < nseg; sg += stride) {
-        const uint32_t i = sg * 64u + lane;
-        const bool valid = i < P.n;
-        Pkt kk;
-        if constexpr ((FLAGS & kNoLookback) != 0u) {
-            kk.cls = FB_CLASS_SESSION;
-            kk.tcp = kk.v4 = true;
-            kk.bad = false;
-            const uint32_t hw[14] = {h.A.x, h.A.y, h.A.z, h.A.w, h.B.x, h.B.y, h.B.z, h.B.w, h.C.x, h.C.y, h.C.z, h.C.w, h.Dz, c.x};
-#pragma unroll
-            for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
-        } else if constexpr (!PARSED) {
-            process_frame(rs, cfg, cfg, h, valid ? c.x : 1u, valid ? c.y : 0u, P.frames_bytes, i, kk);
-        } else {
-            const uint4 a = pin[0], bb = pin[1], cc = pin[2], d = pin[3];
-            const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {bb.x, bb.y, bb.z, bb.w};
-            const uint32_t proto = cc.y & 0xffu, fam = (cc.y >> 8) & 0xffu;
-            kk.bad = false;
-            kk.cls = FB_CLASS_DROP;
-            kk.tcp = kk.v4 = false;
-            if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
-                classify_session(cfg, cfg, proto, fam, src, dst, cc.x & 0xffffu, cc.x >> 16, (d.x >> 8) & 1u,
-                                 d.x & 0xffu, cc.z, cc.w, d.y, kk);
-        }
-        const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
-        const bool is_d = valid && kk.cls == FB_CLASS_DNS;
-        const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
-        const bool counted = is_s || is_f;
-        const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
-        const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
-        if (is_s) {
-            unsigned long long* dd = stage + (size_t)__popcll(m_sess & lmask) * 7;
-#pragma unroll
-            for (int w = 0; w < 7; ++w)
-                dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
-        }
-        __builtin_amdgcn_wave_barrier();
-        // prefetch: headers of the next segment (offsets already here), offsets of the one after
-        if constexpr (!PARSED) {
-            load_headers1(rs, q.x, h);
-            c = make_uint2(vmov(q.x), vmov(q.y));
-            load_q(sg + 2u * stride);
-        } else {
-            load_parsed(sg + stride);
-        }
-        if constexpr ((FLAGS & kNoStore) == 0u) {
-        // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
-            const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<uint8_t*>(P.out) + (size_t)sg * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
-            const uint32_t words = cs * 7u, body = words >> 1;
+    auto step = [&](uint32_t sg, Set& X) {
+            const uint32_t i = sg * 64u + lane;
+            const bool valid = i < P.n;
+            Pkt kk;
+            if constexpr ((FLAGS & kNoLookback) != 0u) {
+                kk.cls = FB_CLASS_SESSION;
+                kk.tcp = kk.v4 = true;
+                kk.bad = false;
+                const uint32_t hw[14] = {X.h.A.x, X.h.A.y, X.h.A.z, X.h.A.w, X.h.B.x, X.h.B.y, X.h.B.z, X.h.B.w, X.h.C.x, X.h.C.y, X.h.C.z, X.h.C.w, X.h.Dz, X.c.x};
     #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t cc = lane + 64u * j;
-                const uint32_t src = min(cc, 223u);
-                const unsigned long long x = stage[2u * src], y = stage[2u * src + 1u];
-                const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? cc * 16u : kOob, 0, 0);
+                for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
+            } else if constexpr (!PARSED) {
+                process_frame(rs, cfg, cfg, X.h, valid ? X.c.x : 1u, valid ? X.c.y : 0u, P.frames_bytes, i, kk);
+            } else {
+                const uint4 a = pin[0], bb = pin[1], cc = pin[2], d = pin[3];
+                const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {bb.x, bb.y, bb.z, bb.w};
+                const uint32_t proto = cc.y & 0xffu, fam = (cc.y >> 8) & 0xffu;
+                kk.bad = false;
+                kk.cls = FB_CLASS_DROP;
+                kk.tcp = kk.v4 = false;
+                if ((proto == 6u || proto == 17u) && (fam == 2u || fam == 10u))
+                    classify_session(cfg, cfg, proto, fam, src, dst, cc.x & 0xffffu, cc.x >> 16, (d.x >> 8) & 1u,
+                                     d.x & 0xffu, cc.z, cc.w, d.y, kk);
             }
-            {
-                const bool tail = (words & 1u) && lane == 0u;
-                const unsigned long long x = stage[words ? words - 1u : 0u];
-                const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b64(v, r_out, tail ? (words - 1u) * 8u : kOob, 0, 0);
+            const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
+            const bool is_d = valid && kk.cls == FB_CLASS_DNS;
+            const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
+            const bool counted = is_s || is_f;
+            const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+            const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
+            if (is_s) {
+                unsigned long long* dd = stage + (size_t)__popcll(m_sess & lmask) * 7;
+    #pragma unroll
+                for (int w = 0; w < 7; ++w)
+                    dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
             }
-            {
-                const u32x4 v = {kk.w[0], kk.w[1], kk.w[2], kk.w[3]};
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    v, r_out, is_d ? kSegBytes - 16u * (1u + (uint32_t)__popcll(m_dns & lmask)) : kOob, 0, 0);
+            __builtin_amdgcn_wave_barrier();
+            // prefetch: headers of this set's next segment (offsets already here), offsets of the
+            // one after
+            if constexpr (!PARSED) fetch(X, sg + 2u * D * stride);
+            else load_parsed(sg + stride);
+            if constexpr ((FLAGS & kNoStore) == 0u) {
+            // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
+                const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<uint8_t*>(P.out) + (size_t)sg * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
+                const uint32_t words = cs * 7u, body = words >> 1;
+        #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t cc = lane + 64u * j;
+                    const uint32_t src = min(cc, 223u);
+                    const unsigned long long x = stage[2u * src], y = stage[2u * src + 1u];
+                    const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? cc * 16u : kOob, 0, 0);
+                }
+                {
+                    const bool tail = (words & 1u) && lane == 0u;
+                    const unsigned long long x = stage[words ? words - 1u : 0u];
+                    const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
+                    __builtin_amdgcn_raw_buffer_store_b64(v, r_out, tail ? (words - 1u) * 8u : kOob, 0, 0);
+                }
+                {
+                    const u32x4 v = {kk.w[0], kk.w[1], kk.w[2], kk.w[3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        v, r_out, is_d ? kSegBytes - 16u * (1u + (uint32_t)__popcll(m_dns & lmask)) : kOob, 0, 0);
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? sg * 4u : kOob, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
             }
-            __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? sg * 4u : kOob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
-        }
-        __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
-        a_s += cs;
-        a_d += cd;
-        a_f += __popcll(__ballot(is_f));
-        a_t += __popcll(__ballot(counted && kk.tcp));
-        a_4 += __popcll(__ballot(counted && kk.v4));
-        a_b += __popcll(__ballot(valid && kk.bad));
-        a_n += __popcll(__ballot(valid));
-        sstamp(2u + min(iter++, 11u));
+            __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
+            a_s += cs;
+            a_d += cd;
+            a_f += __popcll(__ballot(is_f));
+            a_t += __popcll(__ballot(counted && kk.tcp));
+            a_4 += __popcll(__ballot(counted && kk.v4));
+            a_b += __popcll(__ballot(valid && kk.bad));
+            a_n += __popcll(__ballot(valid));
+            sstamp(2u + min(iter++, 11u));
+    };
+    for (; sg + (uint32_t)(D - 1) * stride < nseg; sg += (uint32_t)D * stride) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) step(sg + d * stride, SS[d]);
     }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d)
+        if (sg + d * stride < nseg) step(sg + d * stride, SS[d]);
     sstamp(14);
     // ---- batch stats, no barrier and no partials read-back:
     // every wave adds its counters into LDS; the block's last wave (LDS arrival count) adds the
