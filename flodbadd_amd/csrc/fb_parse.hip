@@ -1,4 +1,6 @@
-// fb_parse.hip -- gfx950 parse + classify kernel (persistent, wave-level lag-1 pipeline).
+// fb_parse.hip -- gfx950 parse + classify kernels: k_parse_seg (streaming, per-wavefront
+// compaction into 64-frame output segments) and k_parse_ws (role-specialised pipeline with one
+// batch-wide compaction).
 //
 // One wavefront lane per frame.  Replaces, per frame:
 //   parse_packet_pcap                 src/packets.rs:603-802 (pnet_packet 0.35.0 decode)
@@ -8,27 +10,11 @@
 //   PACKET_STATS pre-filter counters  src/packets.rs:211-227
 //   map_tcp_flags (history char)      src/packets.rs:561-601
 //
-// Output is stream-compacted in packet order (SESSION records, DNS side records), so each tile
-// needs the global count of records emitted before it: a decoupled look-back.  Measured on a
-// one-tile-per-block kernel (C2, 1M x 64 B): 45 us, 14 us of it look-back waits, because all
-// resident blocks load, then all wait, then all store, with HBM idle during the wait.
-//
-// Here every WAVE is an independent agent with no block barrier in its loop:
-//   grid = co-resident blocks of 4 waves; wave w (of W) owns wave-tiles w, w+W, w+2W, ...
-//   (a wave-tile = 64*R frames; static ownership, no ticket atomics: every tile a look-back
-//   waits on belongs to a running wave because the grid never exceeds residency).
-//   iteration: wait headers(cur) -> decode/classify into registers -> publish cur's count
-//              -> probe the look-back words of PREV (the wave's previous tile, classified one
-//                 iteration ago, so its predecessors are normally published by now)
-//              -> issue header loads of next and offset loads of the tile after (younger than
-//                 the probes, so the probes do not wait for them)
-//              -> finish the look-back (all not-ready lanes re-poll together) -> store prev's
-//                 records with coalesced 16-B stores from the wave's LDS stage -> stage cur.
-//   HBM sees one tile of header loads per wave in flight across the look-back and the stores.
-//
-// Loads: four unaligned 16-B header loads per frame at frame offsets 10, 26, 42 (+ one dword at
-// 66 for IPv6/TCP) so every decoder field sits at a fixed dword/byte position; buffer loads are
-// range-checked against frames_bytes, so nothing reads past the batch.
+// Both kernels share the device functions below (header decode, classification, history char)
+// and differ only in how the emitted records are laid out.  Loads: four unaligned header loads
+// per frame at frame offsets 10, 26, 42 (16 B) and 66 (4 B) so every decoder field sits at a
+// fixed dword/byte position; buffer loads are range-checked against frames_bytes, so nothing
+// reads past the batch.
 #include "fb_internal.h"
 
 namespace fbk {
