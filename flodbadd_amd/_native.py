@@ -12,7 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 GPU_LIB_PATH = os.path.join(PKG, "libflodbadd_gpu.so")
 SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
 
-FB_ABI_VERSION = 1
+FB_ABI_VERSION = 2
 FB_MAX_BATCH_PACKETS = (1 << 27) - 1
 FB_MAX_LAN_V6 = 64
 FB_MAX_OWN_IPS = 64
@@ -43,7 +43,14 @@ STATS_FIELDS = ["total_processed", "tcp_processed", "udp_processed", "ipv4_proce
 STATS_DTYPE = np.dtype([(f, "<u8") for f in STATS_FIELDS])
 FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
     ("outbound_bytes", "<u8"), ("inbound_bytes", "<u8"), ("orig_pkts", "<u8"), ("resp_pkts", "<u8"),
-    ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8")])
+    ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8"),
+    ("first_seen", "<u8"), ("last_seen", "<u8"), ("end_seen", "<u8"), ("hist_len", "<u4"),
+    ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("reserved1", "<u4")])
+# fb_flow_rec positions: (update call << 32) | pkt_index; FB_SEEN_NONE = None
+FB_SEEN_NONE = (1 << 64) - 1
+FB_HIST_CHARS = "SsHhFfRr><Aa-"
+# fb_conn_state -> determine_conn_state string (src/packets.rs:539-559); 0 = None
+CONN_STATES = {0: None, 1: "SF", 2: "S0", 3: "REJ", 4: "S1", 5: "-"}
 LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
 FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
 
@@ -71,7 +78,7 @@ def seg_unpack(out_bytes, seg):
 
 
 assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 56
-assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 88
+assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 128
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
 
 
@@ -114,6 +121,7 @@ GPU_SYMBOLS = [
     ("fb_process_parsed_seg_dev", _I, [_P, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_flow_history_dev", _I, [_P, _P, _P, _P, _P]),
     ("fb_flow_count", _I, [_P, _PU64, _P]),
     ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),

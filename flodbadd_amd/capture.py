@@ -51,7 +51,7 @@ def stats_dict(arr):
 
 class FlodbaddGpuCapture:
     def __init__(self, device=0, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 20,
-                 service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20):
+                 service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20, track_history=False):
         lib = N.gpu_lib()
         self._keep = []
         cfg = N.FbConfig()
@@ -78,6 +78,10 @@ class FlodbaddGpuCapture:
         self.filter = SessionFilter(session_filter)
         self.device = device
         self.flow_capacity = flow_capacity
+        # history strings (src/packets.rs:187-198, 410-426) per table slot, appended batch by batch
+        # from fb_flow_history_dev when track_history is set
+        self.track_history = bool(track_history) and flow_capacity > 0
+        self.histories = {}
 
     # ---- configuration -------------------------------------------------------------------
     def set_filter(self, flt):
@@ -130,6 +134,7 @@ class FlodbaddGpuCapture:
         n_out = C.c_uint32(0)
         N.check(N.gpu_lib().fb_process_parsed(self.ctx, N.ptr(arr) if n else None, n, N.ptr(out), C.byref(n_out),
                                               N.ptr(cls), N.ptr(st), None))
+        self._pull_history(n)
         return BatchResult(out[: n_out.value], np.zeros(0, dtype=N.DNS_OUT_DTYPE), cls[:n], stats_dict(st))
 
     def process_frames(self, frames, offsets):
@@ -157,6 +162,7 @@ class FlodbaddGpuCapture:
             e = sd["error"]
             code = N.FB_ERR_TABLE_FULL if e & 4 else N.FB_ERR_INTERNAL
             raise N.FbError(code, "device error word %d" % e)
+        self._pull_history(n)
         return BatchResult(out, dns, cls, sd)
 
     def process_frames_seg(self, frames, offsets, flow=True):
@@ -180,6 +186,8 @@ class FlodbaddGpuCapture:
         if sd["error"]:
             e = sd["error"]
             raise N.FbError(N.FB_ERR_TABLE_FULL if e & 4 else N.FB_ERR_INTERNAL, "device error word %d" % e)
+        if flow:
+            self._pull_history(((n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES) * N.FB_SEG_FRAMES)
         seg = d_seg.download(np.zeros(nseg, dtype=np.uint32))
         raw = d_out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8))
         out, dns = N.seg_unpack(raw, seg[: (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES])
@@ -187,6 +195,28 @@ class FlodbaddGpuCapture:
         return BatchResult(out, dns, cls, sd)
 
     # ---- session table -----------------------------------------------------------------------
+    def flow_history(self, n_slots):
+        """fb_flow_history_dev: the last update's history characters grouped per flow, packet order
+        inside each flow -> {table slot: str}.  n_slots = that update's record slots (its batch's
+        n frames, dense; ceil(n/64)*64, segmented)."""
+        m = max(int(n_slots), 1)
+        d_h, d_s, d_n = N.DeviceBuffer(m), N.DeviceBuffer(4 * m), N.DeviceBuffer(4)
+        N.check(N.gpu_lib().fb_flow_history_dev(self.ctx, d_h.ptr, d_s.ptr, d_n.ptr, None))
+        k = int(d_n.download(np.zeros(1, dtype=np.uint32))[0])
+        if k == 0:
+            return {}
+        chars = d_h.download(np.zeros(k, dtype=np.uint8), k)
+        slots = d_s.download(np.zeros(k, dtype=np.uint32), 4 * k)
+        cut = np.flatnonzero(np.diff(slots)) + 1
+        starts, ends = np.r_[0, cut], np.r_[cut, k]
+        return {int(slots[a]): chars[a:b].tobytes().decode("ascii") for a, b in zip(starts, ends)}
+
+    def _pull_history(self, n_slots):
+        if not self.track_history:
+            return
+        for slot, run in self.flow_history(n_slots).items():
+            self.histories[slot] = self.histories.get(slot, "") + run
+
     def flow_count(self):
         n = C.c_uint64(0)
         N.check(N.gpu_lib().fb_flow_count(self.ctx, C.byref(n), None))
@@ -201,12 +231,13 @@ class FlodbaddGpuCapture:
 
     def get_sessions(self, is_lan=None):
         """Sessions sorted by the derived Ord of Session (integer counters + derived f64s)."""
-        return flows_to_sessions(self.export_flows(), is_lan)
+        return flows_to_sessions(self.export_flows(), is_lan, self.histories if self.track_history else None)
 
     def clear_all_sessions(self):
         """src/capture.rs:396 (`stop()` clears the table, capture.rs:383)."""
         N.check(N.gpu_lib().fb_flow_clear(self.ctx, None))
         N.check(N.gpu_lib().fb_stream_sync(None))
+        self.histories = {}
 
     def close(self):
         if getattr(self, "ctx", None):

@@ -75,6 +75,19 @@ struct fb_ctx {
     uint32_t last_n = 0;            // packets of the last parse launch (bounds its records)
     unsigned long long* d_partials = nullptr;
     unsigned long long* d_n = nullptr;
+    // ordered per-flow state: update calls since create/clear, table slot of each record slot
+    uint32_t flow_batch = 0;
+    uint32_t* d_rec_flow = nullptr;       // [flow_recs]
+    // the last update, for fb_flow_history_dev
+    const fb_pkt_out* last_recs = nullptr;
+    const uint32_t* last_seg = nullptr;
+    const fb_batch_stats* last_stats = nullptr;
+    uint32_t last_slots = 0;
+    uint32_t* d_hkeys = nullptr;          // [hist_cap] history sort scratch
+    uint8_t* d_hvals = nullptr;
+    void* d_htemp = nullptr;
+    size_t htemp_bytes = 0;
+    uint64_t hist_cap = 0;
     // host-mode staging
     uint8_t* s_frames = nullptr;
     uint64_t s_frames_cap = 0;
@@ -96,17 +109,23 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_entries);
     hipFree(c->d_rows);
     hipFree(c->d_cols);
+    hipFree(c->d_rec_flow);
     c->d_entries = nullptr;
     c->d_rows = c->d_cols = nullptr;
+    c->d_rec_flow = nullptr;
+    c->last_recs = nullptr;  // its rec_flow is gone
     c->flow_recs = 0;
     const uint64_t chunks = recs / kFlowChunk;
     if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
+        hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     c->flow_recs = recs;
     return FB_OK;
 }
+
+static int empty_update(fb_ctx* c);
 
 static int upload_cfg(fb_ctx* c, hipStream_t s) {
     if (!c->cfg_dirty) return FB_OK;
@@ -263,6 +282,10 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_cols);
     hipFree(c->d_partials);
     hipFree(c->d_n);
+    hipFree(c->d_rec_flow);
+    hipFree(c->d_hkeys);
+    hipFree(c->d_hvals);
+    hipFree(c->d_htemp);
     hipFree(c->s_frames);
     hipFree(c->s_offsets);
     hipFree(c->s_out);
@@ -545,6 +568,8 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
     if (n && c->d_table) {
         rc = fb_flow_update_dev(c, c->s_out, c->s_stats, s);
         if (rc) return rc;
+    } else if (c->d_table) {
+        empty_update(c);
     }
     fb_batch_stats st;
     HIP_TRY(hipMemcpyAsync(&st, c->s_stats, sizeof(st), hipMemcpyDeviceToHost, s));
@@ -556,6 +581,13 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
     HIP_TRY(hipStreamSynchronize(s));
     if (n_out) *n_out = (uint32_t)st.n_session;
     if (stats) *stats = st;
+    return FB_OK;
+}
+
+// An update call without records still counts as one (the high word of flow positions).
+static int empty_update(fb_ctx* c) {
+    ++c->flow_batch;
+    c->last_recs = nullptr;
     return FB_OK;
 }
 
@@ -582,8 +614,15 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.parts = c->flow_parts;
     p.part_shift = c->flow_shift;
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
+    p.batch = c->flow_batch;
+    p.rec_flow = c->d_rec_flow;
     HIP_TRY(launch_flow_update(p, chunks, s));
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
+    ++c->flow_batch;
+    c->last_recs = d_recs;
+    c->last_seg = d_seg;
+    c->last_stats = d_stats;
+    c->last_slots = p.max_recs < n_slots ? p.max_recs : n_slots;
     return FB_OK;
 }
 
@@ -596,7 +635,7 @@ int fb_flow_update_seg_dev(fb_ctx* c, const fb_pkt_out* d_out, const uint32_t* d
                            fb_batch_stats* d_stats, void* stream) {
     if (!c || !d_out || !d_seg || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_out, d_seg and d_stats are required");
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
-    if (n == 0) return FB_OK;
+    if (n == 0) return empty_update(c);
     const uint32_t slots = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES;
     return flow_update(c, d_out, d_seg, slots, d_stats, (hipStream_t)stream);
 }
@@ -607,7 +646,8 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     int rc = fb_parse_classify_seg_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream);
-    if (rc || n == 0) return rc;
+    if (rc) return rc;
+    if (n == 0) return empty_update(c);
     return fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
 }
 
@@ -618,8 +658,48 @@ int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, co
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     if (!d_out) return set_err(FB_ERR_INVAL, "d_out is required");
     int rc = fb_parse_classify_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_dns, d_class, d_stats, stream);
-    if (rc || n == 0) return rc;
+    if (rc) return rc;
+    if (n == 0) return empty_update(c);
     return fb_flow_update_dev(c, d_out, d_stats, stream);
+}
+
+int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint32_t* d_n_hist, void* stream) {
+    if (!c || !d_n_hist) return set_err(FB_ERR_INVAL, "ctx and d_n_hist are required");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t n = c->last_recs ? c->last_slots : 0u;
+    if (n && (!d_hist || !d_hist_slot)) return set_err(FB_ERR_INVAL, "d_hist and d_hist_slot are required");
+    if (n > c->hist_cap) {
+        HIP_TRY(hipStreamSynchronize(s));
+        hipFree(c->d_hkeys);
+        hipFree(c->d_hvals);
+        hipFree(c->d_htemp);
+        c->d_hkeys = nullptr;
+        c->d_hvals = nullptr;
+        c->d_htemp = nullptr;
+        c->hist_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(c->flow_recs, n);
+        size_t tb = 0;
+        HIP_TRY(flow_history_temp_bytes((uint32_t)cap, (uint32_t)c->table_cap, &tb));
+        if (hipMalloc(&c->d_hkeys, cap * 4ull) != hipSuccess || hipMalloc(&c->d_hvals, cap) != hipSuccess ||
+            hipMalloc(&c->d_htemp, std::max<size_t>(tb, 16)) != hipSuccess)
+            return set_err(FB_ERR_NOMEM, "history sort scratch (%llu records)", (unsigned long long)cap);
+        c->htemp_bytes = std::max<size_t>(tb, 16);
+        c->hist_cap = cap;
+    }
+    HistParams p;
+    p.recs = c->last_recs;
+    p.seg = c->last_seg;
+    p.stats = c->last_stats;
+    p.rec_flow = c->d_rec_flow;
+    p.n_slots = n;
+    p.sentinel = (uint32_t)c->table_cap;
+    p.keys = c->d_hkeys;
+    p.vals = c->d_hvals;
+    p.n_hist = d_n_hist;
+    HIP_TRY(launch_flow_history(p, c->d_htemp, c->htemp_bytes, d_hist_slot, d_hist, s));
+    return FB_OK;
 }
 
 int fb_flow_count(fb_ctx* c, uint64_t* n_flows, void* stream) {
@@ -677,6 +757,8 @@ int fb_flow_clear(fb_ctx* c, void* stream) {
     if (!c->d_table) return FB_OK;
     DeviceGuard g(c->device);
     HIP_TRY(hipMemsetAsync(c->d_table, 0, c->table_cap * sizeof(FlowSlot), (hipStream_t)stream));
+    c->flow_batch = 0;
+    c->last_recs = nullptr;
     return FB_OK;
 }
 

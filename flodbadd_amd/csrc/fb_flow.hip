@@ -12,14 +12,16 @@
 // is applied in three launches:
 //   K1 k_flow_bucket    one workgroup per chunk of kFlowChunk records: LDS histogram of the
 //                       records' partitions, exclusive scan, then a counting-sort scatter of
-//                       48-B FlowEntry items into the chunk's region of `entries` (partition-
+//                       64-B FlowEntry items into the chunk's region of `entries` (partition-
 //                       major inside the chunk); row b of `rows` = (start, count) per partition.
 //   K1t k_flow_transpose rows[chunk][part] -> cols[part][chunk] (so K2 reads its column
 //                       contiguously).
-//   K2 k_flow_apply     one workgroup per partition: loads the partition's 48-KiB slice into
+//   K2 k_flow_apply     one workgroup per partition: loads the partition's 64-KiB slice into
 //                       LDS, gathers its entries from every chunk, finds/inserts each key in
-//                       the slice and adds the counters with LDS atomics, writes the slice back.
-// Counters are integer sums, so results are bit-exact whatever the order; new_sessions counts
+//                       the slice, adds the counters and reduces the ordered state with LDS
+//                       atomics, folds the ordered state once per slot, writes the slice back.
+// Counters are integer sums, so results are bit-exact whatever the order (the order-dependent
+// history state is reduced to min/max/or, see K2); new_sessions counts
 // the keys inserted (each key is inserted once), updated_sessions the remaining records.
 // The reference hashes Session with SipHash under a random per-process key (dashmap 6.1.0
 // RandomState), so no hash value is a parity target; this table uses fb_flow_hash (below), a
@@ -136,14 +138,18 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         const uint4 a = *reinterpret_cast<const uint4*>(r);
         const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
         const uint4 c = *reinterpret_cast<const uint4*>(r + 8);  // key 8,9 | packet_length | ip_packet_length
-        const uint32_t m = r[12];
+        const uint2 m = *reinterpret_cast<const uint2*>(r + 12);  // flags | meta | hist_char, pkt_index
         const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
         const uint32_t d = atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
-        const uint32_t orig = ((m >> 8) & FB_META_ORIGINATOR) ? 1u : 0u;
+        const uint32_t meta = (m.x >> 8) & 0xFFu;
+        const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
+        const uint32_t hinfo =
+            ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
         uint4* e = reinterpret_cast<uint4*>(out + d);
         e[0] = a;
         e[1] = b;
         e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
+        e[3] = make_uint4(m.y, base + k, hinfo, 0u);
     }
 }
 
@@ -166,15 +172,60 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
 
 // ---------------------------------------------------------------------------------------------
 // K2: apply one partition's entries to its LDS-resident slice.
-constexpr uint32_t kSlotWords = sizeof(FlowSlot) / 8;  // 12 u64 words per slot
+//
+// Ordered state (src/packets.rs:187-198, 410-426).  Entries reach K2 in no particular order, so
+// everything order-dependent is reduced to order-independent LDS atomics keyed by the record
+// slot `rec` (batch order) in a per-slot batch scratch, then folded into the slot once per batch:
+//   first / last packet  = min / max of (rec << 32 | pkt_index)
+//   end (first FIN/RST)  = min of the same over the TCP records with FIN or RST
+//   history characters   = OR of their FB_HIST_CHARS bits, and for the 8 characters that
+//                          determine_conn_state reads (S s H h F f R r) the first rec of each.
+// conn_state at the end packet is determine_conn_state of (the flow's mask from earlier batches
+// | the characters whose first occurrence is at or before the end record): the reference's test
+// `history.contains(c)` only asks which characters the string holds at that moment.
+constexpr uint32_t kSlotWords = sizeof(FlowSlot) / 8;  // 16 u64 words per slot
+constexpr uint32_t kScrWords = 8;                      // per-slot batch scratch, u64 words
+constexpr uint32_t kK2Lds = kFlowSlots * (sizeof(FlowSlot) + kScrWords * 8);
+constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 
 __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character).
+__device__ __forceinline__ uint32_t hist_bit(uint32_t c) {
+    switch (c) {
+        case 'S': return 0u;
+        case 's': return 1u;
+        case 'H': return 2u;
+        case 'h': return 3u;
+        case 'F': return 4u;
+        case 'f': return 5u;
+        case 'R': return 6u;
+        case 'r': return 7u;
+        case '>': return 8u;
+        case '<': return 9u;
+        case 'A': return 10u;
+        case 'a': return 11u;
+        case '-': return 12u;
+        default: return 16u;
+    }
+}
+
+// determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
+__device__ __forceinline__ uint32_t conn_state_of(uint32_t m) {
+    const bool S = m & 1u, H = m & 4u, h = m & 8u, F = m & 16u, f = m & 32u, R = m & 64u, r = m & 128u;
+    if (S && H && F && f) return FB_CONN_SF;
+    if (S && !h && !r) return FB_CONN_S0;
+    if (R || r) return FB_CONN_REJ;
+    if (S && H && !F && !f) return FB_CONN_S1;
+    return FB_CONN_OTHER;
+}
+
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
-__device__ __forceinline__ int apply_entry(unsigned long long* slice, const uint4 e0, const uint4 e1,
-                                           const uint4 e2, uint32_t* err) {
+__device__ __forceinline__ int apply_entry(unsigned long long* slice, unsigned long long* scr, const uint4 e0,
+                                           const uint4 e1, const uint4 e2, const uint4 e3, uint32_t slot_base,
+                                           uint32_t* rec_flow, uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
     const unsigned long long h = flow_hash_words(key);
@@ -224,16 +275,59 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, const uint
     atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
     atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
     atomicAdd(s + 10 + (orig ? 0 : 1), (unsigned long long)e2.w);
+    // ordered state into the batch scratch (see above)
+    unsigned long long* q = scr + (size_t)i * kScrWords;
+    uint32_t* q32 = reinterpret_cast<uint32_t*>(q);
+    const unsigned long long pos = ((unsigned long long)e3.y << 32) | e3.x;
+    atomicMin(q, pos);
+    atomicMax(q + 1, pos);
+    if (result == 1) atomicOr(q32 + 7, 1u);  // inserted by this batch
+    if (e3.z & 0x10000u) {                   // Some(flags): history.push(map_tcp_flags(..))
+        atomicAdd(reinterpret_cast<uint32_t*>(s + 15), 1u);
+        const uint32_t b = hist_bit(e3.z & 0xFFu);
+        if (b < 16u) atomicOr(q32 + 6, 1u << b);
+        if (b < 8u) atomicMin(q32 + 8 + b, e3.y);
+        if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + 2, pos);
+    }
+    if (rec_flow) rec_flow[e3.y] = slot_base + i;
     return result;
 }
 
+// Fold one slot's batch scratch into its ordered state (after every entry was applied).
+__device__ __forceinline__ void finish_slot(unsigned long long* s, const unsigned long long* q, uint32_t batch) {
+    const unsigned long long first = q[0];
+    if (first == ~0ull) return;  // not touched by this batch
+    const uint32_t* q32 = reinterpret_cast<const uint32_t*>(q);
+    const unsigned long long hi = (unsigned long long)batch << 32;
+    if (q32[7] & 1u) {  // new flow: start_time = its first packet, end_time None
+        s[12] = hi | (uint32_t)first;
+        s[14] = FB_SEEN_NONE;
+    }
+    s[13] = hi | (uint32_t)q[1];
+    uint32_t* st = reinterpret_cast<uint32_t*>(s + 15) + 1;
+    const uint32_t old = *st;
+    const uint32_t mask = old & 0xFFFFu;
+    uint32_t cs = old >> 16;
+    const unsigned long long end = q[2];
+    if (end != ~0ull && s[14] == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
+        const uint32_t end_rec = (uint32_t)(end >> 32);
+        uint32_t m = mask;
+#pragma unroll
+        for (uint32_t b = 0; b < 8u; ++b) m |= q32[8 + b] <= end_rec ? 1u << b : 0u;
+        cs = conn_state_of(m) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
+        s[14] = hi | (uint32_t)end;
+    }
+    *st = (mask | q32[6]) | (cs << 16);
+}
+
 __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams P) {
-    extern __shared__ uint4 slice4[];  // kFlowSlots * 96 B
+    extern __shared__ uint4 slice4[];  // kFlowSlots 128-B slots, then kFlowSlots 64-B scratch
     __shared__ uint32_t sp[kFlowK2Threads];
     __shared__ uint32_t ss[kFlowK2Threads];
     __shared__ uint32_t wsum[kFlowK2Threads / 64];
     __shared__ unsigned long long sh[kFlowK2Threads / 64];
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
+    unsigned long long* scr = slice + (size_t)kFlowSlots * kSlotWords;
     const uint32_t part = blockIdx.x;
     const uint32_t n = batch_records(P);
     const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
@@ -247,6 +341,13 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
         constexpr uint32_t kSlice16 = kFlowSlots * sizeof(FlowSlot) / 16u;
         const uint4* g = reinterpret_cast<const uint4*>(P.table + (size_t)part * kFlowSlots);
         for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) slice4[j] = g[j];
+        for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads) {
+            uint4* q = slice4 + kSlice16 + (size_t)j * (kScrWords / 2);
+            q[0] = make_uint4(~0u, ~0u, 0u, 0u);    // first = none, last = 0
+            q[1] = make_uint4(~0u, ~0u, 0u, 0u);    // end = none, character mask, flags
+            q[2] = make_uint4(~0u, ~0u, ~0u, ~0u);  // first rec of S s H h
+            q[3] = make_uint4(~0u, ~0u, ~0u, ~0u);  //                F f R r
+        }
         __syncthreads();
         const uint4* E = reinterpret_cast<const uint4*>(P.entries);
         for (uint32_t g0 = 0; g0 < chunks; g0 += kFlowK2Threads) {
@@ -258,7 +359,7 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
             ss[threadIdx.x] = b * kFlowChunk + (v & 0xFFFFu);
             __syncthreads();
             for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 4u * kFlowK2Threads) {
-                uint4 q[4][3];
+                uint4 q[4][4];
                 uint32_t ne = 0u;
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; ++u) {
@@ -270,16 +371,18 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
                             if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
                         }
                         const size_t idx = (size_t)ss[lo] + (e - sp[lo]);
-                        q[u][0] = E[idx * 3u];
-                        q[u][1] = E[idx * 3u + 1u];
-                        q[u][2] = E[idx * 3u + 2u];
+                        q[u][0] = E[idx * 4u];
+                        q[u][1] = E[idx * 4u + 1u];
+                        q[u][2] = E[idx * 4u + 2u];
+                        q[u][3] = E[idx * 4u + 3u];
                         ne = u + 1u;
                     }
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; ++u) {
                     if (u < ne) {
-                        const int r = apply_entry(slice, q[u][0], q[u][1], q[u][2], P.error);
+                        const int r = apply_entry(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3],
+                                                  part * kFlowSlots, P.rec_flow, P.error);
                         n_new += r == 1;
                         n_upd += r == 0;
                     }
@@ -287,6 +390,9 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
             }
             __syncthreads();
         }
+        for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads)
+            finish_slot(slice + (size_t)j * kSlotWords, scr + (size_t)j * kScrWords, P.batch);
+        __syncthreads();
         uint4* gw = reinterpret_cast<uint4*>(P.table + (size_t)part * kFlowSlots);
         for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) gw[j] = slice4[j];
     }
@@ -344,6 +450,15 @@ __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned
             r.resp_pkts = T[i].cnt[3];
             r.orig_ip_bytes = T[i].cnt[4];
             r.resp_ip_bytes = T[i].cnt[5];
+            r.first_seen = T[i].first_seen;
+            r.last_seen = T[i].last_seen;
+            r.end_seen = T[i].end_seen;
+            r.hist_len = T[i].hist_len;
+            r.hist_mask = (uint16_t)(T[i].hist_state & 0xFFFFu);
+            r.conn_state = (uint8_t)(T[i].hist_state >> 16);
+            r.end_mask = (uint8_t)(T[i].hist_state >> 24);
+            r.slot = (uint32_t)i;
+            r.reserved1 = 0u;
             out[pos] = r;
         }
         __syncthreads();
@@ -370,7 +485,10 @@ hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t 
                        chunks);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_flow_apply, dim3(p.parts), dim3(kFlowK2Threads), kFlowSlots * sizeof(FlowSlot), s, p);
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k_flow_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2Lds);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_flow_apply, dim3(p.parts), dim3(kFlowK2Threads), kK2Lds, s, p);
     return hipGetLastError();
 }
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials, uint32_t nblk,

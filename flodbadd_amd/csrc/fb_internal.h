@@ -72,9 +72,11 @@ struct ParseParams {
 //   64-bit hash, its home slot inside the partition the low bits (linear probing wraps inside
 //   the partition).  One workgroup owns one partition per batch and updates it in LDS, so the
 //   upsert needs no global atomics.
-//   Slot (96 B): tag (0 empty, 1 being inserted [LDS only], else hash | 2), 40-B key,
-//   6 counters in fb_flow_rec order.
-constexpr uint32_t kFlowSlots = 512;             // slots per partition: 48 KiB LDS slice
+//   Slot (128 B): tag (0 empty, 1 being inserted [LDS only], else hash | 2), 40-B key,
+//   6 counters in fb_flow_rec order, then the ordered state: first / last / end positions
+//   ((update call << 32) | pkt_index, FB_SEEN_NONE), hist_len, hist_mask | conn_state << 16 |
+//   end_mask << 24.
+constexpr uint32_t kFlowSlots = 512;             // slots per partition: 64 KiB LDS slice
 constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
 constexpr uint32_t kFlowChunk = 16384;           // records per bucketing workgroup (K1)
 constexpr uint32_t kFlowK1Threads = 1024;
@@ -85,16 +87,25 @@ struct FlowSlot {
     uint32_t key[10];
     unsigned long long cnt[6];  // outbound_bytes, inbound_bytes, orig_pkts, resp_pkts,
                                 // orig_ip_bytes, resp_ip_bytes
+    unsigned long long first_seen, last_seen, end_seen;
+    uint32_t hist_len;
+    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | conn_state << 16 | end_mask << 24
 };
-static_assert(sizeof(FlowSlot) == 96, "flow slot is 96 B");
+static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
-// word 9 (the key's padding), L4 payload bytes, IP bytes.
+// word 9 (the key's padding), L4 payload bytes, IP bytes, then the record's pkt_index, its
+// record slot (the batch order K2 orders the history by) and hist_char | tcp_flags << 8 |
+// has_flags << 16.
 struct FlowEntry {
     uint32_t key[10];
     uint32_t packet_length;
     uint32_t ip_packet_length;
+    uint32_t pkt_index;
+    uint32_t rec;
+    uint32_t hist;
+    uint32_t pad;
 };
-static_assert(sizeof(FlowEntry) == 48, "flow entry is 48 B");
+static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 
 struct FlowParams {
     const fb_pkt_out* recs;
@@ -112,6 +123,8 @@ struct FlowParams {
     uint32_t parts;             // P (power of two)
     uint32_t part_shift;        // 64 - log2(P) (64 when P == 1)
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
+    uint32_t batch;             // update call number since create / clear (positions' high word)
+    uint32_t* rec_flow;         // [max_recs] table slot of each record slot (for the history)
 };
 
 // Launchers (fb_parse.hip / fb_flow.hip).
@@ -131,5 +144,21 @@ hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_
                               hipStream_t s);
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
                              unsigned long long* d_n, hipStream_t s);
+
+// Per-flow history characters of the last update (fb_hist.hip).
+struct HistParams {
+    const fb_pkt_out* recs;     // the update's records (dense or segmented)
+    const uint32_t* seg;        // segmented: record slot i valid iff (i & 63) < (seg[i >> 6] & 0xFFFF)
+    const fb_batch_stats* stats;  // dense: n_session read here
+    const uint32_t* rec_flow;   // table slot of each record slot (k_flow_apply)
+    uint32_t n_slots;           // record slots of the update
+    uint32_t sentinel;          // key of the records that are not sorted in (= table capacity)
+    uint32_t* keys;             // [n_slots] scratch
+    uint8_t* vals;              // [n_slots] scratch
+    uint32_t* n_hist;           // device u32: keyed records
+};
+hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes);
+hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_bytes, uint32_t* hist_slot,
+                               uint8_t* hist, hipStream_t s);
 
 }  // namespace fbk

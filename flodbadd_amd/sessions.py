@@ -12,7 +12,8 @@ import numpy as np
 from dataclasses import dataclass, field
 from typing import List, Optional
 
-from ._native import (FB_FILTER_ALL, FB_FILTER_GLOBAL_ONLY, FB_FILTER_LOCAL_ONLY, FLOW_REC_DTYPE,
+from ._native import (CONN_STATES, FB_FILTER_ALL, FB_FILTER_GLOBAL_ONLY, FB_FILTER_LOCAL_ONLY, FB_SEEN_NONE,
+                      FLOW_REC_DTYPE,
                       META_DST_SERVICE, META_HAS_FLAGS, META_LOCAL_DST, META_LOCAL_SRC, META_ORIGINATOR,
                       META_SELF_DST, META_SELF_SRC, META_SWAP, PARSED_DTYPE, PKT_OUT_DTYPE)
 
@@ -101,6 +102,12 @@ class SessionStats:
     resp_ip_bytes: int = 0
     history: str = ""
     conn_state: Optional[str] = None
+    # positions ((flow update call << 32) | pkt_index) standing for start_time / last_activity /
+    # end_time (src/sessions.rs:74-76); end None until the first FIN/RST
+    first_seen: int = 0
+    last_seen: int = 0
+    end_seen: Optional[int] = None
+    hist_len: int = 0
 
     @property
     def average_packet_size(self):
@@ -181,13 +188,18 @@ def histories_from_records(recs):
     return {k: (h, state.get(k)) for k, h in hist.items()}
 
 
-def flows_to_sessions(flows, is_lan=None):
-    """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session."""
+def flows_to_sessions(flows, is_lan=None, histories=None):
+    """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session.  `histories`
+    ({table slot: str}, FlodbaddGpuCapture.histories) supplies the history strings."""
     assert flows.dtype == FLOW_REC_DTYPE
     out = []
     for r in flows:
+        end = int(r["end_seen"])
         st = SessionStats(int(r["inbound_bytes"]), int(r["outbound_bytes"]), int(r["orig_pkts"]),
-                          int(r["resp_pkts"]), int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]))
+                          int(r["resp_pkts"]), int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]),
+                          histories.get(int(r["slot"]), "") if histories is not None else "",
+                          CONN_STATES[int(r["conn_state"])], int(r["first_seen"]), int(r["last_seen"]),
+                          None if end == FB_SEEN_NONE else end, int(r["hist_len"]))
         s = Session.from_key(r)
         info = SessionInfo(s, st)
         if is_lan is not None:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FB_ABI_VERSION 1u
+#define FB_ABI_VERSION 2u
 #define FB_MAX_BATCH_PACKETS ((1u << 27) - 1u)
 #define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
 #define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
@@ -191,17 +191,51 @@ typedef struct fb_config {
     uint64_t max_batch_bytes;      /* host-mode staging capacity (frame bytes per call)       */
 } fb_config;
 
+/* determine_conn_state (src/packets.rs:539-559) outcome, fixed at the flow's first FIN/RST
+ * packet (src/packets.rs:192-197, 422-426). */
+enum fb_conn_state {
+    FB_CONN_NONE = 0, /* conn_state None: no FIN/RST seen yet */
+    FB_CONN_SF = 1,
+    FB_CONN_S0 = 2,
+    FB_CONN_REJ = 3,
+    FB_CONN_S1 = 4,
+    FB_CONN_OTHER = 5 /* "-" */
+};
+
+/* fb_flow_rec.hist_mask: bit k set <=> the history string contains FB_HIST_CHARS[k]
+ * (map_tcp_flags alphabet, src/packets.rs:561-601). */
+#define FB_HIST_CHARS "SsHhFfRr><Aa-"
+
+/* A packet position in the stream of flow updates of one context: (update call << 32) | pkt_index,
+ * where the update call counts fb_flow_update*_dev / fb_process*_dev calls since fb_create /
+ * fb_flow_clear (from 0).  Stands for the wall-clock `now` the reference samples per packet
+ * (src/packets.rs:209) -- a host maps it to capture timestamps.  FB_SEEN_NONE = None. */
+#define FB_SEEN_NONE 0xFFFFFFFFFFFFFFFFull
+
 /* Flow-table export record: canonical key + SessionStats integer counters
- * (src/sessions.rs:76-82; update rules src/packets.rs:111-120, 383-391). */
+ * (src/sessions.rs:76-82; update rules src/packets.rs:111-120, 383-391) + the ordered per-flow
+ * state (src/packets.rs:187-198, 410-426): positions stand for start_time / last_activity /
+ * end_time, hist_len = history.len(), conn_state as above.  The history string itself comes from
+ * fb_flow_history_dev, batch by batch. */
 typedef struct fb_flow_rec {
-    fb_session_key key;      /*  0 */
-    uint64_t outbound_bytes; /* 40 */
-    uint64_t inbound_bytes;  /* 48 */
-    uint64_t orig_pkts;      /* 56 */
-    uint64_t resp_pkts;      /* 64 */
-    uint64_t orig_ip_bytes;  /* 72 */
-    uint64_t resp_ip_bytes;  /* 80 */
-} fb_flow_rec;               /* 88 bytes */
+    fb_session_key key;      /*   0 */
+    uint64_t outbound_bytes; /*  40 */
+    uint64_t inbound_bytes;  /*  48 */
+    uint64_t orig_pkts;      /*  56 */
+    uint64_t resp_pkts;      /*  64 */
+    uint64_t orig_ip_bytes;  /*  72 */
+    uint64_t resp_ip_bytes;  /*  80 */
+    uint64_t first_seen;     /*  88: position of the flow's first packet (start_time)         */
+    uint64_t last_seen;      /*  96: position of its latest packet (last_activity)            */
+    uint64_t end_seen;       /* 104: position of its first FIN/RST packet (end_time), or NONE */
+    uint32_t hist_len;       /* 112: history.len() (TCP packets of the flow)                  */
+    uint16_t hist_mask;      /* 116: characters present in history (FB_HIST_CHARS bits)       */
+    uint8_t conn_state;      /* 118: fb_conn_state                                             */
+    uint8_t end_mask;        /* 119: hist_mask & 0xFF at end_seen (the characters S s H h F f R r
+                                conn_state was decided on); 0 while end_seen is NONE              */
+    uint32_t slot;           /* 120: table slot (the flow id of fb_flow_history_dev)           */
+    uint32_t reserved1;      /* 124 */
+} fb_flow_rec;               /* 128 bytes */
 
 typedef struct fb_ctx fb_ctx;
 
@@ -301,6 +335,20 @@ int fb_flow_update_seg_dev(fb_ctx* ctx, const fb_pkt_out* d_out, const uint32_t*
 int fb_process_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                        const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
                        uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+
+/*
+ * History characters of the LAST flow update on this context, grouped per flow: a stable sort of
+ * that batch's TCP records (those with FB_META_HAS_FLAGS) by (flow slot, record order), i.e. for
+ * every flow the characters it appended to its history string in this batch, in packet order
+ * (src/packets.rs:187-198, 410-426).  d_hist[p] = fb_pkt_out.hist_char, d_hist_slot[p] = the
+ * flow's fb_flow_rec.slot, for p < *d_n_hist (device u32).  Appending each run to the flow's
+ * string, batch after batch, reproduces the reference's history.  Both arrays need room for the
+ * last update's record slots: the n frames / packets of its batch (dense), ceil(n/64)*64
+ * (segmented); slots past *d_n_hist are scratch.  The update's d_recs (and d_seg, d_stats) must
+ * still be valid.  DEVICE pointers, asynchronous on `stream`.
+ */
+int fb_flow_history_dev(fb_ctx* ctx, uint8_t* d_hist, uint32_t* d_hist_slot, uint32_t* d_n_hist,
+                        void* stream);
 
 int fb_flow_count(fb_ctx* ctx, uint64_t* n_flows, void* stream); /* synchronous */
 /* Copy every flow (slot order) to host memory; *n = flows written (<= cap). Synchronous. */

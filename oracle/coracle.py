@@ -135,12 +135,15 @@ class Flows:
     def history(self, key_rec):
         """key_rec: a PKT_OUT_DTYPE or FLOW_REC_DTYPE element (uses its first 40 bytes)."""
         kb = np.frombuffer(key_rec.tobytes()[:40], dtype=np.uint8).copy()
-        buf = C.create_string_buffer(1 << 16)
-        cs = C.create_string_buffer(8)
-        n = lib().orc_flows_history(self.h, kb.ctypes.data, buf, 1 << 16, cs, 8)
+        if not hasattr(self, "_buf"):
+            self._buf, self._cs = C.create_string_buffer(1 << 16), C.create_string_buffer(8)
+        n = lib().orc_flows_history(self.h, kb.ctypes.data, self._buf, len(self._buf), self._cs, 8)
+        if n > len(self._buf):
+            self._buf = C.create_string_buffer(int(n))
+            n = lib().orc_flows_history(self.h, kb.ctypes.data, self._buf, len(self._buf), self._cs, 8)
         if n < 0:
             return None, None
-        return buf.raw[:n].decode(), (cs.value.decode() or None)
+        return self._buf.raw[:n].decode(), (self._cs.value.decode() or None)
 
     def clear(self):
         lib().orc_flows_clear(self.h)

@@ -370,6 +370,7 @@ typedef struct orc_flow {
 struct orc_flows {
     orc_flow* slots;
     uint64_t cap, count;
+    uint32_t batch; /* update calls since new/clear: the high word of fb_flow_rec positions */
 };
 
 static uint64_t key_hash(const fb_session_key* k) {
@@ -390,6 +391,7 @@ void orc_flows_clear(orc_flows* f) {
     for (uint64_t i = 0; i < f->cap; ++i) free(f->slots[i].hist);
     memset(f->slots, 0, f->cap * sizeof(orc_flow));
     f->count = 0;
+    f->batch = 0;
 }
 
 void orc_flows_free(orc_flows* f) {
@@ -417,17 +419,26 @@ static void grow(orc_flows* f) {
     f->cap = ncap;
 }
 
-/* determine_conn_state, src/packets.rs:539-559. */
-static void conn_state_of(const char* h, uint64_t n, char out[4]) {
+/* determine_conn_state, src/packets.rs:539-559: scans the history string as the reference does.
+ * Returns the fb_conn_state code and writes the string. */
+static uint8_t conn_state_of(const char* h, uint64_t n, char out[4]) {
     int has[128] = {0};
     for (uint64_t i = 0; i < n; ++i) has[(unsigned char)h[i] & 127] = 1;
     const char* s;
-    if (has['S'] && has['H'] && has['F'] && has['f']) s = "SF";
-    else if (has['S'] && !has['h'] && !has['r']) s = "S0";
-    else if (has['R'] || has['r']) s = "REJ";
-    else if (has['S'] && has['H'] && !has['F'] && !has['f']) s = "S1";
-    else s = "-";
+    uint8_t code;
+    if (has['S'] && has['H'] && has['F'] && has['f']) { s = "SF"; code = FB_CONN_SF; }
+    else if (has['S'] && !has['h'] && !has['r']) { s = "S0"; code = FB_CONN_S0; }
+    else if (has['R'] || has['r']) { s = "REJ"; code = FB_CONN_REJ; }
+    else if (has['S'] && has['H'] && !has['F'] && !has['f']) { s = "S1"; code = FB_CONN_S1; }
+    else { s = "-"; code = FB_CONN_OTHER; }
     strcpy(out, s);
+    return code;
+}
+
+/* Position of FB_HIST_CHARS holding c (16 when absent). */
+static uint32_t hist_bit(char c) {
+    const char* p = strchr(FB_HIST_CHARS, c);
+    return (c && p) ? (uint32_t)(p - FB_HIST_CHARS) : 16u;
 }
 
 void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* st) {
@@ -435,10 +446,13 @@ void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch
         const fb_pkt_out* r = &recs[i];
         if ((f->count + 1) * 2 > f->cap) grow(f);
         orc_flow* s = find_slot(f->slots, f->cap, &r->key);
+        const uint64_t pos = ((uint64_t)f->batch << 32) | r->pkt_index; /* stands for `now` */
         if (!s->used) { /* Entry::Vacant, src/packets.rs:344 */
             memset(s, 0, sizeof(*s));
             s->used = 1;
             s->rec.key = r->key;
+            s->rec.first_seen = pos; /* start_time, src/packets.rs:352 */
+            s->rec.end_seen = FB_SEEN_NONE;
             f->count++;
             if (st) st->new_sessions++;
         } else if (st) {
@@ -459,12 +473,19 @@ void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch
                 s->hist = (char*)realloc(s->hist, s->hist_cap);
             }
             s->hist[s->hist_len++] = (char)r->hist_char;
+            s->rec.hist_len = (uint32_t)s->hist_len;
+            const uint32_t b = hist_bit((char)r->hist_char);
+            if (b < 16u) s->rec.hist_mask |= (uint16_t)(1u << b);
             if ((r->tcp_flags & (TCP_FIN | TCP_RST)) && !s->ended) {
-                s->ended = 1;
-                conn_state_of(s->hist, s->hist_len, s->conn_state);
+                s->ended = 1; /* end_time = now, src/packets.rs:192-197, 422-426 */
+                s->rec.end_seen = pos;
+                s->rec.conn_state = conn_state_of(s->hist, s->hist_len, s->conn_state);
+                s->rec.end_mask = (uint8_t)(s->rec.hist_mask & 0xFFu);
             }
         }
+        s->rec.last_seen = pos; /* last_activity, src/packets.rs:184 */
     }
+    f->batch++;
 }
 
 uint64_t orc_flows_count(const orc_flows* f) { return f->count; }

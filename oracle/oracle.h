@@ -83,6 +83,7 @@ orc_flows* orc_flows_new(void);
 void orc_flows_free(orc_flows* f);
 void orc_flows_clear(orc_flows* f);
 /* Upsert records in order; adds new/updated counts into stats (may be NULL). */
+/* One call = one flow-table update (the high word of fb_flow_rec positions, FB_SEEN_NONE etc.). */
 void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* stats);
 uint64_t orc_flows_count(const orc_flows* f);
 /* Export sorted by the derived Ord of Session (src/sessions.rs:23-30). Returns count. */

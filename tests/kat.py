@@ -32,10 +32,17 @@ def key_of(k):
     return Session(Protocol[k[0]], ipaddress.ip_address(k[1]), k[2], ipaddress.ip_address(k[3]), k[4])
 
 
-def check_case(case, records, flows):
-    """Assert everything the reference asserts for this case."""
-    sess = {i.session: i for i in flows_to_sessions(flows)}
+def check_case(case, records, flows, histories=None):
+    """Assert everything the reference asserts for this case.  The flow table's ordered state
+    (hist_len, conn_state) must agree with the history derived from the packet-ordered records;
+    `histories` ({table slot: str}, from fb_flow_history_dev) is checked against it too."""
+    sess = {i.session: i for i in flows_to_sessions(flows, histories=histories)}
     hist = histories_from_records(records)
+    for k, info in sess.items():
+        h, cs = hist.get(k, ("", None))
+        assert info.stats.hist_len == len(h) and info.stats.conn_state == cs, (case["name"], k, info.stats, h, cs)
+        if histories is not None:
+            assert info.stats.history == h, (case["name"], k, info.stats.history, h)
     exp = case["expect"]
     name = case["name"]
     if "n_sessions" in exp:

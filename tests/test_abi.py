@@ -67,6 +67,10 @@ def test_record_layouts():
     assert N.PKT_OUT_DTYPE.fields["packet_length"][1] == 40
     assert N.PKT_OUT_DTYPE.fields["pkt_index"][1] == 52
     assert N.FLOW_REC_DTYPE.fields["outbound_bytes"][1] == 40
+    assert N.FLOW_REC_DTYPE.itemsize == 128
+    for f, off in (("first_seen", 88), ("last_seen", 96), ("end_seen", 104), ("hist_len", 112),
+                   ("hist_mask", 116), ("conn_state", 118), ("slot", 120)):
+        assert N.FLOW_REC_DTYPE.fields[f][1] == off, f
     assert N.DNS_OUT_DTYPE.itemsize == 16
     assert N.STATS_DTYPE.itemsize == 128
 

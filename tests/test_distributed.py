@@ -33,14 +33,15 @@ def _rank_flows(rank, world):
     out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
     fl = coracle.Flows()
     fl.update(out)
-    return fl.export_sorted()
+    return fl.export_sorted(), first
 
 
 def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        merged = global_flow_table(dist, _rank_flows(rank, world))
+        flows, first = _rank_flows(rank, world)
+        merged = global_flow_table(dist, flows, shard_first=first)
         np.save(os.path.join(outdir, "r%d.npy" % rank), merged.view(np.uint8))
     finally:
         dist.destroy_process_group()
@@ -55,7 +56,7 @@ def test_shard_range_covers_batch():
 
 def test_sort_keys_is_derived_ord():
     from oracle import coracle
-    flows = _rank_flows(0, 1)
+    flows = _rank_flows(0, 1)[0]
     rng = np.random.default_rng(1)
     shuffled = flows[rng.permutation(len(flows))]
     assert shuffled[sort_keys(_key_words(shuffled))].tobytes() == flows.tobytes()  # oracle sorts by Ord
@@ -65,7 +66,7 @@ def test_sort_keys_is_derived_ord():
 def test_gloo_world2_global_flow_table(tmp_path):
     world = 2
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
-    ref = _rank_flows(0, 1)  # whole batch, one process
+    ref = _rank_flows(0, 1)[0]  # whole batch, one process: counters and ordered state
     for r in range(world):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
         assert got.tobytes() == ref.tobytes(), r

@@ -133,9 +133,8 @@ def test_seg_flow_table_vs_dense(gpu_capture):
         assert g.stats["updated_sessions"] == int(r_st[0]["updated_sessions"])
     gf = gpu_capture.export_flows()
     rf = flows.export_sorted()
-    w = N.FLOW_REC_DTYPE.itemsize
-    rows = lambda a: sorted(a.tobytes()[i:i + w] for i in range(0, a.nbytes, w))
-    assert len(gf) == len(rf) and rows(gf) == rows(rf)
+    from test_gpu_parity import rows_sorted
+    assert len(gf) == len(rf) and rows_sorted(gf) == rows_sorted(rf)
     gpu_capture.clear_all_sessions()
 
 
