@@ -130,6 +130,19 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps
         flow_ms = sum(b.elapsed_ms(c) for _, b, c in evs) / steps
         stage = dict(parse_ms=parse_ms, flow_ms=flow_ms)
+        # ordered per-flow history of the last update (fb_flow_history_dev: keys + stable radix sort)
+        slots = n if mode == "dense" else (n + 63) // 64 * 64
+        d_h, d_s, d_n = N.DeviceBuffer(slots), N.DeviceBuffer(4 * slots), N.DeviceBuffer(4)
+        h0, h1 = N.Event(), N.Event()
+        N.check(lib.fb_flow_history_dev(ctx, d_h.ptr, d_s.ptr, d_n.ptr, stream.ptr))  # scratch allocation
+        h0.record(stream)
+        for _ in range(5):
+            N.check(lib.fb_flow_history_dev(ctx, d_h.ptr, d_s.ptr, d_n.ptr, stream.ptr))
+        h1.record(stream)
+        stage["history_ms"] = h0.elapsed_ms(h1) / 5
+        stage["history_chars"] = int(d_n.download(np.zeros(1, dtype=np.uint32), stream=stream.ptr)[0])
+        for x in (d_h, d_s, d_n):
+            x.free()
         cnt = C.c_uint64()
         N.check(lib.fb_flow_count(ctx, C.byref(cnt), stream.ptr))
         stage["flows"] = int(cnt.value)
@@ -226,7 +239,7 @@ def host_inclusive_overlap(N, lib, cfg, device, frames, offs, calls=20, n_ctx=2)
                      "H2D + kernel + D2H overlapped across contexts)" % (n_ctx, n_ctx))
 
 
-def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device):
+def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device, shard_first):
     """BASELINE config C5's exchange after the timed region: this rank's shard through the fused
     parse + classify + flow-table kernel, then the global per-flow counter merge
     (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce SUM over RCCL)."""
@@ -248,7 +261,7 @@ def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device):
     got = C.c_uint64()
     t0 = time.perf_counter()
     N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
-    merged = global_flow_table(dist_nccl, flows[: got.value], device=device)
+    merged = global_flow_table(dist_nccl, flows[: got.value], device=device, shard_first=shard_first)
     el = time.perf_counter() - t0
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
@@ -348,6 +361,7 @@ def main():
     if main_r["stage"]:
         sg = main_r["stage"]
         extra["c4_stages"] = dict(parse_ms=round(sg["parse_ms"], 4), flow_update_ms=round(sg["flow_ms"], 4),
+                                  history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
@@ -393,7 +407,7 @@ def main():
                 get_world_size = staticmethod(lambda group=None: tdist.get_world_size(g))
                 all_gather = staticmethod(lambda a, b, group=None: tdist.all_gather(a, b, group=g))
                 all_reduce = staticmethod(lambda t, op, group=None: tdist.all_reduce(t, op=op, group=g))
-            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], _D, dev)
+            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], _D, dev, rank * n)
         except Exception as e:  # the exchange is reported, never allowed to break the bench line
             extra["c5_flow_reduce"] = {"error": repr(e)[:300]}
 

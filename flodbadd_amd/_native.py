@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-GPU_LIB_PATH = os.path.join(PKG, "libflodbadd_gpu.so")
+GPU_LIB_PATH = os.environ.get("FLODBADD_GPU_LIB") or os.path.join(PKG, "libflodbadd_gpu.so")  # override: tools/
 SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
 
 FB_ABI_VERSION = 2

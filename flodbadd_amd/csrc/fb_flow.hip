@@ -289,7 +289,9 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, unsigned l
         if (b < 8u) atomicMin(q32 + 8 + b, e3.y);
         if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + 2, pos);
     }
+#ifndef FB_NO_REC_FLOW
     if (rec_flow) rec_flow[e3.y] = slot_base + i;
+#endif
     return result;
 }
 

@@ -80,7 +80,10 @@ constexpr uint32_t kFlowSlots = 512;             // slots per partition: 64 KiB 
 constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
 constexpr uint32_t kFlowChunk = 16384;           // records per bucketing workgroup (K1)
 constexpr uint32_t kFlowK1Threads = 1024;
-constexpr uint32_t kFlowK2Threads = 256;
+#ifndef FB_K2_THREADS
+#define FB_K2_THREADS 1024  // 16 waves: the apply is latency-bound (256: 2.35 ms, 512: 1.64, 1024: 1.39 at C4)
+#endif
+constexpr uint32_t kFlowK2Threads = FB_K2_THREADS;
 constexpr uint64_t kFlowMaxCapacity = (uint64_t)kFlowSlots * kFlowMaxParts;
 struct FlowSlot {
     unsigned long long tag;
