@@ -39,13 +39,16 @@ def algorithmic_bytes(offsets, n_session, n_dns):
     return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
 
 
-def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg"):
+def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1):
     """Time `steps` launches of the hot path.  mode "seg": fb_parse_classify_seg_dev (records
     compacted per 64-frame wavefront segment, no cross-workgroup dependency); mode "dense":
     fb_parse_classify_dev (one batch-wide compaction through a decoupled look-back).
     flow=True (C4): the two stages of fb_process[_seg]_dev -- parse + classify, then the
     session-table upsert with per-flow counters -- with an event between them so each stage is
-    timed."""
+    timed.
+    bpl > 1 (mode "seg", no flow): each launch covers bpl batches (fb_parse_classify_seg_batches_dev,
+    one batch = one step, each with its own outputs and stats), so `steps` steps take
+    ceil(steps / bpl) launches."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n)
     nbytes = frames.nbytes
@@ -63,6 +66,36 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
             d_dns = N.DeviceBuffer(n * N.DNS_OUT_DTYPE.itemsize)
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
         bufs.append((d_fr, d_off, d_out, d_dns, d_st))
+
+    if bpl > 1:
+        assert mode == "seg" and not flow and rotate % bpl == 0, (mode, flow, rotate, bpl)
+        groups = []
+        for j in range(rotate // bpl):
+            d = np.zeros(bpl, dtype=N.SEG_BATCH_DTYPE)
+            for t in range(bpl):
+                d_fr, d_off, d_out, d_seg, d_st = bufs[j * bpl + t]
+                d[t] = (d_fr.ptr.value, nbytes, d_off.ptr.value, n, 0, d_out.ptr.value, d_seg.ptr.value, 0,
+                        d_st.ptr.value)
+            groups.append(d)
+
+    def launch(j, count):
+        """Launch j of a multi-batch run: batches j*bpl .. j*bpl+count-1."""
+        rc = lib.fb_parse_classify_seg_batches_dev(ctx, N.ptr(groups[j % len(groups)]), count, stream.ptr)
+        if rc != 0:
+            raise RuntimeError(lib.fb_last_error().decode())
+
+    def run_steps(k):
+        """k steps; returns the number of kernel launches."""
+        if bpl == 1:
+            for i in range(k):
+                step(i)
+            return k
+        full, rest = divmod(k, bpl)
+        for j in range(full):
+            launch(j, bpl)
+        if rest:
+            launch(full, rest)
+        return full + (1 if rest else 0)
 
     def step(i, ev=None):
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
@@ -84,8 +117,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
 
     if flow:
         N.check(lib.fb_flow_clear(ctx, stream.ptr))
-    for i in range(warmup):
-        step(i)
+    run_steps(warmup)
     stream.sync()
     st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
     if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
@@ -99,13 +131,14 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     stream.sync()
     t0 = time.perf_counter()
     ev0.record(stream)
-    for i in range(steps):
-        if flow:
+    if flow:
+        for i in range(steps):
             evs[i][0].record(stream)
             step(i, evs[i][1])
             evs[i][2].record(stream)
-        else:
-            step(i)
+        launches = steps
+    else:
+        launches = run_steps(steps)
     ev1.record(stream)
     stream.sync()
     t1 = time.perf_counter()
@@ -151,7 +184,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     for b in bufs:
         for x in b:
             x.free()
-    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage,
+    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage, launches=launches,
                 stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
@@ -295,12 +328,15 @@ def cpu_baseline(frames, offs, seconds):
                        % (passes, n, el))
 
 
-def load_traffic(config_id):
+def load_traffic(config_id, bpl=1):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (tools/prof_summary.py), scaled to `bpl` batches per launch."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(str(config_id), {}).get("hbm_bytes_per_launch")
+            d = json.load(f).get(str(config_id), {})
+        b = d.get("hbm_bytes_per_launch")
+        return None if b is None else b / d.get("batches_per_launch", 1) * bpl
     except (OSError, ValueError):
         return None
 
@@ -321,6 +357,9 @@ def main():
     ap.add_argument("--mode", choices=["seg", "dense"], default="seg",
                     help="output layout: per-wavefront segments (default) or one batch-wide compaction")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
+    ap.add_argument("--batches-per-launch", type=int, default=None,
+                    help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
+                         "default = the rotated batches (C2 8, C3 4), 1 for C4")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -351,10 +390,13 @@ def main():
 
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
     rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
+    bpl = (args.batches_per_launch or rotate) if (args.mode == "seg" and args.config != 4) else 1
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
-                        flow=args.config == 4, mode=args.mode)
-    per_launch_s = main_r["ev_ms"] / 1e3 / args.steps
-    achieved = main_r["algo_bytes"] / per_launch_s / 1e9
+                        flow=args.config == 4, mode=args.mode, bpl=bpl)
+    # the dominant kernel's launches: algorithmic bytes per launch / average launch duration
+    per_launch_s = main_r["ev_ms"] / 1e3 / main_r["launches"]
+    algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
+    achieved = algo_per_launch / per_launch_s / 1e9
     value = world * n * args.steps / main_r["elapsed"] / 1e6
 
     extra = {}
@@ -365,6 +407,15 @@ def main():
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
+    if bpl > 1:  # the same workload with one batch per launch
+        st_1 = max(args.steps // 2, 10)
+        r1 = run_config(N, lib, ctx, args.config, n, st_1, max(args.warmup // 2, 2), rotate, rank, world, dist,
+                        mode=args.mode, bpl=1)
+        pl1 = r1["ev_ms"] / 1e3 / r1["launches"]
+        extra["single_batch_launch"] = dict(value=round(world * n * st_1 / r1["elapsed"] / 1e6, 2),
+                                            unit="Mpackets/s", ms_per_step=round(r1["elapsed"] * 1e3 / st_1, 4),
+                                            roofline_achieved_GBs=round(r1["algo_bytes"] / pl1 / 1e9, 1),
+                                            roofline_frac=round(r1["algo_bytes"] / pl1 / 1e9 / HBM_PEAK_GBS, 4))
     if not args.no_other_mode:
         other = "dense" if args.mode == "seg" else "seg"
         st_o = max(args.steps // 2, 10)
@@ -377,14 +428,15 @@ def main():
                                       roofline_frac=round(ro["algo_bytes"] / plo / 1e9 / HBM_PEAK_GBS, 4))
     if not args.no_imix and args.config == 2:
         steps3 = max(args.steps // 2, 10)
+        bpl3 = 4 if args.mode == "seg" and bpl > 1 else 1
         r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist,
-                        mode=args.mode)
+                        mode=args.mode, bpl=bpl3)
         pl3 = r3["ev_ms"] / 1e3 / steps3
         extra["imix_c3"] = dict(value=round(world * (1 << 20) * steps3 / r3["elapsed"] / 1e6, 2),
                                 unit="Mpackets/s", ms_per_step=round(r3["elapsed"] * 1e3 / steps3, 4),
                                 roofline_achieved_GBs=round(r3["algo_bytes"] / pl3 / 1e9, 1),
                                 roofline_frac=round(r3["algo_bytes"] / pl3 / 1e9 / HBM_PEAK_GBS, 4),
-                                algo_bytes_per_launch=r3["algo_bytes"])
+                                batches_per_launch=bpl3, algo_bytes_per_batch=r3["algo_bytes"])
 
     if not args.no_host and rank == 0 and args.config == 2:
         extra["host_inclusive_c2"] = host_inclusive(N, lib, ctx, main_r["frames"], main_r["offs"])
@@ -431,14 +483,15 @@ def main():
             "dtype": "u8",
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.config], "frames_per_gpu_per_step": n,
-                       "rotated_batches": rotate, "filter": "GlobalOnly",
-                       "output": ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)"
+                       "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
+                       "output": ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
+                                  "%d batches per launch, each with its own outputs and stats)" % bpl
                                   if args.mode == "seg" else
                                   "batch-wide compaction (fb_parse_classify_dev)"),
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
-                         "algo_bytes_per_launch": main_r["algo_bytes"],
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, bpl),
+                         "algo_bytes_per_launch": int(algo_per_launch),
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 5)},
             "cpu_baseline": cpu,
             "batch_stats": main_r["stats"],

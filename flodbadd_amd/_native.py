@@ -56,6 +56,12 @@ FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "
 
 FB_SEG_FRAMES = 64
 SEG_BYTES = FB_SEG_FRAMES * 56
+FB_MAX_SEG_BATCHES = 12
+# fb_seg_batch: one batch of fb_parse_classify_seg_batches_dev (device pointers as integers)
+SEG_BATCH_DTYPE = np.dtype([("d_frames", "<u8"), ("frames_bytes", "<u8"), ("d_offsets", "<u8"), ("n", "<u4"),
+                            ("reserved", "<u4"), ("d_out", "<u8"), ("d_seg", "<u8"), ("d_class", "<u8"),
+                            ("d_stats", "<u8")])
+assert SEG_BATCH_DTYPE.itemsize == 64
 
 
 def seg_unpack(out_bytes, seg):
@@ -119,6 +125,7 @@ GPU_SYMBOLS = [
     ("fb_process_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_parse_classify_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_process_parsed_seg_dev", _I, [_P, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_parse_classify_seg_batches_dev", _I, [_P, _P, _U32, _P]),
     ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_history_dev", _I, [_P, _P, _P, _P, _P]),

@@ -354,7 +354,7 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
 }
 
 // Shared launch of the segmented streaming kernel (frames or parsed packets).
-static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s) {
+static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s, const SegBatches* batches = nullptr) {
     const uint64_t units = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
     int rc = ensure_status(c, units, s);
     if (rc) return rc;
@@ -374,11 +374,63 @@ static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s) {
     p.error = c->d_error + (p.epoch & 1u);
     p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
     p.dbg = nullptr;
+    SegBatches sb;
+    memset(&sb, 0, sizeof(sb));
+    if (!batches) {  // one batch, described by p
+        sb.count = 1;
+        SegBatch& B = sb.b[0];
+        B.frames = p.frames;
+        B.offsets = p.offsets;
+        B.out = p.out;
+        B.seg = p.seg;
+        B.cls = p.cls;
+        B.stats = p.stats;
+        B.n = n;
+        B.frames_bytes = p.frames_bytes;
+        sb.total_segs = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    } else {
+        sb = *batches;
+    }
     const uint32_t waves = parse_seg_block_threads() / 64u;
-    const uint32_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    const uint32_t nseg = sb.total_segs;
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (nseg + waves - 1) / waves));
-    HIP_TRY(launch_parse_seg(p, grid, s));
+    HIP_TRY(launch_parse_seg(p, sb, grid, s));
     return FB_OK;
+}
+
+int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, uint32_t count, void* stream) {
+    if (!c || !batches || count == 0 || count > FB_MAX_SEG_BATCHES)
+        return set_err(FB_ERR_INVAL, "ctx, batches and 1 <= count <= FB_MAX_SEG_BATCHES are required");
+    SegBatches sb;
+    memset(&sb, 0, sizeof(sb));
+    uint32_t segs = 0, n_max = 0;
+    for (uint32_t k = 0; k < count; ++k) {
+        const fb_seg_batch& x = batches[k];
+        if (!x.d_stats) return set_err(FB_ERR_INVAL, "batch %u: d_stats is required", k);
+        if (x.n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "batch %u: n > FB_MAX_BATCH_PACKETS", k);
+        if (x.frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "batch %u: frames_bytes must be < 4 GiB", k);
+        if (!x.d_offsets || (x.n && (!x.d_out || !x.d_seg)))
+            return set_err(FB_ERR_INVAL, "batch %u: d_offsets, d_out and d_seg are required", k);
+        if (x.n && x.frames_bytes && !x.d_frames) return set_err(FB_ERR_INVAL, "batch %u: d_frames is NULL", k);
+        SegBatch& B = sb.b[k];
+        B.frames = x.d_frames;
+        B.offsets = x.d_offsets;
+        B.out = x.d_out;
+        B.seg = x.d_seg;
+        B.cls = x.d_class;
+        B.stats = x.d_stats;
+        B.n = x.n;
+        B.frames_bytes = (uint32_t)x.frames_bytes;
+        B.seg_start = segs;
+        segs += (x.n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+        n_max = std::max(n_max, x.n);
+    }
+    sb.count = count;
+    sb.total_segs = segs;
+    DeviceGuard g(c->device);
+    ParseParams p;
+    memset(&p, 0, sizeof(p));
+    return launch_seg(c, p, n_max, (hipStream_t)stream, &sb);
 }
 
 int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,

@@ -22,9 +22,9 @@ inline uint64_t stat_slots(uint64_t units) { return units > kMaxBlocks ? units :
 //   rsum[rsum_words(units)]  k_parse_ws: per-round sums of unit aggregates (round r = units
 //                          [r*G, (r+1)*G)) [epoch:8 | 0 | n_dns:27 | n_session:28];
 //                          k_parse_seg: 3 epoch-tagged partial-count words per block
-//   tick[64]              k_parse_seg arrival tickets (u32), two epoch-parity sets of 16
+//   tick[128 u64]         k_parse_seg packed stats words, 8 per batch of a launch
 inline uint64_t rsum_words(uint64_t units) { return units > 4ull * kMaxBlocks ? units : 4ull * kMaxBlocks; }
-inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + rsum_words(units) + 64ull; }
+inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + rsum_words(units) + 128ull; }
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
@@ -55,7 +55,7 @@ struct ParseParams {
     unsigned long long* tagg;   // [units]
     unsigned long long* wstat;  // [kMaxBlocks][2]
     unsigned long long* rsum;   // [rounds] round sums (k_parse_ws look-back) / block partials (k_parse_seg)
-    uint32_t* tick;             // [2][16] arrival tickets (k_parse_seg)
+    uint32_t* tick;             // k_parse_seg: 8 packed u64 stats words per batch of the launch
     uint32_t* seg;              // k_parse_seg: per 64-frame segment, n_session | n_dns << 16
     const DevConfig* cfg;
     uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
@@ -65,6 +65,27 @@ struct ParseParams {
     uint32_t* error;       // this launch's error word (epoch parity); nonzero: a bounded spin expired
     uint32_t* error_next;  // the other parity's word, zeroed by this launch for the next one
     unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
+};
+
+// Batches of one k_parse_seg launch (fb_parse_classify_seg_batches_dev): the launch streams over
+// the concatenation of their segments; batch k owns global segments [seg_start, next seg_start).
+constexpr uint32_t kMaxSegBatches = FB_MAX_SEG_BATCHES;
+struct SegBatch {
+    const uint8_t* frames;
+    const uint32_t* offsets;
+    fb_pkt_out* out;
+    uint32_t* seg;
+    uint8_t* cls;
+    fb_batch_stats* stats;
+    uint32_t n;
+    uint32_t frames_bytes;
+    uint32_t seg_start;
+    uint32_t pad;
+};
+struct SegBatches {
+    SegBatch b[kMaxSegBatches];
+    uint32_t count;
+    uint32_t total_segs;
 };
 
 // Flow (session) table, partitioned for owner-computes updates (fb_flow.hip):
@@ -134,7 +155,7 @@ struct FlowParams {
 hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse(int* blocks_per_cu);
-hipError_t launch_parse_seg(const ParseParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse_seg(int* blocks_per_cu);
 uint32_t parse_seg_block_threads();
 uint32_t parse_unit_frames();  // frames per look-back unit of the product parse kernel

@@ -787,8 +787,9 @@ __global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
 // tail, the j-th at byte (sg+1)*3584 - 16*(j+1).  seg[sg] = n_session | n_dns << 16.  No wave
 // waits for any other: no look-back, no cross-block prefix -- the kernel streams at the rate of
 // its loads and stores.  Consumers (the session-table update, the host wrapper) read the
-// segments through seg[].  Batch stats: per-block partials (epoch-tagged) + arrival tickets
-// sharded by blockIdx % 8; the last arrival sums the partials.
+// segments through seg[].  One launch may cover several batches (fb_parse_classify_seg_batches_dev):
+// the waves stream over the concatenation of their segments, each batch with its own frames,
+// outputs and stats.  Batch stats: packed per-batch device words, see the end of the kernel.
 // ============================================================================================
 #ifndef FB_SEG_WAVES
 #define FB_SEG_WAVES 16
@@ -806,18 +807,18 @@ constexpr uint32_t kSegBytes = 64u * 56u;  // one segment of output: 64 record s
 
 // Ablations (tools/ubench_ws.hip): kNoStore drops every store, kNoLookback here means "no
 // classification" (each frame becomes a SESSION record of raw header words).
-template <bool PARSED, uint32_t FLAGS = kFlagsProduct>
-__global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_parse_seg(const ParseParams P) {
+template <bool PARSED, uint32_t FLAGS = kFlagsProduct, bool MULTI = false>
+__global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_parse_seg(const ParseParams P,
+                                                                                      const SegBatches SB) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: segment resources in SGPRs
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t nseg = (P.n + 63u) / 64u;
-    const uint32_t ep = P.epoch;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.frames, (short)0, (int)P.frames_bytes, 0x00020000);
+    const uint32_t nseg = SB.total_segs;  // segments of all the launch's batches
+    const uint32_t nb = MULTI ? SB.count : 1u;
+    constexpr uint32_t kAcc = kMaxSegBatches * 10u;
     __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
     __shared__ unsigned long long s_stage[kSegWaves][64 * 7];
-    __shared__ uint32_t s_acc[11];  // block counters (see the stats section) + wave arrivals
+    __shared__ uint32_t s_acc[kAcc + 1];  // per batch: block counters (see the stats section); wave arrivals
     const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
     const unsigned long long lmask = (1ull << lane) - 1ull;
     unsigned long long* stage = s_stage[wave];
@@ -831,7 +832,21 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     sstamp(0);
     uint32_t iter = 0;
     uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
-    if (tid < 11u) s_acc[tid] = 0u;  // published by the prologue barrier
+    uint32_t a_k = 0u;  // the batch the counters belong to
+    if (tid <= kAcc) s_acc[tid] = 0u;  // published by the prologue barrier
+
+    // Batch of global segment g.  A wave visits its segments in increasing order, and so do its
+    // header fetches and its offsets loads, so each keeps a monotone cursor (wave-uniform scalar
+    // compares against the kernel arguments; single-batch launches compile it away).
+    uint32_t k_q = 0u, k_h = 0u, k_s = 0u;
+    auto batch_of = [&](uint32_t& k, uint32_t g) {
+        if constexpr (MULTI)
+            while (k + 1u < nb && g >= SB.b[k + 1u].seg_start) ++k;
+        return k;
+    };
+    auto frames_rsrc = [&](uint32_t k) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)SB.b[k].frames, (short)0, (int)SB.b[k].frames_bytes, 0x00020000);
+    };
 
     // One segment per iteration with the next segment's header loads in flight.  Every store of
     // an iteration is an unconditional buffer store (lanes with nothing to write use an offset
@@ -841,9 +856,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     constexpr uint32_t kOob = 0x80000000u;
     const uint32_t stride = G * kSegWaves;
-    const __amdgpu_buffer_rsrc_t r_seg = __builtin_amdgcn_make_buffer_rsrc(P.seg, (short)0, (int)(nseg * 4u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t r_cls =
-        __builtin_amdgcn_make_buffer_rsrc(P.cls, (short)0, P.cls ? (int)P.n : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_drop = __builtin_amdgcn_make_buffer_rsrc(SB.b[0].seg, (short)0, 0, 0x00020000);
     auto vmov = [](uint32_t x) {
         uint32_t y;
         asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
@@ -856,6 +869,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     // no back-edge copy of a pending load), X.q <- offsets of the one after.  Every step issues
     // the same VMEM sequence (4 header loads, 2 offset loads, 8 stores) and the prologue mirrors
     // it with dropped stores, so the compiler's vmcnt waits let D-1 younger steps' traffic pass.
+    // Segments past the launch's end clamp to the last batch's last offset (nothing is read
+    // out of bounds; the step that would use them never runs).
     constexpr int D = kSegDepth;
     struct Set {
         Hdr h;
@@ -863,19 +878,21 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     };
     Set SS[D];
     uint4 pin[4];
-    auto load_q = [&](uint32_t sg, uint2& q) {
-        const uint32_t i = sg * 64u + lane;
-        q = make_uint2(P.offsets[min(i, P.n)], P.offsets[min(i + 1u, P.n)]);
+    auto load_q = [&](uint32_t g, uint2& q) {
+        const uint32_t k = batch_of(k_q, g);
+        const uint32_t i = (g - SB.b[k].seg_start) * 64u + lane, n = SB.b[k].n;
+        const uint32_t* off = SB.b[k].offsets;
+        q = make_uint2(off[min(i, n)], off[min(i + 1u, n)]);
     };
-    auto fetch = [&](Set& X, uint32_t next_q) {
-        load_headers1(rs, X.q.x, X.h);
+    auto fetch = [&](Set& X, uint32_t g_h, uint32_t next_q) {  // X.q holds segment g_h's offsets
+        load_headers1(frames_rsrc(batch_of(k_h, g_h)), X.q.x, X.h);
         X.c = make_uint2(vmov(X.q.x), vmov(X.q.y));
         load_q(next_q, X.q);
     };
     auto dropped_stores = [&]() {
         if constexpr ((FLAGS & kNoStore) == 0u) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_seg, kOob + 64u * j, 0, 0);
+            for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
         }
     };
     auto load_parsed = [&](uint32_t sg) {
@@ -917,7 +934,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     if constexpr (!PARSED) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            fetch(SS[d], sg + (uint32_t)(d + D) * stride);
+            fetch(SS[d], sg + d * stride, sg + (uint32_t)(d + D) * stride);
             dropped_stores();
         }
     } else {
@@ -925,9 +942,28 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     }
     ws_tick();  // configuration in LDS (LDS-only barrier: the header loads stay in flight)
     sstamp(1);
+    // a wave's counters go to LDS whenever its segments move on to the next batch
+    auto flush = [&]() {
+        const uint32_t a_tot = a_s + a_f;
+        const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
+        if (lane < 10u) {
+            uint32_t v = 0u;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
+            __hip_atomic_fetch_add(&s_acc[a_k * 10u + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        a_s = a_d = a_f = a_t = a_4 = a_b = a_n = 0u;
+    };
     auto step = [&](uint32_t sg, Set& X) {
-            const uint32_t i = sg * 64u + lane;
-            const bool valid = i < P.n;
+            const uint32_t k = batch_of(k_s, sg);
+            if (MULTI && k != a_k) {
+                flush();
+                a_k = k;
+            }
+            const SegBatch& B = SB.b[k];
+            const uint32_t ls = sg - B.seg_start;  // the segment within its batch
+            const uint32_t i = ls * 64u + lane;
+            const bool valid = i < B.n;
             Pkt kk;
             if constexpr ((FLAGS & kNoLookback) != 0u) {
                 kk.cls = FB_CLASS_SESSION;
@@ -937,7 +973,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     #pragma unroll
                 for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
             } else if constexpr (!PARSED) {
-                process_frame(rs, cfg, cfg, X.h, valid ? X.c.x : 1u, valid ? X.c.y : 0u, P.frames_bytes, i, kk);
+                process_frame(frames_rsrc(k), cfg, cfg, X.h, valid ? X.c.x : 1u, valid ? X.c.y : 0u, B.frames_bytes, i,
+                              kk);
             } else {
                 const uint4 a = pin[0], bb = pin[1], cc = pin[2], d = pin[3];
                 const uint32_t src[4] = {a.x, a.y, a.z, a.w}, dst[4] = {bb.x, bb.y, bb.z, bb.w};
@@ -964,12 +1001,16 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             __builtin_amdgcn_wave_barrier();
             // prefetch: headers of this set's next segment (offsets already here), offsets of the
             // one after
-            if constexpr (!PARSED) fetch(X, sg + 2u * D * stride);
+            if constexpr (!PARSED) fetch(X, sg + D * stride, sg + 2u * D * stride);
             else load_parsed(sg + stride);
             if constexpr ((FLAGS & kNoStore) == 0u) {
             // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
                 const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
-                    reinterpret_cast<uint8_t*>(P.out) + (size_t)sg * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
+                    reinterpret_cast<uint8_t*>(B.out) + (size_t)ls * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
+                const __amdgpu_buffer_rsrc_t r_seg =
+                    __builtin_amdgcn_make_buffer_rsrc(B.seg, (short)0, (int)(((B.n + 63u) / 64u) * 4u), 0x00020000);
+                const __amdgpu_buffer_rsrc_t r_cls =
+                    __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)B.n : 0, 0x00020000);
                 const uint32_t words = cs * 7u, body = words >> 1;
         #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -990,7 +1031,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                     __builtin_amdgcn_raw_buffer_store_b128(
                         v, r_out, is_d ? kSegBytes - 16u * (1u + (uint32_t)__popcll(m_dns & lmask)) : kOob, 0, 0);
                 }
-                __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? sg * 4u : kOob, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? ls * 4u : kOob, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
             }
             __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
@@ -1012,51 +1053,46 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         if (sg + d * stride < nseg) step(sg + d * stride, SS[d]);
     sstamp(14);
     // ---- batch stats, no barrier and no partials read-back:
-    // every wave adds its counters into LDS; the block's last wave (LDS arrival count) adds the
-    // block's counters into 5 packed device words [ticket:10 | hi:27 | lo:27] (one atomic per
-    // word, lanes 0-4 in parallel); the block whose add brings a word's ticket to G owns that
-    // word's final totals (old + its own add), writes those two stats fields and zeroes the word
-    // for the next launch.  The derived counts (total, udp, ipv6, drop) are linear, so they are
-    // counted per wave and summed like the others.
+    // every wave adds its counters into LDS (per batch); the block's last wave (LDS arrival
+    // count) adds the block's counters of every batch into that batch's 5 packed device words
+    // [ticket:10 | hi:27 | lo:27] (one atomic per word, lanes 5k..5k+4 for batch k in parallel);
+    // the block whose add brings a word's ticket to G owns that word's final totals (old + its
+    // own add), writes those two stats fields and zeroes the word for the next launch.  The
+    // derived counts (total, udp, ipv6, drop) are linear, so they are counted per wave and summed
+    // like the others.
     {
-        const uint32_t a_tot = a_s + a_f;
-        const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
-        if (lane < 10u) {
-            uint32_t v = 0u;
-#pragma unroll
-            for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
-            __hip_atomic_fetch_add(&s_acc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        flush();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         uint32_t arrived = 0u;
-        if (lane == 0u) arrived = __hip_atomic_fetch_add(&s_acc[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0u) arrived = __hip_atomic_fetch_add(&s_acc[kAcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         arrived = __shfl(arrived, 0, 64);
-        if (arrived == (uint32_t)kSegWaves - 1u && lane < 5u) {
+        if (arrived == (uint32_t)kSegWaves - 1u && lane < 5u * nb) {
             asm volatile("" ::: "memory");
-            const unsigned long long lo = s_acc[2u * lane], hi = s_acc[2u * lane + 1u];
-            unsigned long long* word = reinterpret_cast<unsigned long long*>(P.tick) + lane;
+            const uint32_t k = lane / 5u, j = lane - 5u * k;
+            const unsigned long long lo = s_acc[k * 10u + 2u * j], hi = s_acc[k * 10u + 2u * j + 1u];
+            unsigned long long* word = reinterpret_cast<unsigned long long*>(P.tick) + k * 8u + j;
             const unsigned long long add = (1ull << 54) | (hi << 27) | lo;
             const unsigned long long old = __hip_atomic_fetch_add(word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((old >> 54) == (unsigned long long)G - 1u) {
                 const unsigned long long t = old + add, m27 = (1ull << 27) - 1ull;
                 const unsigned long long f_lo = t & m27, f_hi = (t >> 27) & m27;
                 __hip_atomic_store(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                fb_batch_stats* S = P.stats;
+                fb_batch_stats* S = SB.b[k].stats;
                 if (S) {
-                    if (lane == 0u) {
+                    if (j == 0u) {
                         S->n_session = f_lo;
                         S->n_filtered = f_hi;
                         S->new_sessions = 0ull;
                         S->updated_sessions = 0ull;
                         S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
-                    } else if (lane == 1u) {
+                    } else if (j == 1u) {
                         S->n_dns = f_lo;
                         S->bad_offsets = f_hi;
-                    } else if (lane == 2u) {
+                    } else if (j == 2u) {
                         S->tcp_processed = f_lo;
                         S->udp_processed = f_hi;
-                    } else if (lane == 3u) {
+                    } else if (j == 3u) {
                         S->ipv4_processed = f_lo;
                         S->ipv6_processed = f_hi;
                     } else {
@@ -1070,9 +1106,11 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     sstamp(15);
 }
 
-hipError_t launch_parse_seg(const ParseParams& p, uint32_t grid, hipStream_t s) {
-    if (p.parsed) hipLaunchKernelGGL((k_parse_seg<true>), dim3(grid), dim3(kSegThreads), 0, s, p);
-    else hipLaunchKernelGGL((k_parse_seg<false>), dim3(grid), dim3(kSegThreads), 0, s, p);
+hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s) {
+    if (p.parsed) hipLaunchKernelGGL((k_parse_seg<true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
+    else if (sb.count > 1u)
+        hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct, true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
+    else hipLaunchKernelGGL((k_parse_seg<false>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     return hipGetLastError();
 }
 hipError_t occupancy_parse_seg(int* blocks_per_cu) {

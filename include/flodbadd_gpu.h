@@ -323,6 +323,28 @@ int fb_parse_classify_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t fra
                               const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out,
                               uint32_t* d_seg, uint8_t* d_class, fb_batch_stats* d_stats,
                               void* stream);
+/*
+ * Several segmented batches in ONE launch: the same results as fb_parse_classify_seg_dev called
+ * once per batch (each batch its own frames, offsets, d_out, d_seg, d_class, d_stats), but the
+ * kernel streams from one batch into the next without a launch boundary, so the per-launch
+ * start-up (configuration load, the first offsets -> headers round trips) and the tail are paid
+ * once.  `batches` is a HOST array of `count` (1..FB_MAX_SEG_BATCHES) descriptors holding DEVICE
+ * pointers; each batch follows the fb_parse_classify_seg_dev rules.  Asynchronous.
+ */
+#define FB_MAX_SEG_BATCHES 12u
+typedef struct fb_seg_batch {
+    const uint8_t* d_frames;
+    uint64_t frames_bytes;     /* < 4 GiB */
+    const uint32_t* d_offsets; /* n + 1 entries */
+    uint32_t n;
+    uint32_t reserved;         /* 0 */
+    fb_pkt_out* d_out;         /* ceil(n/64)*64 records */
+    uint32_t* d_seg;           /* ceil(n/64) words */
+    uint8_t* d_class;          /* n bytes, or NULL */
+    fb_batch_stats* d_stats;   /* required */
+} fb_seg_batch;                /* 64 bytes */
+int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, uint32_t count, void* stream);
+
 /* fb_process_parsed_dev with segmented output (same segment layout; no DNS records). */
 int fb_process_parsed_seg_dev(fb_ctx* ctx, const fb_parsed_pkt* d_in, uint32_t n,
                               fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,

@@ -47,9 +47,9 @@ def _run_seg(cap, frames, offs, flow=False):
     return raw, seg, cls, st
 
 
-def _check(cap, frames, offs, flt=2, **cfg_kw):
+def _check(cap, frames, offs, flt=2, res=None, **cfg_kw):
     n = len(offs) - 1
-    raw, seg, cls, st = _run_seg(cap, frames, offs)
+    raw, seg, cls, st = _run_seg(cap, frames, offs) if res is None else res
     r_out, r_dns, r_cls, r_st = coracle.parse_classify(coracle.make_cfg(flt, **cfg_kw), frames, offs)
     assert np.array_equal(cls, r_cls)
     assert np.array_equal(seg, _expected_seg(r_out, r_dns, n))
@@ -165,3 +165,58 @@ def test_seg_parsed_path(gpu_capture):
     st2 = d_st2.download(np.zeros(1, dtype=N.STATS_DTYPE))
     dense2 = d_out2.download(np.zeros(int(st2[0]["n_session"]), dtype=N.PKT_OUT_DTYPE))
     assert g_out.tobytes() == dense2.tobytes()
+
+
+def _run_batches(cap, batches):
+    """fb_parse_classify_seg_batches_dev over several batches in one launch."""
+    lib = N.gpu_lib()
+    desc = np.zeros(len(batches), dtype=N.SEG_BATCH_DTYPE)
+    keep, outs = [], []
+    for k, (frames, offs) in enumerate(batches):
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        n = offs.size - 1
+        nseg = max((n + 63) // 64, 1)
+        d_fr = N.DeviceBuffer(max(frames.nbytes, 1))
+        if frames.nbytes:
+            d_fr.upload(frames)
+        d_off = N.DeviceBuffer(offs.nbytes).upload(offs)
+        d_out = N.DeviceBuffer(nseg * N.SEG_BYTES)
+        d_out.memset(0xA5)
+        d_seg, d_cls, d_st = N.DeviceBuffer(nseg * 4), N.DeviceBuffer(max(n, 1)), N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        d_st.memset(0x5A)  # every batch's stats must be written, empty ones included
+        desc[k] = (d_fr.ptr.value, frames.nbytes, d_off.ptr.value, n, 0, d_out.ptr.value, d_seg.ptr.value,
+                   d_cls.ptr.value, d_st.ptr.value)
+        keep += [d_fr, d_off]
+        outs.append((n, nseg, d_out, d_seg, d_cls, d_st))
+    N.check(lib.fb_parse_classify_seg_batches_dev(cap.ctx, N.ptr(desc), len(batches), None))
+    res = []
+    for n, nseg, d_out, d_seg, d_cls, d_st in outs:
+        st = d_st.download(np.zeros(1, dtype=N.STATS_DTYPE))
+        raw = d_out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8))
+        seg = d_seg.download(np.zeros(nseg, dtype=np.uint32))[: (n + 63) // 64]
+        cls = d_cls.download(np.zeros(max(n, 1), dtype=np.uint8))[:n]
+        res.append((raw, seg, cls, st))
+    return res
+
+
+def test_seg_batches_one_launch(gpu_capture):
+    """Several batches of different shapes (an empty one, a 1-frame one, IMIX, edge frames) in
+    one launch: each batch equals the oracle exactly as a separate launch would."""
+    batches = [synth.generate(2, 5000), fg.pack([]), synth.generate(3, 70001),
+               fg.pack([fg.tcp_frame("1.2.3.4", 1000, "5.6.7.8", 80, fg.SYN, 0)]),
+               fg.pack([f for _, f in fg.edge_cases()] * 3), synth.generate(4, 200000, first=7)]
+    for rep in range(3):  # across the per-batch stats words' reuse
+        for (frames, offs), res in zip(batches, _run_batches(gpu_capture, batches)):
+            _check(gpu_capture, frames, offs, res=res)
+    full = [synth.generate(2, 1 << 16, first=k << 16) for k in range(N.FB_MAX_SEG_BATCHES)]
+    for (frames, offs), res in zip(full, _run_batches(gpu_capture, full)):
+        _check(gpu_capture, frames, offs, res=res)
+
+
+def test_seg_batches_rejects_bad_counts(gpu_capture):
+    lib = N.gpu_lib()
+    desc = np.zeros(N.FB_MAX_SEG_BATCHES + 1, dtype=N.SEG_BATCH_DTYPE)
+    assert lib.fb_parse_classify_seg_batches_dev(gpu_capture.ctx, N.ptr(desc), 0, None) == N.FB_ERR_INVAL
+    assert lib.fb_parse_classify_seg_batches_dev(gpu_capture.ctx, N.ptr(desc), len(desc), None) == N.FB_ERR_INVAL
+    assert lib.fb_parse_classify_seg_batches_dev(gpu_capture.ctx, N.ptr(desc), 1, None) == N.FB_ERR_INVAL  # no stats

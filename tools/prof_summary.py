@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--kernel", default=None, help="substring of the dominant kernel's name (default k_parse_seg)")
     ap.add_argument("--algo-bytes", type=float, default=None, help="algorithmic bytes per launch (bench line)")
+    ap.add_argument("--bpl", type=int, default=1, help="batches per launch of the profiled bench run")
     a = ap.parse_args()
     global PARSE_KERNEL
     if a.kernel:
@@ -92,7 +93,7 @@ def main():
             tag=a.tag, kernel=PARSE_KERNEL, launches_fetch=nf, launches_write=nw,
             fetch_size_kib_median=fkb, write_size_kib_median=wkb,
             fetch_bytes_raw=fetch_raw, fetch_bytes_corrected_x2=fetch_corr, write_bytes=write_raw,
-            hbm_bytes_per_launch=hbm,
+            hbm_bytes_per_launch=hbm, batches_per_launch=a.bpl, hbm_bytes_per_batch=hbm / a.bpl,
             algo_bytes_per_launch=a.algo_bytes,
             note=("separate --pmc passes; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports 1/2 of "
                   "16-B-per-lane streaming reads); our header loads are 16-B per lane but unaligned and "
