@@ -357,6 +357,7 @@ def main():
     ap.add_argument("--mode", choices=["seg", "dense"], default="seg",
                     help="output layout: per-wavefront segments (default) or one batch-wide compaction")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
+    ap.add_argument("--no-single-launch", action="store_true", help="skip timing one batch per launch")
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
                          "default = the rotated batches (C2 8, C3 4), 1 for C4")
@@ -407,7 +408,7 @@ def main():
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
-    if bpl > 1:  # the same workload with one batch per launch
+    if bpl > 1 and not args.no_single_launch:  # the same workload with one batch per launch
         st_1 = max(args.steps // 2, 10)
         r1 = run_config(N, lib, ctx, args.config, n, st_1, max(args.warmup // 2, 2), rotate, rank, world, dist,
                         mode=args.mode, bpl=1)
@@ -484,8 +485,9 @@ def main():
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.config], "frames_per_gpu_per_step": n,
                        "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
-                       "output": ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
-                                  "%d batches per launch, each with its own outputs and stats)" % bpl
+                       "output": (("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
+                                   "%d batches per launch, each with its own outputs and stats)" % bpl) if bpl > 1 else
+                                  "per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)"
                                   if args.mode == "seg" else
                                   "batch-wide compaction (fb_parse_classify_dev)"),
                        "parallelism": "packet-index shards x%d" % world},
