@@ -95,6 +95,17 @@ class FbConfig(C.Structure):
                 ("reserved0", C.c_uint32), ("max_batch_bytes", C.c_uint64)]
 
 
+class FbRingConfig(C.Structure):
+    _fields_ = [("slots", C.c_uint32), ("max_packets", C.c_uint32), ("max_bytes", C.c_uint64),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+FB_RING_NO_FLOW = 1
+RING_DNS_DTYPE = np.dtype([("packet_seq", "<u8"), ("payload_offset", "<u8"), ("payload_length", "<u4"),
+                           ("protocol", "u1"), ("family", "u1"), ("reserved", "<u2")])
+assert RING_DNS_DTYPE.itemsize == 24
+
+
 class NativeLibraryMissing(RuntimeError):
     pass
 
@@ -134,6 +145,15 @@ GPU_SYMBOLS = [
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),
     ("fb_flow_clear", _I, [_P, _P]),
     ("fb_flow_hash", _U64, [_P]),
+    ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),
+    ("fb_ring_destroy", _I, [_P]),
+    ("fb_ring_push", _I, [_P, _P, _U32]),
+    ("fb_ring_push_block", _I, [_P, _P, _P, _U32]),
+    ("fb_ring_reserve", _P, [_P, _U32]),
+    ("fb_ring_submit", _I, [_P]),
+    ("fb_ring_sync", _I, [_P]),
+    ("fb_ring_stats", _I, [_P, _P, _PU64, _PU64]),
+    ("fb_ring_poll_dns", _I, [_P, _P, _U32, _P, _U64, _PU32, _PU64]),
     ("fb_dev_alloc", _I, [C.POINTER(C.c_void_p), _U64]),
     ("fb_dev_free", _I, [_P]),
     ("fb_host_alloc_pinned", _I, [C.POINTER(C.c_void_p), _U64]),

@@ -13,14 +13,15 @@
 #include <algorithm>
 #include <new>
 
+#include "fb_host.h"
 #include "fb_internal.h"
 #include "service_ports_default.inc"  // kDefaultServiceBitmap[8192] (generated at build time)
 
 using namespace fbk;
 
-namespace {
+namespace fbk {
 
-thread_local char g_err[512] = "";
+static thread_local char g_err[512] = "";
 
 int set_err(int code, const char* fmt, ...) {
     va_list ap;
@@ -30,26 +31,7 @@ int set_err(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                     \
-    do {                                                                                  \
-        hipError_t _e = (expr);                                                           \
-        if (_e != hipSuccess)                                                             \
-            return set_err(FB_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));    \
-    } while (0)
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-}  // namespace
+}  // namespace fbk
 
 struct fb_ctx {
     int device = 0;
@@ -98,6 +80,8 @@ struct fb_ctx {
     uint64_t s_pkts_cap = 0;
     fb_batch_stats* s_stats = nullptr;
 };
+
+int fbk::ctx_device(const fb_ctx* c) { return c->device; }
 
 // Session-table update scratch for batches of up to `recs` records (grown, never shrunk).
 static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {

@@ -383,6 +383,45 @@ int fb_flow_clear(fb_ctx* ctx, void* stream); /* clear_all_sessions, src/capture
  * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */
 uint64_t fb_flow_hash(const fb_session_key* key);
 
+/* ---- host ingest ring (replaces the reader thread -> Vec<u8> -> mpsc(1000) -> processor path,
+ *      src/capture.rs:1016, 1082-1142, 1183-1249) ---------------------------------------------
+ * The producer (capture callback) appends frames to the current batch of a ring of pinned host
+ * batches; a full batch is submitted as H2D (copy stream) -> fb_process_dev (parse + classify +
+ * session-table upsert, or fb_parse_classify_dev with FB_RING_NO_FLOW) -> batch stats back, while
+ * the producer fills the next one.  With every batch in flight the producer waits for the oldest
+ * (no drop-on-full).  The session table stays in HBM (fb_flow_export); DNS side records come back
+ * with their payload bytes (fb_ring_poll_dns).  One producer thread per ring, one ring per ctx. */
+typedef struct fb_ring fb_ring;
+typedef struct fb_ring_config {
+    uint32_t slots;       /* pinned batches, 2..64 (0 = 4)                       */
+    uint32_t max_packets; /* frames per batch                                    */
+    uint64_t max_bytes;   /* frame bytes per batch, < 4 GiB                      */
+    uint32_t flags;       /* FB_RING_*                                           */
+    uint32_t reserved;
+} fb_ring_config;
+#define FB_RING_NO_FLOW 1u /* parse + classify only, no session-table update */
+typedef struct fb_ring_dns {
+    uint64_t packet_seq;     /* frames pushed into the ring before this one          */
+    uint64_t payload_offset; /* into the payload buffer of fb_ring_poll_dns          */
+    uint32_t payload_length;
+    uint8_t protocol;        /* 6 / 17 */
+    uint8_t family;          /* 2 / 10 */
+    uint16_t reserved;
+} fb_ring_dns; /* 24 bytes */
+fb_ring* fb_ring_create(fb_ctx* ctx, const fb_ring_config* cfg); /* NULL on failure */
+int fb_ring_destroy(fb_ring* r);
+int fb_ring_push(fb_ring* r, const uint8_t* frame, uint32_t caplen);            /* copies one frame */
+int fb_ring_push_block(fb_ring* r, const uint8_t* frames, const uint32_t* offsets, uint32_t n);
+uint8_t* fb_ring_reserve(fb_ring* r, uint32_t caplen); /* zero-copy: write the frame there before the
+                                                           next push/reserve/submit; NULL on error */
+int fb_ring_submit(fb_ring* r);                        /* submit the partly filled batch now      */
+int fb_ring_sync(fb_ring* r);                          /* submit + wait for every batch           */
+/* Totals over the completed batches (fields summed, error OR-ed), batches completed, frames pushed. */
+int fb_ring_stats(fb_ring* r, fb_batch_stats* total, uint64_t* batches, uint64_t* frames);
+/* Dequeue DNS side records of completed batches, their payloads packed into `payload`. */
+int fb_ring_poll_dns(fb_ring* r, fb_ring_dns* out, uint32_t cap, uint8_t* payload, uint64_t payload_cap,
+                     uint32_t* n, uint64_t* n_bytes);
+
 /* ---- small device-memory helpers (so hosts without a GPU runtime binding can drive the
  *      device-resident entry points, e.g. through ctypes) ------------------------------- */
 int fb_dev_alloc(void** p, uint64_t bytes);

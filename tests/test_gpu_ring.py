@@ -1,0 +1,118 @@
+"""Host ingest ring (fb_ring_*) against the oracle: frames pushed one by one,
+in blocks and through zero-copy reservations come out as the same per-batch results as the
+oracle run over the same batch cuts -- cumulative stats, the session table (counters and ordered
+state) and the DNS side records with their payload bytes -- with fewer pinned slots than batches
+(the producer waits for the oldest batch instead of dropping)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import framegen as fg
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from oracle import coracle
+from test_gpu_parity import rows_sorted
+
+pytestmark = pytest.mark.gpu
+
+
+def _ring(cap, slots, max_packets, max_bytes, flags=0):
+    cfg = N.FbRingConfig(slots, max_packets, max_bytes, flags, 0)
+    r = N.gpu_lib().fb_ring_create(cap.ctx, C.byref(cfg))
+    assert r, N.gpu_lib().fb_last_error()
+    return C.c_void_p(r)
+
+
+def _poll_dns(lib, r):
+    out = np.zeros(1 << 16, dtype=N.RING_DNS_DTYPE)
+    buf = np.zeros(1 << 22, dtype=np.uint8)
+    n, nb = C.c_uint32(), C.c_uint64()
+    N.check(lib.fb_ring_poll_dns(r, N.ptr(out), len(out), N.ptr(buf), buf.nbytes, C.byref(n), C.byref(nb)))
+    recs = out[: n.value]
+    return [(int(d["packet_seq"]), int(d["protocol"]), bytes(buf[d["payload_offset"]: d["payload_offset"] + d["payload_length"]]))
+            for d in recs]
+
+
+def _oracle_batches(frames, offs, per_batch, flows):
+    """The oracle over the ring's batch cuts (every `per_batch` frames); returns totals + DNS."""
+    cfg = coracle.make_cfg(2)
+    n = len(offs) - 1
+    tot = np.zeros(1, dtype=N.STATS_DTYPE)
+    dns = []
+    for a in range(0, n, per_batch):
+        b = min(n, a + per_batch)
+        o = offs[a: b + 1] - offs[a]
+        fr = frames[offs[a]: offs[b]]
+        out, d, _, st = coracle.parse_classify(cfg, fr, o)
+        flows.update(out, st)
+        for k in N.STATS_FIELDS:
+            if not k.startswith("reserved"):
+                tot[0][k] += st[0][k]
+        for x in d:
+            pl = bytes(fr[x["payload_offset"]: x["payload_offset"] + x["payload_length"]])
+            dns.append((a + int(x["pkt_index"]), int(x["protocol"]), pl))
+    return tot, dns
+
+
+@pytest.mark.parametrize("how", ["block", "push", "reserve"])
+def test_ring_vs_oracle(gpu_capture, how):
+    frames, offs = synth.generate(3, 20000, first=11)
+    extra, eo = fg.pack([f for _, f in fg.edge_cases()])
+    frames = np.concatenate([frames, extra])
+    offs = np.concatenate([offs, offs[-1] + eo[1:]]).astype(np.uint32)
+    n = len(offs) - 1
+    per = 3000  # 7 batches through 3 pinned slots
+    lib = N.gpu_lib()
+    gpu_capture.clear_all_sessions()
+    r = _ring(gpu_capture, 3, per, 64 << 20)
+    try:
+        if how == "block":
+            N.check(lib.fb_ring_push_block(r, N.ptr(frames), N.ptr(offs), 5000))
+            rest = np.ascontiguousarray(offs[5000:] - offs[5000], dtype=np.uint32)  # kept alive for the call
+            tail = frames[offs[5000]:]
+            N.check(lib.fb_ring_push_block(r, N.ptr(tail), N.ptr(rest), n - 5000))
+        elif how == "push":
+            for i in range(n):
+                f = np.ascontiguousarray(frames[offs[i]: offs[i + 1]])
+                N.check(lib.fb_ring_push(r, N.ptr(f), len(f)))
+        else:
+            for i in range(n):
+                ln = int(offs[i + 1] - offs[i])
+                p = lib.fb_ring_reserve(r, ln)
+                assert p
+                C.memmove(p, frames[offs[i]: offs[i + 1]].ctypes.data, ln)
+        N.check(lib.fb_ring_sync(r))
+        tot = np.zeros(1, dtype=N.STATS_DTYPE)
+        nb, nf = C.c_uint64(), C.c_uint64()
+        N.check(lib.fb_ring_stats(r, N.ptr(tot), C.byref(nb), C.byref(nf)))
+        got_dns = _poll_dns(lib, r)
+    finally:
+        lib.fb_ring_destroy(r)
+    flows = coracle.Flows()
+    r_tot, r_dns = _oracle_batches(frames, offs, per, flows)
+    assert nf.value == n and nb.value == (n + per - 1) // per
+    for k in N.STATS_FIELDS:
+        if not k.startswith("reserved"):
+            assert int(tot[0][k]) == int(r_tot[0][k]), k
+    assert got_dns == r_dns
+    assert rows_sorted(gpu_capture.export_flows()) == rows_sorted(flows.export_sorted())
+    gpu_capture.clear_all_sessions()
+
+
+def test_ring_bad_arguments(gpu_capture):
+    lib = N.gpu_lib()
+    bad = N.FbRingConfig(1, 100, 1 << 20, 0, 0)
+    assert not lib.fb_ring_create(gpu_capture.ctx, C.byref(bad))
+    r = _ring(gpu_capture, 2, 4, 256)
+    try:
+        big = np.zeros(300, dtype=np.uint8)
+        assert lib.fb_ring_push(r, N.ptr(big), 300) == N.FB_ERR_INVAL  # frame > max_bytes
+        offs = np.array([0, 10, 5], dtype=np.uint32)
+        assert lib.fb_ring_push_block(r, N.ptr(big), N.ptr(offs), 2) == N.FB_ERR_INVAL
+        N.check(lib.fb_ring_sync(r))  # nothing pushed: no batch
+        nb = C.c_uint64()
+        N.check(lib.fb_ring_stats(r, None, C.byref(nb), None))
+        assert nb.value == 0
+    finally:
+        lib.fb_ring_destroy(r)
