@@ -150,6 +150,7 @@ GPU_SYMBOLS = [
     ("fb_ring_push", _I, [_P, _P, _U32]),
     ("fb_ring_push_block", _I, [_P, _P, _P, _U32]),
     ("fb_ring_reserve", _P, [_P, _U32]),
+    ("fb_ring_reserve_block", _P, [_P, _U32, _U64, C.POINTER(C.c_void_p), _PU32]),
     ("fb_ring_submit", _I, [_P]),
     ("fb_ring_sync", _I, [_P]),
     ("fb_ring_stats", _I, [_P, _P, _PU64, _PU64]),

@@ -52,6 +52,7 @@ struct fb_ring {
     std::vector<RingSlot> slots;
     uint32_t cur = 0;          // the batch being filled
     hipStream_t copy = nullptr, compute = nullptr;
+    hipStream_t dnsq = nullptr;  // DNS side-record read-back (never queued behind later H2D copies)
     fb_batch_stats total{};
     uint64_t batches = 0;
     uint64_t seq = 0;          // frames accepted so far
@@ -120,8 +121,8 @@ int complete(fb_ring* r, RingSlot& s) {
     r->batches++;
     const uint64_t nd = std::min<uint64_t>(st.n_dns, s.n);
     if (nd) {
-        HIP_TRY(hipMemcpyAsync(s.h_dns, s.d_dns, nd * sizeof(fb_dns_out), hipMemcpyDeviceToHost, r->copy));
-        HIP_TRY(hipStreamSynchronize(r->copy));
+        HIP_TRY(hipMemcpyAsync(s.h_dns, s.d_dns, nd * sizeof(fb_dns_out), hipMemcpyDeviceToHost, r->dnsq));
+        HIP_TRY(hipStreamSynchronize(r->dnsq));
         for (uint64_t k = 0; k < nd; ++k) {
             const fb_dns_out& d = s.h_dns[k];
             fb_ring_dns x{};
@@ -201,7 +202,8 @@ fb_ring* fb_ring_create(fb_ctx* ctx, const fb_ring_config* cfg) {
     r->cfg = c;
     r->slots.resize(c.slots);
     bool ok = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&r->compute, hipStreamNonBlocking) == hipSuccess;
+              hipStreamCreateWithFlags(&r->compute, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&r->dnsq, hipStreamNonBlocking) == hipSuccess;
     for (auto& s : r->slots) ok = ok && alloc_slot(s, c);
     if (!ok) {
         fb_ring_destroy(r);
@@ -219,6 +221,7 @@ int fb_ring_destroy(fb_ring* r) {
     for (auto& s : r->slots) free_slot(s);
     if (r->copy) (void)hipStreamDestroy(r->copy);
     if (r->compute) (void)hipStreamDestroy(r->compute);
+    if (r->dnsq) (void)hipStreamDestroy(r->dnsq);
     delete r;
     return FB_OK;
 }
@@ -232,6 +235,26 @@ uint8_t* fb_ring_reserve(fb_ring* r, uint32_t caplen) {
     s.h_offsets[s.n++] = (uint32_t)s.bytes;
     s.bytes += caplen;
     r->seq++;
+    return p;
+}
+
+uint8_t* fb_ring_reserve_block(fb_ring* r, uint32_t n, uint64_t bytes, uint32_t** offsets, uint32_t* base) {
+    if (!r || !offsets || !base || n == 0 || n > r->cfg.max_packets || bytes > r->cfg.max_bytes) {
+        set_err(FB_ERR_INVAL, "reserve_block: 1 <= n <= max_packets, bytes <= max_bytes, offsets/base required");
+        return nullptr;
+    }
+    DeviceGuard g(r->device);
+    const RingSlot& f = r->slots[r->cur];
+    if (f.n + n > r->cfg.max_packets || f.bytes + bytes > r->cfg.max_bytes) {
+        if (submit(r)) return nullptr;
+    }
+    RingSlot& s = r->slots[r->cur];
+    uint8_t* p = s.h_frames + s.bytes;
+    *offsets = s.h_offsets + s.n;
+    *base = (uint32_t)s.bytes;
+    s.n += n;
+    s.bytes += bytes;
+    r->seq += n;
     return p;
 }
 

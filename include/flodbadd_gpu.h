@@ -414,6 +414,10 @@ int fb_ring_push(fb_ring* r, const uint8_t* frame, uint32_t caplen);            
 int fb_ring_push_block(fb_ring* r, const uint8_t* frames, const uint32_t* offsets, uint32_t n);
 uint8_t* fb_ring_reserve(fb_ring* r, uint32_t caplen); /* zero-copy: write the frame there before the
                                                            next push/reserve/submit; NULL on error */
+/* Zero-copy block for bulk producers (TPACKET_V3 blocks, capture engines): room for n frames of
+ * `bytes` in total in one batch.  The caller writes the frames at the returned pointer and
+ * offsets[k] = *base + (start of frame k within that area), k < n, before the next ring call. */
+uint8_t* fb_ring_reserve_block(fb_ring* r, uint32_t n, uint64_t bytes, uint32_t** offsets, uint32_t* base);
 int fb_ring_submit(fb_ring* r);                        /* submit the partly filled batch now      */
 int fb_ring_sync(fb_ring* r);                          /* submit + wait for every batch           */
 /* Totals over the completed batches (fields summed, error OR-ed), batches completed, frames pushed. */
