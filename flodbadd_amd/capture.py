@@ -249,3 +249,62 @@ class FlodbaddGpuCapture:
             self.close()
         except Exception:
             pass
+
+
+class IngestRing:
+    """fb_ring_* (include/flodbadd_gpu.h): the capture reader's batch ring in front of a
+    FlodbaddGpuCapture's context -- replaces the reader -> Vec<u8> -> mpsc(1000) -> processor
+    path (src/capture.rs:1016, 1082-1142).  Frames are appended into pinned batches, each full
+    batch is copied in, parsed, classified and upserted into the context's session table on the
+    GPU while the next one fills; the producer waits (never drops) when every batch is in flight."""
+
+    def __init__(self, capture, slots=4, max_packets=1 << 20, max_bytes=64 << 20, flow=True):
+        self.lib = N.gpu_lib()
+        cfg = N.FbRingConfig(slots, max_packets, max_bytes, 0 if flow else N.FB_RING_NO_FLOW, 0)
+        r = self.lib.fb_ring_create(capture.ctx, C.byref(cfg))
+        if not r:
+            raise N.FbError(N.FB_ERR_INVAL, self.lib.fb_last_error().decode(errors="replace"))
+        self.r = C.c_void_p(r)
+        self.capture = capture  # the context must outlive the ring
+
+    def push(self, frame):
+        f = np.frombuffer(bytes(frame), dtype=np.uint8)
+        N.check(self.lib.fb_ring_push(self.r, N.ptr(f) if f.size else None, f.size))
+
+    def push_block(self, frames, offsets):
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        N.check(self.lib.fb_ring_push_block(self.r, N.ptr(frames), N.ptr(offsets), offsets.size - 1))
+
+    def sync(self):
+        N.check(self.lib.fb_ring_sync(self.r))
+
+    def stats(self):
+        """(PACKET_STATS totals over the completed batches, batches completed, frames pushed)."""
+        tot = np.zeros(1, dtype=N.STATS_DTYPE)
+        nb, nf = C.c_uint64(), C.c_uint64()
+        N.check(self.lib.fb_ring_stats(self.r, N.ptr(tot), C.byref(nb), C.byref(nf)))
+        return stats_dict(tot), nb.value, nf.value
+
+    def poll_dns(self, max_records=1 << 16, max_bytes=1 << 24):
+        """DNS side records of completed batches: [(packet_seq, protocol, family, payload bytes)]
+        -- what the reference hands to process_dns_packet (src/capture.rs:1051-1057)."""
+        out = np.zeros(max_records, dtype=N.RING_DNS_DTYPE)
+        buf = np.zeros(max_bytes, dtype=np.uint8)
+        n, nb = C.c_uint32(), C.c_uint64()
+        N.check(self.lib.fb_ring_poll_dns(self.r, N.ptr(out), max_records, N.ptr(buf), max_bytes, C.byref(n),
+                                          C.byref(nb)))
+        return [(int(d["packet_seq"]), int(d["protocol"]), int(d["family"]),
+                 buf[int(d["payload_offset"]): int(d["payload_offset"]) + int(d["payload_length"])].tobytes())
+                for d in out[: n.value]]
+
+    def close(self):
+        if getattr(self, "r", None):
+            self.lib.fb_ring_destroy(self.r)
+            self.r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

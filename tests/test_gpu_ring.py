@@ -116,3 +116,29 @@ def test_ring_bad_arguments(gpu_capture):
         assert nb.value == 0
     finally:
         lib.fb_ring_destroy(r)
+
+
+def test_ingest_ring_wrapper(gpu_capture):
+    """flodbadd_amd.capture.IngestRing: per-frame pushes incl. DNS over UDP and TCP, then the
+    DNS payloads and totals the oracle gives for the same single batch."""
+    from flodbadd_amd.capture import IngestRing
+    frames = [fg.udp_frame("10.0.0.2", 5000 + i, "8.8.8.8", 53, 20 + i) for i in range(40)] + \
+             [fg.tcp_frame("10.0.0.3", 7000 + i, "1.1.1.1", 443, fg.ACK, 10) for i in range(60)] + \
+             [f for _, f in fg.edge_cases()]
+    buf, offs = fg.pack(frames)
+    gpu_capture.clear_all_sessions()
+    ring = IngestRing(gpu_capture, slots=2, max_packets=4096, max_bytes=1 << 20)
+    try:
+        for f in frames:
+            ring.push(f)
+        ring.sync()
+        st, nb, nf = ring.stats()
+        dns = ring.poll_dns()
+    finally:
+        ring.close()
+    flows = coracle.Flows()
+    r_tot, r_dns = _oracle_batches(buf, offs, 4096, flows)
+    assert nb == 1 and nf == len(frames)
+    assert st["n_dns"] == int(r_tot[0]["n_dns"]) and st["n_session"] == int(r_tot[0]["n_session"])
+    assert [(s, p, pl) for s, p, _, pl in dns] == r_dns
+    gpu_capture.clear_all_sessions()
