@@ -51,6 +51,14 @@ FB_SEEN_NONE = (1 << 64) - 1
 FB_HIST_CHARS = "SsHhFfRr><Aa-"
 # fb_conn_state -> determine_conn_state string (src/packets.rs:539-559); 0 = None
 CONN_STATES = {0: None, 1: "SF", 2: "S0", 3: "REJ", 4: "S1", 5: "-"}
+ASN_RANGE_DTYPE = np.dtype([("start", "<u4", (4,)), ("end", "<u4", (4,)), ("as_number", "<u4"), ("record", "<u4"),
+                            ("reserved", "<u4", (2,))])
+CIDR_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("prefix", "<u4"), ("list", "<u4"),
+                       ("reserved", "<u4")])
+FLOW_ENRICH_DTYPE = np.dtype([("slot", "<u4"), ("flags", "<u4"), ("src_asn", "<i4"), ("dst_asn", "<i4"),
+                              ("src_blacklists", "<u8"), ("dst_blacklists", "<u8")])
+FB_MAX_BLACKLISTS = 64
+ENRICH_LOCAL_SRC, ENRICH_LOCAL_DST, ENRICH_SELF_SRC, ENRICH_SELF_DST = 1, 2, 4, 8
 LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
 FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
 
@@ -86,6 +94,7 @@ def seg_unpack(out_bytes, seg):
 assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 56
 assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 128
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
+assert ASN_RANGE_DTYPE.itemsize == 48 and CIDR_DTYPE.itemsize == 32 and FLOW_ENRICH_DTYPE.itemsize == 32
 
 
 class FbConfig(C.Structure):
@@ -140,6 +149,10 @@ GPU_SYMBOLS = [
     ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_history_dev", _I, [_P, _P, _P, _P, _P]),
+    ("fb_set_asn_tables", _I, [_P, _P, _U32, _P, _U32]),
+    ("fb_set_blacklists", _I, [_P, _P, _U32]),
+    ("fb_ip_lookup_dev", _I, [_P, _P, _U32, _P, _P, _P]),
+    ("fb_flow_enrich_dev", _I, [_P, _U32, _P, _U64, _P, _P]),
     ("fb_flow_count", _I, [_P, _PU64, _P]),
     ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),

@@ -233,6 +233,39 @@ class FlodbaddGpuCapture:
         """Sessions sorted by the derived Ord of Session (integer counters + derived f64s)."""
         return flows_to_sessions(self.export_flows(), is_lan, self.histories if self.track_history else None)
 
+    # ---- new-session enrichment (src/packets.rs:429-485) -------------------------------------
+    def set_asn_tables(self, v4, v6):
+        """ASN_RANGE_DTYPE tables (flodbadd_amd.enrich.asn_tables_from_tsv) -> fb_set_asn_tables."""
+        v4 = np.ascontiguousarray(v4, dtype=N.ASN_RANGE_DTYPE)
+        v6 = np.ascontiguousarray(v6, dtype=N.ASN_RANGE_DTYPE)
+        N.check(N.gpu_lib().fb_set_asn_tables(self.ctx, N.ptr(v4) if len(v4) else None, len(v4),
+                                              N.ptr(v6) if len(v6) else None, len(v6)))
+
+    def set_blacklists(self, cidrs):
+        """CIDR_DTYPE ranges (flodbadd_amd.enrich.blacklists_from_json) -> fb_set_blacklists."""
+        cidrs = np.ascontiguousarray(cidrs, dtype=N.CIDR_DTYPE)
+        N.check(N.gpu_lib().fb_set_blacklists(self.ctx, N.ptr(cidrs) if len(cidrs) else None, len(cidrs)))
+
+    def ip_lookup(self, ips):
+        """get_asn + is_ip_blacklisted for addresses (strings / ipaddress objects) ->
+        (int32 ASN records, -1 = None; uint64 list masks)."""
+        t = own_ip_table(list(ips))
+        n = len(t)
+        d_ip = N.DeviceBuffer(max(t.nbytes, 1))
+        if n:
+            d_ip.upload(t)
+        d_a, d_l = N.DeviceBuffer(max(4 * n, 4)), N.DeviceBuffer(max(8 * n, 8))
+        N.check(N.gpu_lib().fb_ip_lookup_dev(self.ctx, d_ip.ptr, n, d_a.ptr, d_l.ptr, None))
+        return d_a.download(np.zeros(max(n, 1), dtype=np.int32))[:n], d_l.download(np.zeros(max(n, 1), dtype=np.uint64))[:n]
+
+    def enrich(self, new_only=False):
+        """fb_flow_enrich_dev -> FLOW_ENRICH_DTYPE records (slot-keyed; join with export_flows)."""
+        cap = max(self.flow_count(), 1)
+        d_out, d_n = N.DeviceBuffer(cap * N.FLOW_ENRICH_DTYPE.itemsize), N.DeviceBuffer(8)
+        N.check(N.gpu_lib().fb_flow_enrich_dev(self.ctx, 1 if new_only else 0, d_out.ptr, cap, d_n.ptr, None))
+        m = min(int(d_n.download(np.zeros(1, dtype=np.uint64))[0]), cap)
+        return d_out.download(np.zeros(cap, dtype=N.FLOW_ENRICH_DTYPE))[:m]
+
     def clear_all_sessions(self):
         """src/capture.rs:396 (`stop()` clears the table, capture.rs:383)."""
         N.check(N.gpu_lib().fb_flow_clear(self.ctx, None))

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <new>
+#include <vector>
 
 #include "fb_host.h"
 #include "fb_internal.h"
@@ -70,6 +71,15 @@ struct fb_ctx {
     void* d_htemp = nullptr;
     size_t htemp_bytes = 0;
     uint64_t hist_cap = 0;
+    // enrichment tables (fb_set_asn_tables / fb_set_blacklists)
+    fb_asn_range* d_asn4 = nullptr;
+    fb_asn_range* d_asn6 = nullptr;
+    uint32_t n_asn4 = 0, n_asn6 = 0;
+    uint32_t* d_bl4_pos = nullptr;
+    unsigned long long* d_bl4_mask = nullptr;
+    uint4* d_bl6_pos = nullptr;
+    unsigned long long* d_bl6_mask = nullptr;
+    uint32_t m_bl4 = 0, m_bl6 = 0;
     // host-mode staging
     uint8_t* s_frames = nullptr;
     uint64_t s_frames_cap = 0;
@@ -82,6 +92,38 @@ struct fb_ctx {
 };
 
 int fbk::ctx_device(const fb_ctx* c) { return c->device; }
+
+namespace fbk {
+bool build_blacklist_tables(const fb_cidr* nets, uint32_t n, std::vector<uint32_t>& p4,
+                            std::vector<unsigned long long>& m4, std::vector<uint4>& p6,
+                            std::vector<unsigned long long>& m6);
+}
+
+static EnrichTables enrich_tables(const fb_ctx* c) {
+    EnrichTables t;
+    t.asn4 = c->d_asn4;
+    t.asn6 = c->d_asn6;
+    t.n4 = c->n_asn4;
+    t.n6 = c->n_asn6;
+    t.bl4_pos = c->d_bl4_pos;
+    t.bl4_mask = c->d_bl4_mask;
+    t.bl6_pos = c->d_bl6_pos;
+    t.bl6_mask = c->d_bl6_mask;
+    t.m4 = c->m_bl4;
+    t.m6 = c->m_bl6;
+    return t;
+}
+
+// Replace a device array with a copy of host data (n elements); empty -> nullptr.
+template <typename T>
+static int upload_array(T** d, const T* h, size_t n) {
+    if (*d) (void)hipFree(*d);
+    *d = nullptr;
+    if (n == 0) return FB_OK;
+    if (hipMalloc((void**)d, n * sizeof(T)) != hipSuccess) return set_err(FB_ERR_NOMEM, "enrichment table");
+    HIP_TRY(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    return FB_OK;
+}
 
 // Session-table update scratch for batches of up to `recs` records (grown, never shrunk).
 static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
@@ -267,6 +309,12 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_partials);
     hipFree(c->d_n);
     hipFree(c->d_rec_flow);
+    hipFree(c->d_asn4);
+    hipFree(c->d_asn6);
+    hipFree(c->d_bl4_pos);
+    hipFree(c->d_bl4_mask);
+    hipFree(c->d_bl6_pos);
+    hipFree(c->d_bl6_mask);
     hipFree(c->d_hkeys);
     hipFree(c->d_hvals);
     hipFree(c->d_htemp);
@@ -735,6 +783,81 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     p.vals = c->d_hvals;
     p.n_hist = d_n_hist;
     HIP_TRY(launch_flow_history(p, c->d_htemp, c->htemp_bytes, d_hist_slot, d_hist, s));
+    return FB_OK;
+}
+
+// ---- enrichment ----------------------------------------------------------------------------
+static bool asn_less(const fb_asn_range& a, const fb_asn_range& b, bool v6) {
+    const int nw = v6 ? 4 : 1;
+    for (int k = 0; k < nw; ++k)
+        if (a.start[k] != b.start[k]) return a.start[k] < b.start[k];
+    for (int k = 0; k < nw; ++k)
+        if (a.end[k] != b.end[k]) return a.end[k] < b.end[k];
+    return false;
+}
+
+static bool asn_valid(const fb_asn_range& a, bool v6) {  // start <= end (src/asn_db.rs:111-128)
+    const int nw = v6 ? 4 : 1;
+    for (int k = 0; k < nw; ++k)
+        if (a.start[k] != a.end[k]) return a.start[k] < a.end[k];
+    return true;
+}
+
+int fb_set_asn_tables(fb_ctx* c, const fb_asn_range* v4, uint32_t n4, const fb_asn_range* v6, uint32_t n6) {
+    if (!c || (n4 && !v4) || (n6 && !v6)) return set_err(FB_ERR_INVAL, "bad arguments");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipDeviceSynchronize());  // no launch may still read the old tables
+    // Db::from_tsv: drop start > end, then the stable sort by (start, end) (src/asn_db.rs:111-137)
+    std::vector<fb_asn_range> a4, a6;
+    for (uint32_t i = 0; i < n4; ++i)
+        if (asn_valid(v4[i], false)) a4.push_back(v4[i]);
+    for (uint32_t i = 0; i < n6; ++i)
+        if (asn_valid(v6[i], true)) a6.push_back(v6[i]);
+    std::stable_sort(a4.begin(), a4.end(), [](const fb_asn_range& x, const fb_asn_range& y) { return asn_less(x, y, false); });
+    std::stable_sort(a6.begin(), a6.end(), [](const fb_asn_range& x, const fb_asn_range& y) { return asn_less(x, y, true); });
+    int rc = upload_array(&c->d_asn4, a4.data(), a4.size());
+    if (!rc) rc = upload_array(&c->d_asn6, a6.data(), a6.size());
+    c->n_asn4 = rc ? 0 : (uint32_t)a4.size();
+    c->n_asn6 = rc ? 0 : (uint32_t)a6.size();
+    return rc;
+}
+
+int fb_set_blacklists(fb_ctx* c, const fb_cidr* nets, uint32_t n) {
+    if (!c || (n && !nets)) return set_err(FB_ERR_INVAL, "bad arguments");
+    std::vector<uint32_t> p4;
+    std::vector<unsigned long long> m4, m6;
+    std::vector<uint4> p6;
+    if (!build_blacklist_tables(nets, n, p4, m4, p6, m6))
+        return set_err(FB_ERR_INVAL, "blacklist entry with a bad family, prefix or list (< %u)", FB_MAX_BLACKLISTS);
+    DeviceGuard g(c->device);
+    HIP_TRY(hipDeviceSynchronize());
+    int rc = upload_array(&c->d_bl4_pos, p4.data(), p4.size());
+    if (!rc) rc = upload_array(&c->d_bl4_mask, m4.data(), m4.size());
+    if (!rc) rc = upload_array(&c->d_bl6_pos, p6.data(), p6.size());
+    if (!rc) rc = upload_array(&c->d_bl6_mask, m6.data(), m6.size());
+    c->m_bl4 = rc ? 0 : (uint32_t)p4.size();
+    c->m_bl6 = rc ? 0 : (uint32_t)p6.size();
+    return rc;
+}
+
+int fb_ip_lookup_dev(fb_ctx* c, const fb_ip* d_ips, uint32_t n, int32_t* d_asn, uint64_t* d_lists, void* stream) {
+    if (!c || (n && !d_ips)) return set_err(FB_ERR_INVAL, "bad arguments");
+    DeviceGuard g(c->device);
+    HIP_TRY(launch_ip_lookup(enrich_tables(c), d_ips, n, d_asn, (unsigned long long*)d_lists, (hipStream_t)stream));
+    return FB_OK;
+}
+
+int fb_flow_enrich_dev(fb_ctx* c, uint32_t new_only, fb_flow_enrich* d_out, uint64_t cap, uint64_t* d_n,
+                       void* stream) {
+    if (!c || !d_n || (cap && !d_out)) return set_err(FB_ERR_INVAL, "bad arguments");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
+    if (!c->d_table || (new_only && c->flow_batch == 0)) return FB_OK;
+    int rc = upload_cfg(c, s);
+    if (rc) return rc;
+    HIP_TRY(launch_flow_enrich(enrich_tables(c), c->d_cfg, c->d_table, c->table_cap, new_only ? 1u : 0u,
+                               c->flow_batch - 1u, d_out, cap, (unsigned long long*)d_n, s));
     return FB_OK;
 }
 

@@ -67,6 +67,38 @@ struct ParseParams {
     unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
 };
 
+// is_lan_ip, src/ip.rs:55-156, 199-242.
+__device__ __forceinline__ bool lan_v4(uint32_t v) {
+    uint32_t a = v >> 24, b = (v >> 16) & 0xffu;
+    return v == 0u || v == 0xffffffffu || a == 127u || (v >> 28) == 0xEu || (v >> 16) == 0xA9FEu ||
+           a == 10u || (a == 172u && b >= 16u && b <= 31u) || (v >> 16) == 0xC0A8u;
+}
+__device__ __forceinline__ bool lan_v6(const DevConfig* c, const DevConfig* g, const uint32_t w[4]) {
+    uint32_t s0 = w[0] >> 16;
+    if ((w[0] | w[1] | w[2] | w[3]) == 0u) return true;                       // ::
+    if ((w[0] | w[1] | w[2]) == 0u && w[3] == 1u) return true;                // ::1
+    if ((s0 & 0xffc0u) == 0xfe80u || (s0 & 0xff00u) == 0xff00u || (s0 & 0xfe00u) == 0xfc00u)
+        return true;                                                          // fe80::/10 ff00::/8 fc00::/7
+    const uint32_t nl = c->n_lan_v6;                                          // uniform loop
+    for (uint32_t i = 0; i < nl; ++i) {
+        const LanV6& e = g->lan_v6[i];
+        if ((w[0] & e.mask[0]) == e.net[0] && (w[1] & e.mask[1]) == e.net[1] &&
+            (w[2] & e.mask[2]) == e.net[2] && (w[3] & e.mask[3]) == e.net[3])
+            return true;
+    }
+    return false;
+}
+__device__ __forceinline__ bool own_ip(const DevConfig* c, const DevConfig* g, uint32_t fam, const uint32_t w[4]) {
+    const uint32_t no = c->n_own;
+    bool hit = false;
+    for (uint32_t i = 0; i < no; ++i) {
+        const fb_ip& o = g->own[i];
+        hit |= o.family == fam && o.addr[0] == w[0] && o.addr[1] == w[1] && o.addr[2] == w[2] &&
+               o.addr[3] == w[3];
+    }
+    return hit;
+}
+
 // Batches of one k_parse_seg launch (fb_parse_classify_seg_batches_dev): the launch streams over
 // the concatenation of their segments; batch k owns global segments [seg_start, next seg_start).
 constexpr uint32_t kMaxSegBatches = FB_MAX_SEG_BATCHES;
@@ -184,5 +216,24 @@ struct HistParams {
 hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes);
 hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_bytes, uint32_t* hist_slot,
                                uint8_t* hist, hipStream_t s);
+
+// Enrichment tables (fb_set_asn_tables / fb_set_blacklists, fb_enrich.hip).  Blacklists are
+// flattened per family into disjoint elementary intervals: bl*_pos[i] = first address of
+// interval i (ascending), bl*_mask[i] = the lists whose ranges cover it; an address takes the
+// mask of the last interval starting at or before it (none: 0).
+struct EnrichTables {
+    const fb_asn_range* asn4;
+    const fb_asn_range* asn6;
+    const uint32_t* bl4_pos;
+    const unsigned long long* bl4_mask;
+    const uint4* bl6_pos;  // 4 words, session_key order (word 0 most significant)
+    const unsigned long long* bl6_mask;
+    uint32_t n4, n6, m4, m6;
+};
+hipError_t launch_ip_lookup(const EnrichTables& t, const fb_ip* ips, uint32_t n, int32_t* asn,
+                            unsigned long long* lists, hipStream_t s);
+hipError_t launch_flow_enrich(const EnrichTables& t, const DevConfig* cfg, const FlowSlot* table,
+                              unsigned long long cap, uint32_t new_only, uint32_t batch, fb_flow_enrich* out,
+                              unsigned long long out_cap, unsigned long long* d_n, hipStream_t s);
 
 }  // namespace fbk

@@ -32,38 +32,6 @@ __device__ __forceinline__ uint32_t bswap(uint32_t w) { return __builtin_bswap32
 
 __device__ __forceinline__ uint32_t svc(const uint32_t* bm, uint32_t p) { return (bm[p >> 5] >> (p & 31)) & 1u; }
 
-// is_lan_ip, src/ip.rs:55-156, 199-242.
-__device__ __forceinline__ bool lan_v4(uint32_t v) {
-    uint32_t a = v >> 24, b = (v >> 16) & 0xffu;
-    return v == 0u || v == 0xffffffffu || a == 127u || (v >> 28) == 0xEu || (v >> 16) == 0xA9FEu ||
-           a == 10u || (a == 172u && b >= 16u && b <= 31u) || (v >> 16) == 0xC0A8u;
-}
-__device__ __forceinline__ bool lan_v6(const DevConfig* c, const DevConfig* g, const uint32_t w[4]) {
-    uint32_t s0 = w[0] >> 16;
-    if ((w[0] | w[1] | w[2] | w[3]) == 0u) return true;                       // ::
-    if ((w[0] | w[1] | w[2]) == 0u && w[3] == 1u) return true;                // ::1
-    if ((s0 & 0xffc0u) == 0xfe80u || (s0 & 0xff00u) == 0xff00u || (s0 & 0xfe00u) == 0xfc00u)
-        return true;                                                          // fe80::/10 ff00::/8 fc00::/7
-    const uint32_t nl = c->n_lan_v6;                                          // uniform loop
-    for (uint32_t i = 0; i < nl; ++i) {
-        const LanV6& e = g->lan_v6[i];
-        if ((w[0] & e.mask[0]) == e.net[0] && (w[1] & e.mask[1]) == e.net[1] &&
-            (w[2] & e.mask[2]) == e.net[2] && (w[3] & e.mask[3]) == e.net[3])
-            return true;
-    }
-    return false;
-}
-__device__ __forceinline__ bool own_ip(const DevConfig* c, const DevConfig* g, uint32_t fam, const uint32_t w[4]) {
-    const uint32_t no = c->n_own;
-    bool hit = false;
-    for (uint32_t i = 0; i < no; ++i) {
-        const fb_ip& o = g->own[i];
-        hit |= o.family == fam && o.addr[0] == w[0] && o.addr[1] == w[1] && o.addr[2] == w[2] &&
-               o.addr[3] == w[3];
-    }
-    return hit;
-}
-
 // map_tcp_flags, src/packets.rs:561-601.
 __device__ __forceinline__ uint32_t hist_char(uint32_t fl, uint32_t plen, bool orig) {
     uint32_t c;

@@ -372,6 +372,56 @@ int fb_process_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_byt
 int fb_flow_history_dev(fb_ctx* ctx, uint8_t* d_hist, uint32_t* d_hist_slot, uint32_t* d_n_hist,
                         void* stream);
 
+/* ---- new-session enrichment (src/packets.rs:429-485; ASN src/asn.rs:32-63 + src/asn_db.rs:144-166;
+ *      blacklists src/blacklists.rs:205-260, 456-560) -------------------------------------------- */
+/* One ASN range (Db's RecordInternal, src/asn_db.rs:47-54) with IPs in session_key word layout.
+ * One table per family, sorted by (start, end) as Db::from_tsv leaves it (src/asn_db.rs:137);
+ * `record` is the caller's index of (as_number, country, owner). */
+typedef struct fb_asn_range {
+    uint32_t start[4];
+    uint32_t end[4];
+    uint32_t as_number;
+    uint32_t record;
+    uint32_t reserved[2];
+} fb_asn_range; /* 48 bytes */
+/* One IpNet of blacklist `list` (< FB_MAX_BLACKLISTS): addr/prefix as parsed (the host bits of
+ * addr are ignored, as IpNet::contains does); a plain IP is a /32 or /128 (src/blacklists.rs:128-135). */
+typedef struct fb_cidr {
+    uint32_t addr[4];
+    uint32_t family; /* 2 / 10 */
+    uint32_t prefix;
+    uint32_t list;
+    uint32_t reserved;
+} fb_cidr; /* 32 bytes */
+#define FB_MAX_BLACKLISTS 64u
+int fb_set_asn_tables(fb_ctx* ctx, const fb_asn_range* v4, uint32_t n4, const fb_asn_range* v6, uint32_t n6);
+int fb_set_blacklists(fb_ctx* ctx, const fb_cidr* nets, uint32_t n);
+/* Batched get_asn + is_ip_blacklisted for arbitrary addresses: d_asn[i] = fb_asn_range.record of
+ * Db::lookup (its exact binary search), -1 = None; d_lists[i] bit l = some range of blacklist l
+ * contains the address.  Either output may be NULL.  DEVICE pointers, asynchronous. */
+int fb_ip_lookup_dev(fb_ctx* ctx, const fb_ip* d_ips, uint32_t n, int32_t* d_asn, uint64_t* d_lists,
+                     void* stream);
+/* The per-new-session lookups of process_parsed_packet for the flows in the table. */
+typedef struct fb_flow_enrich {
+    uint32_t slot;           /* fb_flow_rec.slot                                                  */
+    uint32_t flags;          /* FB_ENRICH_* (src/packets.rs:429-435)                               */
+    int32_t src_asn;         /* record of get_asn(src_ip) when !is_local_src, else -1 (packets.rs:468-485) */
+    int32_t dst_asn;
+    uint64_t src_blacklists; /* lists containing src_ip when !is_local_src (blacklists.rs:545-556) */
+    uint64_t dst_blacklists;
+} fb_flow_enrich;            /* 32 bytes */
+enum fb_enrich_bits {
+    FB_ENRICH_LOCAL_SRC = 1u, /* is_lan_ip(key.src_ip) */
+    FB_ENRICH_LOCAL_DST = 2u,
+    FB_ENRICH_SELF_SRC = 4u,  /* own_ips.contains(key.src_ip) */
+    FB_ENRICH_SELF_DST = 8u
+};
+/* Enrich every flow of the table (new_only = 0) or only those the last update call created
+ * (new_only = 1: the reference does these lookups when it inserts a session).  Records in no
+ * particular order; *d_n (device u64) receives the count.  DEVICE pointers, asynchronous. */
+int fb_flow_enrich_dev(fb_ctx* ctx, uint32_t new_only, fb_flow_enrich* d_out, uint64_t cap, uint64_t* d_n,
+                       void* stream);
+
 int fb_flow_count(fb_ctx* ctx, uint64_t* n_flows, void* stream); /* synchronous */
 /* Copy every flow (slot order) to host memory; *n = flows written (<= cap). Synchronous. */
 int fb_flow_export(fb_ctx* ctx, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream);

@@ -12,6 +12,7 @@ ROOT = os.path.dirname(HERE)
 BITMAP_PATH = os.path.join(ROOT, "flodbadd_amd", "data", "service_ports.bin")
 
 # Record layouts are defined once, in the product's binding of include/flodbadd_gpu.h.
+from flodbadd_amd import _native as N  # noqa: E402
 from flodbadd_amd._native import (DNS_OUT_DTYPE, FB_IP_DTYPE, FLOW_REC_DTYPE, LAN_V6_DTYPE, PARSED_DTYPE,  # noqa: E402
                                   PKT_OUT_DTYPE, STATS_DTYPE)
 
@@ -43,6 +44,13 @@ def lib():
         L.orc_parse_classify.argtypes = [P, P, U64, P, U32, P, C.POINTER(U32), P, C.POINTER(U32), P, P]
         L.orc_process_parsed.restype = C.c_int
         L.orc_process_parsed.argtypes = [P, P, U32, P, C.POINTER(U32), P, P]
+        L.orc_asn_prepare.restype = C.c_uint32
+        L.orc_asn_prepare.argtypes = [P, C.c_uint32, C.c_uint32]
+        L.orc_asn_lookup.restype = C.c_int32
+        L.orc_asn_lookup.argtypes = [P, C.c_uint32, C.c_uint32, P]
+        L.orc_blacklist_mask.restype = U64
+        L.orc_blacklist_mask.argtypes = [P, C.c_uint32, C.c_uint32, P]
+        L.orc_enrich_keys.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P]
         L.orc_flows_new.restype = P
         L.orc_flows_free.argtypes = [P]
         L.orc_flows_clear.argtypes = [P]
@@ -110,6 +118,45 @@ def process_parsed(cfg, parsed):
     lib().orc_process_parsed(C.byref(cfg), parsed.ctypes.data if n else None, n, out.ctypes.data, C.byref(no),
                              cls.ctypes.data, st.ctypes.data)
     return out[: no.value], cls[:n], st
+
+
+def asn_prepare(table, family):
+    """Db::from_tsv's filter + stable sort of one family's ASN_RANGE_DTYPE table (a copy)."""
+    t = np.ascontiguousarray(table, dtype=N.ASN_RANGE_DTYPE).copy()
+    m = lib().orc_asn_prepare(t.ctypes.data if len(t) else None, len(t), family)
+    return t[:m]
+
+
+def enrich_keys(cfg, a4, a6, cidrs, keys):
+    """orc_enrich_keys over 40-B keys (any record array whose first 40 bytes are the key);
+    a4/a6 already through asn_prepare."""
+    kb = np.ascontiguousarray(np.frombuffer(b"".join(k.tobytes()[:40] for k in keys), dtype=np.uint8))
+    n = len(keys)
+    out = np.zeros(max(n, 1), dtype=N.FLOW_ENRICH_DTYPE)
+    a4 = np.ascontiguousarray(a4, dtype=N.ASN_RANGE_DTYPE)
+    a6 = np.ascontiguousarray(a6, dtype=N.ASN_RANGE_DTYPE)
+    cidrs = np.ascontiguousarray(cidrs, dtype=N.CIDR_DTYPE)
+    lib().orc_enrich_keys(C.byref(cfg), a4.ctypes.data if len(a4) else None, len(a4),
+                          a6.ctypes.data if len(a6) else None, len(a6), cidrs.ctypes.data if len(cidrs) else None,
+                          len(cidrs), kb.ctypes.data if n else None, n, out.ctypes.data)
+    return out[:n]
+
+
+def ip_lookup(a4, a6, cidrs, ips):
+    """Db::lookup + the blacklist scan for addresses -> (int32 records, uint64 masks)."""
+    from flodbadd_amd.sessions import ip_to_words
+    a4 = np.ascontiguousarray(a4, dtype=N.ASN_RANGE_DTYPE)
+    a6 = np.ascontiguousarray(a6, dtype=N.ASN_RANGE_DTYPE)
+    cidrs = np.ascontiguousarray(cidrs, dtype=N.CIDR_DTYPE)
+    asn, lists = [], []
+    for ip in ips:
+        w, fam = ip_to_words(ip)
+        w = np.ascontiguousarray(w, dtype=np.uint32)
+        t = a6 if fam == 10 else a4
+        asn.append(lib().orc_asn_lookup(t.ctypes.data if len(t) else None, len(t), fam, w.ctypes.data))
+        lists.append(lib().orc_blacklist_mask(cidrs.ctypes.data if len(cidrs) else None, len(cidrs), fam,
+                                              w.ctypes.data))
+    return np.array(asn, dtype=np.int32), np.array(lists, dtype=np.uint64)
 
 
 class Flows:

@@ -546,3 +546,100 @@ uint64_t orc_pipeline(const orc_cfg* c, orc_flows* fl, const uint8_t* frames, ui
     if (fl) orc_flows_update(fl, scratch, no, st);
     return n;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * New-session enrichment (src/packets.rs:429-485): ASN (src/asn.rs:32-63, src/asn_db.rs:82-166)
+ * and blacklists (src/blacklists.rs:205-260 is_ip_in_blacklist, 456-560 the session pass).
+ * ------------------------------------------------------------------------------------- */
+static int ip_cmp_fam(int v6, const uint32_t* a, const uint32_t* b) {
+    for (int k = 0; k < (v6 ? 4 : 1); ++k)
+        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return 0;
+}
+
+typedef struct { fb_asn_range r; uint32_t idx; int v6; } asn_sort_item;
+static int asn_item_cmp(const void* x, const void* y) {
+    const asn_sort_item* a = (const asn_sort_item*)x;
+    const asn_sort_item* b = (const asn_sort_item*)y;
+    int c = ip_cmp_fam(a->v6, a->r.start, b->r.start);
+    if (!c) c = ip_cmp_fam(a->v6, a->r.end, b->r.end);
+    if (!c) c = a->idx < b->idx ? -1 : (a->idx > b->idx ? 1 : 0); /* Vec::sort is stable */
+    return c;
+}
+
+/* Db::from_tsv's filtering (start <= end) + `records.sort()` (src/asn_db.rs:111-137), in place;
+ * returns the kept count. */
+uint32_t orc_asn_prepare(fb_asn_range* recs, uint32_t n, uint32_t family) {
+    const int v6 = family == 10;
+    asn_sort_item* t = (asn_sort_item*)malloc((n ? n : 1) * sizeof(asn_sort_item));
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (ip_cmp_fam(v6, recs[i].start, recs[i].end) <= 0) {
+            t[m].r = recs[i];
+            t[m].idx = i;
+            t[m].v6 = v6;
+            ++m;
+        }
+    qsort(t, m, sizeof(asn_sort_item), asn_item_cmp);
+    for (uint32_t i = 0; i < m; ++i) recs[i] = t[i].r;
+    free(t);
+    return m;
+}
+
+/* Db::lookup (src/asn_db.rs:144-166), literally: returns the record, or -1 for None. */
+int32_t orc_asn_lookup(const fb_asn_range* recs, uint32_t n, uint32_t family, const uint32_t ip[4]) {
+    const int v6 = family == 10;
+    uint64_t low = 0, high = n;
+    while (low < high) {
+        const uint64_t mid = (low + high) / 2;
+        const fb_asn_range* rec = &recs[mid];
+        if (ip_cmp_fam(v6, rec->start, ip) <= 0 && ip_cmp_fam(v6, ip, rec->end) <= 0) return (int32_t)rec->record;
+        if (ip_cmp_fam(v6, ip, rec->start) < 0) high = mid;
+        else low = mid + 1;
+    }
+    return -1;
+}
+
+/* IpNet::contains(&IpAddr): same family and network() <= ip <= broadcast(). */
+static int net_contains(const fb_cidr* c, uint32_t family, const uint32_t ip[4]) {
+    if (c->family != family) return 0;
+    const int words = family == 10 ? 4 : 1;
+    for (int k = 0; k < words; ++k) {
+        const int bits = (int)c->prefix - 32 * k;
+        const uint32_t m = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : 0xFFFFFFFFu << (32 - bits));
+        if ((ip[k] & m) != (c->addr[k] & m)) return 0;
+    }
+    return 1;
+}
+
+/* For every list: does some range of it contain ip (is_ip_in_blacklist's linear scan). */
+uint64_t orc_blacklist_mask(const fb_cidr* nets, uint32_t n, uint32_t family, const uint32_t ip[4]) {
+    uint64_t m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (net_contains(&nets[i], family, ip)) m |= 1ull << nets[i].list;
+    return m;
+}
+
+/* The per-new-session lookups for `nk` keys (slot = index).  The ASN tables must have been
+ * through orc_asn_prepare. */
+void orc_enrich_keys(const orc_cfg* c, const fb_asn_range* a4, uint32_t n4, const fb_asn_range* a6, uint32_t n6,
+                     const fb_cidr* nets, uint32_t nn, const fb_session_key* keys, uint32_t nk,
+                     fb_flow_enrich* out) {
+    for (uint32_t i = 0; i < nk; ++i) {
+        const fb_session_key* k = &keys[i];
+        const uint32_t fam = k->family;
+        const int ls = orc_is_lan_ip(c, fam, k->src_ip), ld = orc_is_lan_ip(c, fam, k->dst_ip);
+        fb_flow_enrich* r = &out[i];
+        memset(r, 0, sizeof(*r));
+        r->slot = i;
+        r->flags = (ls ? FB_ENRICH_LOCAL_SRC : 0) | (ld ? FB_ENRICH_LOCAL_DST : 0) |
+                   (is_own_ip(c, fam, k->src_ip) ? FB_ENRICH_SELF_SRC : 0) |
+                   (is_own_ip(c, fam, k->dst_ip) ? FB_ENRICH_SELF_DST : 0);
+        const fb_asn_range* A = fam == 10 ? a6 : a4;
+        const uint32_t na = fam == 10 ? n6 : n4;
+        r->src_asn = ls ? -1 : orc_asn_lookup(A, na, fam, k->src_ip);
+        r->dst_asn = ld ? -1 : orc_asn_lookup(A, na, fam, k->dst_ip);
+        r->src_blacklists = ls ? 0 : orc_blacklist_mask(nets, nn, fam, k->src_ip);
+        r->dst_blacklists = ld ? 0 : orc_blacklist_mask(nets, nn, fam, k->dst_ip);
+    }
+}

@@ -93,6 +93,14 @@ int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* b
                           uint64_t cap, char* conn_state, uint64_t cs_cap);
 
 /* Bench helper: parse+classify+upsert with a scratch record buffer; returns packets done. */
+/* ---- new-session enrichment (ASN src/asn_db.rs:82-166, blacklists src/blacklists.rs:205-260) ---- */
+uint32_t orc_asn_prepare(fb_asn_range* recs, uint32_t n, uint32_t family);
+int32_t orc_asn_lookup(const fb_asn_range* recs, uint32_t n, uint32_t family, const uint32_t ip[4]);
+uint64_t orc_blacklist_mask(const fb_cidr* nets, uint32_t n, uint32_t family, const uint32_t ip[4]);
+void orc_enrich_keys(const orc_cfg* c, const fb_asn_range* a4, uint32_t n4, const fb_asn_range* a6, uint32_t n6,
+                     const fb_cidr* nets, uint32_t nn, const fb_session_key* keys, uint32_t nk,
+                     fb_flow_enrich* out);
+
 uint64_t orc_pipeline(const orc_cfg* cfg, orc_flows* flows, const uint8_t* frames,
                       uint64_t frames_bytes, const uint32_t* offsets, uint32_t n,
                       fb_pkt_out* scratch, fb_batch_stats* stats);

@@ -1,0 +1,135 @@
+"""GPU new-session enrichment (fb_ip_lookup_dev, fb_flow_enrich_dev) against
+the oracle's literal restatement: Db::lookup's binary search (src/asn_db.rs:144-166) and the
+linear IpNet::contains scan over every blacklist range (src/blacklists.rs:205-260), bit-exact,
+on the reference's known answers, on random tables with overlapping ranges and boundary
+addresses, and on whole flow tables (flags, both ASN records, both list masks)."""
+import ipaddress
+import random
+
+import numpy as np
+import pytest
+
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from flodbadd_amd.enrich import asn_tables_from_tsv, blacklists_from_json
+from flodbadd_amd.sessions import SessionFilter, words_to_ip
+from oracle import coracle
+from test_enrich_oracle import TSV
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_tables(seed):
+    rnd = random.Random(seed)
+    rows = []
+    for _ in range(3000):  # v4, mostly disjoint with some overlaps and duplicates
+        a = rnd.randrange(1 << 32)
+        b = min((1 << 32) - 1, a + rnd.choice([0, 1, 255, 4095, 65535, 1 << 20]))
+        rows.append("%s\t%s\t%d\tC%d\tO%d" % (ipaddress.IPv4Address(a), ipaddress.IPv4Address(b), rnd.randrange(1, 70000),
+                                               rnd.randrange(9), rnd.randrange(99)))
+    for _ in range(1500):
+        a = rnd.randrange(1 << 128)
+        b = min((1 << 128) - 1, a + rnd.choice([0, 1, 1 << 64, 1 << 80, 1 << 100]))
+        rows.append("%s\t%s\t%d\tC\tO" % (ipaddress.IPv6Address(a), ipaddress.IPv6Address(b), rnd.randrange(1, 70000)))
+    rows.append("255.255.255.0\t255.255.255.255\t9\tZZ\tedge")
+    v4, v6, recs = asn_tables_from_tsv("\n".join(rows))
+    lists = []
+    for l in range(40):
+        rng = []
+        for _ in range(rnd.randrange(0, 60)):
+            if rnd.random() < 0.7:
+                rng.append("%s/%d" % (ipaddress.IPv4Address(rnd.randrange(1 << 32)), rnd.choice([0, 1, 8, 16, 24, 30, 32])))
+            else:
+                rng.append("%s/%d" % (ipaddress.IPv6Address(rnd.randrange(1 << 128)), rnd.choice([0, 3, 32, 64, 127, 128])))
+        lists.append({"name": "l%d" % l, "ip_ranges": rng})
+    lists.append({"name": "max", "ip_ranges": ["255.255.255.255", "ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff"]})
+    cidrs, names = blacklists_from_json({"blacklists": lists})
+    return v4, v6, recs, cidrs, names
+
+
+def _probe_ips(v4, v6, cidrs, seed, n=4000):
+    rnd = random.Random(seed)
+    ips = []
+    for t in (v4, v6):
+        for r in t[: 400]:
+            fam = 2 if t is v4 else 10
+            for w in (r["start"], r["end"]):
+                ip = int(words_to_ip(w, fam))
+                for d in (-1, 0, 1):
+                    if 0 <= ip + d < (1 << (32 if fam == 2 else 128)):
+                        ips.append(str(ipaddress.ip_address(ip + d) if fam == 2 else ipaddress.IPv6Address(ip + d)))
+    for c in cidrs[:300]:
+        ips.append(str(words_to_ip(c["addr"], int(c["family"]))))
+    ips += [str(ipaddress.IPv4Address(rnd.randrange(1 << 32))) for _ in range(n)]
+    ips += [str(ipaddress.IPv6Address(rnd.randrange(1 << 128))) for _ in range(n // 4)]
+    ips += ["0.0.0.0", "255.255.255.255", "::", "ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff"]
+    return ips
+
+
+def test_ip_lookup_known_answers(gpu_capture):
+    v4, v6, recs = asn_tables_from_tsv(TSV)
+    cidrs, names = blacklists_from_json({"blacklists": [
+        {"name": "base", "ip_ranges": ["192.168.0.0/16", "10.0.0.0/8", "8.8.8.8/32"]},
+        {"name": "v6", "ip_ranges": ["2001:db8::/32", "::1/128"]}]})
+    gpu_capture.set_asn_tables(v4, v6)
+    gpu_capture.set_blacklists(cidrs)
+    ips = ["217.147.96.0", "2001:200::1", "0.0.0.0", "192.168.1.1", "1.2.3.4", "8.8.8.8", "::1", "2002:db8::1"]
+    ga, gl = gpu_capture.ip_lookup(ips)
+    ra, rl = coracle.ip_lookup(coracle.asn_prepare(v4, 2), coracle.asn_prepare(v6, 10), cidrs, ips)
+    assert np.array_equal(ga, ra) and np.array_equal(gl, rl)
+    assert recs[ga[0]][0] == 174 and recs[ga[1]][0] == 2500 and ga[2] == -1
+    assert list(gl) == [0, 0, 0, 1, 0, 1, 2, 0]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_ip_lookup_random_tables(gpu_capture, seed):
+    v4, v6, recs, cidrs, names = _random_tables(seed)
+    gpu_capture.set_asn_tables(v4, v6)
+    gpu_capture.set_blacklists(cidrs)
+    ips = _probe_ips(v4, v6, cidrs, seed)
+    ga, gl = gpu_capture.ip_lookup(ips)
+    ra, rl = coracle.ip_lookup(coracle.asn_prepare(v4, 2), coracle.asn_prepare(v6, 10), cidrs, ips)
+    assert np.array_equal(ga, ra), [(ips[i], ga[i], ra[i]) for i in np.flatnonzero(ga != ra)[:5]]
+    assert np.array_equal(gl, rl), [(ips[i], gl[i], rl[i]) for i in np.flatnonzero(gl != rl)[:5]]
+    assert (ga >= 0).sum() > 100 and (gl != 0).sum() > 100
+
+
+def test_flow_enrich_vs_oracle(gpu_capture):
+    from flodbadd_amd.capture import lan_v6_table, own_ip_table
+    v4, v6, recs, cidrs, names = _random_tables(7)
+    gpu_capture.clear_all_sessions()
+    gpu_capture.set_asn_tables(v4, v6)
+    gpu_capture.set_blacklists(cidrs)
+    lan = [("2001:db8:abcd:12::1", 64)]
+    own = ["10.0.0.5", "1.1.1.1"]
+    gpu_capture.set_lan_v6(lan)
+    gpu_capture.set_own_ips(own)
+    cfg = coracle.make_cfg(2, lan_v6=lan_v6_table(lan), own_ips=own_ip_table(own))
+    a4, a6 = coracle.asn_prepare(v4, 2), coracle.asn_prepare(v6, 10)
+    try:
+        seen = set()
+        for b in range(2):
+            frames, offs = synth.generate(3, 40000, first=b * 40000)
+            gpu_capture.process_frames(frames, offs)
+            flows = gpu_capture.export_flows()
+            by_slot = {int(f["slot"]): f for f in flows}
+            for new_only in (False, True):
+                e = gpu_capture.enrich(new_only=new_only)
+                slots = [int(x["slot"]) for x in e]
+                assert len(set(slots)) == len(slots)
+                if not new_only:
+                    assert sorted(slots) == sorted(by_slot)
+                else:
+                    assert sorted(slots) == sorted(s for s in by_slot if s not in seen)
+                ref = coracle.enrich_keys(cfg, a4, a6, cidrs, [by_slot[s] for s in slots])
+                for f in ("flags", "src_asn", "dst_asn", "src_blacklists", "dst_blacklists"):
+                    assert np.array_equal(e[f], ref[f]), f
+            seen |= set(by_slot)
+        assert (e["flags"] & N.ENRICH_LOCAL_SRC).any() and (e["src_asn"] >= 0).any()
+    finally:
+        gpu_capture.set_lan_v6([])
+        gpu_capture.set_own_ips([])
+        gpu_capture.set_asn_tables(np.zeros(0, dtype=N.ASN_RANGE_DTYPE), np.zeros(0, dtype=N.ASN_RANGE_DTYPE))
+        gpu_capture.set_blacklists(np.zeros(0, dtype=N.CIDR_DTYPE))
+        gpu_capture.clear_all_sessions()
+        gpu_capture.set_filter(SessionFilter.All)
