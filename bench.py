@@ -179,6 +179,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         cnt = C.c_uint64()
         N.check(lib.fb_flow_count(ctx, C.byref(cnt), stream.ptr))
         stage["flows"] = int(cnt.value)
+        stage.update(enrich_timing(N, lib, ctx, int(cnt.value), stream))
     else:
         assert st2.tobytes() == st.tobytes()
     for b in bufs:
@@ -186,6 +187,51 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
             x.free()
     return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage, launches=launches,
                 stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
+
+
+def enrich_timing(N, lib, ctx, flows, stream, reps=5):
+    """New-session enrichment (fb_flow_enrich_dev) over every flow of the C4 table against
+    IPtoASN-sized synthetic tables: 500k IPv4 + 100k IPv6 ASN ranges, 50k blacklist ranges in 32
+    lists (deterministic)."""
+    rng = np.random.default_rng(0xA5A5)
+
+    def ranges(n, v6):
+        t = np.zeros(n, dtype=N.ASN_RANGE_DTYPE)
+        if v6:
+            hi = np.sort(rng.integers(0x20000000, 0x2FFFFFFF, n, dtype=np.uint64)).astype(np.uint32)
+            t["start"][:, 0] = hi
+            t["end"][:, 0] = hi
+            t["end"][:, 1:] = 0xFFFFFFFF
+        else:
+            st = np.sort(rng.choice(np.uint64(1 << 32) - np.uint64(1 << 16), n, replace=False)).astype(np.uint64)
+            t["start"][:, 0] = st.astype(np.uint32)
+            t["end"][:, 0] = (st + rng.integers(0, 4096, n).astype(np.uint64)).astype(np.uint32)
+        t["as_number"] = rng.integers(1, 400000, n)
+        t["record"] = np.arange(n)
+        return t
+    a4, a6 = ranges(500000, False), ranges(100000, True)
+    bl = np.zeros(50000, dtype=N.CIDR_DTYPE)
+    bl["family"] = 2
+    bl["addr"][:, 0] = rng.integers(0, 1 << 32, len(bl), dtype=np.uint64).astype(np.uint32)
+    bl["prefix"] = rng.choice([16, 20, 24, 28, 32], len(bl))
+    bl["list"] = rng.integers(0, 32, len(bl))
+    N.check(lib.fb_set_asn_tables(ctx, N.ptr(a4), len(a4), N.ptr(a6), len(a6)))
+    N.check(lib.fb_set_blacklists(ctx, N.ptr(bl), len(bl)))
+    d_out, d_n = N.DeviceBuffer(max(flows, 1) * N.FLOW_ENRICH_DTYPE.itemsize), N.DeviceBuffer(8)
+    e0, e1 = N.Event(), N.Event()
+    N.check(lib.fb_flow_enrich_dev(ctx, 0, d_out.ptr, flows, d_n.ptr, stream.ptr))
+    e0.record(stream)
+    for _ in range(reps):
+        N.check(lib.fb_flow_enrich_dev(ctx, 0, d_out.ptr, flows, d_n.ptr, stream.ptr))
+    e1.record(stream)
+    ms = e0.elapsed_ms(e1) / reps
+    got = int(d_n.download(np.zeros(1, dtype=np.uint64), stream=stream.ptr)[0])
+    N.check(lib.fb_set_asn_tables(ctx, None, 0, None, 0))
+    N.check(lib.fb_set_blacklists(ctx, None, 0))
+    for b in (d_out, d_n):
+        b.free()
+    return dict(enrich_ms=round(ms, 4), enrich_flows=got, enrich_Mflows_s=round(got / ms / 1e3, 1),
+                enrich_tables="500k v4 + 100k v6 ASN ranges, 50k blacklist ranges / 32 lists")
 
 
 def host_inclusive(N, lib, ctx, frames, offs, calls=20):
@@ -409,6 +455,8 @@ def main():
         sg = main_r["stage"]
         extra["c4_stages"] = dict(parse_ms=round(sg["parse_ms"], 4), flow_update_ms=round(sg["flow_ms"], 4),
                                   history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
+                                  enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
+                                  enrich_tables=sg["enrich_tables"],
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
