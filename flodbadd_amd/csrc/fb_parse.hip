@@ -830,16 +830,30 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
         return y;
     };
-    // kSegDepth segments of header loads in flight per wave: set d (headers h, the segment's
-    // offsets c, and q = the offsets of the set's next segment) serves the wave's segments
-    // d, d+D, d+2D, ... (loop unrolled by D, so no set is indexed at run time).  After a
-    // segment: X.h <- headers of the set's next segment from X.q, X.c <- X.q (explicit v_mov:
-    // no back-edge copy of a pending load), X.q <- offsets of the one after.  Every step issues
-    // the same VMEM sequence (4 header loads, 2 offset loads, 8 stores) and the prologue mirrors
-    // it with dropped stores, so the compiler's vmcnt waits let D-1 younger steps' traffic pass.
-    // Segments past the launch's end clamp to the last batch's last offset (nothing is read
-    // out of bounds; the step that would use them never runs).
+    // Segment hand-out: the block owns the segments b*W + j + k*stride (W waves, j < W, k >= 0),
+    // numbered L = k*W + j in address order.  The waves of a CU are not served evenly by the
+    // memory pipeline (with a static share per wave the first wave of a block left after ~55 %
+    // of the time of its last one), so after a static first two (L = wave, wave + W) each wave
+    // takes the block's next L from an LDS counter, one step ahead of use: a wave that is
+    // served faster processes more segments, and the block finishes when its work is done, not
+    // when its slowest wave is.  A wave's L (hence its segments) still increase monotonically.
+    // One segment of header loads in flight per wave: X.h = headers of the current segment,
+    // X.c its offsets, X.q the offsets of the wave's next segment.  After a segment:
+    // X.h <- headers of the next segment from X.q, X.c <- X.q (explicit v_mov: no back-edge copy
+    // of a pending load), X.q <- offsets of the one after.  Every step issues the same VMEM
+    // sequence (4 header loads, 2 offset loads, 8 stores) and the prologue mirrors it with
+    // dropped stores, so the compiler's vmcnt waits let the stores pass.  Segments past the
+    // launch's end clamp to the last batch's last offset (nothing is read out of bounds; the
+    // step that would use them never runs).
     constexpr int D = kSegDepth;
+    static_assert(D == 1, "one segment of header loads in flight (dynamic hand-out)");
+    __shared__ uint32_t s_next;  // the block's next segment number L to hand out
+    auto seg_of = [&](uint32_t L) { return b * kSegWaves + L % kSegWaves + (L / kSegWaves) * stride; };
+    auto grab = [&]() {
+        uint32_t v = 0u;
+        if (lane == 0u) v = __hip_atomic_fetch_add(&s_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
     struct Set {
         Hdr h;
         uint2 c, q;
@@ -874,7 +888,9 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     // Prologue: the configuration loads and the first offsets loads are issued together (the
     // header loads then wait for one round trip, not two), the configuration goes to LDS, and
     // an LDS-only barrier publishes it while the header loads stay in flight.
-    uint32_t sg = b * kSegWaves + wave;
+    uint32_t Lc = wave, Ln = wave + kSegWaves;  // the wave's current and next segment numbers
+    uint32_t sg = seg_of(Lc);
+    if (tid == 0u) s_next = 2u * kSegWaves;  // published by the prologue barrier
     constexpr uint32_t kCfg16 = kCfgLdsBytes / 16, kCfgIt = (kCfg16 + kSegThreads - 1) / kSegThreads;
     uint4 cfgv[kCfgIt];
     {
@@ -883,8 +899,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         for (uint32_t it = 0; it < kCfgIt; ++it) cfgv[it] = src[min(tid + it * kSegThreads, kCfg16 - 1u)];
     }
     if constexpr (!PARSED) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) load_q(sg + d * stride, SS[d].q);
+        load_q(sg, SS[0].q);
     } else {
         load_parsed(sg);
     }
@@ -899,15 +914,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         for (uint32_t k = tid; k < no; k += kSegThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
         if (b == 0u && tid == 0u) *P.error_next = 0u;  // other parity's word, for the next launch
     }
-    if constexpr (!PARSED) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            fetch(SS[d], sg + d * stride, sg + (uint32_t)(d + D) * stride);
-            dropped_stores();
-        }
-    } else {
-        dropped_stores();
-    }
+    if constexpr (!PARSED) fetch(SS[0], sg, seg_of(Ln));
+    dropped_stores();
     ws_tick();  // configuration in LDS (LDS-only barrier: the header loads stay in flight)
     sstamp(1);
     // a wave's counters go to LDS whenever its segments move on to the next batch
@@ -922,7 +930,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         }
         a_s = a_d = a_f = a_t = a_4 = a_b = a_n = 0u;
     };
-    auto step = [&](uint32_t sg, Set& X) {
+    auto step = [&](uint32_t sg, Set& X, uint32_t g_next, uint32_t g_after) {
             const uint32_t k = batch_of(k_s, sg);
             if (MULTI && k != a_k) {
                 flush();
@@ -969,8 +977,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             __builtin_amdgcn_wave_barrier();
             // prefetch: headers of this set's next segment (offsets already here), offsets of the
             // one after
-            if constexpr (!PARSED) fetch(X, sg + D * stride, sg + 2u * D * stride);
-            else load_parsed(sg + stride);
+            if constexpr (!PARSED) fetch(X, g_next, g_after);
+            else load_parsed(g_next);
             if constexpr ((FLAGS & kNoStore) == 0u) {
             // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
                 const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
@@ -1012,13 +1020,14 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             a_n += __popcll(__ballot(valid));
             sstamp(2u + min(iter++, 11u));
     };
-    for (; sg + (uint32_t)(D - 1) * stride < nseg; sg += (uint32_t)D * stride) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) step(sg + d * stride, SS[d]);
+    while (sg < nseg) {
+        const uint32_t La = grab();
+        const uint32_t g_next = seg_of(Ln);
+        step(sg, SS[0], g_next, seg_of(La));
+        Lc = Ln;
+        Ln = La;
+        sg = g_next;
     }
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d)
-        if (sg + d * stride < nseg) step(sg + d * stride, SS[d]);
     sstamp(14);
     // ---- batch stats, no barrier and no partials read-back:
     // every wave adds its counters into LDS (per batch); the block's last wave (LDS arrival

@@ -127,6 +127,15 @@ int main(int argc, char** argv) {
         p.error = err + (epoch & 1u); p.error_next = err + ((epoch & 1u) ^ 1u); p.dbg = dbg;
         return p;
     };
+    auto sb1 = [&](const fbk::ParseParams& p) {  // one-batch launch descriptor of k_parse_seg
+        fbk::SegBatches sb;
+        memset(&sb, 0, sizeof(sb));
+        sb.count = 1;
+        sb.b[0].frames = p.frames; sb.b[0].offsets = p.offsets; sb.b[0].out = p.out; sb.b[0].seg = p.seg;
+        sb.b[0].cls = p.cls; sb.b[0].stats = p.stats; sb.b[0].n = p.n; sb.b[0].frames_bytes = p.frames_bytes;
+        sb.total_segs = (p.n + 63u) / 64u;
+        return sb;
+    };
     uint64_t caps = 0;
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;
@@ -161,10 +170,10 @@ int main(int argc, char** argv) {
                 case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
                 case 6: case 7: case 8: case 9: {
                     fbk::ParseParams pp = params(r); pp.seg = dseg; pp.dns = nullptr;
-                    if (v == 6) hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
-                    if (v == 7) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
-                    if (v == 8) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
-                    if (v == 9) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+                    if (v == 6) hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
+                    if (v == 7) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
+                    if (v == 8) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
+                    if (v == 9) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
                 } break;
                 case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
                 }
@@ -190,7 +199,7 @@ int main(int argc, char** argv) {
         CK(hipMemset(sd, 0, sw * 8));
         for (int w = 0; w < 3; ++w) {
             fbk::ParseParams pp = params(w % R); pp.seg = dseg; pp.dns = nullptr; pp.dbg = sd;
-            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp);
+            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
         }
         CK(hipStreamSynchronize(s));
         std::vector<unsigned long long> st2(sw);
@@ -219,6 +228,22 @@ int main(int argc, char** argv) {
                 printf("{\"by\": \"%s\", \"k\": %d, \"prologue_us\": [%.2f, %.2f, %.2f], \"exit_us\": [%.2f, %.2f, %.2f]}\n",
                        key == 0 ? "xcd" : "third", k, qq(v, 0), qq(v, .5), qq(v, 1), qq(e, 0), qq(e, .5), qq(e, 1));
             }
+        }
+        {   // per block: exit of its first and last wave (intra- vs inter-CU imbalance)
+            std::vector<double> bmin, bmax, spread;
+            for (size_t b = 0; b < sgrid; ++b) {
+                double lo = 1e30, hi = 0;
+                for (int w = 0; w < fbk::kSegWaves; ++w) {
+                    const unsigned long long t = st2[(b * fbk::kSegWaves + w) * 16 + 15];
+                    if (!t) continue;
+                    lo = std::min(lo, (t - z) * 0.01);
+                    hi = std::max(hi, (t - z) * 0.01);
+                }
+                if (hi > 0) { bmin.push_back(lo); bmax.push_back(hi); spread.push_back(hi - lo); }
+            }
+            printf("{\"block_first_exit_us\": [%.2f, %.2f, %.2f], \"block_last_exit_us\": [%.2f, %.2f, %.2f], "
+                   "\"block_spread_us\": [%.2f, %.2f, %.2f]}\n", qq(bmin, 0), qq(bmin, .5), qq(bmin, 1), qq(bmax, 0),
+                   qq(bmax, .5), qq(bmax, 1), qq(spread, 0), qq(spread, .5), qq(spread, 1));
         }
         CK(hipFree(sd));
     }
