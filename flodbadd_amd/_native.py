@@ -58,6 +58,15 @@ CIDR_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("prefix", "<u4
 FLOW_ENRICH_DTYPE = np.dtype([("slot", "<u4"), ("flags", "<u4"), ("src_asn", "<i4"), ("dst_asn", "<i4"),
                               ("src_blacklists", "<u8"), ("dst_blacklists", "<u8")])
 FB_MAX_BLACKLISTS = 64
+# fb_dns_msg + constants (include/flodbadd_gpu.h, DNS divert parse)
+DNS_MSG_DTYPE = np.dtype([("pkt_index", "<u4"), ("id", "<u2"), ("status", "u1"), ("flags", "u1"),
+                          ("questions", "<u2"), ("answers", "<u2"), ("name_len", "<u2"), ("n_addrs", "u1"),
+                          ("reserved", "u1")])
+FB_DNS_MAX_NAME, FB_DNS_MAX_ADDRS = 256, 8
+DNS_QUERY, DNS_HAS_QUESTION, DNS_REVERSE, DNS_NAME_TRUNCATED, DNS_ADDRS_TRUNCATED = 1, 2, 4, 8, 16
+DNS_STATUS = ["ok", "header_too_short", "unexpected_eof", "bad_pointer", "unknown_label_format", "label_not_ascii",
+              "invalid_query_type", "invalid_query_class", "invalid_type", "invalid_class", "wrong_rdata_length",
+              "additional_opt"]
 ENRICH_LOCAL_SRC, ENRICH_LOCAL_DST, ENRICH_SELF_SRC, ENRICH_SELF_DST = 1, 2, 4, 8
 LAN_V6_DTYPE = np.dtype([("net", "<u4", (4,)), ("prefix", "<u4"), ("reserved", "<u4", (3,))])
 FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "<u4", (3,))])
@@ -95,6 +104,7 @@ assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_
 assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 128
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
 assert ASN_RANGE_DTYPE.itemsize == 48 and CIDR_DTYPE.itemsize == 32 and FLOW_ENRICH_DTYPE.itemsize == 32
+assert DNS_MSG_DTYPE.itemsize == 16
 
 
 class FbConfig(C.Structure):
@@ -153,6 +163,7 @@ GPU_SYMBOLS = [
     ("fb_set_blacklists", _I, [_P, _P, _U32]),
     ("fb_ip_lookup_dev", _I, [_P, _P, _U32, _P, _P, _P]),
     ("fb_flow_enrich_dev", _I, [_P, _U32, _P, _U64, _P, _P]),
+    ("fb_dns_parse_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_flow_count", _I, [_P, _PU64, _P]),
     ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),

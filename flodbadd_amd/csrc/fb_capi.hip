@@ -861,6 +861,15 @@ int fb_flow_enrich_dev(fb_ctx* c, uint32_t new_only, fb_flow_enrich* d_out, uint
     return FB_OK;
 }
 
+int fb_dns_parse_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const fb_dns_out* d_dns, uint32_t n,
+                     const fb_batch_stats* d_stats, fb_dns_msg* d_msgs, char* d_names, fb_ip* d_addrs, void* stream) {
+    if (!c || (n && (!d_dns || !d_msgs || !d_names || !d_addrs || !d_frames)))
+        return set_err(FB_ERR_INVAL, "bad arguments");
+    DeviceGuard g(c->device);
+    HIP_TRY(launch_dns_parse(d_frames, frames_bytes, d_dns, n, d_stats, d_msgs, d_names, d_addrs, (hipStream_t)stream));
+    return FB_OK;
+}
+
 int fb_flow_count(fb_ctx* c, uint64_t* n_flows, void* stream) {
     if (!c || !n_flows) return set_err(FB_ERR_INVAL, "bad arguments");
     *n_flows = 0;

@@ -236,4 +236,7 @@ hipError_t launch_flow_enrich(const EnrichTables& t, const DevConfig* cfg, const
                               unsigned long long cap, uint32_t new_only, uint32_t batch, fb_flow_enrich* out,
                               unsigned long long out_cap, unsigned long long* d_n, hipStream_t s);
 
+hipError_t launch_dns_parse(const uint8_t* frames, unsigned long long frames_bytes, const fb_dns_out* dns, uint32_t n,
+                            const fb_batch_stats* stats, fb_dns_msg* msgs, char* names, fb_ip* addrs, hipStream_t s);
+
 }  // namespace fbk

@@ -422,6 +422,52 @@ enum fb_enrich_bits {
 int fb_flow_enrich_dev(fb_ctx* ctx, uint32_t new_only, fb_flow_enrich* d_out, uint64_t cap, uint64_t* d_n,
                        void* stream);
 
+/* ---- DNS divert parse (src/dns.rs:35-99: DnsPacket::parse of dns-parser 0.8.0, then the query /
+ *      response bookkeeping) ------------------------------------------------------------------ */
+#define FB_DNS_MAX_NAME 256u  /* bytes of the dotted first-question name kept per message */
+#define FB_DNS_MAX_ADDRS 8u   /* A / AAAA answers kept per message */
+enum fb_dns_status {          /* DnsPacket::parse outcome (dns_parser::Error variants) */
+    FB_DNS_OK = 0,
+    FB_DNS_HEADER_TOO_SHORT = 1,
+    FB_DNS_UNEXPECTED_EOF = 2,
+    FB_DNS_BAD_POINTER = 3,
+    FB_DNS_UNKNOWN_LABEL_FORMAT = 4,
+    FB_DNS_LABEL_NOT_ASCII = 5,
+    FB_DNS_INVALID_QUERY_TYPE = 6,
+    FB_DNS_INVALID_QUERY_CLASS = 7,
+    FB_DNS_INVALID_TYPE = 8,
+    FB_DNS_INVALID_CLASS = 9,
+    FB_DNS_WRONG_RDATA_LENGTH = 10,
+    FB_DNS_ADDITIONAL_OPT = 11
+};
+enum fb_dns_flags {
+    FB_DNS_QUERY = 1u,            /* header.query (QR bit clear)                              */
+    FB_DNS_HAS_QUESTION = 2u,     /* questions.get(0) is Some                                 */
+    FB_DNS_REVERSE = 4u,          /* the first qname ends with .in-addr.arpa / .ip6.arpa      */
+    FB_DNS_NAME_TRUNCATED = 8u,   /* the name is longer than FB_DNS_MAX_NAME - 1 bytes         */
+    FB_DNS_ADDRS_TRUNCATED = 16u  /* more than FB_DNS_MAX_ADDRS A / AAAA answers              */
+};
+typedef struct fb_dns_msg {
+    uint32_t pkt_index;  /* the frame (fb_dns_out.pkt_index)                          */
+    uint16_t id;         /* header.id (the transaction id the bookkeeping keys on)   */
+    uint8_t status;      /* fb_dns_status                                            */
+    uint8_t flags;       /* fb_dns_flags                                             */
+    uint16_t questions;  /* header counts                                            */
+    uint16_t answers;
+    uint16_t name_len;   /* bytes of names[i] (dotted, no terminator needed)         */
+    uint8_t n_addrs;     /* A / AAAA answers in addrs[i * FB_DNS_MAX_ADDRS ..]        */
+    uint8_t reserved;
+} fb_dns_msg;            /* 16 bytes */
+/* Parse the DNS payloads of a batch's DNS side records (fb_parse_classify_dev's d_dns) the way
+ * DnsPacket::parse does, keeping what process_dns_packet uses: id, query bit, the first
+ * question's name, the A / AAAA answers in order.  n = d_dns entries; with d_stats non-NULL only
+ * the first d_stats->n_dns (read on the device) are parsed.  d_names: n * FB_DNS_MAX_NAME bytes,
+ * d_addrs: n * FB_DNS_MAX_ADDRS fb_ip.  DEVICE pointers, asynchronous.  The ordered bookkeeping
+ * (pending queries by id, resolutions) stays on the host: a few operations per DNS packet. */
+int fb_dns_parse_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes, const fb_dns_out* d_dns,
+                     uint32_t n, const fb_batch_stats* d_stats, fb_dns_msg* d_msgs, char* d_names,
+                     fb_ip* d_addrs, void* stream);
+
 int fb_flow_count(fb_ctx* ctx, uint64_t* n_flows, void* stream); /* synchronous */
 /* Copy every flow (slot order) to host memory; *n = flows written (<= cap). Synchronous. */
 int fb_flow_export(fb_ctx* ctx, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream);

@@ -51,6 +51,8 @@ def lib():
         L.orc_blacklist_mask.restype = U64
         L.orc_blacklist_mask.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.orc_enrich_keys.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P]
+        L.orc_dns_parse.restype = C.c_uint32
+        L.orc_dns_parse.argtypes = [P, C.c_uint32, C.c_uint32, P, C.c_char_p, P]
         L.orc_flows_new.restype = P
         L.orc_flows_free.argtypes = [P]
         L.orc_flows_clear.argtypes = [P]
@@ -157,6 +159,17 @@ def ip_lookup(a4, a6, cidrs, ips):
         lists.append(lib().orc_blacklist_mask(cidrs.ctypes.data if len(cidrs) else None, len(cidrs), fam,
                                               w.ctypes.data))
     return np.array(asn, dtype=np.int32), np.array(lists, dtype=np.uint64)
+
+
+def dns_parse(payload, pkt_index=0):
+    """orc_dns_parse -> (DNS_MSG_DTYPE record, name bytes, [fb_ip addrs])."""
+    pl = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+    r = np.zeros(1, dtype=N.DNS_MSG_DTYPE)
+    name = C.create_string_buffer(N.FB_DNS_MAX_NAME)
+    addrs = np.zeros(N.FB_DNS_MAX_ADDRS, dtype=FB_IP_DTYPE)
+    lib().orc_dns_parse(pl.ctypes.data if pl.size else None, pl.size, pkt_index, r.ctypes.data, name,
+                        addrs.ctypes.data)
+    return r[0], name.raw[: int(r[0]["name_len"])], addrs[: int(r[0]["n_addrs"])]
 
 
 class Flows:

@@ -643,3 +643,218 @@ void orc_enrich_keys(const orc_cfg* c, const fb_asn_range* a4, uint32_t n4, cons
         r->dst_blacklists = ld ? 0 : orc_blacklist_mask(nets, nn, fam, k->dst_ip);
     }
 }
+
+/* ---------------------------------------------------------------------------------------
+ * DNS divert parse: dns_parser::Packet::parse (dns-parser 0.8.0, restated from its published
+ * source; the crate is a git dependency absent from the reference mount -> parity unpinned) and
+ * what process_dns_packet reads from it (src/dns.rs:35-99).  Written in the crate's slice style:
+ * a Name is scanned over `data` (a suffix of the message or an RDATA slice) with pointers into
+ * `original` (the whole message).
+ * ------------------------------------------------------------------------------------- */
+typedef struct { const uint8_t* p; uint32_t n; } dslice;
+
+static uint32_t rd16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+
+/* Name::scan: returns an fb_dns_status; *byte_len as Name::byte_len(). */
+static uint32_t dn_scan(dslice data, dslice original, uint32_t* byte_len) {
+    dslice pd = data;
+    size_t pos = 0;
+    long return_pos = -1;
+    if (pd.n <= pos) return FB_DNS_UNEXPECTED_EOF;
+    size_t largest_pos = original.n;
+    uint8_t byte = pd.p[pos];
+    while (byte != 0) {
+        if (pd.n <= pos) return FB_DNS_UNEXPECTED_EOF;
+        if ((byte & 0xC0) == 0xC0) {
+            if (pd.n < pos + 2) return FB_DNS_UNEXPECTED_EOF;
+            size_t off = rd16(pd.p + pos) & 0x3FFF;
+            if (off >= original.n) return FB_DNS_UNEXPECTED_EOF;
+            if (return_pos < 0) return_pos = (long)pos;
+            if (off >= largest_pos) return FB_DNS_BAD_POINTER;
+            largest_pos = off;
+            pos = 0;
+            pd.p = original.p + off;
+            pd.n = original.n - (uint32_t)off;
+        } else if ((byte & 0xC0) == 0) {
+            size_t end = pos + byte + 1;
+            if (pd.n < end) return FB_DNS_UNEXPECTED_EOF;
+            for (size_t k = pos + 1; k < end; ++k)
+                if (pd.p[k] & 0x80) return FB_DNS_LABEL_NOT_ASCII;
+            pos = end;
+            if (pd.n <= pos) return FB_DNS_UNEXPECTED_EOF;
+        } else {
+            return FB_DNS_UNKNOWN_LABEL_FORMAT;
+        }
+        byte = pd.p[pos];
+    }
+    *byte_len = return_pos >= 0 ? (uint32_t)return_pos + 2 : (uint32_t)pos + 1;
+    return FB_DNS_OK;
+}
+
+/* Name's Display, recursively as the crate writes it. */
+static void dn_fmt(const uint8_t* labels, dslice original, char* out, size_t* n) {
+    size_t pos = 0;
+    for (;;) {
+        uint8_t byte = labels[pos];
+        if (byte == 0) return;
+        if ((byte & 0xC0) == 0xC0) {
+            size_t off = rd16(labels + pos) & 0x3FFF;
+            if (pos != 0) out[(*n)++] = '.';
+            dn_fmt(original.p + off, original, out, n);
+            return;
+        }
+        if (pos != 0) out[(*n)++] = '.';
+        memcpy(out + *n, labels + pos + 1, byte);
+        *n += byte;
+        pos += byte + 1;
+    }
+}
+
+static int qtype_ok(uint32_t t) { return (t >= 1 && t <= 16 && t != 3) || t == 28 || t == 33 || (t >= 252 && t <= 255); }
+static int type_ok(uint32_t t) { return (t >= 1 && t <= 16 && t != 3) || t == 28 || t == 33 || t == 41 || t == 47; }
+
+/* RData::parse for the types the crate decodes (others: RData::Unknown, never an error). */
+static uint32_t rdata_parse(uint32_t typ, dslice rd, dslice original) {
+    uint32_t bl, b2;
+    switch (typ) {
+        case 1: return rd.n == 4 ? FB_DNS_OK : FB_DNS_WRONG_RDATA_LENGTH;
+        case 28: return rd.n == 16 ? FB_DNS_OK : FB_DNS_WRONG_RDATA_LENGTH;
+        case 2: case 5: case 12: return dn_scan(rd, original, &bl);
+        case 15: {
+            if (rd.n < 3) return FB_DNS_WRONG_RDATA_LENGTH;
+            dslice s = {rd.p + 2, rd.n - 2};
+            return dn_scan(s, original, &bl);
+        }
+        case 33: {
+            if (rd.n < 7) return FB_DNS_WRONG_RDATA_LENGTH;
+            dslice s = {rd.p + 6, rd.n - 6};
+            return dn_scan(s, original, &bl);
+        }
+        case 6: {
+            uint32_t st = dn_scan(rd, original, &bl);
+            if (st) return st;
+            dslice s = {rd.p + bl, rd.n - bl};
+            st = dn_scan(s, original, &b2);
+            if (st) return st;
+            return rd.n - bl - b2 < 20 ? FB_DNS_WRONG_RDATA_LENGTH : FB_DNS_OK;
+        }
+        case 16: {
+            if (rd.n < 1) return FB_DNS_WRONG_RDATA_LENGTH;
+            size_t pos = 0;
+            while (pos < rd.n) {
+                size_t l = rd.p[pos];
+                pos += 1;
+                if (rd.n < l + pos) return FB_DNS_WRONG_RDATA_LENGTH;
+                pos += l;
+            }
+            return FB_DNS_OK;
+        }
+        default: return FB_DNS_OK;
+    }
+}
+
+/* parse_record; answers' A / AAAA collected into addrs. */
+static uint32_t parse_record(dslice data, size_t* offset, int answer, fb_ip* addrs, uint32_t* na, uint32_t* flags) {
+    uint32_t bl;
+    dslice s = {data.p + *offset, data.n - (uint32_t)*offset};
+    uint32_t st = dn_scan(s, data, &bl);
+    if (st) return st;
+    *offset += bl;
+    if (*offset + 10 > data.n) return FB_DNS_UNEXPECTED_EOF;
+    uint32_t typ = rd16(data.p + *offset);
+    if (!type_ok(typ)) return FB_DNS_INVALID_TYPE;
+    *offset += 2;
+    uint32_t cls = rd16(data.p + *offset);
+    if (typ != 41 && !((cls & 0x7FFF) >= 1 && (cls & 0x7FFF) <= 4)) return FB_DNS_INVALID_CLASS;
+    *offset += 2 + 4; /* class, ttl */
+    size_t rdlen = rd16(data.p + *offset);
+    *offset += 2;
+    if (*offset + rdlen > data.n) return FB_DNS_UNEXPECTED_EOF;
+    dslice rd = {data.p + *offset, (uint32_t)rdlen};
+    st = rdata_parse(typ, rd, data);
+    if (st) return st;
+    if (answer && (typ == 1 || typ == 28)) {
+        if (*na < FB_DNS_MAX_ADDRS) {
+            fb_ip* a = &addrs[(*na)++];
+            memset(a, 0, sizeof(*a));
+            a->family = typ == 28 ? 10 : 2;
+            for (int k = 0; k < (typ == 28 ? 4 : 1); ++k) a->addr[k] = be32(rd.p + 4 * k);
+        } else {
+            *flags |= FB_DNS_ADDRS_TRUNCATED;
+        }
+    }
+    *offset += rdlen;
+    return FB_DNS_OK;
+}
+
+static int ends_with(const char* s, size_t n, const char* sfx) {
+    size_t l = strlen(sfx);
+    return n >= l && memcmp(s + n - l, sfx, l) == 0;
+}
+
+/* Packet::parse + the fields process_dns_packet reads. name: >= FB_DNS_MAX_NAME bytes. */
+uint32_t orc_dns_parse(const uint8_t* payload, uint32_t len, uint32_t pkt_index, fb_dns_msg* r, char* name,
+                       fb_ip* addrs) {
+    memset(r, 0, sizeof(*r));
+    r->pkt_index = pkt_index;
+    dslice data = {payload, len};
+    uint32_t st = FB_DNS_OK, flags = 0, na = 0;
+    if (len < 12) {
+        r->status = FB_DNS_HEADER_TOO_SHORT;
+        return r->status;
+    }
+    r->id = (uint16_t)rd16(payload);
+    uint32_t qd = rd16(payload + 4), an = rd16(payload + 6), ns = rd16(payload + 8), ar = rd16(payload + 10);
+    r->questions = (uint16_t)qd;
+    r->answers = (uint16_t)an;
+    if ((payload[2] & 0x80) == 0) flags |= FB_DNS_QUERY;
+    size_t offset = 12, q0 = 0;
+    for (uint32_t q = 0; q < qd && !st; ++q) {
+        uint32_t bl;
+        dslice s = {payload + offset, len - (uint32_t)offset};
+        st = dn_scan(s, data, &bl);
+        if (st) break;
+        if (q == 0) q0 = offset;
+        offset += bl;
+        if (offset + 4 > len) { st = FB_DNS_UNEXPECTED_EOF; break; }
+        if (!qtype_ok(rd16(payload + offset))) { st = FB_DNS_INVALID_QUERY_TYPE; break; }
+        offset += 2;
+        uint32_t qc = rd16(payload + offset) & 0x7FFF;
+        if (!((qc >= 1 && qc <= 4) || qc == 255)) { st = FB_DNS_INVALID_QUERY_CLASS; break; }
+        offset += 2;
+    }
+    for (uint32_t k = 0; k < an && !st; ++k) st = parse_record(data, &offset, 1, addrs, &na, &flags);
+    for (uint32_t k = 0; k < ns && !st; ++k) st = parse_record(data, &offset, 0, addrs, &na, &flags);
+    int have_opt = 0;
+    for (uint32_t k = 0; k < ar && !st; ++k) {
+        if (offset + 3 <= len && payload[offset] == 0 && payload[offset + 1] == 0 && payload[offset + 2] == 41) {
+            offset += 1;
+            if (have_opt) { st = FB_DNS_ADDITIONAL_OPT; break; }
+            have_opt = 1;
+            if (offset + 10 > len) { st = FB_DNS_UNEXPECTED_EOF; break; } /* parse_opt_record */
+            offset += 8;
+            size_t rdlen = rd16(payload + offset);
+            offset += 2;
+            if (offset + rdlen > len) { st = FB_DNS_UNEXPECTED_EOF; break; }
+            offset += rdlen;
+        } else {
+            st = parse_record(data, &offset, 0, addrs, &na, &flags);
+        }
+    }
+    r->status = (uint8_t)st;
+    if (st) return st;
+    if (qd > 0) {
+        char* full = (char*)malloc(len * 2 + 16); /* a scanned name's Display is bounded by the message */
+        size_t n = 0;
+        dn_fmt(payload + q0, data, full, &n);
+        flags |= FB_DNS_HAS_QUESTION;
+        if (ends_with(full, n, ".in-addr.arpa") || ends_with(full, n, ".ip6.arpa")) flags |= FB_DNS_REVERSE;
+        if (n > FB_DNS_MAX_NAME - 1) flags |= FB_DNS_NAME_TRUNCATED;
+        r->name_len = (uint16_t)(n < FB_DNS_MAX_NAME - 1 ? n : FB_DNS_MAX_NAME - 1);
+        memcpy(name, full, r->name_len);
+        free(full);
+    }
+    r->flags = (uint8_t)flags;
+    r->n_addrs = (uint8_t)na;
+    return FB_DNS_OK;
+}

@@ -14,6 +14,10 @@
  *   src/ip.rs:55-242         is_lan_ip
  *   src/sessions.rs:658-692  is_local_session! / is_global_session! / filter_sessions
  *   src/port_vulns.rs:213-228 get_name_from_port (as a 65536-bit "has a name" bitmap)
+ *   src/asn_db.rs:82-166     Db::from_tsv filtering/sort + Db::lookup (ASN)
+ *   src/blacklists.rs:205-260 is_ip_in_blacklist (IpNet::contains scan)
+ *   src/dns.rs:35-99         process_dns_packet's use of dns_parser::Packet::parse (dns-parser
+ *                            0.8.0, NOT vendored: DNS parse parity is "unpinned" too)
  * Output records use the same C layout as include/flodbadd_gpu.h so results compare
  * byte-for-byte.
  */
@@ -100,6 +104,10 @@ uint64_t orc_blacklist_mask(const fb_cidr* nets, uint32_t n, uint32_t family, co
 void orc_enrich_keys(const orc_cfg* c, const fb_asn_range* a4, uint32_t n4, const fb_asn_range* a6, uint32_t n6,
                      const fb_cidr* nets, uint32_t nn, const fb_session_key* keys, uint32_t nk,
                      fb_flow_enrich* out);
+
+/* ---- DNS divert parse (dns-parser 0.8.0 Packet::parse restated; src/dns.rs:35-99) ---- */
+uint32_t orc_dns_parse(const uint8_t* payload, uint32_t len, uint32_t pkt_index, fb_dns_msg* r, char* name,
+                       fb_ip* addrs);
 
 uint64_t orc_pipeline(const orc_cfg* cfg, orc_flows* flows, const uint8_t* frames,
                       uint64_t frames_bytes, const uint32_t* offsets, uint32_t n,
