@@ -173,20 +173,29 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
 // ---------------------------------------------------------------------------------------------
 // K2: apply one partition's entries to its LDS-resident slice.
 //
+// LDS: the slots' first 96 B (tag, key, counters) + a 40-B per-slot batch scratch = 68 KiB, so two
+// workgroups share a CU and one's slice load / write-back overlaps the other's apply (at one
+// workgroup per CU, with the ordered fields in LDS too, the phases ran back to back).
+//
 // Ordered state (src/packets.rs:187-198, 410-426).  Entries reach K2 in no particular order, so
-// everything order-dependent is reduced to order-independent LDS atomics keyed by the record
-// slot `rec` (batch order) in a per-slot batch scratch, then folded into the slot once per batch:
-//   first / last packet  = min / max of (rec << 32 | pkt_index)
-//   end (first FIN/RST)  = min of the same over the TCP records with FIN or RST
-//   history characters   = OR of their FB_HIST_CHARS bits, and for the 8 characters that
-//                          determine_conn_state reads (S s H h F f R r) the first rec of each.
-// conn_state at the end packet is determine_conn_state of (the flow's mask from earlier batches
-// | the characters whose first occurrence is at or before the end record): the reference's test
-// `history.contains(c)` only asks which characters the string holds at that moment.
-constexpr uint32_t kSlotWords = sizeof(FlowSlot) / 8;  // 16 u64 words per slot
-constexpr uint32_t kScrWords = 8;                      // per-slot batch scratch, u64 words
-constexpr uint32_t kK2Lds = kFlowSlots * (sizeof(FlowSlot) + kScrWords * 8);
+// everything order-dependent is reduced to order-independent LDS atomics over the record slot
+// `rec` (batch order) in the scratch, then folded into the slot's ordered fields (in HBM, read
+// and written once per touched slot) at the end:
+//   first / last packet  = min / max rec; end (first FIN/RST) = min rec of the TCP records with
+//                          FIN or RST; their pkt_index (and the end packet's character) are read
+//                          back from the records
+//   history              = count, OR of the FB_HIST_CHARS bits, first rec of S s H h.
+// conn_state at the end packet is determine_conn_state over the characters the history holds
+// then: the flow's mask from earlier batches | S s H h whose first occurrence is at or before the
+// end record | the end packet's own character.  F f R r need no first occurrence: each comes from
+// a FIN or RST packet, and the first of those IS the end packet (the reference's string tests
+// `history.contains(c)` only ask which characters are present).
+constexpr uint32_t kSlotWords = 12;  // u64 words of a slot kept in LDS: tag, key[5], counters[6]
+constexpr uint32_t kScrU32 = 10;     // per-slot batch scratch, u32 words
+constexpr uint32_t kK2Lds = kFlowSlots * (kSlotWords * 8 + kScrU32 * 4);
 constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
+// scratch words
+constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
 
 __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -223,9 +232,9 @@ __device__ __forceinline__ uint32_t conn_state_of(uint32_t m) {
 }
 
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
-__device__ __forceinline__ int apply_entry(unsigned long long* slice, unsigned long long* scr, const uint4 e0,
-                                           const uint4 e1, const uint4 e2, const uint4 e3, uint32_t slot_base,
-                                           uint32_t* rec_flow, uint32_t* err) {
+__device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
+                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* rec_flow,
+                                           uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
     const unsigned long long h = flow_hash_words(key);
@@ -275,61 +284,73 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, unsigned l
     atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
     atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
     atomicAdd(s + 10 + (orig ? 0 : 1), (unsigned long long)e2.w);
-    // ordered state into the batch scratch (see above)
-    unsigned long long* q = scr + (size_t)i * kScrWords;
-    uint32_t* q32 = reinterpret_cast<uint32_t*>(q);
-    const unsigned long long pos = ((unsigned long long)e3.y << 32) | e3.x;
-    atomicMin(q, pos);
-    atomicMax(q + 1, pos);
-    if (result == 1) atomicOr(q32 + 7, 1u);  // inserted by this batch
-    if (e3.z & 0x10000u) {                   // Some(flags): history.push(map_tcp_flags(..))
-        atomicAdd(reinterpret_cast<uint32_t*>(s + 15), 1u);
-        const uint32_t b = hist_bit(e3.z & 0xFFu);
-        if (b < 16u) atomicOr(q32 + 6, 1u << b);
-        if (b < 8u) atomicMin(q32 + 8 + b, e3.y);
-        if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + 2, pos);
-    }
-#ifndef FB_NO_REC_FLOW
     if (rec_flow) rec_flow[e3.y] = slot_base + i;
+#ifdef FB_NO_ORDERED  // ablation: counters only
+    (void)scr;
+    return result;
 #endif
+    // ordered state into the batch scratch (see above)
+    uint32_t* q = scr + (size_t)i * kScrU32;
+    const uint32_t rec = e3.y;
+    atomicMin(q + kScFirst, rec);
+    atomicMax(q + kScLast, rec);
+    if (result == 1) atomicOr(q + kScMask, 1u << 16);  // inserted by this batch
+    if (e3.z & 0x10000u) {                              // Some(flags): history.push(map_tcp_flags(..))
+        atomicAdd(q + kScCount, 1u);
+        const uint32_t b = hist_bit(e3.z & 0xFFu);
+        if (b < 16u) atomicOr(q + kScMask, 1u << b);
+        if (b < 4u) atomicMin(q + kScChar + b, rec);
+        if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + kScEnd, rec);
+    }
     return result;
 }
 
-// Fold one slot's batch scratch into its ordered state (after every entry was applied).
-__device__ __forceinline__ void finish_slot(unsigned long long* s, const unsigned long long* q, uint32_t batch) {
-    const unsigned long long first = q[0];
-    if (first == ~0ull) return;  // not touched by this batch
-    const uint32_t* q32 = reinterpret_cast<const uint32_t*>(q);
+// Fold one slot's batch scratch into its ordered fields in HBM (after every entry was applied).
+__device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, const fb_pkt_out* recs, uint32_t batch) {
+    const uint32_t first = q[kScFirst];
+    if (first == ~0u) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
-    if (q32[7] & 1u) {  // new flow: start_time = its first packet, end_time None
-        s[12] = hi | (uint32_t)first;
-        s[14] = FB_SEEN_NONE;
+    auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
+    };
+    const uint32_t flags = q[kScMask];
+    unsigned long long end_seen;
+    uint32_t state, len;
+    if (flags & (1u << 16)) {  // new flow: start_time = its first packet, end_time None
+        g->first_seen = hi | rec_word(first).y;
+        end_seen = FB_SEEN_NONE;
+        state = 0u;
+        len = 0u;
+    } else {
+        end_seen = g->end_seen;
+        state = g->hist_state;
+        len = g->hist_len;
     }
-    s[13] = hi | (uint32_t)q[1];
-    uint32_t* st = reinterpret_cast<uint32_t*>(s + 15) + 1;
-    const uint32_t old = *st;
-    const uint32_t mask = old & 0xFFFFu;
-    uint32_t cs = old >> 16;
-    const unsigned long long end = q[2];
-    if (end != ~0ull && s[14] == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
-        const uint32_t end_rec = (uint32_t)(end >> 32);
-        uint32_t m = mask;
+    g->last_seen = hi | rec_word(q[kScLast]).y;
+    const uint32_t mask = state & 0xFFFFu;
+    uint32_t cs = state >> 16;
+    const uint32_t end = q[kScEnd];
+    if (end != ~0u && end_seen == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
+        const uint2 w = rec_word(end);
+        uint32_t m = mask | (1u << hist_bit((w.x >> 16) & 0xFFu));
 #pragma unroll
-        for (uint32_t b = 0; b < 8u; ++b) m |= q32[8 + b] <= end_rec ? 1u << b : 0u;
+        for (uint32_t b = 0; b < 4u; ++b) m |= q[kScChar + b] <= end ? 1u << b : 0u;
         cs = conn_state_of(m) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
-        s[14] = hi | (uint32_t)end;
+        end_seen = hi | w.y;
     }
-    *st = (mask | q32[6]) | (cs << 16);
+    g->end_seen = end_seen;
+    g->hist_len = len + q[kScCount];
+    g->hist_state = (mask | (flags & 0xFFFFu)) | (cs << 16);
 }
 
 __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams P) {
-    extern __shared__ uint4 slice4[];  // kFlowSlots 128-B slots, then kFlowSlots 64-B scratch
+    extern __shared__ uint4 slice4[];  // kFlowSlots 96-B slot heads, then kFlowSlots 40-B scratch
     __shared__ uint32_t sp[kFlowK2Threads];
     __shared__ uint32_t ss[kFlowK2Threads];
     __shared__ uint32_t wsum[kFlowK2Threads / 64];
     __shared__ unsigned long long sh[kFlowK2Threads / 64];
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
-    unsigned long long* scr = slice + (size_t)kFlowSlots * kSlotWords;
+    uint32_t* scr = reinterpret_cast<uint32_t*>(slice + (size_t)kFlowSlots * kSlotWords);
     const uint32_t part = blockIdx.x;
     const uint32_t n = batch_records(P);
     const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
@@ -340,15 +361,16 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
     if (total != 0ull) {
-        constexpr uint32_t kSlice16 = kFlowSlots * sizeof(FlowSlot) / 16u;
-        const uint4* g = reinterpret_cast<const uint4*>(P.table + (size_t)part * kFlowSlots);
-        for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) slice4[j] = g[j];
-        for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads) {
-            uint4* q = slice4 + kSlice16 + (size_t)j * (kScrWords / 2);
-            q[0] = make_uint4(~0u, ~0u, 0u, 0u);    // first = none, last = 0
-            q[1] = make_uint4(~0u, ~0u, 0u, 0u);    // end = none, character mask, flags
-            q[2] = make_uint4(~0u, ~0u, ~0u, ~0u);  // first rec of S s H h
-            q[3] = make_uint4(~0u, ~0u, ~0u, ~0u);  //                F f R r
+        constexpr uint32_t kHead16 = kSlotWords * 8u / 16u;  // 6 uint4 per slot head
+        FlowSlot* T = P.table + (size_t)part * kFlowSlots;
+        const uint4* g = reinterpret_cast<const uint4*>(T);
+        for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
+            const uint32_t sl = j / kHead16, w = j - sl * kHead16;
+            slice4[j] = g[(size_t)sl * (sizeof(FlowSlot) / 16u) + w];
+        }
+        for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
+            const uint32_t w = j % kScrU32;
+            scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
         }
         __syncthreads();
         const uint4* E = reinterpret_cast<const uint4*>(P.entries);
@@ -393,10 +415,12 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
             __syncthreads();
         }
         for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads)
-            finish_slot(slice + (size_t)j * kSlotWords, scr + (size_t)j * kScrWords, P.batch);
-        __syncthreads();
-        uint4* gw = reinterpret_cast<uint4*>(P.table + (size_t)part * kFlowSlots);
-        for (uint32_t j = threadIdx.x; j < kSlice16; j += kFlowK2Threads) gw[j] = slice4[j];
+            finish_slot(T + j, scr + (size_t)j * kScrU32, P.recs, P.batch);
+        uint4* gw = reinterpret_cast<uint4*>(T);
+        for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
+            const uint32_t sl = j / kHead16, w = j - sl * kHead16;
+            gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
+        }
     }
     n_new = block_sum(n_new, sh);
     n_upd = block_sum(n_upd, sh);

@@ -134,7 +134,7 @@ constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacit
 constexpr uint32_t kFlowChunk = 16384;           // records per bucketing workgroup (K1)
 constexpr uint32_t kFlowK1Threads = 1024;
 #ifndef FB_K2_THREADS
-#define FB_K2_THREADS 1024  // 16 waves: the apply is latency-bound (256: 2.35 ms, 512: 1.64, 1024: 1.39 at C4)
+#define FB_K2_THREADS 512  // two 8-wave workgroups per CU (68 KiB LDS each): 1.26 ms for the C4 update vs 1.38 at one 16-wave workgroup
 #endif
 constexpr uint32_t kFlowK2Threads = FB_K2_THREADS;
 constexpr uint64_t kFlowMaxCapacity = (uint64_t)kFlowSlots * kFlowMaxParts;
