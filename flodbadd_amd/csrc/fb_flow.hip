@@ -140,7 +140,8 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         const uint4 c = *reinterpret_cast<const uint4*>(r + 8);  // key 8,9 | packet_length | ip_packet_length
         const uint2 m = *reinterpret_cast<const uint2*>(r + 12);  // flags | meta | hist_char, pkt_index
         const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-        const uint32_t d = atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+        const unsigned long long fh = flow_hash_words(key);
+        const uint32_t d = atomicAdd(&hist[part_of(fh, P.part_shift)], 1u);
         const uint32_t meta = (m.x >> 8) & 0xFFu;
         const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
         const uint32_t hinfo =
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         e[0] = a;
         e[1] = b;
         e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
-        e[3] = make_uint4(m.y, base + k, hinfo, 0u);
+        e[3] = make_uint4(m.y, base + k, hinfo, (uint32_t)fh);  // low hash word: K2's home slot + tag filter
     }
 }
 
@@ -237,14 +238,15 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
                                            uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    const unsigned long long h = flow_hash_words(key);
-    const unsigned long long want = h | 2ull;
+    // K1 hands over the low word of the key's hash: the home slot and a 32-bit tag filter (the
+    // 64-bit tag, hash | 2, is only computed to insert)
+    const uint32_t h32 = e3.w, want32 = h32 | 2u;
     const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
     const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
     const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
     const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
     const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
-    uint32_t i = (uint32_t)h & (kFlowSlots - 1u);
+    uint32_t i = h32 & (kFlowSlots - 1u);
     int result = -1;
     unsigned long long* s = nullptr;
     for (uint32_t probe = 0; probe < kFlowSlots; ++probe) {
@@ -258,7 +260,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
                 s[3] = kw2;
                 s[4] = kw3;
                 s[5] = kw4;
-                __hip_atomic_store(s, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(s, flow_hash_words(key) | 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 result = 1;
                 break;
             }
@@ -270,7 +272,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
             t = lds_ld(s);
             if (++spins > (1u << 22)) { atomicOr(err, 2u); return -1; }
         }
-        if (t == want && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) {
+        if ((uint32_t)t == want32 && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) {
             result = 0;
             break;
         }

@@ -150,8 +150,8 @@ struct FlowSlot {
 static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
 // word 9 (the key's padding), L4 payload bytes, IP bytes, then the record's pkt_index, its
-// record slot (the batch order K2 orders the history by) and hist_char | tcp_flags << 8 |
-// has_flags << 16.
+// record slot (the batch order K2 orders the history by), hist_char | tcp_flags << 8 |
+// has_flags << 16, and the low word of the key's hash.
 struct FlowEntry {
     uint32_t key[10];
     uint32_t packet_length;
@@ -159,7 +159,7 @@ struct FlowEntry {
     uint32_t pkt_index;
     uint32_t rec;
     uint32_t hist;
-    uint32_t pad;
+    uint32_t hash_lo;  // low word of fb_flow_hash(key)
 };
 static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 
