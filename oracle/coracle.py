@@ -51,6 +51,7 @@ def lib():
         L.orc_blacklist_mask.restype = U64
         L.orc_blacklist_mask.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.orc_enrich_keys.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P]
+        L.orc_parse_classify_mt.argtypes = [P, P, U64, P, U32, P, P, P, P, P, C.c_int]
         L.orc_dns_parse.restype = C.c_uint32
         L.orc_dns_parse.argtypes = [P, C.c_uint32, C.c_uint32, P, C.c_char_p, P]
         L.orc_flows_new.restype = P

@@ -858,3 +858,47 @@ uint32_t orc_dns_parse(const uint8_t* payload, uint32_t len, uint32_t pkt_index,
     r->n_addrs = (uint8_t)na;
     return FB_DNS_OK;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * All-cores CPU baseline: the batch split into `threads` contiguous ranges,
+ * each parsed + classified by orc_parse_classify into a thread-local region, then compacted into
+ * packet order.  Same outputs as one orc_parse_classify over the batch (checked in tests).
+ * ------------------------------------------------------------------------------------- */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+int orc_parse_classify_mt(const orc_cfg* c, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
+                          uint32_t n, fb_pkt_out* out, uint32_t* n_out, fb_dns_out* dns, uint32_t* n_dns,
+                          fb_batch_stats* st, int threads) {
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n) threads = n ? (int)n : 1;
+    uint32_t cs[256], cd[256];
+    fb_batch_stats ts[256];
+    if (threads > 256) threads = 256;
+#pragma omp parallel for num_threads(threads) schedule(static, 1)
+    for (int t = 0; t < threads; ++t) {
+        const uint32_t a = (uint32_t)((uint64_t)n * t / threads), b = (uint32_t)((uint64_t)n * (t + 1) / threads);
+        /* frames [a, b): offsets stay absolute, pkt_index relative -> fixed below */
+        orc_parse_classify(c, frames, frames_bytes, offsets + a, b - a, out + a, &cs[t], dns + a, &cd[t], NULL, &ts[t]);
+        for (uint32_t k = 0; k < cs[t]; ++k) out[a + k].pkt_index += a;
+        for (uint32_t k = 0; k < cd[t]; ++k) dns[a + k].pkt_index += a;
+    }
+    /* compaction into packet order + stats merge */
+    uint32_t so = 0, sd = 0;
+    fb_batch_stats m;
+    memset(&m, 0, sizeof(m));
+    for (int t = 0; t < threads; ++t) {
+        const uint32_t a = (uint32_t)((uint64_t)n * t / threads);
+        if (so != a) memmove(out + so, out + a, (size_t)cs[t] * sizeof(fb_pkt_out));
+        if (sd != a) memmove(dns + sd, dns + a, (size_t)cd[t] * sizeof(fb_dns_out));
+        so += cs[t];
+        sd += cd[t];
+        uint64_t* dst = (uint64_t*)&m;
+        const uint64_t* src = (const uint64_t*)&ts[t];
+        for (size_t k = 0; k < sizeof(m) / 8; ++k) dst[k] += src[k];
+    }
+    if (n_out) *n_out = so;
+    if (n_dns) *n_dns = sd;
+    if (st) *st = m;
+    return 0;
+}

@@ -105,6 +105,11 @@ void orc_enrich_keys(const orc_cfg* c, const fb_asn_range* a4, uint32_t n4, cons
                      const fb_cidr* nets, uint32_t nn, const fb_session_key* keys, uint32_t nk,
                      fb_flow_enrich* out);
 
+/* All-cores baseline: `threads` contiguous ranges in parallel (OpenMP), compacted in packet order. */
+int orc_parse_classify_mt(const orc_cfg* cfg, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
+                          uint32_t n, fb_pkt_out* out, uint32_t* n_out, fb_dns_out* dns, uint32_t* n_dns,
+                          fb_batch_stats* stats, int threads);
+
 /* ---- DNS divert parse (dns-parser 0.8.0 Packet::parse restated; src/dns.rs:35-99) ---- */
 uint32_t orc_dns_parse(const uint8_t* payload, uint32_t len, uint32_t pkt_index, fb_dns_msg* r, char* name,
                        fb_ip* addrs);
