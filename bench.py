@@ -39,7 +39,8 @@ def algorithmic_bytes(offsets, n_session, n_dns):
     return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
 
 
-def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1):
+def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1,
+               synth_kw=None):
     """Time `steps` launches of the hot path.  mode "seg": fb_parse_classify_seg_dev (records
     compacted per 64-frame wavefront segment, no cross-workgroup dependency); mode "dense":
     fb_parse_classify_dev (one batch-wide compaction through a decoupled look-back).
@@ -50,7 +51,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     one batch = one step, each with its own outputs and stats), so `steps` steps take
     ceil(steps / bpl) launches."""
     from flodbadd_amd import synth
-    frames, offs = synth.generate(config_id, n, first=rank * n)
+    frames, offs = synth.generate(config_id, n, first=rank * n, **(synth_kw or {}))
     nbytes = frames.nbytes
     stream = N.Stream()
     nseg = (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES
@@ -480,6 +481,14 @@ def main():
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
+    if args.config == 4 and not args.no_other_mode:  # C4 also with Zipf(1.1) flow popularity
+        rz = run_config(N, lib, ctx, 4, n, max(args.steps // 2, 5), max(args.warmup // 2, 2), rotate, rank, world,
+                        dist, flow=True, mode=args.mode, synth_kw=dict(zipf=1, zipf_s=1.1))
+        sz = rz["stage"]
+        extra["c4_zipf"] = dict(value=round(world * n * max(args.steps // 2, 5) / rz["elapsed"] / 1e6, 2),
+                                unit="Mpackets/s", parse_ms=round(sz["parse_ms"], 4),
+                                flow_update_ms=round(sz["flow_ms"], 4), flows_in_table=sz["flows"],
+                                history_ms=round(sz["history_ms"], 4))
     if bpl > 1 and not args.no_single_launch:  # the same workload with one batch per launch
         st_1 = max(args.steps // 2, 10)
         r1 = run_config(N, lib, ctx, args.config, n, st_1, max(args.warmup // 2, 2), rotate, rank, world, dist,
