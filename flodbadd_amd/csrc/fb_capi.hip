@@ -61,6 +61,9 @@ struct fb_ctx {
     // ordered per-flow state: update calls since create/clear, table slot of each record slot
     uint32_t flow_batch = 0;
     uint32_t* d_rec_flow = nullptr;       // [flow_recs]
+    uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
+    uint32_t* d_comb_ctl = nullptr;       // [2] its counters
+    uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
     // the last update, for fb_flow_history_dev
     const fb_pkt_out* last_recs = nullptr;
     const uint32_t* last_seg = nullptr;
@@ -136,17 +139,23 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_rows);
     hipFree(c->d_cols);
     hipFree(c->d_rec_flow);
+    hipFree(c->d_hot);
+    hipFree(c->d_comb_ctl);
+    hipFree(c->d_agg_slot);
     c->d_entries = nullptr;
     c->d_rows = c->d_cols = nullptr;
-    c->d_rec_flow = nullptr;
+    c->d_rec_flow = c->d_hot = c->d_comb_ctl = c->d_agg_slot = nullptr;
     c->last_recs = nullptr;  // its rec_flow is gone
     c->flow_recs = 0;
     const uint64_t chunks = recs / kFlowChunk;
     if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
         hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess)
+        hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&c->d_comb_ctl, 8) != hipSuccess ||
+        hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
+    HIP_TRY(hipMemsetAsync(c->d_comb_ctl, 0, 8, s));
     c->flow_recs = recs;
     return FB_OK;
 }
@@ -309,6 +318,9 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_partials);
     hipFree(c->d_n);
     hipFree(c->d_rec_flow);
+    hipFree(c->d_hot);
+    hipFree(c->d_comb_ctl);
+    hipFree(c->d_agg_slot);
     hipFree(c->d_asn4);
     hipFree(c->d_asn6);
     hipFree(c->d_bl4_pos);
@@ -700,6 +712,10 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
     p.rec_flow = c->d_rec_flow;
+    p.hot = c->d_hot;
+    p.ctl = c->d_comb_ctl;
+    p.agg_slot = c->d_agg_slot;
+    p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     HIP_TRY(launch_flow_update(p, chunks, s));
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
     ++c->flow_batch;
@@ -777,6 +793,7 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     p.seg = c->last_seg;
     p.stats = c->last_stats;
     p.rec_flow = c->d_rec_flow;
+    p.agg_slot = c->d_agg_slot;
     p.n_slots = n;
     p.sentinel = (uint32_t)c->table_cap;
     p.keys = c->d_hkeys;

@@ -14,6 +14,8 @@
 //                       records' partitions, exclusive scan, then a counting-sort scatter of
 //                       64-B FlowEntry items into the chunk's region of `entries` (partition-
 //                       major inside the chunk); row b of `rows` = (start, count) per partition.
+//   K1c k_flow_combine  the hot (chunk, partition) groups K1 listed are reduced per key in place
+//                       (skewed popularity: one hot flow would otherwise run through one CU).
 //   K1t k_flow_transpose rows[chunk][part] -> cols[part][chunk] (so K2 reads its column
 //                       contiguously).
 //   K2 k_flow_apply     one workgroup per partition: loads the partition's 64-KiB slice into
@@ -92,6 +94,10 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
     return !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
 }
 
+// A (chunk, partition) group of at least this many records (and 4x the chunk's mean) is combined
+// per key by k_flow_combine before K2.
+constexpr uint32_t kCombMin = 24;
+
 // ---------------------------------------------------------------------------------------------
 // K1: bucket one chunk of records by partition (counting sort in LDS).
 __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams P) {
@@ -124,9 +130,14 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     uint32_t total;
     uint32_t run = block_excl_scan(local, wsum, total);
     uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
+    const uint32_t hot_min = max(kCombMin, 4u * ((cnt + P.parts - 1u) / P.parts));
     for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
         const uint32_t c = hist[j];
         row[j] = run | (c << 16);
+        if (c >= hot_min && P.hot) {  // hand the group to k_flow_combine
+            const uint32_t h = atomicAdd(P.ctl, 1u);
+            if (h < P.hot_cap) P.hot[h] = blockIdx.x << 13 | j;
+        }
         hist[j] = run;  // becomes the scatter cursor
         run += c;
     }
@@ -160,6 +171,10 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
     __shared__ uint32_t tile[64][65];
     const uint32_t p0 = blockIdx.x * 64u, c0 = blockIdx.y * 64u;
     const uint32_t tx = threadIdx.x & 63u, ty = threadIdx.x >> 6;
+    if (P.ctl && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // k_flow_combine is done with them
+        P.ctl[0] = 0u;
+        P.ctl[1] = 0u;
+    }
     for (uint32_t y = ty; y < 64u; y += 4u) {
         const uint32_t c = c0 + y, p = p0 + tx;
         tile[y][tx] = (c < chunks && p < P.parts) ? P.rows[(size_t)c * P.parts + p] : 0u;
@@ -232,25 +247,24 @@ __device__ __forceinline__ uint32_t conn_state_of(uint32_t m) {
     return FB_CONN_OTHER;
 }
 
-// Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
-__device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
-                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* rec_flow,
-                                           uint32_t* err) {
-    const uint32_t orig = (e2.y >> 16) & 1u;
-    const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    // K1 hands over the low word of the key's hash: the home slot and a 32-bit tag filter (the
-    // 64-bit tag, hash | 2, is only computed to insert)
-    const uint32_t h32 = e3.w, want32 = h32 | 2u;
+// Find or insert `key` in an LDS open-addressing table of kSlots slots of kStride u64 words
+// (tag: 0 empty, 1 being inserted, hash | 2; then the 5 key words), home slot h32 & (kSlots-1).
+// h32 = the low word of the key's hash, handed over by K1: home slot and a 32-bit tag filter
+// (the 64-bit tag is only computed to insert).  Returns 1 inserted, 0 found (*slot set),
+// -1 table full, -2 spin expired.
+template <uint32_t kStride, uint32_t kSlots>
+__device__ __forceinline__ int lds_upsert(unsigned long long* tab, const uint32_t key[10], uint32_t h32,
+                                          uint32_t& slot) {
+    const uint32_t want32 = h32 | 2u;
     const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
     const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
     const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
     const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
     const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
-    uint32_t i = h32 & (kFlowSlots - 1u);
+    uint32_t i = h32 & (kSlots - 1u);
     int result = -1;
-    unsigned long long* s = nullptr;
-    for (uint32_t probe = 0; probe < kFlowSlots; ++probe) {
-        s = slice + (size_t)i * kSlotWords;
+    for (uint32_t probe = 0; probe < kSlots; ++probe) {
+        unsigned long long* s = tab + (size_t)i * kStride;
         unsigned long long t = lds_ld(s);
         if (t == 0ull) {
             const unsigned long long old = atomicCAS(s, 0ull, 1ull);
@@ -270,18 +284,52 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
         while (t == 1ull) {  // another lane of this workgroup is publishing the slot's key
             __builtin_amdgcn_s_sleep(1);
             t = lds_ld(s);
-            if (++spins > (1u << 22)) { atomicOr(err, 2u); return -1; }
+            if (++spins > (1u << 22)) return -2;
         }
         if ((uint32_t)t == want32 && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) {
             result = 0;
             break;
         }
-        i = (i + 1u) & (kFlowSlots - 1u);
+        i = (i + 1u) & (kSlots - 1u);
     }
+    slot = i;
+    return result;
+}
+
+// Lookup only (no concurrent inserts): the slot of `key`, or ~0u.
+template <uint32_t kStride, uint32_t kSlots>
+__device__ __forceinline__ uint32_t lds_find(const unsigned long long* tab, const uint32_t key[10], uint32_t h32) {
+    const uint32_t want32 = h32 | 2u;
+    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
+    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
+    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
+    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
+    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
+    uint32_t i = h32 & (kSlots - 1u);
+    for (uint32_t probe = 0; probe < kSlots; ++probe) {
+        const unsigned long long* s = tab + (size_t)i * kStride;
+        const unsigned long long t = s[0];
+        if (t == 0ull) return ~0u;
+        if ((uint32_t)t == want32 && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4)
+            return i;
+        i = (i + 1u) & (kSlots - 1u);
+    }
+    return ~0u;
+}
+
+// Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
+__device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
+                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* rec_flow,
+                                           uint32_t* err) {
+    const uint32_t orig = (e2.y >> 16) & 1u;
+    const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
+    uint32_t i;
+    const int result = lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
     if (result < 0) {
-        atomicOr(err, 4u);  // partition full
+        atomicOr(err, result == -2 ? 2u : 4u);  // spin expired / partition full
         return -1;
     }
+    unsigned long long* s = slice + (size_t)i * kSlotWords;
     // originator -> outbound_bytes/orig_pkts/orig_ip_bytes, else inbound/resp (packets.rs:111-120)
     atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
     atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
@@ -303,6 +351,55 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
         if (b < 16u) atomicOr(q + kScMask, 1u << b);
         if (b < 4u) atomicMin(q + kScChar + b, rec);
         if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + kScEnd, rec);
+    }
+    return result;
+}
+
+// A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
+// the group's partial sums / minima / maxima.  Its records' rec_flow point at agg_slot[id].
+__device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
+                                              const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
+                                              const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
+                                              uint32_t* err) {
+    const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
+    uint32_t i;
+    const int result = lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
+    if (result < 0) {
+        atomicOr(err, result == -2 ? 2u : 4u);
+        return -1;
+    }
+    unsigned long long* s = slice + (size_t)i * kSlotWords;
+    const unsigned long long ob = t0.x | ((unsigned long long)t0.y << 32), ib = t0.z | ((unsigned long long)t0.w << 32);
+    const unsigned long long oi = t1.x | ((unsigned long long)t1.y << 32), ri = t1.z | ((unsigned long long)t1.w << 32);
+    const uint32_t op = t2.x & 0xFFFFu, rp = t2.x >> 16;
+    if (op) {
+        atomicAdd(s + 6, ob);
+        atomicAdd(s + 8, (unsigned long long)op);
+        atomicAdd(s + 10, oi);
+    }
+    if (rp) {
+        atomicAdd(s + 7, ib);
+        atomicAdd(s + 9, (unsigned long long)rp);
+        atomicAdd(s + 11, ri);
+    }
+    if (agg_slot) agg_slot[e3.x] = slot_base + i;
+#ifdef FB_NO_ORDERED
+    (void)scr;
+    return result;
+#endif
+    uint32_t* q = scr + (size_t)i * kScrU32;
+    atomicMin(q + kScFirst, e2.z);
+    atomicMax(q + kScLast, e2.w);
+    const uint32_t hc = e3.z & 0xFFFFu;
+    const uint32_t m = (e3.z >> 16) | (result == 1 ? 1u << 16 : 0u);
+    if (m) atomicOr(q + kScMask, m);
+    if (hc) {
+        atomicAdd(q + kScCount, hc);
+        const uint32_t c[4] = {t2.z, t2.w, t3.x, t3.y};
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b)
+            if (c[b] != ~0u) atomicMin(q + kScChar + b, c[b]);
+        if (e3.y != ~0u) atomicMin(q + kScEnd, e3.y);
     }
     return result;
 }
@@ -345,7 +442,143 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
     g->hist_state = (mask | (flags & 0xFFFFu)) | (cs << 16);
 }
 
-__global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams P) {
+// ---------------------------------------------------------------------------------------------
+// K1c: combine the records of one key inside the hot (chunk, partition) groups K1 listed.
+//
+// With skewed flow popularity one partition can hold a large share of a batch (Zipf(1.1): the
+// hottest flow carries ~12 % of the records), and K2 gives a partition to ONE workgroup.  Here
+// every hot group (>= kCombMin records and >= 4x the chunk's mean) is reduced per key in LDS by
+// its own workgroup, spread over the whole chip, and rewritten in place: the records of keys met
+// once stay as they are, packed to the front; each key met more than once becomes one combined
+// entry (two units) behind them; the group's row count shrinks accordingly.  The partial sums are
+// the same integer sums / minima / maxima K2 computes, so the result is bit-identical.
+constexpr uint32_t kCombSlots = 512;     // a valid partition holds <= kFlowSlots keys
+constexpr uint32_t kCombThreads = 256;
+constexpr uint32_t kCombGrid = 512;
+constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
+                   kCfRecs = 10, kCfId = 11, kCfHash = 12, kCombF = 13;  // u32 fields of a key (kCfChar..+3)
+struct CombLds {
+    unsigned long long tab[kCombSlots * 6];    // tag + key words (lds_upsert layout)
+    unsigned long long bytes[kCombSlots * 4];  // outbound, inbound, orig ip, resp ip
+    uint32_t f[kCombSlots * kCombF];
+    uint32_t wsum[kCombThreads / 64];
+    uint32_t base;
+};
+
+__global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
+    __shared__ CombLds L;
+    const uint32_t n_hot = min(P.ctl[0], P.hot_cap);
+    uint4* E = reinterpret_cast<uint4*>(P.entries);
+    for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
+        const uint32_t grp = P.hot[h], chunk = grp >> 13, part = grp & 8191u;
+        uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
+        const uint32_t row = *rowp, cnt = row >> 16;
+        const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
+        for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
+            L.tab[j * 6] = 0ull;
+#pragma unroll
+            for (uint32_t w = 0; w < 4u; ++w) L.bytes[j * 4 + w] = 0ull;
+#pragma unroll
+            for (uint32_t w = 0; w < kCombF; ++w)
+                L.f[j * kCombF + w] = (w == kCfFirst || w == kCfEnd || (w >= kCfChar && w < kCfChar + 4)) ? ~0u : 0u;
+        }
+        __syncthreads();
+        // reduce per key (a key the table cannot take stays a plain entry)
+        for (uint32_t k = threadIdx.x; k < cnt; k += kCombThreads) {
+            const uint4* e = E + (s0 + k) * 4u;
+            const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+            const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
+            uint32_t j;
+            if (lds_upsert<6, kCombSlots>(L.tab, key, e3.w, j) < 0) continue;
+            const uint32_t orig = (e2.y >> 16) & 1u, rec = e3.y;
+            uint32_t* f = L.f + j * kCombF;
+            atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e2.z);
+            atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e2.w);
+            atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
+            atomicAdd(f + kCfRecs, 1u);
+            f[kCfHash] = e3.w;  // every lane of the key stores the same word
+            atomicMin(f + kCfFirst, rec);
+            atomicMax(f + kCfLast, rec);
+            if (e3.z & 0x10000u) {
+                atomicAdd(f + kCfHcnt, 1u);
+                const uint32_t b = hist_bit(e3.z & 0xFFu);
+                if (b < 16u) atomicOr(f + kCfMask, 1u << b);
+                if (b < 4u) atomicMin(f + kCfChar + b, rec);
+                if ((e3.z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec);
+            }
+        }
+        __syncthreads();
+        // number the keys met more than once; one global atomic per group for their ids
+        constexpr uint32_t kPer = kCombSlots / kCombThreads;
+        uint32_t nc = 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) nc += L.f[(threadIdx.x * kPer + u) * kCombF + kCfRecs] >= 2u;
+        uint32_t n_comb;
+        uint32_t rank = block_excl_scan(nc, L.wsum, n_comb);
+        if (n_comb == 0u) continue;  // uniform across the block; the table is re-initialised above
+        if (threadIdx.x == 0) L.base = atomicAdd(P.ctl + 1, n_comb);
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+            uint32_t* f = L.f + (threadIdx.x * kPer + u) * kCombF;
+            if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
+        }
+        __syncthreads();
+        const uint32_t id0 = L.base;
+        // pack the remaining plain entries to the front, tile by tile (a tile is loaded before any
+        // of its stores, and stores land below the next tile)
+        uint32_t cursor = 0u;
+        for (uint32_t t = 0; t < cnt; t += kCombThreads) {
+            const uint32_t k = t + threadIdx.x;
+            uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+            uint32_t keep = 0u;
+            if (k < cnt) {
+                const uint4* e = E + (s0 + k) * 4u;
+                q0 = e[0];
+                q1 = e[1];
+                q2 = e[2];
+                q3 = e[3];
+                const uint32_t key[10] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y & 0xFFFFu};
+                const uint32_t j = lds_find<6, kCombSlots>(L.tab, key, q3.w);
+                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u)
+                    P.rec_flow[q3.y] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                else
+                    keep = 1u;
+            }
+            uint32_t kept;
+            const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
+            if (keep) {
+                uint4* o = E + (s0 + cursor + pos) * 4u;
+                o[0] = q0;
+                o[1] = q1;
+                o[2] = q2;
+                o[3] = q3;
+            }
+            cursor += kept;
+        }
+        // the combined entries behind them
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+            const uint32_t j = threadIdx.x * kPer + u;
+            const uint32_t* f = L.f + j * kCombF;
+            if (f[kCfRecs] < 2u) continue;
+            const unsigned long long* tw = L.tab + j * 6;
+            const unsigned long long* by = L.bytes + j * 4;
+            uint4* o = E + (s0 + cursor + 2u * f[kCfId]) * 4u;
+            o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
+            o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
+            o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
+            o[3] = make_uint4(id0 + f[kCfId], f[kCfEnd], f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
+            o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
+            o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
+            o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
+            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], 0u);
+        }
+        if (threadIdx.x == 0) *rowp = (row & 0xFFFFu) | ((cursor + 2u * n_comb) << 16);
+        __syncthreads();  // the table is re-initialised for the next group
+    }
+}
+
+__global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_flow_apply(const FlowParams P) {
     extern __shared__ uint4 slice4[];  // kFlowSlots 96-B slot heads, then kFlowSlots 40-B scratch
     __shared__ uint32_t sp[kFlowK2Threads];
     __shared__ uint32_t ss[kFlowK2Threads];
@@ -386,6 +619,7 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
             __syncthreads();
             for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 4u * kFlowK2Threads) {
                 uint4 q[4][4];
+                uint32_t ix[4];
                 uint32_t ne = 0u;
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; ++u) {
@@ -396,17 +630,28 @@ __global__ __launch_bounds__(kFlowK2Threads) void k_flow_apply(const FlowParams 
                             const uint32_t mid = (lo + hi + 1u) >> 1;
                             if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
                         }
-                        const size_t idx = (size_t)ss[lo] + (e - sp[lo]);
-                        q[u][0] = E[idx * 4u];
-                        q[u][1] = E[idx * 4u + 1u];
-                        q[u][2] = E[idx * 4u + 2u];
-                        q[u][3] = E[idx * 4u + 3u];
+                        const uint32_t idx = ss[lo] + (e - sp[lo]);
+                        ix[u] = idx;
+                        q[u][0] = E[(size_t)idx * 4u];
+                        q[u][1] = E[(size_t)idx * 4u + 1u];
+                        q[u][2] = E[(size_t)idx * 4u + 2u];
+                        q[u][3] = E[(size_t)idx * 4u + 3u];
                         ne = u + 1u;
                     }
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; ++u) {
-                    if (u < ne) {
+                    if (u >= ne || (q[u][2].y & kEntTail)) continue;  // second unit of a combined entry
+                    if (q[u][2].y & kEntCombined) {
+                        const uint4* t = E + ((size_t)ix[u] + 1u) * 4u;
+                        const uint4 t3 = t[3];
+                        const int r = apply_combined(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3], t[0], t[1],
+                                                     t[2], t3, part * kFlowSlots, P.agg_slot, P.error);
+                        if (r >= 0) {
+                            n_new += r == 1;
+                            n_upd += t3.z - (r == 1 ? 1u : 0u);
+                        }
+                    } else {
                         const int r = apply_entry(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3],
                                                   part * kFlowSlots, P.rec_flow, P.error);
                         n_new += r == 1;
@@ -509,6 +754,11 @@ hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t 
     hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), p.parts * sizeof(uint32_t), s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (p.hot) {
+        hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_flow_transpose, dim3((p.parts + 63u) / 64u, (chunks + 63u) / 64u), dim3(256), 0, s, p,
                        chunks);
     e = hipGetLastError();

@@ -32,7 +32,12 @@ __global__ __launch_bounds__(256) void k_hist_keys(const HistParams P) {
             keyed = ((w >> 8) & FB_META_HAS_FLAGS) != 0u;
             ch = (w >> 16) & 0xFFu;
         }
-        P.keys[i] = keyed ? P.rec_flow[i] : P.sentinel;
+        uint32_t slot = P.sentinel;
+        if (keyed) {
+            slot = P.rec_flow[i];
+            if (slot & kRecFlowCombined) slot = P.agg_slot[slot & ~kRecFlowCombined];  // k_flow_combine
+        }
+        P.keys[i] = slot;
         P.vals[i] = (uint8_t)ch;
         cnt += keyed;
     }

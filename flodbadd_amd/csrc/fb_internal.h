@@ -162,6 +162,14 @@ struct FlowEntry {
     uint32_t hash_lo;  // low word of fb_flow_hash(key)
 };
 static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
+// A combined entry (k_flow_combine: the records of one key in one hot bucketing group) takes two
+// consecutive FlowEntry units.  Head: key[0..8], key[9] | kEntCombined, first rec, last rec,
+// combined id, end rec (first FIN/RST, ~0 none), hist count | hist mask << 16, hash_lo.  Tail:
+// outbound, inbound, orig ip, resp ip bytes (u64), orig | resp pkts << 16, kEntTail, first rec
+// of S s H h (~0 none), records, 0.
+constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the originator)
+constexpr uint32_t kEntTail = 1u << 18;
+constexpr uint32_t kRecFlowCombined = 0x80000000u;  // rec_flow value: combined id, slot in agg_slot
 
 struct FlowParams {
     const fb_pkt_out* recs;
@@ -181,6 +189,10 @@ struct FlowParams {
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
     uint32_t batch;             // update call number since create / clear (positions' high word)
     uint32_t* rec_flow;         // [max_recs] table slot of each record slot (for the history)
+    uint32_t* hot;              // [hot_cap] (chunk << 13 | part) groups K1 hands to k_flow_combine
+    uint32_t* ctl;              // [2] hot groups, combined entries (reset by K1t)
+    uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
+    uint32_t hot_cap;
 };
 
 // Launchers (fb_parse.hip / fb_flow.hip).
@@ -206,7 +218,9 @@ struct HistParams {
     const fb_pkt_out* recs;     // the update's records (dense or segmented)
     const uint32_t* seg;        // segmented: record slot i valid iff (i & 63) < (seg[i >> 6] & 0xFFFF)
     const fb_batch_stats* stats;  // dense: n_session read here
-    const uint32_t* rec_flow;   // table slot of each record slot (k_flow_apply)
+    const uint32_t* rec_flow;   // table slot of each record slot (k_flow_apply), or
+                                // kRecFlowCombined | combined id
+    const uint32_t* agg_slot;   // table slot of each combined entry
     uint32_t n_slots;           // record slots of the update
     uint32_t sentinel;          // key of the records that are not sorted in (= table capacity)
     uint32_t* keys;             // [n_slots] scratch

@@ -771,10 +771,10 @@ __global__ __launch_bounds__(kWsThreads) void k_parse_ws(const ParseParams P) {
 // outputs and stats.  Batch stats: packed per-batch device words, see the end of the kernel.
 // ============================================================================================
 #ifndef FB_SEG_WAVES
-#define FB_SEG_WAVES 16
+#define FB_SEG_WAVES 8
 #endif
 #ifndef FB_SEG_BPC
-#define FB_SEG_BPC 1
+#define FB_SEG_BPC 3
 #endif
 #ifndef FB_SEG_DEPTH
 #define FB_SEG_DEPTH 1

@@ -123,3 +123,33 @@ def test_history_buffer_contract(gpu_capture):
     d_n = N.DeviceBuffer(4)
     N.check(N.gpu_lib().fb_flow_history_dev(gpu_capture.ctx, None, None, d_n.ptr, None))
     assert int(d_n.download(np.zeros(1, dtype=np.uint32))[0]) == 0
+
+
+@pytest.mark.parametrize("seg", [False, True], ids=["dense", "seg"])
+def test_history_hot_flows_combined(seg):
+    """Hot (chunk, partition) groups are combined per key before the apply (k_flow_combine):
+    four flows carry most of each batch with random TCP flags in both directions (S, SA, A, PA,
+    F, R ... so first S/s/H/h, the first FIN/RST and conn_state all come out of partial
+    reductions), interleaved with cold flows, a small table (many keys per partition) and three
+    batches so the ordered state also spans updates."""
+    import random
+    rnd = random.Random(7)
+    hot = [("10.0.0.%d" % (i + 1), 40000 + i, "93.184.216.%d" % (i + 1), 443) for i in range(4)]
+    flag_set = [fg.SYN, fg.SYN | fg.ACK, fg.ACK, fg.ACK | fg.PSH, fg.FIN | fg.ACK, fg.RST, fg.RST | fg.ACK, 0]
+    batches = []
+    for b in range(3):
+        frames = []
+        for k in range(40000):
+            if rnd.random() < 0.8:
+                s, sp, d, dp = hot[rnd.randrange(4)]
+                fl = rnd.choices(flag_set, weights=[1, 1, 60, 30, 1, 0.5, 0.5, 1])[0]
+                if rnd.random() < 0.5:
+                    s, sp, d, dp = d, dp, s, sp
+                frames.append(fg.tcp_frame(s, sp, d, dp, fl, rnd.randrange(64)))
+            else:
+                c = rnd.randrange(3000)
+                frames.append(fg.tcp_frame("172.16.%d.%d" % (c >> 8, c & 255), 1024 + c, "8.8.4.4", 53 + 1 + c % 7,
+                                           rnd.choice(flag_set), 10))
+        batches.append(fg.pack(frames))
+    gf = _run(batches, seg=seg, capacity=1 << 14)
+    assert (gf["hist_len"] > 10000).sum() == 4
