@@ -432,6 +432,8 @@ def main():
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
                          "default = the rotated batches (C2 8, C3 4), 1 for C4")
+    ap.add_argument("--zipf", type=float, default=None,
+                    help="profiling: the main run with Zipf(s) flow popularity instead of uniform")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -464,7 +466,8 @@ def main():
     rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
     bpl = (args.batches_per_launch or rotate) if (args.mode == "seg" and args.config != 4) else 1
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
-                        flow=args.config == 4, mode=args.mode, bpl=bpl)
+                        flow=args.config == 4, mode=args.mode, bpl=bpl,
+                        synth_kw=dict(zipf=1, zipf_s=args.zipf) if args.zipf else None)
     # the dominant kernel's launches: algorithmic bytes per launch / average launch duration
     per_launch_s = main_r["ev_ms"] / 1e3 / main_r["launches"]
     algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
@@ -563,7 +566,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
-            "config": {"workload": WORKLOADS[args.config], "frames_per_gpu_per_step": n,
+            "config": {"workload": WORKLOADS[args.config] + (" (Zipf(%g) flow popularity)" % args.zipf if args.zipf else ""), "frames_per_gpu_per_step": n,
                        "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
                        "output": (("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
                                    "%d batches per launch, each with its own outputs and stats)" % bpl) if bpl > 1 else

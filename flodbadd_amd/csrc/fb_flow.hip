@@ -96,7 +96,10 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
 
 // A (chunk, partition) group of at least this many records (and 4x the chunk's mean) is combined
 // per key by k_flow_combine before K2.
-constexpr uint32_t kCombMin = 24;
+#ifndef FB_COMB_MIN
+#define FB_COMB_MIN 48
+#endif
+constexpr uint32_t kCombMin = FB_COMB_MIN;
 
 // ---------------------------------------------------------------------------------------------
 // K1: bucket one chunk of records by partition (counting sort in LDS).
@@ -452,9 +455,19 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
 // once stay as they are, packed to the front; each key met more than once becomes one combined
 // entry (two units) behind them; the group's row count shrinks accordingly.  The partial sums are
 // the same integer sums / minima / maxima K2 computes, so the result is bit-identical.
-constexpr uint32_t kCombSlots = 512;     // a valid partition holds <= kFlowSlots keys
+#ifndef FB_COMB_SLOTS
+#define FB_COMB_SLOTS 256
+#endif
+#ifndef FB_COMB_GRID
+#define FB_COMB_GRID 1024
+#endif
+// 256 keys (34 KiB of LDS, four workgroups per CU) x 1024 workgroups, groups >= 48 records: C4
+// Zipf update 1.39 ms, against 1.74 ms at 512 keys x 512 / >= 24 (fixed cost per group: table
+// init, barriers, the id atomic) and 1.50 ms at >= 48 with 512 keys (tools/sweep_comb.sh).
+constexpr uint32_t kCombSlots = FB_COMB_SLOTS;  // keys past a full table stay plain entries
 constexpr uint32_t kCombThreads = 256;
-constexpr uint32_t kCombGrid = 512;
+constexpr uint32_t kCombGrid = FB_COMB_GRID;
+static_assert(kCombSlots % kCombThreads == 0, "each thread numbers kCombSlots / kCombThreads keys");
 constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
                    kCfRecs = 10, kCfId = 11, kCfHash = 12, kCombF = 13;  // u32 fields of a key (kCfChar..+3)
 struct CombLds {
