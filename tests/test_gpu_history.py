@@ -153,3 +153,34 @@ def test_history_hot_flows_combined(seg):
         batches.append(fg.pack(frames))
     gf = _run(batches, seg=seg, capacity=1 << 14)
     assert (gf["hist_len"] > 10000).sum() == 4
+
+
+def test_history_combine_table_overflow():
+    """A hot group with more distinct keys than k_flow_combine's LDS table holds (256): 32
+    partitions, ~400 cold flows each and one hot flow at 12 % put ~270 keys into the hot
+    partition's group per chunk, so some keys stay plain entries beside the combined ones."""
+    import random
+    rnd = random.Random(11)
+    flag_set = [fg.SYN, fg.SYN | fg.ACK, fg.ACK, fg.ACK | fg.PSH, fg.FIN | fg.ACK, fg.RST]
+    batches = []
+    for b in range(2):
+        frames = []
+        for k in range(49152):
+            fl = rnd.choices(flag_set, weights=[1, 1, 60, 30, 1, 1])[0]
+            if rnd.random() < 0.12:
+                frames.append(fg.tcp_frame("10.9.8.7", 50000, "93.184.216.34", 443, fl, 20))
+            else:
+                c = rnd.randrange(13000)
+                frames.append(fg.tcp_frame("172.%d.%d.%d" % (16 + (c >> 16), (c >> 8) & 255, c & 255), 2000 + c % 50000,
+                                           "9.9.9.9", 443, fl, 5))
+        batches.append(fg.pack(frames))
+    # precondition (host-side hash): a hot group of the first batch holds > 256 distinct keys
+    lib = N.gpu_lib()
+    recs = coracle.parse_classify(coracle.make_cfg(2), *batches[0])[0]
+    groups = {}
+    for i in range(len(recs)):
+        h = lib.fb_flow_hash(N.ptr(recs[i: i + 1]))
+        groups.setdefault((i // 16384, h >> 59), []).append(recs[i: i + 1].tobytes()[:40])
+    assert max(len(set(v)) for v in groups.values() if len(v) >= 2048) > 256
+    gf = _run(batches, capacity=1 << 14)
+    assert (gf["hist_len"] > 10000).sum() == 1
