@@ -20,6 +20,7 @@
 namespace fbk {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Cache policy (buffer instruction aux bits) of the frame-header loads and the record stores.
 // Records are stored `nt` (aux 2): +2-3 % at C2 in interleaved A/B runs.  The header loads stay
@@ -57,10 +58,43 @@ __device__ __forceinline__ uint32_t hist_char(uint32_t fl, uint32_t plen, bool o
     return orig ? c : c + 32u;  // lower-case for the responder
 }
 
+// Header window of a frame at offset o.  The decoder wants f[10..57] and f[66..69] as dwords
+// (so the IPv4/IPv6/TCP fields sit at fixed dword positions), but frame offsets are arbitrary and
+// o + 10 is 2 mod 4 for the usual 4-aligned frames: 16-B loads at such addresses cost ~8 % of a
+// load/store stream on MI355X (tools/ubench_align.hip: 3.9 vs 4.2 TB/s).  So the loads are
+// dword-aligned at a = (o + 10) & ~3 and the window is realigned in registers (v_alignbyte by
+// s = (o + 10) & 3, hdr_view below) when the frame is decoded.
+#ifndef FB_HDR_ALIGNED
+#define FB_HDR_ALIGNED 1
+#endif
 struct Hdr {
+#if FB_HDR_ALIGNED
+    u32x4 A, B, C;   // f[a .. a+48)
+    uint32_t E;      // f[a+48 .. a+52)
+    uint32_t D0, D1; // f[a+56 .. a+64)  (holds f[66..69])
+#else
     u32x4 A, B, C;  // f[10..25] f[26..41] f[42..57]
     uint32_t Dz;    // f[66..69] (IPv6 TCP data offset + flags)
+#endif
 };
+
+// f[10..57] as A, B, C and f[66..69] as Dz, for the frame at offset o.
+__device__ __forceinline__ void hdr_view(const Hdr& h, uint32_t o, u32x4& A, u32x4& B, u32x4& C, uint32_t& Dz) {
+#if FB_HDR_ALIGNED
+    const uint32_t s = (o + 10u) & 3u;
+    auto al = [s](uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbyte(hi, lo, s); };
+    A = u32x4{al(h.A.y, h.A.x), al(h.A.z, h.A.y), al(h.A.w, h.A.z), al(h.B.x, h.A.w)};
+    B = u32x4{al(h.B.y, h.B.x), al(h.B.z, h.B.y), al(h.B.w, h.B.z), al(h.C.x, h.B.w)};
+    C = u32x4{al(h.C.y, h.C.x), al(h.C.z, h.C.y), al(h.C.w, h.C.z), al(h.E, h.C.w)};
+    Dz = al(h.D1, h.D0);
+#else
+    (void)o;
+    A = h.A;
+    B = h.B;
+    C = h.C;
+    Dz = h.Dz;
+#endif
+}
 
 struct Pkt {
     uint32_t cls;         // fb_class after filtering
@@ -141,7 +175,9 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     const bool okoff = o1 >= o0 && o1 <= fbytes;
     k.bad = !okoff;
     const uint32_t L = okoff ? o1 - o0 : 0u;
-    const u32x4 A = h.A, B = h.B, C = h.C;
+    u32x4 A, B, C;
+    uint32_t Dz;
+    hdr_view(h, o0, A, B, C, Dz);
     if (L < 14u) return;                       // EthernetPacket::new -> None
     const uint32_t et = be16_hi(A.x);          // f[12..13]
     const uint32_t n = L - 14u;
@@ -179,7 +215,7 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
         iplen = plen6 + 40u;
         fam = 10u;
         d0 = C.w;                                            // f[54..57]
-        d3 = h.Dz;                                           // f[66..69]
+        d3 = Dz;                                             // f[66..69]
     } else {
         return;                                              // VLAN, ARP, ... -> None
     }
@@ -311,10 +347,21 @@ __device__ void write_batch_stats(const ParseParams& P, unsigned long long tot_c
 }
 
 __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_t o, Hdr& h) {
+#if FB_HDR_ALIGNED
+    const uint32_t a = (o + 10u) & ~3u;
+    h.A = ld16(rs, a);
+    h.B = ld16(rs, a + 16u);
+    h.C = ld16(rs, a + 32u);
+    h.E = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 48u, 0, FB_LD_AUX);
+    const u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(rs, a + 56u, 0, FB_LD_AUX);
+    h.D0 = d.x;
+    h.D1 = d.y;
+#else
     h.A = ld16(rs, o + 10u);
     h.B = ld16(rs, o + 26u);
     h.C = ld16(rs, o + 42u);
     h.Dz = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 66u, 0, FB_LD_AUX);
+#endif
 }
 
 // ---- round look-back (k_parse_ws) -----------------------------------------------------------
@@ -328,7 +375,6 @@ __device__ __forceinline__ void load_headers1(__amdgpu_buffer_rsrc_t rs, uint32_
 template <uint32_t FLAGS>
 __device__ unsigned long long lookback_round(const ParseParams& P, uint32_t r, uint32_t b, uint32_t G,
                                              unsigned long long agg, uint32_t& spins) {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t ep = P.epoch;
     const __amdgpu_buffer_rsrc_t ra =
@@ -956,7 +1002,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                 kk.cls = FB_CLASS_SESSION;
                 kk.tcp = kk.v4 = true;
                 kk.bad = false;
-                const uint32_t hw[14] = {X.h.A.x, X.h.A.y, X.h.A.z, X.h.A.w, X.h.B.x, X.h.B.y, X.h.B.z, X.h.B.w, X.h.C.x, X.h.C.y, X.h.C.z, X.h.C.w, X.h.Dz, X.c.x};
+                const uint32_t hw[14] = {X.h.A.x, X.h.A.y, X.h.A.z, X.h.A.w, X.h.B.x, X.h.B.y, X.h.B.z, X.h.B.w, X.h.C.x, X.h.C.y, X.h.C.z, X.h.C.w, X.h.A.x ^ X.h.C.w, X.c.x};
     #pragma unroll
                 for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
             } else if constexpr (!PARSED) {
