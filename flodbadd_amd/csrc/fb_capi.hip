@@ -712,6 +712,9 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
     p.rec_flow = c->d_rec_flow;
+#ifdef FB_NO_RECFLOW  // ablation: no per-record slot for the history
+    p.rec_flow = nullptr;
+#endif
     p.hot = c->d_hot;
     p.ctl = c->d_comb_ctl;
     p.agg_slot = c->d_agg_slot;

@@ -463,7 +463,7 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
 #endif
 // 256 keys (34 KiB of LDS, four workgroups per CU) x 1024 workgroups, groups >= 48 records: C4
 // Zipf update 1.39 ms, against 1.74 ms at 512 keys x 512 / >= 24 (fixed cost per group: table
-// init, barriers, the id atomic) and 1.50 ms at >= 48 with 512 keys (tools/sweep_comb.sh).
+// init, barriers, the id atomic) and 1.50 ms at >= 48 with 512 keys (tools/sweep_flow.sh, ZIPF=1.1).
 constexpr uint32_t kCombSlots = FB_COMB_SLOTS;  // keys past a full table stay plain entries
 constexpr uint32_t kCombThreads = 256;
 constexpr uint32_t kCombGrid = FB_COMB_GRID;

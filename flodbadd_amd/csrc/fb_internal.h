@@ -131,8 +131,14 @@ struct SegBatches {
 //   end_mask << 24.
 constexpr uint32_t kFlowSlots = 512;             // slots per partition: 64 KiB LDS slice
 constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
-constexpr uint32_t kFlowChunk = 16384;           // records per bucketing workgroup (K1)
-constexpr uint32_t kFlowK1Threads = 1024;
+#ifndef FB_FLOW_CHUNK
+#define FB_FLOW_CHUNK 16384
+#endif
+#ifndef FB_K1_THREADS
+#define FB_K1_THREADS 1024
+#endif
+constexpr uint32_t kFlowChunk = FB_FLOW_CHUNK;   // records per bucketing workgroup (K1)
+constexpr uint32_t kFlowK1Threads = FB_K1_THREADS;
 #ifndef FB_K2_THREADS
 #define FB_K2_THREADS 512  // two 8-wave workgroups per CU (68 KiB LDS each): 1.26 ms for the C4 update vs 1.38 at one 16-wave workgroup
 #endif
