@@ -213,6 +213,10 @@ constexpr uint32_t kSlotWords = 12;  // u64 words of a slot kept in LDS: tag, ke
 constexpr uint32_t kScrU32 = 10;     // per-slot batch scratch, u32 words
 constexpr uint32_t kK2Lds = kFlowSlots * (kSlotWords * 8 + kScrU32 * 4);
 constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
+#ifndef FB_K2_CPT
+#define FB_K2_CPT 2
+#endif
+constexpr uint32_t kK2Cpt = FB_K2_CPT;  // bucketing chunks per K2 thread and round (C4: 640 chunks, one round)
 // scratch words
 constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
 
@@ -593,8 +597,8 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
 
 __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_flow_apply(const FlowParams P) {
     extern __shared__ uint4 slice4[];  // kFlowSlots 96-B slot heads, then kFlowSlots 40-B scratch
-    __shared__ uint32_t sp[kFlowK2Threads];
-    __shared__ uint32_t ss[kFlowK2Threads];
+    __shared__ uint32_t sp[kK2Cpt * kFlowK2Threads];
+    __shared__ uint32_t ss[kK2Cpt * kFlowK2Threads];
     __shared__ uint32_t wsum[kFlowK2Threads / 64];
     __shared__ unsigned long long sh[kFlowK2Threads / 64];
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
@@ -622,13 +626,24 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         }
         __syncthreads();
         const uint4* E = reinterpret_cast<const uint4*>(P.entries);
-        for (uint32_t g0 = 0; g0 < chunks; g0 += kFlowK2Threads) {
-            const uint32_t b = g0 + threadIdx.x;
-            const uint32_t v = b < chunks ? col[b] : 0u;
+        for (uint32_t g0 = 0; g0 < chunks; g0 += kK2Cpt * kFlowK2Threads) {
+            // kK2Cpt consecutive chunks per thread: one round for batches up to kK2Cpt x 512 chunks
+            uint32_t v[kK2Cpt], mine = 0u;
+#pragma unroll
+            for (uint32_t c = 0; c < kK2Cpt; ++c) {
+                const uint32_t b = g0 + threadIdx.x * kK2Cpt + c;
+                v[c] = b < chunks ? col[b] : 0u;
+                mine += v[c] >> 16;
+            }
             uint32_t tot;
-            const uint32_t pre = block_excl_scan(v >> 16, wsum, tot);
-            sp[threadIdx.x] = pre;
-            ss[threadIdx.x] = b * kFlowChunk + (v & 0xFFFFu);
+            uint32_t pre = block_excl_scan(mine, wsum, tot);
+#pragma unroll
+            for (uint32_t c = 0; c < kK2Cpt; ++c) {
+                const uint32_t j = threadIdx.x * kK2Cpt + c;
+                sp[j] = pre;
+                ss[j] = (g0 + j) * kFlowChunk + (v[c] & 0xFFFFu);
+                pre += v[c] >> 16;
+            }
             __syncthreads();
             for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 4u * kFlowK2Threads) {
                 uint4 q[4][4];
@@ -638,7 +653,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 for (uint32_t u = 0; u < 4u; ++u) {
                     const uint32_t e = e0 + u * kFlowK2Threads;
                     if (e < tot) {
-                        uint32_t lo = 0u, hi = kFlowK2Threads - 1u;  // largest j with sp[j] <= e
+                        uint32_t lo = 0u, hi = kK2Cpt * kFlowK2Threads - 1u;  // largest j with sp[j] <= e
                         while (lo < hi) {
                             const uint32_t mid = (lo + hi + 1u) >> 1;
                             if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
