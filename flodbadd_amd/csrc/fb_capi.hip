@@ -60,7 +60,8 @@ struct fb_ctx {
     unsigned long long* d_n = nullptr;
     // ordered per-flow state: update calls since create/clear, table slot of each record slot
     uint32_t flow_batch = 0;
-    uint32_t* d_rec_flow = nullptr;       // [flow_recs]
+    uint32_t* d_rec_flow = nullptr;       // [flow_recs] entry position per record slot
+    uint32_t* d_ent_slot = nullptr;       // [flow_recs] table slot per entry
     uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* d_comb_ctl = nullptr;       // [2] its counters
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
@@ -139,9 +140,11 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_rows);
     hipFree(c->d_cols);
     hipFree(c->d_rec_flow);
+    hipFree(c->d_ent_slot);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
+    c->d_ent_slot = nullptr;
     c->d_entries = nullptr;
     c->d_rows = c->d_cols = nullptr;
     c->d_rec_flow = c->d_hot = c->d_comb_ctl = c->d_agg_slot = nullptr;
@@ -149,7 +152,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     c->flow_recs = 0;
     const uint64_t chunks = recs / kFlowChunk;
     if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
-        hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess || hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&c->d_hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&c->d_comb_ctl, 8) != hipSuccess ||
@@ -318,6 +321,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_partials);
     hipFree(c->d_n);
     hipFree(c->d_rec_flow);
+    hipFree(c->d_ent_slot);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
@@ -712,6 +716,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
     p.rec_flow = c->d_rec_flow;
+    p.ent_slot = c->d_ent_slot;
 #ifdef FB_NO_RECFLOW  // ablation: no per-record slot for the history
     p.rec_flow = nullptr;
 #endif
@@ -796,6 +801,7 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     p.seg = c->last_seg;
     p.stats = c->last_stats;
     p.rec_flow = c->d_rec_flow;
+    p.ent_slot = c->d_ent_slot;
     p.agg_slot = c->d_agg_slot;
     p.n_slots = n;
     p.sentinel = (uint32_t)c->table_cap;

@@ -165,6 +165,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         e[1] = b;
         e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
         e[3] = make_uint4(m.y, base + k, hinfo, (uint32_t)fh);  // low hash word: K2's home slot + tag filter
+        if (P.rec_flow) P.rec_flow[base + k] = base + d;  // the record's entry (coalesced; K2 fills ent_slot)
     }
 }
 
@@ -216,7 +217,11 @@ constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 #ifndef FB_K2_CPT
 #define FB_K2_CPT 2
 #endif
-constexpr uint32_t kK2Cpt = FB_K2_CPT;  // bucketing chunks per K2 thread and round (C4: 640 chunks, one round)
+constexpr uint32_t kK2Cpt = FB_K2_CPT;
+#ifndef FB_K2_EPT
+#define FB_K2_EPT 4
+#endif
+constexpr uint32_t kK2Ept = FB_K2_EPT;  // entries gathered per thread before they are applied  // bucketing chunks per K2 thread and round (C4: 640 chunks, one round)
 // scratch words
 constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
 
@@ -326,8 +331,8 @@ __device__ __forceinline__ uint32_t lds_find(const unsigned long long* tab, cons
 
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
 __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
-                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* rec_flow,
-                                           uint32_t* err) {
+                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* ent_slot,
+                                           uint32_t idx, uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
     uint32_t i;
@@ -341,7 +346,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
     atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
     atomicAdd(s + 10 + (orig ? 0 : 1), (unsigned long long)e2.w);
-    if (rec_flow) rec_flow[e3.y] = slot_base + i;
+    if (ent_slot) ent_slot[idx] = slot_base + i;
 #ifdef FB_NO_ORDERED  // ablation: counters only
     (void)scr;
     return result;
@@ -556,14 +561,16 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 q3 = e[3];
                 const uint32_t key[10] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y & 0xFFFFu};
                 const uint32_t j = lds_find<6, kCombSlots>(L.tab, key, q3.w);
-                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u)
-                    P.rec_flow[q3.y] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
-                else
+                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) {
+                    if (P.rec_flow) P.rec_flow[q3.y] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                } else {
                     keep = 1u;
+                }
             }
             uint32_t kept;
             const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
             if (keep) {
+                if (P.rec_flow) P.rec_flow[q3.y] = (uint32_t)(s0 + cursor + pos);  // the entry moved
                 uint4* o = E + (s0 + cursor + pos) * 4u;
                 o[0] = q0;
                 o[1] = q1;
@@ -645,12 +652,12 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 pre += v[c] >> 16;
             }
             __syncthreads();
-            for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 4u * kFlowK2Threads) {
-                uint4 q[4][4];
-                uint32_t ix[4];
+            for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += kK2Ept * kFlowK2Threads) {
+                uint4 q[kK2Ept][4];
+                uint32_t ix[kK2Ept];
                 uint32_t ne = 0u;
 #pragma unroll
-                for (uint32_t u = 0; u < 4u; ++u) {
+                for (uint32_t u = 0; u < kK2Ept; ++u) {
                     const uint32_t e = e0 + u * kFlowK2Threads;
                     if (e < tot) {
                         uint32_t lo = 0u, hi = kK2Cpt * kFlowK2Threads - 1u;  // largest j with sp[j] <= e
@@ -668,7 +675,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     }
                 }
 #pragma unroll
-                for (uint32_t u = 0; u < 4u; ++u) {
+                for (uint32_t u = 0; u < kK2Ept; ++u) {
                     if (u >= ne || (q[u][2].y & kEntTail)) continue;  // second unit of a combined entry
                     if (q[u][2].y & kEntCombined) {
                         const uint4* t = E + ((size_t)ix[u] + 1u) * 4u;
@@ -681,7 +688,8 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                         }
                     } else {
                         const int r = apply_entry(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3],
-                                                  part * kFlowSlots, P.rec_flow, P.error);
+                                                  part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix[u],
+                                                  P.error);
                         n_new += r == 1;
                         n_upd += r == 0;
                     }

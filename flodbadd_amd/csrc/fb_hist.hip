@@ -3,7 +3,7 @@
 // The reference appends map_tcp_flags(..) to the flow's `history` String for every TCP packet
 // (src/packets.rs:187-198 occupied, 410-426 vacant), so a flow's history is its TCP packets'
 // characters in arrival order.  k_flow_apply (fb_flow.hip) records the table slot of every
-// record slot of the batch in `rec_flow`; here the batch's TCP records are stably sorted by that
+// record slot of the batch via `rec_flow` (entry position) and `ent_slot` / `agg_slot`; here the batch's TCP records are stably sorted by that
 // slot, which groups each flow's characters into one run while keeping packet order inside it:
 //   k_hist_keys : key[i] = rec_flow[i] for a valid record with FB_META_HAS_FLAGS, else the
 //                 sentinel (= table capacity, sorts last); value[i] = the record's hist_char;
@@ -34,8 +34,8 @@ __global__ __launch_bounds__(256) void k_hist_keys(const HistParams P) {
         }
         uint32_t slot = P.sentinel;
         if (keyed) {
-            slot = P.rec_flow[i];
-            if (slot & kRecFlowCombined) slot = P.agg_slot[slot & ~kRecFlowCombined];  // k_flow_combine
+            const uint32_t v = P.rec_flow[i];  // entry position, or a k_flow_combine id
+            slot = (v & kRecFlowCombined) ? P.agg_slot[v & ~kRecFlowCombined] : P.ent_slot[v];
         }
         P.keys[i] = slot;
         P.vals[i] = (uint8_t)ch;

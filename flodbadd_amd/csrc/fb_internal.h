@@ -194,7 +194,9 @@ struct FlowParams {
     uint32_t part_shift;        // 64 - log2(P) (64 when P == 1)
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
     uint32_t batch;             // update call number since create / clear (positions' high word)
-    uint32_t* rec_flow;         // [max_recs] table slot of each record slot (for the history)
+    uint32_t* rec_flow;         // [max_recs] per record slot: its entry position (K1, moved by K1c)
+                                // or kRecFlowCombined | combined id (for the history)
+    uint32_t* ent_slot;         // [max_recs] table slot of each plain entry (K2; coalesced writes)
     uint32_t* hot;              // [hot_cap] (chunk << 13 | part) groups K1 hands to k_flow_combine
     uint32_t* ctl;              // [2] hot groups, combined entries (reset by K1t)
     uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
@@ -224,8 +226,8 @@ struct HistParams {
     const fb_pkt_out* recs;     // the update's records (dense or segmented)
     const uint32_t* seg;        // segmented: record slot i valid iff (i & 63) < (seg[i >> 6] & 0xFFFF)
     const fb_batch_stats* stats;  // dense: n_session read here
-    const uint32_t* rec_flow;   // table slot of each record slot (k_flow_apply), or
-                                // kRecFlowCombined | combined id
+    const uint32_t* rec_flow;   // entry position of each record slot, or kRecFlowCombined | combined id
+    const uint32_t* ent_slot;   // table slot of each plain entry (k_flow_apply)
     const uint32_t* agg_slot;   // table slot of each combined entry
     uint32_t n_slots;           // record slots of the update
     uint32_t sentinel;          // key of the records that are not sorted in (= table capacity)
