@@ -181,6 +181,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         N.check(lib.fb_flow_count(ctx, C.byref(cnt), stream.ptr))
         stage["flows"] = int(cnt.value)
         stage.update(enrich_timing(N, lib, ctx, int(cnt.value), stream))
+        stage.update(dns_timing(N, lib, ctx, stream))
     else:
         assert st2.tobytes() == st.tobytes()
     for b in bufs:
@@ -233,6 +234,35 @@ def enrich_timing(N, lib, ctx, flows, stream, reps=5):
         b.free()
     return dict(enrich_ms=round(ms, 4), enrich_flows=got, enrich_Mflows_s=round(got / ms / 1e3, 1),
                 enrich_tables="500k v4 + 100k v6 ASN ranges, 50k blacklist ranges / 32 lists")
+
+
+def dns_timing(N, lib, ctx, stream, n=1 << 20, reps=10):
+    """DNS divert parse (fb_dns_parse_dev) over a device-resident batch of 1M
+    port-53 payloads (synth.dns_workload: queries, reverse lookups, CNAME + A/AAAA responses)."""
+    from flodbadd_amd import synth
+    payload, rec = synth.dns_workload(n)
+    d_fr = N.DeviceBuffer(payload.nbytes).upload(payload)
+    d_dns = N.DeviceBuffer(rec.nbytes).upload(rec)
+    d_msg = N.DeviceBuffer(n * N.DNS_MSG_DTYPE.itemsize)
+    d_names = N.DeviceBuffer(n * N.FB_DNS_MAX_NAME)
+    d_addrs = N.DeviceBuffer(n * N.FB_DNS_MAX_ADDRS * N.FB_IP_DTYPE.itemsize)
+
+    def call():
+        N.check(lib.fb_dns_parse_dev(ctx, d_fr.ptr, payload.nbytes, d_dns.ptr, n, None, d_msg.ptr, d_names.ptr,
+                                     d_addrs.ptr, stream.ptr))
+    call()
+    e0, e1 = N.Event(), N.Event()
+    e0.record(stream)
+    for _ in range(reps):
+        call()
+    e1.record(stream)
+    ms = e0.elapsed_ms(e1) / reps
+    msgs = d_msg.download(np.zeros(n, dtype=N.DNS_MSG_DTYPE), stream=stream.ptr)
+    ok = int((msgs["status"] == 0).sum())
+    for b in (d_fr, d_dns, d_msg, d_names, d_addrs):
+        b.free()
+    return dict(dns_parse_ms=round(ms, 4), dns_msgs=n, dns_ok=ok, dns_Mmsgs_s=round(n / ms / 1e3, 1),
+                dns_payload_GBs=round(payload.nbytes / ms / 1e6, 1))
 
 
 def host_inclusive(N, lib, ctx, frames, offs, calls=20):
@@ -481,6 +511,9 @@ def main():
                                   history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
                                   enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
                                   enrich_tables=sg["enrich_tables"],
+                                  dns_parse_ms=sg["dns_parse_ms"], dns_Mmsgs_s=sg["dns_Mmsgs_s"],
+                                  dns_payload_GBs=sg["dns_payload_GBs"], dns_ok=sg["dns_ok"],
+                                  dns_workload="1M port-53 payloads (synth.dns_workload), device-resident",
                                   flows_in_table=sg["flows"],
                                   parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
                                   flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))

@@ -71,3 +71,55 @@ def generate(config_id, n, first=0, threads=None, frames_out=None, **overrides):
         threads = min(16, os.cpu_count() or 1)
     lib.fb_synth_fill(C.byref(cfg), first, n, offsets.ctypes.data, frames.ctypes.data, threads)
     return frames, offsets
+
+
+def dns_workload(n, seed=0xD115):
+    """A device-benchmark DNS divert batch: `n` port-53 payloads (RFC 1035 wire format) and their
+    DNS_OUT_DTYPE side records, cycling through 512 distinct messages: queries (A / AAAA / PTR,
+    with and without EDNS) and responses (CNAME chain + A / AAAA answers, compression pointers),
+    the shapes src/dns.rs handles.  Returns (payload uint8[bytes], records)."""
+    import struct
+    from . import _native as N
+    rnd = np.random.default_rng(seed)
+
+    def name(s, ptr=None):
+        out = b"".join(bytes([len(x)]) + x.encode() for x in s.split(".") if x)
+        return out + (struct.pack("!H", 0xC000 | ptr) if ptr is not None else b"\0")
+
+    def rr(owner, typ, rdata):
+        return owner + struct.pack("!HHIH", typ, 1, 300, len(rdata)) + rdata
+
+    msgs = []
+    for i in range(512):
+        tx = int(rnd.integers(0, 1 << 16))
+        host = "h%d.svc%d.example%d.com" % (i, i % 37, i % 5)
+        kind = i % 4
+        if kind == 0:    # A query with EDNS
+            m = struct.pack("!HHHHHH", tx, 0x0100, 1, 0, 0, 1) + name(host) + struct.pack("!HH", 1, 1) + \
+                b"\0" + struct.pack("!HHBBHH", 41, 1232, 0, 0, 0, 0)
+        elif kind == 1:  # AAAA query
+            m = struct.pack("!HHHHHH", tx, 0x0100, 1, 0, 0, 0) + name(host) + struct.pack("!HH", 28, 1)
+        elif kind == 2:  # reverse lookup
+            m = struct.pack("!HHHHHH", tx, 0x0100, 1, 0, 0, 0) + \
+                name("%d.%d.0.10.in-addr.arpa" % (i & 255, i >> 8)) + struct.pack("!HH", 12, 1)
+        else:            # response: CNAME + 2 A + 1 AAAA, names compressed against the question
+            q = name(host) + struct.pack("!HH", 1, 1)
+            an = rr(b"\xc0\x0c", 5, name("edge%d.cdn.example.net" % i)) + \
+                rr(b"\xc0\x0c", 1, struct.pack("!I", 0x5DB8D800 | (i & 255))) + \
+                rr(b"\xc0\x0c", 1, struct.pack("!I", 0x5DB8D900 | (i & 255))) + \
+                rr(b"\xc0\x0c", 28, bytes([0x26, 0x06, 0x28, 0]) + bytes(11) + bytes([i & 255]))
+            m = struct.pack("!HHHHHH", tx, 0x8180, 1, 4, 0, 0) + q + an
+        msgs.append(m)
+    lens = np.array([len(m) for m in msgs], dtype=np.uint64)
+    base = np.frombuffer(b"".join(msgs), dtype=np.uint8)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    reps = (n + 511) // 512
+    payload = np.tile(base, reps)
+    idx = np.arange(n, dtype=np.uint64)
+    rec = np.zeros(n, dtype=N.DNS_OUT_DTYPE)
+    rec["pkt_index"] = idx
+    rec["payload_offset"] = (idx // 512) * np.uint64(base.nbytes) + starts[idx % 512]
+    rec["payload_length"] = lens[idx % 512]
+    rec["protocol"] = 17
+    rec["family"] = 2
+    return payload, rec
