@@ -66,6 +66,68 @@ __device__ __forceinline__ unsigned long long bl_lookup(const EnrichTables& t, c
     return v6 ? t.bl6_mask[lo - 1u] : t.bl4_mask[lo - 1u];
 }
 
+// The four lookups of a new flow (ASN and blacklist mask of src and dst) as independent searches
+// advanced in one loop, so each step issues up to four loads together: the binary searches are
+// chains of dependent loads (latency-bound), and interleaving them keeps 4x the loads in flight.
+// Same probes as asn_lookup / bl_lookup.  A local ip (`skip`) gets -1 / 0 without a search.
+__device__ __forceinline__ void flow_lookups(const EnrichTables& t, bool v6, const uint32_t* const ip[2],
+                                             const bool skip[2], int32_t asn[2], unsigned long long bl[2]) {
+    const fb_asn_range* A = v6 ? t.asn6 : t.asn4;
+    const uint32_t na = v6 ? t.n6 : t.n4, nb = v6 ? t.m6 : t.m4;
+    uint32_t alo[2], ahi[2], blo[2], bhi[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        alo[k] = 0u;
+        ahi[k] = skip[k] ? 0u : na;
+        blo[k] = 0u;
+        bhi[k] = skip[k] ? 0u : nb;
+        asn[k] = -1;
+    }
+    for (;;) {
+        bool on_a[2], on_b[2];
+        uint4 st[2], en[2], bp[2];
+        uint32_t am[2], bm[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {  // issue every active search's probe
+            on_a[k] = alo[k] < ahi[k];
+            on_b[k] = blo[k] < bhi[k];
+            am[k] = (alo[k] + ahi[k]) >> 1;
+            bm[k] = (blo[k] + bhi[k]) >> 1;
+            if (on_a[k]) {
+                st[k] = *reinterpret_cast<const uint4*>(A[am[k]].start);
+                en[k] = *reinterpret_cast<const uint4*>(A[am[k]].end);
+            }
+            if (on_b[k]) bp[k] = v6 ? t.bl6_pos[bm[k]] : make_uint4(t.bl4_pos[bm[k]], 0u, 0u, 0u);
+        }
+        if (!(on_a[0] || on_a[1] || on_b[0] || on_b[1])) break;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (on_a[k]) {  // Db::lookup, src/asn_db.rs:144-166
+                const uint32_t sw[4] = {st[k].x, st[k].y, st[k].z, st[k].w}, ew[4] = {en[k].x, en[k].y, en[k].z, en[k].w};
+                const bool ge_start = !ip_lt(ip[k], sw, v6), le_end = !ip_lt(ew, ip[k], v6);
+                if (ge_start && le_end) {
+                    asn[k] = (int32_t)A[am[k]].record;
+                    ahi[k] = alo[k];  // found: the search ends
+                } else if (!ge_start) {
+                    ahi[k] = am[k];
+                } else {
+                    alo[k] = am[k] + 1u;
+                }
+            }
+            if (on_b[k]) {  // first interval starting > ip
+                const uint32_t pw[4] = {bp[k].x, bp[k].y, bp[k].z, bp[k].w};
+                if (v6 ? ip_lt(ip[k], pw, true) : ip[k][0] < pw[0]) bhi[k] = bm[k];
+                else blo[k] = bm[k] + 1u;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        bl[k] = 0ull;
+        if (!skip[k] && blo[k] > 0u) bl[k] = v6 ? t.bl6_mask[blo[k] - 1u] : t.bl4_mask[blo[k] - 1u];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ip_lookup(const EnrichTables t, const fb_ip* ips, uint32_t n, int32_t* asn,
                                                    unsigned long long* lists) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -111,14 +173,17 @@ __global__ __launch_bounds__(256) void k_flow_enrich(const EnrichTables t, const
             r.flags = (ls ? FB_ENRICH_LOCAL_SRC : 0u) | (ld ? FB_ENRICH_LOCAL_DST : 0u) |
                       (own_ip(cfg, cfg, fam, src) ? FB_ENRICH_SELF_SRC : 0u) |
                       (own_ip(cfg, cfg, fam, dst) ? FB_ENRICH_SELF_DST : 0u);
-            const fb_asn_range* A = v6 ? t.asn6 : t.asn4;
-            const uint32_t na = v6 ? t.n6 : t.n4;
             // ASN only for non-local ips (src/packets.rs:468-485); so the blacklist ips
             // (src/blacklists.rs:545-556)
-            r.src_asn = ls ? -1 : asn_lookup(A, na, src, v6);
-            r.dst_asn = ld ? -1 : asn_lookup(A, na, dst, v6);
-            r.src_blacklists = ls ? 0ull : bl_lookup(t, src, v6);
-            r.dst_blacklists = ld ? 0ull : bl_lookup(t, dst, v6);
+            const uint32_t* const ips[2] = {src, dst};
+            const bool skip[2] = {ls, ld};
+            int32_t asn[2];
+            unsigned long long bl[2];
+            flow_lookups(t, v6, ips, skip, asn, bl);
+            r.src_asn = asn[0];
+            r.dst_asn = asn[1];
+            r.src_blacklists = bl[0];
+            r.dst_blacklists = bl[1];
             out[pos] = r;
         }
         __syncthreads();
@@ -132,11 +197,14 @@ hipError_t launch_ip_lookup(const EnrichTables& t, const fb_ip* ips, uint32_t n,
     return hipGetLastError();
 }
 
+#ifndef FB_ENRICH_GRID
+#define FB_ENRICH_GRID 8192ull  // one slot per thread up to 2^21 slots: 0.38 ms vs 0.43 at 2048 (C4)
+#endif
 hipError_t launch_flow_enrich(const EnrichTables& t, const DevConfig* cfg, const FlowSlot* table,
                               unsigned long long cap, uint32_t new_only, uint32_t batch, fb_flow_enrich* out,
                               unsigned long long out_cap, unsigned long long* d_n, hipStream_t s) {
     unsigned long long g = (cap + 255ull) / 256ull;
-    if (g > 2048ull) g = 2048ull;
+    if (g > FB_ENRICH_GRID) g = FB_ENRICH_GRID;
     if (g == 0ull) g = 1ull;
     hipLaunchKernelGGL(k_flow_enrich, dim3((uint32_t)g), dim3(256), 0, s, t, cfg, table, cap, new_only, batch, out,
                        out_cap, d_n);
