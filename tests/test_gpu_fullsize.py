@@ -1,0 +1,85 @@
+"""GPU parity at BASELINE.json's full sizes, bit-exact against the C oracle (it finishes these
+sizes in seconds), plus size-independent properties of the same runs.
+
+* C2 / C3: 1,048,576 frames per batch (configs[1], configs[2]); two distinct full batches through
+  ONE `fb_parse_classify_seg_batches_dev` launch with the filter bench.py uses (GlobalOnly, the
+  `FlodbaddCapture::new` default, src/capture.rs:108) -- the headline launch, batch for batch.
+* C4: 10,485,760 IMIX frames (configs[3]) through `fb_process_seg_dev` (parse + session upsert,
+  src/packets.rs:202-537), then a second 2M-frame batch that mostly updates existing flows; the
+  exported table equals the oracle's DashMap restatement row for row.
+"""
+import numpy as np
+import pytest
+
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from flodbadd_amd.sessions import SessionFilter
+from oracle import coracle
+from test_gpu_segmented import _check, _run_batches
+
+pytestmark = pytest.mark.gpu
+
+FULL = 1 << 20
+
+
+def _conserved(st, n):
+    """Every frame lands in exactly one class (src/packets.rs:603-802 returns Some or None; the
+    filter at 321-327 drops the rest)."""
+    s = st[0]
+    assert int(s["n_session"]) + int(s["n_dns"]) + int(s["n_drop"]) + int(s["n_filtered"]) == n
+    assert int(s["total_processed"]) == int(s["ipv4_processed"]) + int(s["ipv6_processed"])
+    assert int(s["error"]) == 0 and int(s["bad_offsets"]) == 0
+
+
+@pytest.mark.parametrize("cid", [2, 3])
+def test_full_size_headline_launch(gpu_capture, cid):
+    batches = [synth.generate(cid, FULL, first=k * FULL) for k in range(2)]
+    flt = SessionFilter.GlobalOnly
+    gpu_capture.set_filter(flt)
+    try:
+        res = _run_batches(gpu_capture, batches)
+    finally:
+        gpu_capture.set_filter(SessionFilter.All)
+    for (frames, offs), r in zip(batches, res):
+        _check(gpu_capture, frames, offs, flt=int(flt), res=r)
+        _conserved(r[3], FULL)
+
+
+def _void_sorted(arr):
+    """Order-independent view of flow rows (table slot zeroed: placement, not content)."""
+    arr = arr.copy()
+    arr["slot"] = 0
+    return np.sort(np.ascontiguousarray(arr).view("V%d" % arr.dtype.itemsize).ravel())
+
+
+def test_full_size_c4_session_table(gpu_capture):
+    cap = gpu_capture
+    cap.clear_all_sessions()
+    cfg = coracle.make_cfg(int(SessionFilter.All))
+    flows = coracle.Flows()
+    n_records = 0
+    payload = 0
+    for n, first in ((10 * FULL, 0), (2 * FULL, 10 * FULL)):
+        frames, offs = synth.generate(4, n, first=first)
+        g = cap.process_frames_seg(frames, offs)
+        r_out, r_dns, r_cls, r_st = coracle.parse_classify(cfg, frames, offs)
+        assert np.array_equal(g.cls, r_cls)
+        assert g.records.tobytes() == r_out.tobytes(), "session records differ"
+        assert g.dns.tobytes() == r_dns.tobytes(), "dns records differ"
+        st = np.zeros(1, dtype=N.STATS_DTYPE)
+        flows.update(r_out, st)
+        assert g.stats["new_sessions"] == int(st[0]["new_sessions"])
+        assert g.stats["updated_sessions"] == int(st[0]["updated_sessions"])
+        assert g.stats["new_sessions"] + g.stats["updated_sessions"] == g.stats["n_session"]
+        n_records += len(r_out)
+        payload += int(r_out["packet_length"].astype(np.int64).sum())
+        del frames, offs, g, r_out, r_dns, r_cls
+    gflows = cap.export_flows()
+    rflows = flows.export_sorted()
+    assert len(gflows) == len(rflows) == cap.flow_count()
+    # size-independent: every record counted once, every payload byte once
+    assert int(gflows["orig_pkts"].sum() + gflows["resp_pkts"].sum()) == n_records
+    assert int(gflows["outbound_bytes"].sum() + gflows["inbound_bytes"].sum()) == payload
+    assert np.array_equal(_void_sorted(gflows), _void_sorted(rflows))
+    cap.clear_all_sessions()
+    assert cap.flow_count() == 0
