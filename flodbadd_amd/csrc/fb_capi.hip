@@ -62,6 +62,8 @@ struct fb_ctx {
     uint32_t flow_batch = 0;
     uint32_t* d_rec_flow = nullptr;       // [flow_recs] entry position per record slot
     uint32_t* d_ent_slot = nullptr;       // [flow_recs] table slot per entry
+    uint32_t* d_rec_part = nullptr;       // [flow_recs] partition per record slot (fb_process_seg_dev)
+    const fb_pkt_out* part_recs = nullptr;  // the records d_rec_part was written for (one update)
     uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* d_comb_ctl = nullptr;       // [2] its counters
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
@@ -141,9 +143,12 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_cols);
     hipFree(c->d_rec_flow);
     hipFree(c->d_ent_slot);
+    hipFree(c->d_rec_part);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
+    c->d_rec_part = nullptr;
+    c->part_recs = nullptr;
     c->d_ent_slot = nullptr;
     c->d_entries = nullptr;
     c->d_rows = c->d_cols = nullptr;
@@ -153,6 +158,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     const uint64_t chunks = recs / kFlowChunk;
     if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
         hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess || hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&c->d_hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&c->d_comb_ctl, 8) != hipSuccess ||
@@ -322,6 +328,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_n);
     hipFree(c->d_rec_flow);
     hipFree(c->d_ent_slot);
+    hipFree(c->d_rec_part);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
@@ -402,7 +409,8 @@ static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipS
 }
 
 // Shared launch of the segmented streaming kernel (frames or parsed packets).
-static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s, const SegBatches* batches = nullptr) {
+static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s, const SegBatches* batches = nullptr,
+                      bool want_parts = false) {
     const uint64_t units = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
     int rc = ensure_status(c, units, s);
     if (rc) return rc;
@@ -411,6 +419,11 @@ static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s, cons
     rc = ensure_flow_scratch(c, n, s);
     if (rc) return rc;
     c->last_n = n;
+    // fb_process_seg_dev: the kernel also writes each SESSION record slot's table partition, so
+    // the update's histogram pass reads 4 B per record instead of the record
+    p.rec_part = (want_parts && !batches && c->d_table) ? c->d_rec_part : nullptr;
+    p.part_shift = c->flow_shift;
+    c->part_recs = p.rec_part ? p.out : nullptr;
     p.tagg = c->d_status;
     p.wstat = p.tagg + c->status_tiles;
     p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
@@ -481,9 +494,9 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, ui
     return launch_seg(c, p, n_max, (hipStream_t)stream, &sb);
 }
 
-int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
-                              uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,
-                              fb_batch_stats* d_stats, void* stream) {
+static int parse_seg(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets, uint32_t n,
+                     fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class, fb_batch_stats* d_stats, void* stream,
+                     bool want_parts) {
     if (!c || !d_stats) return set_err(FB_ERR_INVAL, "ctx and d_stats are required");
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
     if (frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "frames_bytes must be < 4 GiB");
@@ -505,7 +518,13 @@ int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frame
     p.stats = d_stats;
     p.seg = d_seg;
     p.frames_bytes = (uint32_t)frames_bytes;
-    return launch_seg(c, p, n, s);
+    return launch_seg(c, p, n, s, nullptr, want_parts);
+}
+
+int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                              uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,
+                              fb_batch_stats* d_stats, void* stream) {
+    return parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, false);
 }
 
 int fb_process_parsed_seg_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
@@ -724,6 +743,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ctl = c->d_comb_ctl;
     p.agg_slot = c->d_agg_slot;
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
+    p.rec_part = (d_seg && c->part_recs == d_recs) ? c->d_rec_part : nullptr;  // written by this batch's parse
+    c->part_recs = nullptr;
     HIP_TRY(launch_flow_update(p, chunks, s));
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
     ++c->flow_batch;
@@ -753,10 +774,10 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
                        void* stream) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
-    int rc = fb_parse_classify_seg_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream);
-    if (rc) return rc;
-    if (n == 0) return empty_update(c);
-    return fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
+    int rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
+    if (rc == FB_OK) rc = n == 0 ? empty_update(c) : fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
+    c->part_recs = nullptr;  // the partitions serve this update only
+    return rc;
 }
 
 int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,

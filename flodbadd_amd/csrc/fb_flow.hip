@@ -32,23 +32,7 @@
 
 namespace fbk {
 
-__host__ __device__ inline unsigned long long flow_hash_words(const uint32_t k[10]) {
-    unsigned long long h = 0x9E3779B97F4A7C15ull;
-    for (int j = 0; j < 10; j += 2) {
-        const unsigned long long w = (unsigned long long)k[j] | ((unsigned long long)k[j + 1] << 32);
-        h ^= w;
-        h *= 0xBF58476D1CE4E5B9ull;
-        h ^= h >> 31;
-    }
-    h ^= h >> 33;
-    h *= 0xFF51AFD7ED558CCDull;
-    h ^= h >> 33;
-    return h;
-}
-
-__device__ __forceinline__ uint32_t part_of(unsigned long long h, uint32_t shift) {
-    return shift >= 64u ? 0u : (uint32_t)(h >> shift);
-}
+// flow_hash_words / part_of: fb_internal.h (the parse kernel computes the partition too).
 
 // Inclusive wave scan + block exclusive scan of one u32 per thread (blockDim multiple of 64).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
@@ -115,14 +99,19 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     const fb_pkt_out* R = P.recs + base;
     for (uint32_t j = threadIdx.x; j < P.parts; j += kFlowK1Threads) hist[j] = 0u;
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
-        if (!slot_valid(P, base + k)) continue;
-        const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
-        const uint4 a = *reinterpret_cast<const uint4*>(r);
-        const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
-        const uint2 c = *reinterpret_cast<const uint2*>(r + 8);
-        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-        atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+    if (P.rec_part) {  // partitions from the parse of this batch: 4 B per record instead of 40
+        for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads)
+            if (slot_valid(P, base + k)) atomicAdd(&hist[P.rec_part[base + k]], 1u);
+    } else {
+        for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
+            if (!slot_valid(P, base + k)) continue;
+            const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
+            const uint4 a = *reinterpret_cast<const uint4*>(r);
+            const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
+            const uint2 c = *reinterpret_cast<const uint2*>(r + 8);
+            const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+            atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+        }
     }
     __syncthreads();
     // exclusive scan of hist[0..parts): each thread owns E consecutive partitions

@@ -65,6 +65,8 @@ struct ParseParams {
     uint32_t* error;       // this launch's error word (epoch parity); nonzero: a bounded spin expired
     uint32_t* error_next;  // the other parity's word, zeroed by this launch for the next one
     unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
+    uint32_t* rec_part;       // k_parse_seg (one batch): partition of each SESSION record slot, or nullptr
+    uint32_t part_shift;      // FlowParams::part_shift of the context's table
 };
 
 // is_lan_ip, src/ip.rs:55-156, 199-242.
@@ -177,6 +179,26 @@ constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the origina
 constexpr uint32_t kEntTail = 1u << 18;
 constexpr uint32_t kRecFlowCombined = 0x80000000u;  // rec_flow value: combined id, slot in agg_slot
 
+// fb_flow_hash of a 40-B session_key (10 words, word 9 = protocol | family << 8) and the
+// partition it falls in (top bits).
+__host__ __device__ inline unsigned long long flow_hash_words(const uint32_t k[10]) {
+    unsigned long long h = 0x9E3779B97F4A7C15ull;
+    for (int j = 0; j < 10; j += 2) {
+        const unsigned long long w = (unsigned long long)k[j] | ((unsigned long long)k[j + 1] << 32);
+        h ^= w;
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t part_of(unsigned long long h, uint32_t shift) {
+    return shift >= 64u ? 0u : (uint32_t)(h >> shift);
+}
+
 struct FlowParams {
     const fb_pkt_out* recs;
     const uint32_t* seg;        // non-null: recs are 64-record segments, record slot i valid iff
@@ -201,6 +223,9 @@ struct FlowParams {
     uint32_t* ctl;              // [2] hot groups, combined entries (reset by K1t)
     uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
     uint32_t hot_cap;
+    const uint32_t* rec_part;   // non-null: partition of each SESSION record slot, written by the
+                                // segmented parse of the same batch (fb_process_seg_dev); K1's
+                                // histogram pass then reads 4 B per record instead of the record
 };
 
 // Launchers (fb_parse.hip / fb_flow.hip).

@@ -289,6 +289,8 @@ constexpr uint32_t kFlagsProduct = 0u;
 constexpr uint32_t kNoLookback = 1u;  // base offsets = tile start (wrong output, timing only)
 constexpr uint32_t kNoStore = 2u;     // no record / dns stores (timing only)
 constexpr uint32_t kStamps = 4u;      // per-unit s_memrealtime stamps into P.dbg
+constexpr uint32_t kPartOut = 8u;     // k_parse_seg: also the flow-table partition of each SESSION
+                                      // record slot (P.rec_part), for the update that follows
 
 constexpr unsigned long long kIncBit = 1ull << 55;
 constexpr unsigned long long kCnt28 = (1ull << 28) - 1ull;
@@ -931,7 +933,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     auto dropped_stores = [&]() {
         if constexpr ((FLAGS & kNoStore) == 0u) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
+            for (int j = 0; j < ((FLAGS & kPartOut) ? 9 : 8); ++j)
+                __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
         }
     };
     auto load_parsed = [&](uint32_t sg) {
@@ -1066,6 +1069,14 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                 }
                 __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? ls * 4u : kOob, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
+                if constexpr ((FLAGS & kPartOut) != 0u) {  // the record slot's table partition (K1's histogram)
+                    const __amdgpu_buffer_rsrc_t r_part = __builtin_amdgcn_make_buffer_rsrc(
+                        P.rec_part + (size_t)ls * 64u, (short)0, 256, 0x00020000);
+                    const uint32_t key[10] = {kk.w[0], kk.w[1], kk.w[2], kk.w[3], kk.w[4],
+                                              kk.w[5], kk.w[6], kk.w[7], kk.w[8], kk.w[9] & 0xFFFFu};
+                    __builtin_amdgcn_raw_buffer_store_b32(part_of(flow_hash_words(key), P.part_shift), r_part,
+                                                          is_s ? (uint32_t)__popcll(m_sess & lmask) * 4u : kOob, 0, 0);
+                }
             }
             __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
             a_s += cs;
@@ -1142,6 +1153,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 
 hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s) {
     if (p.parsed) hipLaunchKernelGGL((k_parse_seg<true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
+    else if (p.rec_part && sb.count == 1u)
+        hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct | kPartOut>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     else if (sb.count > 1u)
         hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct, true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     else hipLaunchKernelGGL((k_parse_seg<false>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
