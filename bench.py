@@ -625,8 +625,11 @@ def main():
                        "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
                        "output": (("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
                                    "%d batches per launch, each with its own outputs and stats)" % bpl) if bpl > 1 else
-                                  "per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)"
+                                  ("per-64-frame wavefront-compacted segments + session-table upsert "
+                                   "(fb_process_seg_dev)" if args.config == 4 else
+                                   "per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)")
                                   if args.mode == "seg" else
+                                  "batch-wide compaction (fb_process_dev)" if args.config == 4 else
                                   "batch-wide compaction (fb_parse_classify_dev)"),
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
