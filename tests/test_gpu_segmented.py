@@ -138,6 +138,50 @@ def test_seg_flow_table_vs_dense(gpu_capture):
     gpu_capture.clear_all_sessions()
 
 
+def test_seg_partition_handoff_is_per_call(gpu_capture):
+    """The fused call's parse hands record partitions to its own update only: fused and split
+    calls interleaved on different buffers (split: fb_parse_classify_seg_dev, then
+    fb_flow_update_seg_dev on a buffer the fused call never saw; an update of the fused call's
+    buffer again with the other batch's records in it) still build the oracle's table."""
+    lib = N.gpu_lib()
+    bs = [synth.generate(4, 50000 + 777 * (2 - b), first=b * 60000) for b in range(3)]  # A holds batch 2 too
+    cap = gpu_capture
+    cap.clear_all_sessions()
+    flows = coracle.Flows()
+    cfg = coracle.make_cfg(2)
+
+    def bufs(frames, offs):
+        n = len(offs) - 1
+        nseg = (n + 63) // 64
+        d_fr = N.DeviceBuffer(frames.nbytes).upload(np.ascontiguousarray(frames))
+        d_off = N.DeviceBuffer(offs.nbytes).upload(np.ascontiguousarray(offs, dtype=np.uint32))
+        return n, d_fr, d_off, N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), \
+            N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+
+    A = bufs(*bs[0])
+    B = bufs(*bs[1])
+    n, d_fr, d_off, d_out, d_seg, d_st = A
+    N.check(lib.fb_process_seg_dev(cap.ctx, d_fr.ptr, bs[0][0].nbytes, d_off.ptr, n, d_out.ptr, d_seg.ptr, None,
+                                   d_st.ptr, None))
+    n, d_fr, d_off, d_out, d_seg, d_st = B
+    N.check(lib.fb_parse_classify_seg_dev(cap.ctx, d_fr.ptr, bs[1][0].nbytes, d_off.ptr, n, d_out.ptr, d_seg.ptr,
+                                          None, d_st.ptr, None))
+    N.check(lib.fb_flow_update_seg_dev(cap.ctx, d_out.ptr, d_seg.ptr, n, d_st.ptr, None))
+    # batch 2 parsed into A's output buffer by a plain call, then updated
+    n2, d_fr2, d_off2, _, _, _ = bufs(*bs[2])
+    n, _, _, d_out, d_seg, d_st = A
+    N.check(lib.fb_parse_classify_seg_dev(cap.ctx, d_fr2.ptr, bs[2][0].nbytes, d_off2.ptr, n2, d_out.ptr, d_seg.ptr,
+                                          None, d_st.ptr, None))
+    N.check(lib.fb_flow_update_seg_dev(cap.ctx, d_out.ptr, d_seg.ptr, n2, d_st.ptr, None))
+    for frames, offs in bs:
+        flows.update(coracle.parse_classify(cfg, frames, offs)[0], np.zeros(1, dtype=N.STATS_DTYPE))
+    gf = cap.export_flows()
+    rf = flows.export_sorted()
+    from test_gpu_parity import rows_sorted
+    assert len(gf) == len(rf) and rows_sorted(gf) == rows_sorted(rf)
+    cap.clear_all_sessions()
+
+
 def test_seg_parsed_path(gpu_capture):
     """fb_process_parsed_seg_dev == fb_process_parsed_dev on the same SessionPacketData."""
     frames, offs = synth.generate(3, 20000)
