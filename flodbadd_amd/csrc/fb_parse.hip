@@ -1153,10 +1153,10 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 
 hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s) {
     if (p.parsed) hipLaunchKernelGGL((k_parse_seg<true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
-    else if (p.rec_part && sb.count == 1u)
-        hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct | kPartOut>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     else if (sb.count > 1u)
         hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct, true>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
+    else if (p.rec_part)  // instantiated after the headline instance: its code placement is unchanged
+        hipLaunchKernelGGL((k_parse_seg<false, kFlagsProduct | kPartOut>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     else hipLaunchKernelGGL((k_parse_seg<false>), dim3(grid), dim3(kSegThreads), 0, s, p, sb);
     return hipGetLastError();
 }
