@@ -556,7 +556,9 @@ def main():
                                             unit="Mpackets/s", ms_per_step=round(r1["elapsed"] * 1e3 / st_1, 4),
                                             roofline_achieved_GBs=round(r1["algo_bytes"] / pl1 / 1e9, 1),
                                             roofline_frac=round(r1["algo_bytes"] / pl1 / 1e9 / HBM_PEAK_GBS, 4))
-    if not args.no_other_mode:
+    # N > 1: the scaling line needs only the headline path; the dense layout's persistent
+    # look-back kernel also needs all its workgroups resident on the device
+    if not args.no_other_mode and world == 1:
         other = "dense" if args.mode == "seg" else "seg"
         st_o = max(args.steps // 2, 10)
         ro = run_config(N, lib, ctx, args.config, n, st_o, max(args.warmup // 2, 2), rotate, rank, world, dist,
