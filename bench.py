@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- Mpackets/s of device-resident parse + 5-tuple classify on MI355X.
 
-One step = one pass of the hot path (fb_parse_classify_dev: parse_packet_pcap + the per-packet
-part of process_parsed_packet, src/packets.rs:202-802) over one batch of synthetic frames that
-is already resident in HBM.  Default workload = BASELINE.json configs[1] (C2): 1,048,576 x 64-B
-IPv4/TCP frames per GPU.  Batches rotate over R distinct device buffers so the working set
-(> 1 GB) exceeds the 256 MB Infinity Cache and the timing is HBM-bound, not MALL-bound.
+One step = one pass of the hot path (k_parse_seg: parse_packet_pcap + the per-packet part of
+process_parsed_packet, src/packets.rs:202-802) over one batch of synthetic frames that is already
+resident in HBM.  Default workload = BASELINE.json configs[1] (C2): 1,048,576 x 64-B IPv4/TCP
+frames per GPU.  Batches rotate over R distinct device buffer sets (C2: 32, 4 GB) so the working
+set exceeds the 256 MB Infinity Cache and the timing is HBM-bound, not MALL-bound; consecutive
+steps share launches of up to 32 batches (fb_parse_classify_seg_batches_dev), split evenly.
 
 Multi-GPU: one process per GPU (torchrun); packets are sharded by index (each rank owns the
 contiguous range [rank*n, (rank+1)*n) of the virtual batch) with no data-path collective
@@ -25,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MAX_SEG_BATCHES = 32  # FB_MAX_SEG_BATCHES, include/flodbadd_gpu.h
 WORKLOADS = {
     2: "C2: 1,048,576 x 64-B IPv4/TCP frames per GPU, device-resident (BASELINE configs[1])",
     3: "C3: 1,048,576-frame IMIX 64/576/1500 (7:4:1), IPv4+IPv6, TCP+UDP per GPU, device-resident",
@@ -39,17 +41,28 @@ def algorithmic_bytes(offsets, n_session, n_dns):
     return int(np.minimum(caplen, 128).sum()) + 4 * len(offsets) + 56 * int(n_session) + 16 * int(n_dns)
 
 
+def plan_launches(k, bpl):
+    """Split k consecutive steps into ceil(k / bpl) launches of near-equal size (a short final
+    launch would pay the per-launch start-up and tail for a fraction of the batches)."""
+    if k <= 0:
+        return []
+    m = -(-k // bpl)
+    q, r = divmod(k, m)
+    return [q + 1] * r + [q] * (m - r)
+
+
 def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1,
                synth_kw=None):
-    """Time `steps` launches of the hot path.  mode "seg": fb_parse_classify_seg_dev (records
-    compacted per 64-frame wavefront segment, no cross-workgroup dependency); mode "dense":
-    fb_parse_classify_dev (one batch-wide compaction through a decoupled look-back).
-    flow=True (C4): the two stages of fb_process[_seg]_dev -- parse + classify, then the
-    session-table upsert with per-flow counters -- with an event between them so each stage is
-    timed.
-    bpl > 1 (mode "seg", no flow): each launch covers bpl batches (fb_parse_classify_seg_batches_dev,
-    one batch = one step, each with its own outputs and stats), so `steps` steps take
-    ceil(steps / bpl) launches."""
+    """Time `steps` steps (one step = one batch through the hot path).  mode "seg":
+    fb_parse_classify_seg_dev (records compacted per 64-frame wavefront segment, no
+    cross-workgroup dependency); mode "dense": fb_parse_classify_dev (the same kernel + the
+    batch-wide compaction of fb_compact.hip).  flow=True (C4): fb_process[_seg]_dev -- parse +
+    classify, then the session-table upsert -- with the context's stage event recorded between
+    the two, so each stage is timed inside the fused call.
+    bpl > 1 (mode "seg", no flow): consecutive steps share launches of up to bpl batches
+    (fb_parse_classify_seg_batches_dev; each batch its own outputs and stats), split evenly by
+    plan_launches.  Batch i uses buffer set i % rotate, so rotate >= bpl keeps the batches of a
+    launch distinct."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n, **(synth_kw or {}))
     nbytes = frames.nbytes
@@ -68,67 +81,58 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
         bufs.append((d_fr, d_off, d_out, d_dns, d_st))
 
-    if bpl > 1:
-        assert mode == "seg" and not flow and rotate % bpl == 0, (mode, flow, rotate, bpl)
-        groups = []
-        for j in range(rotate // bpl):
-            d = np.zeros(bpl, dtype=N.SEG_BATCH_DTYPE)
-            for t in range(bpl):
-                d_fr, d_off, d_out, d_seg, d_st = bufs[j * bpl + t]
-                d[t] = (d_fr.ptr.value, nbytes, d_off.ptr.value, n, 0, d_out.ptr.value, d_seg.ptr.value, 0,
-                        d_st.ptr.value)
-            groups.append(d)
+    def descriptors(first, count):
+        d = np.zeros(count, dtype=N.SEG_BATCH_DTYPE)
+        for t in range(count):
+            d_fr, d_off, d_out, d_seg, d_st = bufs[(first + t) % rotate]
+            d[t] = (d_fr.ptr.value, nbytes, d_off.ptr.value, n, 0, d_out.ptr.value, d_seg.ptr.value, 0, d_st.ptr.value)
+        return d
 
-    def launch(j, count):
-        """Launch j of a multi-batch run: batches j*bpl .. j*bpl+count-1."""
-        rc = lib.fb_parse_classify_seg_batches_dev(ctx, N.ptr(groups[j % len(groups)]), count, stream.ptr)
-        if rc != 0:
-            raise RuntimeError(lib.fb_last_error().decode())
-
-    def run_steps(k):
-        """k steps; returns the number of kernel launches."""
+    def plan(k):
+        """Launch descriptors of k steps, built before the timed region."""
         if bpl == 1:
+            return None
+        assert mode == "seg" and not flow and rotate >= bpl, (mode, flow, rotate, bpl)
+        out, first = [], 0
+        for c in plan_launches(k, bpl):
+            out.append((descriptors(first, c), c))
+            first += c
+        return out
+
+    def run_steps(k, launches):
+        """k steps; returns the number of kernel launches."""
+        if launches is None:
             for i in range(k):
                 step(i)
             return k
-        full, rest = divmod(k, bpl)
-        for j in range(full):
-            launch(j, bpl)
-        if rest:
-            launch(full, rest)
-        return full + (1 if rest else 0)
+        for d, c in launches:
+            rc = lib.fb_parse_classify_seg_batches_dev(ctx, d.ctypes.data, c, stream.ptr)
+            if rc != 0:
+                raise RuntimeError(lib.fb_last_error().decode())
+        return len(launches)
 
-    def step(i, ev=None):
+    def step(i):
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
         if mode == "seg" and flow:
             # fb_process_seg_dev: parse + session upsert in one call (the parse also hands each
             # record's table partition to the update's histogram pass)
             rc = lib.fb_process_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None, d_st.ptr,
                                         stream.ptr)
-            if ev is not None:
-                ev.record(stream)
-            if rc != 0:
-                raise RuntimeError(lib.fb_last_error().decode())
-            return
-        if mode == "seg":
+        elif mode == "seg":
             rc = lib.fb_parse_classify_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
                                                d_st.ptr, stream.ptr)
+        elif flow:
+            rc = lib.fb_process_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None, d_st.ptr,
+                                    stream.ptr)
         else:
             rc = lib.fb_parse_classify_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
                                            d_st.ptr, stream.ptr)
-        if rc == 0 and flow:
-            if ev is not None:
-                ev.record(stream)
-            if mode == "seg":
-                rc = lib.fb_flow_update_seg_dev(ctx, d_out.ptr, d_dns.ptr, n, d_st.ptr, stream.ptr)
-            else:
-                rc = lib.fb_flow_update_dev(ctx, d_out.ptr, d_st.ptr, stream.ptr)
         if rc != 0:
             raise RuntimeError(lib.fb_last_error().decode())
 
     if flow:
         N.check(lib.fb_flow_clear(ctx, stream.ptr))
-    run_steps(warmup)
+    run_steps(warmup, plan(warmup))
     stream.sync()
     st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
     if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
@@ -136,20 +140,28 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     if flow and int(st[0]["new_sessions"]) + int(st[0]["updated_sessions"]) != int(st[0]["n_session"]):
         raise RuntimeError("flow upsert lost records: %s" % st)
     ev0, ev1 = N.Event(), N.Event()
-    evs = [(N.Event(), N.Event(), N.Event()) for _ in range(steps)] if flow else None
+    launches = plan(steps)
+    if flow:
+        # per step: start, the stage event (recorded by the library between parse and update), end
+        evs = [(N.Event(), N.Event(), N.Event()) for _ in range(steps)]
+
+        def run_timed():
+            for i in range(steps):
+                evs[i][0].record(stream)
+                N.check(lib.fb_set_stage_event(ctx, evs[i][1].ptr))
+                step(i)
+                evs[i][2].record(stream)
+            N.check(lib.fb_set_stage_event(ctx, None))
+            return steps
+    else:
+        def run_timed():
+            return run_steps(steps, launches)
     if dist:
         dist.barrier()
     stream.sync()
     t0 = time.perf_counter()
     ev0.record(stream)
-    if flow:
-        for i in range(steps):
-            evs[i][0].record(stream)
-            step(i, evs[i][1])
-            evs[i][2].record(stream)
-        launches = steps
-    else:
-        launches = run_steps(steps)
+    n_launch = run_timed()
     ev1.record(stream)
     stream.sync()
     t1 = time.perf_counter()
@@ -171,20 +183,10 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         same = [k for k in st.dtype.names if k not in ("new_sessions", "updated_sessions")]
         assert all(int(st2[0][k]) == int(st[0][k]) for k in same), (st, st2)
         assert int(st2[0]["updated_sessions"]) + int(st2[0]["new_sessions"]) == int(st2[0]["n_session"])
+        # the parse stage as it runs inside the fused call (for fb_process_seg_dev: the
+        # partition-writing instance of k_parse_seg), the update the rest of the step
         parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps
         flow_ms = sum(b.elapsed_ms(c) for _, b, c in evs) / steps
-        if mode == "seg":
-            # one fused call per step: time the parse alone on the same batch, the update is the rest
-            step_ms = parse_ms + flow_ms
-            d_fr, d_off, d_out, d_dns, d_st = bufs[0]
-            p0, p1 = N.Event(), N.Event()
-            p0.record(stream)
-            for _ in range(5):
-                N.check(lib.fb_parse_classify_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr,
-                                                      None, d_st.ptr, stream.ptr))
-            p1.record(stream)
-            parse_ms = p0.elapsed_ms(p1) / 5
-            flow_ms = step_ms - parse_ms
         stage = dict(parse_ms=parse_ms, flow_ms=flow_ms)
         # ordered per-flow history of the last update (fb_flow_history_dev: keys + stable radix sort)
         slots = n if mode == "dense" else (n + 63) // 64 * 64
@@ -209,8 +211,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     for b in bufs:
         for x in b:
             x.free()
-    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage, launches=launches,
-                stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
+    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage,
+                launches=n_launch, stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
 def enrich_timing(N, lib, ctx, flows, stream, reps=5):
@@ -515,8 +517,11 @@ def main():
     ctx = C.c_void_p(ctx)
 
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
-    rotate = args.rotate or (8 if args.config == 2 else (4 if args.config == 3 else 1))
-    bpl = (args.batches_per_launch or rotate) if (args.mode == "seg" and args.config != 4) else 1
+    # C2: 32 distinct batches (4 GB, far past the 256 MB Infinity Cache), so any K <= 32 steps is
+    # one launch and longer runs are near-equal launches of up to 32 batches (plan_launches)
+    rotate = args.rotate or (32 if args.config == 2 else (12 if args.config == 3 else 1))
+    bpl = min(args.batches_per_launch or rotate, rotate, MAX_SEG_BATCHES) \
+        if (args.mode == "seg" and args.config != 4) else 1
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
                         flow=args.config == 4, mode=args.mode, bpl=bpl,
                         synth_kw=dict(zipf=1, zipf_s=args.zipf) if args.zipf else None)
@@ -530,6 +535,8 @@ def main():
     if main_r["stage"]:
         sg = main_r["stage"]
         extra["c4_stages"] = dict(parse_ms=round(sg["parse_ms"], 4), flow_update_ms=round(sg["flow_ms"], 4),
+                                  stages_note="split by the stage event fb_process%s_dev records between its "
+                                              "parse and its update" % ("_seg" if args.mode == "seg" else ""),
                                   history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
                                   enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
                                   enrich_tables=sg["enrich_tables"],
@@ -570,14 +577,15 @@ def main():
                                       roofline_frac=round(ro["algo_bytes"] / plo / 1e9 / HBM_PEAK_GBS, 4))
     if not args.no_imix and args.config == 2:
         steps3 = max(args.steps // 2, 10)
-        bpl3 = 4 if args.mode == "seg" and bpl > 1 else 1
-        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 4, rank, world, dist,
+        bpl3 = 12 if args.mode == "seg" and bpl > 1 else 1
+        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 12, rank, world, dist,
                         mode=args.mode, bpl=bpl3)
-        pl3 = r3["ev_ms"] / 1e3 / steps3
+        pl3 = r3["ev_ms"] / 1e3 / r3["launches"]
+        algo3 = r3["algo_bytes"] * steps3 / r3["launches"]
         extra["imix_c3"] = dict(value=round(world * (1 << 20) * steps3 / r3["elapsed"] / 1e6, 2),
                                 unit="Mpackets/s", ms_per_step=round(r3["elapsed"] * 1e3 / steps3, 4),
-                                roofline_achieved_GBs=round(r3["algo_bytes"] / pl3 / 1e9, 1),
-                                roofline_frac=round(r3["algo_bytes"] / pl3 / 1e9 / HBM_PEAK_GBS, 4),
+                                roofline_achieved_GBs=round(algo3 / pl3 / 1e9, 1),
+                                roofline_frac=round(algo3 / pl3 / 1e9 / HBM_PEAK_GBS, 4),
                                 batches_per_launch=bpl3, algo_bytes_per_batch=r3["algo_bytes"])
 
     if not args.no_host and rank == 0 and args.config == 2:

@@ -73,7 +73,7 @@ FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "
 
 FB_SEG_FRAMES = 64
 SEG_BYTES = FB_SEG_FRAMES * 56
-FB_MAX_SEG_BATCHES = 12
+FB_MAX_SEG_BATCHES = 32
 # fb_seg_batch: one batch of fb_parse_classify_seg_batches_dev (device pointers as integers)
 SEG_BATCH_DTYPE = np.dtype([("d_frames", "<u8"), ("frames_bytes", "<u8"), ("d_offsets", "<u8"), ("n", "<u4"),
                             ("reserved", "<u4"), ("d_out", "<u8"), ("d_seg", "<u8"), ("d_class", "<u8"),
@@ -147,6 +147,7 @@ GPU_SYMBOLS = [
     ("fb_set_service_bitmap", _I, [_P, _P]),
     ("fb_set_lan_v6", _I, [_P, _P, _U32]),
     ("fb_set_own_ips", _I, [_P, _P, _U32]),
+    ("fb_set_stage_event", _I, [_P, _P]),
     ("fb_parse_classify_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_parse_classify", _I, [_P, _P, _U64, _P, _U32, _P, _PU32, _P, _PU32, _P, _P, _P]),
     ("fb_process_parsed_dev", _I, [_P, _P, _U32, _P, _P, _P, _P]),
@@ -155,6 +156,7 @@ GPU_SYMBOLS = [
     ("fb_process_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_parse_classify_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_process_parsed_seg_dev", _I, [_P, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_seg_compact_dev", _I, [_P, _P, _P, _U32, _P, _P, _P]),
     ("fb_parse_classify_seg_batches_dev", _I, [_P, _P, _U32, _P]),
     ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),

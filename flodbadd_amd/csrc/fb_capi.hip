@@ -39,13 +39,18 @@ struct fb_ctx {
     DevConfig* h_cfg = nullptr;  // host shadow
     DevConfig* d_cfg = nullptr;
     bool cfg_dirty = true;
-    unsigned long long* d_status = nullptr;
-    uint64_t status_tiles = 0;
-    uint32_t epoch = 0;
-    // persistent parse kernel: grid = co-resident blocks (halved after a protocol failure)
-    uint32_t grid = 0;
+    unsigned long long* d_tick = nullptr;  // [kTickWords] k_parse_seg stats words
+    bool need_reset = true;       // zero the tick + error words before the next launch
+    uint32_t epoch = 0;           // parse launches so far: its parity picks the launch's error word
     uint32_t seg_grid = 0;        // streaming segmented kernel: co-resident blocks
-    uint32_t* d_error = nullptr;  // [2] error words, indexed by epoch parity
+    uint32_t* d_error = nullptr;  // [2] error words, indexed by launch parity
+    // dense output (fb_parse_classify_dev & co., fb_seg_compact_dev): segment counts + their scan
+    uint32_t* d_cseg = nullptr;            // [cseg_cap] segment counts (dense pass 1)
+    unsigned long long* d_cpre = nullptr;  // [cseg_cap] batch-wide offset of every segment
+    unsigned long long* d_ctsum = nullptr; // [seg_scan_tiles(cseg_cap)] scan tile sums
+    uint64_t cseg_cap = 0;                 // segments
+    hipEvent_t stage_event = nullptr;  // fb_set_stage_event (caller-owned): recorded between the
+                                       // parse and the update of fb_process[_seg]_dev
     // flow table
     FlowSlot* d_table = nullptr;
     uint64_t table_cap = 0;
@@ -98,6 +103,14 @@ struct fb_ctx {
 };
 
 int fbk::ctx_device(const fb_ctx* c) { return c->device; }
+
+// A call (or a ring batch) reported a nonzero device error word: the scratch the launches share
+// (stats tick words, error words) is zeroed before the context's next launch.
+int fbk::ctx_report_error(fb_ctx* c, uint64_t e) {
+    c->need_reset = true;
+    if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full (error word %llu)", (unsigned long long)e);
+    return set_err(FB_ERR_INTERNAL, "device error word %llu", (unsigned long long)e);
+}
 
 namespace fbk {
 bool build_blacklist_tables(const fb_cidr* nets, uint32_t n, std::vector<uint32_t>& p4,
@@ -180,25 +193,34 @@ static int upload_cfg(fb_ctx* c, hipStream_t s) {
     return FB_OK;
 }
 
-// Look-back scratch sized for `tiles`; (re)zeroed on growth and when the 8-bit epoch wraps.
-static int ensure_status(fb_ctx* c, uint64_t tiles, hipStream_t s) {
-    if (tiles <= c->status_tiles && c->epoch < kMaxEpoch) return FB_OK;
-    HIP_TRY(hipStreamSynchronize(s));
-    if (tiles > c->status_tiles) {
-        if (c->d_status) HIP_TRY(hipFree(c->d_status));
-        c->d_status = nullptr;
-        uint64_t want = std::max<uint64_t>(tiles, 1024);
-        if (hipMalloc(&c->d_status, scratch_words(want) * 8ull) != hipSuccess) {
-            c->status_tiles = 0;
-            return set_err(FB_ERR_NOMEM, "look-back scratch (%llu tiles)", (unsigned long long)want);
-        }
-        c->status_tiles = want;
-    }
-    // Stream-ordered: the launches run on `s`, which may be a non-blocking stream that does not
-    // synchronise with the null stream (a plain hipMemset here raced the next launch).
-    HIP_TRY(hipMemsetAsync(c->d_status, 0, scratch_words(c->status_tiles) * 8ull, s));
+// Zero the stats tick words and both error words before the next launch (at create, and after
+// a call reported an error).  Stream-ordered: the launches run on `s`, which may be a
+// non-blocking stream that does not synchronise with the null stream.
+static int reset_launch_scratch(fb_ctx* c, hipStream_t s) {
+    if (!c->need_reset) return FB_OK;
+    HIP_TRY(hipMemsetAsync(c->d_tick, 0, kTickWords * 8ull, s));
     HIP_TRY(hipMemsetAsync(c->d_error, 0, 16, s));
-    c->epoch = 0;  // epoch 0 is never used by a launch
+    c->need_reset = false;
+    return FB_OK;
+}
+
+// Scan scratch of the dense entry points, for batches of up to `n` frames (grown, never shrunk).
+static int ensure_compact_scratch(fb_ctx* c, uint64_t n, hipStream_t s) {
+    const uint64_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    if (nseg <= c->cseg_cap) return FB_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(c->d_cseg);
+    hipFree(c->d_cpre);
+    hipFree(c->d_ctsum);
+    c->d_cseg = nullptr;
+    c->d_cpre = nullptr;
+    c->d_ctsum = nullptr;
+    c->cseg_cap = 0;
+    const uint64_t want = std::max<uint64_t>(nseg, 1024);
+    if (hipMalloc(&c->d_cseg, want * 4ull) != hipSuccess || hipMalloc(&c->d_cpre, want * 8ull) != hipSuccess ||
+        hipMalloc(&c->d_ctsum, seg_scan_tiles((uint32_t)want) * 8ull) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "dense-output scratch (%llu segments)", (unsigned long long)want);
+    c->cseg_cap = want;
     return FB_OK;
 }
 
@@ -254,17 +276,8 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
     if (!c) { set_err(FB_ERR_NOMEM, "fb_ctx"); return nullptr; }
     c->device = device;
     {
-        // Residency: the occupancy API, capped by the SGPR rule of MI355X_MICROARCH.md
-        // ("Residency"): at most floor(800 / (sgpr_alloc + 16)) waves per SIMD, i.e. 6 at the
-        // 106-SGPR worst case, 24 per CU.  The kernel needs every block resident (look-back).
-        int bpc = 0;
-        if (occupancy_parse(&bpc) != hipSuccess || bpc < 1) bpc = 1;
-        int use = std::min(bpc, std::max(1, 24 / (int)parse_block_waves()));
-        if (const char* e = getenv("FB_BLOCKS_PER_CU")) {
-            const int want = atoi(e);
-            if (want >= 1 && want < use) use = want;
-        }
-        c->grid = std::min<uint32_t>((uint32_t)(use * prop.multiProcessorCount), kMaxBlocks);  // FB_BLOCKS_PER_CU: tuning cap
+        // The segmented kernel streams with no inter-workgroup wait; its grid is the co-resident
+        // block count only so that every block stays busy until the batch is done.
         int sb = 0;
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
@@ -282,6 +295,8 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
     }
     ok = ok && hipMalloc(&c->d_cfg, sizeof(DevConfig)) == hipSuccess;
     ok = ok && hipMalloc(&c->d_error, 16) == hipSuccess && hipMemset(c->d_error, 0, 16) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_tick, kTickWords * 8ull) == hipSuccess &&
+         hipMemset(c->d_tick, 0, kTickWords * 8ull) == hipSuccess;
     ok = ok && hipMalloc(&c->d_n, 16) == hipSuccess;
     if (ok && cfg->flow_capacity > kFlowMaxCapacity) {
         set_err(FB_ERR_INVAL, "flow_capacity %llu > %llu slots", (unsigned long long)cfg->flow_capacity,
@@ -301,10 +316,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
              hipMalloc(&c->d_partials, 2ull * c->flow_parts * 8ull) == hipSuccess;
         ok = ok && ensure_flow_scratch(c, cfg->max_batch_packets, nullptr) == FB_OK;
     }
-    if (ok) {
-        uint64_t tiles = ((uint64_t)cfg->max_batch_packets + parse_unit_frames() - 1) / parse_unit_frames();
-        ok = ensure_status(c, tiles, nullptr) == FB_OK && upload_cfg(c, nullptr) == FB_OK;
-    }
+    ok = ok && upload_cfg(c, nullptr) == FB_OK;
     if (!ok) {
         if (g_err[0] == 0) set_err(FB_ERR_NOMEM, "device allocation failed");
         fb_destroy(c);
@@ -318,7 +330,10 @@ int fb_destroy(fb_ctx* c) {
     DeviceGuard g(c->device);
     (void)hipDeviceSynchronize();
     hipFree(c->d_cfg);
-    hipFree(c->d_status);
+    hipFree(c->d_tick);
+    hipFree(c->d_cseg);
+    hipFree(c->d_cpre);
+    hipFree(c->d_ctsum);
     hipFree(c->d_error);
     hipFree(c->d_table);
     hipFree(c->d_entries);
@@ -372,6 +387,12 @@ int fb_set_lan_v6(fb_ctx* c, const fb_lan_v6* nets, uint32_t n) {
     return FB_OK;
 }
 
+int fb_set_stage_event(fb_ctx* c, void* event) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    c->stage_event = (hipEvent_t)event;  // the caller's event (fb_event_create); not owned
+    return FB_OK;
+}
+
 int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
     if (!c || n > FB_MAX_OWN_IPS || (n && !ips)) return set_err(FB_ERR_INVAL, "bad own-ip table");
     c->h_cfg->n_own = n;
@@ -380,83 +401,57 @@ int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
     return FB_OK;
 }
 
-// Shared launch of the parse/classify kernel (frames) or its parsed-packet instantiation.
-static int launch_batch(fb_ctx* c, ParseParams& p, uint32_t n, bool parsed, hipStream_t s) {
-    const uint64_t tiles = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
-    int rc = ensure_status(c, tiles, s);
+// Launch of the segmented streaming kernel over `sb` (frames, or the parsed packets `parsed`).
+// `want_parts`: one frame batch whose session table update follows (fb_process_seg_dev) -- the
+// kernel also writes each SESSION record slot's table partition, so the update's histogram pass
+// reads 4 B per record instead of the record.
+static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_parsed_pkt* parsed, hipStream_t s,
+                      bool want_parts = false, SegPass pass = SegPass::kSegments, fb_pkt_out* dense_out = nullptr,
+                      fb_dns_out* dense_dns = nullptr) {
+    int rc = reset_launch_scratch(c, s);
+    if (!rc) rc = upload_cfg(c, s);
+    if (!rc) rc = ensure_flow_scratch(c, n_max, s);
     if (rc) return rc;
-    rc = upload_cfg(c, s);
-    if (rc) return rc;
-    rc = ensure_flow_scratch(c, n, s);
-    if (rc) return rc;
-    c->last_n = n;
-    p.tagg = c->d_status;
-    p.wstat = p.tagg + c->status_tiles;
-    p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
-    p.tick = reinterpret_cast<uint32_t*>(p.rsum + rsum_words(c->status_tiles));
-    p.seg = nullptr;
+    c->last_n = n_max;
+    ParseParams p;
+    memset(&p, 0, sizeof(p));
+    p.pre = c->d_cpre;
+    p.dense_out = dense_out;
+    p.dense_dns = dense_dns;
+    p.parsed = parsed;
+    p.n = parsed ? sb.b[0].n : 0u;
+    p.rec_part = (want_parts && sb.count == 1u && c->d_table) ? c->d_rec_part : nullptr;
+    p.part_shift = c->flow_shift;
+    c->part_recs = p.rec_part ? sb.b[0].out : nullptr;
     p.cfg = c->d_cfg;
-    p.n = n;
-    p.num_tiles = (uint32_t)tiles;
-    p.epoch = ++c->epoch;
-    p.error = c->d_error + (p.epoch & 1u);
-    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
+    p.tick = c->d_tick;
+    // dense pass 2 belongs to pass 1's launch: same error word, no new parity
+    const uint32_t launch = pass == SegPass::kDenseOut ? c->epoch : ++c->epoch;
+    p.error = c->d_error + (launch & 1u);
+    p.error_next = c->d_error + ((launch & 1u) ^ 1u);
     p.dbg = nullptr;
-    const uint32_t grid = std::min<uint32_t>(p.num_tiles, c->grid);
-    if (parsed) HIP_TRY(launch_process_parsed(p, grid, s));
-    else HIP_TRY(launch_parse_classify(p, grid, s));
+    const uint32_t waves = parse_seg_block_threads() / 64u;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (sb.total_segs + waves - 1) / waves));
+    HIP_TRY(launch_parse_seg(p, sb, grid, s, pass));
     return FB_OK;
 }
 
-// Shared launch of the segmented streaming kernel (frames or parsed packets).
-static int launch_seg(fb_ctx* c, ParseParams& p, uint32_t n, hipStream_t s, const SegBatches* batches = nullptr,
-                      bool want_parts = false) {
-    const uint64_t units = ((uint64_t)n + parse_unit_frames() - 1) / parse_unit_frames();
-    int rc = ensure_status(c, units, s);
-    if (rc) return rc;
-    rc = upload_cfg(c, s);
-    if (rc) return rc;
-    rc = ensure_flow_scratch(c, n, s);
-    if (rc) return rc;
-    c->last_n = n;
-    // fb_process_seg_dev: the kernel also writes each SESSION record slot's table partition, so
-    // the update's histogram pass reads 4 B per record instead of the record
-    p.rec_part = (want_parts && !batches && c->d_table) ? c->d_rec_part : nullptr;
-    p.part_shift = c->flow_shift;
-    c->part_recs = p.rec_part ? p.out : nullptr;
-    p.tagg = c->d_status;
-    p.wstat = p.tagg + c->status_tiles;
-    p.rsum = p.wstat + 2ull * stat_slots(c->status_tiles);
-    p.tick = reinterpret_cast<uint32_t*>(p.rsum + rsum_words(c->status_tiles));
-    p.cfg = c->d_cfg;
-    p.n = n;
-    p.num_tiles = (uint32_t)units;
-    p.epoch = ++c->epoch;
-    p.error = c->d_error + (p.epoch & 1u);
-    p.error_next = c->d_error + ((p.epoch & 1u) ^ 1u);
-    p.dbg = nullptr;
+static SegBatches one_batch(const uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets, uint32_t n,
+                            fb_pkt_out* out, uint32_t* seg, uint8_t* cls, fb_batch_stats* stats) {
     SegBatches sb;
     memset(&sb, 0, sizeof(sb));
-    if (!batches) {  // one batch, described by p
-        sb.count = 1;
-        SegBatch& B = sb.b[0];
-        B.frames = p.frames;
-        B.offsets = p.offsets;
-        B.out = p.out;
-        B.seg = p.seg;
-        B.cls = p.cls;
-        B.stats = p.stats;
-        B.n = n;
-        B.frames_bytes = p.frames_bytes;
-        sb.total_segs = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
-    } else {
-        sb = *batches;
-    }
-    const uint32_t waves = parse_seg_block_threads() / 64u;
-    const uint32_t nseg = sb.total_segs;
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (nseg + waves - 1) / waves));
-    HIP_TRY(launch_parse_seg(p, sb, grid, s));
-    return FB_OK;
+    sb.count = 1;
+    SegBatch& B = sb.b[0];
+    B.frames = frames;
+    B.offsets = offsets;
+    B.out = out;
+    B.seg = seg;
+    B.cls = cls;
+    B.stats = stats;
+    B.n = n;
+    B.frames_bytes = (uint32_t)frames_bytes;
+    sb.total_segs = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    return sb;
 }
 
 int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, uint32_t count, void* stream) {
@@ -464,7 +459,8 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, ui
         return set_err(FB_ERR_INVAL, "ctx, batches and 1 <= count <= FB_MAX_SEG_BATCHES are required");
     SegBatches sb;
     memset(&sb, 0, sizeof(sb));
-    uint32_t segs = 0, n_max = 0;
+    uint64_t segs = 0;
+    uint32_t n_max = 0;
     for (uint32_t k = 0; k < count; ++k) {
         const fb_seg_batch& x = batches[k];
         if (!x.d_stats) return set_err(FB_ERR_INVAL, "batch %u: d_stats is required", k);
@@ -482,16 +478,15 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, ui
         B.stats = x.d_stats;
         B.n = x.n;
         B.frames_bytes = (uint32_t)x.frames_bytes;
-        B.seg_start = segs;
+        B.seg_start = (uint32_t)segs;
         segs += (x.n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
         n_max = std::max(n_max, x.n);
     }
+    if (segs > 0xFFFFFFFFull / FB_SEG_FRAMES) return set_err(FB_ERR_INVAL, "too many frames in one launch");
     sb.count = count;
-    sb.total_segs = segs;
+    sb.total_segs = (uint32_t)segs;
     DeviceGuard g(c->device);
-    ParseParams p;
-    memset(&p, 0, sizeof(p));
-    return launch_seg(c, p, n_max, (hipStream_t)stream, &sb);
+    return launch_seg(c, sb, n_max, nullptr, (hipStream_t)stream);
 }
 
 static int parse_seg(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets, uint32_t n,
@@ -508,17 +503,8 @@ static int parse_seg(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, 
         HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
         return FB_OK;
     }
-    ParseParams p;
-    p.parsed = nullptr;
-    p.frames = d_frames;
-    p.offsets = d_offsets;
-    p.out = d_out;
-    p.dns = nullptr;
-    p.cls = d_class;
-    p.stats = d_stats;
-    p.seg = d_seg;
-    p.frames_bytes = (uint32_t)frames_bytes;
-    return launch_seg(c, p, n, s, nullptr, want_parts);
+    return launch_seg(c, one_batch(d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats), n, nullptr,
+                      s, want_parts);
 }
 
 int fb_parse_classify_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
@@ -538,17 +524,44 @@ int fb_process_parsed_seg_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, 
         HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
         return FB_OK;
     }
-    ParseParams p;
-    p.parsed = d_in;
-    p.frames = nullptr;
-    p.offsets = nullptr;
-    p.out = d_out;
-    p.dns = nullptr;
-    p.cls = d_class;
-    p.stats = d_stats;
-    p.seg = d_seg;
-    p.frames_bytes = 0;
-    return launch_seg(c, p, n, s);
+    return launch_seg(c, one_batch(nullptr, 0, nullptr, n, d_out, d_seg, d_class, d_stats), n, d_in, s);
+}
+
+int fb_seg_compact_dev(fb_ctx* c, const fb_pkt_out* d_seg_out, const uint32_t* d_seg, uint32_t n, fb_pkt_out* d_out,
+                       fb_dns_out* d_dns, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (n && (!d_seg_out || !d_seg)) return set_err(FB_ERR_INVAL, "d_seg_out and d_seg are required");
+    if (n == 0 || (!d_out && !d_dns)) return FB_OK;
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_compact_scratch(c, n, s);
+    if (rc) return rc;
+    HIP_TRY(launch_seg_compact(d_seg_out, d_seg, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES, c->d_cpre, c->d_ctsum,
+                               d_out, d_dns, s));
+    return FB_OK;
+}
+
+// Dense output in two passes of the segmented kernel (fb_compact.hip): pass 1 counts every 64-frame
+// segment (classes and batch stats too), the scan turns the counts into batch-wide offsets, pass 2
+// parses again and stores each record at its offset -- at C2 the frames are still in the Infinity
+// Cache for pass 2.  No kernel of the path waits on another workgroup.
+static int parse_dense(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                       const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns, uint8_t* d_class,
+                       fb_batch_stats* d_stats, hipStream_t s) {
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
+        return FB_OK;
+    }
+    int rc = ensure_compact_scratch(c, n, s);
+    if (rc) return rc;
+    rc = launch_seg(c, one_batch(d_frames, frames_bytes, d_offsets, n, nullptr, c->d_cseg, d_class, d_stats), n, d_in,
+                    s, false, SegPass::kCount);
+    if (rc || (!d_out && !d_dns)) return rc;
+    const uint32_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    HIP_TRY(launch_seg_scan(c->d_cseg, nseg, c->d_cpre, c->d_ctsum, s));
+    return launch_seg(c, one_batch(d_frames, frames_bytes, d_offsets, n, nullptr, nullptr, nullptr, nullptr), n, d_in, s,
+                      false, SegPass::kDenseOut, d_out, d_dns);
 }
 
 int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes,
@@ -560,21 +573,8 @@ int fb_parse_classify_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_by
     if (n && !d_offsets) return set_err(FB_ERR_INVAL, "d_offsets is NULL");
     if (n && frames_bytes && !d_frames) return set_err(FB_ERR_INVAL, "d_frames is NULL");
     DeviceGuard g(c->device);
-    hipStream_t s = (hipStream_t)stream;
-    if (n == 0) {
-        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
-        return FB_OK;
-    }
-    ParseParams p;
-    p.parsed = nullptr;
-    p.frames = d_frames;
-    p.offsets = d_offsets;
-    p.out = d_out;
-    p.dns = d_dns;
-    p.cls = d_class;
-    p.stats = d_stats;
-    p.frames_bytes = (uint32_t)frames_bytes;
-    return launch_batch(c, p, n, false, s);
+    return parse_dense(c, d_frames, frames_bytes, d_offsets, nullptr, n, d_out, d_dns, d_class, d_stats,
+                       (hipStream_t)stream);
 }
 
 int fb_process_parsed_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out,
@@ -583,21 +583,7 @@ int fb_process_parsed_dev(fb_ctx* c, const fb_parsed_pkt* d_in, uint32_t n, fb_p
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
     if (n && !d_in) return set_err(FB_ERR_INVAL, "d_in is NULL");
     DeviceGuard g(c->device);
-    hipStream_t s = (hipStream_t)stream;
-    if (n == 0) {
-        HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
-        return FB_OK;
-    }
-    ParseParams p;
-    p.parsed = d_in;
-    p.frames = nullptr;
-    p.offsets = nullptr;
-    p.out = d_out;
-    p.dns = nullptr;
-    p.cls = d_class;
-    p.stats = d_stats;
-    p.frames_bytes = 0;
-    return launch_batch(c, p, n, true, s);
+    return parse_dense(c, nullptr, 0, nullptr, d_in, n, d_out, nullptr, d_class, d_stats, (hipStream_t)stream);
 }
 
 static int ensure_staging(fb_ctx* c, uint64_t n, uint64_t bytes) {
@@ -630,12 +616,7 @@ static int check_error_word(fb_ctx* c, hipStream_t s) {
     uint32_t e = 0;
     HIP_TRY(hipMemcpyAsync(&e, c->d_error + (c->epoch & 1u), 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (e) {
-        c->epoch = kMaxEpoch;  // force a scratch + error-word reset before the next launch
-        if (e & 1u) c->grid = std::max<uint32_t>(c->grid / 2u, 1u);  // look-back starved: shrink
-        if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full");
-        return set_err(FB_ERR_INTERNAL, "kernel bounded spin expired (code %u)", e);
-    }
+    if (e) return ctx_report_error(c, e);
     return FB_OK;
 }
 
@@ -775,6 +756,8 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     int rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
+    if (rc == FB_OK && c->stage_event) rc = hipEventRecord(c->stage_event, (hipStream_t)stream) == hipSuccess
+                                                ? FB_OK : set_err(FB_ERR_HIP, "stage event record failed");
     if (rc == FB_OK) rc = n == 0 ? empty_update(c) : fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
     c->part_recs = nullptr;  // the partitions serve this update only
     return rc;
@@ -788,6 +771,7 @@ int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, co
     if (!d_out) return set_err(FB_ERR_INVAL, "d_out is required");
     int rc = fb_parse_classify_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_dns, d_class, d_stats, stream);
     if (rc) return rc;
+    if (c->stage_event) HIP_TRY(hipEventRecord(c->stage_event, (hipStream_t)stream));
     if (n == 0) return empty_update(c);
     return fb_flow_update_dev(c, d_out, d_stats, stream);
 }

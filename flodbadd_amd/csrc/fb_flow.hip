@@ -106,9 +106,9 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
             if (!slot_valid(P, base + k)) continue;
             const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
-            const uint4 a = *reinterpret_cast<const uint4*>(r);
-            const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
-            const uint2 c = *reinterpret_cast<const uint2*>(r + 8);
+            const uint4 a = ld_u4(r);
+            const uint4 b = ld_u4(r + 4);
+            const uint2 c = ld_u2(r + 8);
             const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
             atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
         }
@@ -138,10 +138,10 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
         if (!slot_valid(P, base + k)) continue;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
-        const uint4 a = *reinterpret_cast<const uint4*>(r);
-        const uint4 b = *reinterpret_cast<const uint4*>(r + 4);
-        const uint4 c = *reinterpret_cast<const uint4*>(r + 8);  // key 8,9 | packet_length | ip_packet_length
-        const uint2 m = *reinterpret_cast<const uint2*>(r + 12);  // flags | meta | hist_char, pkt_index
+        const uint4 a = ld_u4(r);
+        const uint4 b = ld_u4(r + 4);
+        const uint4 c = ld_u4(r + 8);   // key 8,9 | packet_length | ip_packet_length
+        const uint2 m = ld_u2(r + 12);  // flags | meta | hist_char, pkt_index
         const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
         const unsigned long long fh = flow_hash_words(key);
         const uint32_t d = atomicAdd(&hist[part_of(fh, P.part_shift)], 1u);
@@ -411,7 +411,7 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
     if (first == ~0u) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
     auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
-        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
+        return ld_u2(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
     };
     const uint32_t flags = q[kScMask];
     unsigned long long end_seen;

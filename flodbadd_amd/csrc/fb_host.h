@@ -10,6 +10,9 @@ namespace fbk {
 int set_err(int code, const char* fmt, ...);
 // The device a context was created on.
 int ctx_device(const fb_ctx* c);
+// Record a nonzero device error word `e` of a call or ring batch: the context zeroes its launch
+// scratch before the next launch; returns the matching fb_err (FB_ERR_TABLE_FULL / INTERNAL).
+int ctx_report_error(fb_ctx* c, uint64_t e);
 
 struct DeviceGuard {
     int prev = -1;

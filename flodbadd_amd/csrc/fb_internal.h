@@ -8,23 +8,9 @@
 
 namespace fbk {
 
-// Upper bound on parse blocks per launch (per-block stats slots).
-constexpr uint32_t kMaxBlocks = 4096;
-
-// Look-back scratch (one allocation per context, zeroed when the 8-bit epoch wraps):
-//   tagg[units]           unit status   [epoch:8 | INC:1 | n_dns:27 | n_session:28]
-//   wstat[slots][2]       per-block pre-filter counters (slots = stat_slots(units)) [epoch:8 | n_tcp:28 | n_filtered:28],
-//                                                      [epoch:8 | n_bad:28 | n_ipv4:28]
-// Epoch-tagged words need no per-launch zeroing.
-constexpr uint32_t kMaxEpoch = 255;
-// Stats slots: one pair per block, and a grid never exceeds max(kMaxBlocks, units).
-inline uint64_t stat_slots(uint64_t units) { return units > kMaxBlocks ? units : kMaxBlocks; }
-//   rsum[rsum_words(units)]  k_parse_ws: per-round sums of unit aggregates (round r = units
-//                          [r*G, (r+1)*G)) [epoch:8 | 0 | n_dns:27 | n_session:28];
-//                          k_parse_seg: 3 epoch-tagged partial-count words per block
-//   tick[128 u64]         k_parse_seg packed stats words, 8 per batch of a launch
-inline uint64_t rsum_words(uint64_t units) { return units > 4ull * kMaxBlocks ? units : 4ull * kMaxBlocks; }
-inline uint64_t scratch_words(uint64_t units) { return units + 2ull * stat_slots(units) + rsum_words(units) + 128ull; }
+// Launch scratch (one allocation per context): tick[8 * FB_MAX_SEG_BATCHES] u64, k_parse_seg's
+// packed per-batch stats words; the block that completes a word zeroes it for the next launch.
+constexpr uint32_t kTickWords = 8u * FB_MAX_SEG_BATCHES;
 
 // Device-resident configuration (uploaded lazily, stream-ordered, before a launch).
 struct LanV6 {
@@ -44,30 +30,35 @@ struct DevConfig {
 };
 constexpr uint32_t kCfgLdsBytes = 16u + FB_SERVICE_BITMAP_BYTES;
 
+// Per-launch parameters of k_parse_seg beside its batch descriptors (SegBatches).
 struct ParseParams {
-    const fb_parsed_pkt* parsed;  // parsed-packet path (fb_process_parsed*) instead of frames
-    const uint8_t* frames;
-    const uint32_t* offsets;
-    fb_pkt_out* out;
-    fb_dns_out* dns;
-    uint8_t* cls;
-    fb_batch_stats* stats;
-    unsigned long long* tagg;   // [units]
-    unsigned long long* wstat;  // [kMaxBlocks][2]
-    unsigned long long* rsum;   // [rounds] round sums (k_parse_ws look-back) / block partials (k_parse_seg)
-    uint32_t* tick;             // k_parse_seg: 8 packed u64 stats words per batch of the launch
-    uint32_t* seg;              // k_parse_seg: per 64-frame segment, n_session | n_dns << 16
+    const fb_parsed_pkt* parsed;  // parsed-packet instance (fb_process_parsed*): the input records
+    uint32_t n;                   // parsed-packet instance: records in `parsed`
+    uint32_t part_shift;          // FlowParams::part_shift of the context's table
     const DevConfig* cfg;
-    uint32_t frames_bytes;  // min(frames_bytes, 2^32 - 1)
-    uint32_t n;
-    uint32_t num_tiles;
-    uint32_t epoch;
-    uint32_t* error;       // this launch's error word (epoch parity); nonzero: a bounded spin expired
-    uint32_t* error_next;  // the other parity's word, zeroed by this launch for the next one
-    unsigned long long* dbg;  // diagnostic stamps (ablation builds only; nullptr in the product)
-    uint32_t* rec_part;       // k_parse_seg (one batch): partition of each SESSION record slot, or nullptr
-    uint32_t part_shift;      // FlowParams::part_shift of the context's table
+    unsigned long long* tick;     // [kTickWords] packed stats words, 8 per batch of the launch
+    uint32_t* error;              // this launch's error word (launch parity); set by the flow kernels
+    uint32_t* error_next;         // the other parity's word, zeroed by this launch for the next one
+    unsigned long long* dbg;      // diagnostic stamps (ablation builds only; nullptr in the product)
+    uint32_t* rec_part;           // one batch: partition of each SESSION record slot, or nullptr
+    const unsigned long long* pre;  // dense pass 2: per segment n_session | n_dns << 32 before it
+    fb_pkt_out* dense_out;        // dense pass 2: batch-wide SESSION records (or nullptr)
+    fb_dns_out* dense_dns;        // dense pass 2: batch-wide DNS records (or nullptr)
 };
+// 16 / 8 bytes at a 4-B aligned address: 56-B records (fb_pkt_out, fb_parsed_pkt) are only 8-B
+// aligned at odd indices, so a uint4 dereference there would claim an alignment the data lacks
+// (undefined behaviour the compiler did act on: a k_parse_seg instance read a parsed record's
+// words rotated by one until its loads went through byte offsets).
+__device__ __forceinline__ uint4 ld_u4(const uint32_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+__device__ __forceinline__ uint2 ld_u2(const uint32_t* p) {
+    uint2 v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
 
 // is_lan_ip, src/ip.rs:55-156, 199-242.
 __device__ __forceinline__ bool lan_v4(uint32_t v) {
@@ -228,15 +219,22 @@ struct FlowParams {
                                 // histogram pass then reads 4 B per record instead of the record
 };
 
-// Launchers (fb_parse.hip / fb_flow.hip).
-hipError_t launch_parse_classify(const ParseParams& p, uint32_t grid, hipStream_t s);
-hipError_t launch_process_parsed(const ParseParams& p, uint32_t grid, hipStream_t s);
-hipError_t occupancy_parse(int* blocks_per_cu);
-hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s);
+// Launchers (fb_parse.hip / fb_compact.hip / fb_flow.hip).
+// Which k_parse_seg instance: the segmented output; dense pass 1 (segment counts, classes, stats);
+// dense pass 2 (records to batch-wide positions from the scanned counts, ParseParams::pre).
+enum class SegPass { kSegments, kCount, kDenseOut };
+hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s,
+                            SegPass pass = SegPass::kSegments);
 hipError_t occupancy_parse_seg(int* blocks_per_cu);
 uint32_t parse_seg_block_threads();
-uint32_t parse_unit_frames();  // frames per look-back unit of the product parse kernel
-uint32_t parse_block_waves();  // waves per block of the product parse kernel
+// Exclusive scan of segment count words into pre[nseg] (u64 n_session | n_dns << 32), and the
+// dense copy of a segmented batch (fb_seg_compact_dev); out / dns may each be NULL.
+// tsum: scratch of seg_scan_tiles(nseg) words.
+uint32_t seg_scan_tiles(uint32_t nseg);
+hipError_t launch_seg_scan(const uint32_t* seg, uint32_t nseg, unsigned long long* pre, unsigned long long* tsum,
+                           hipStream_t s);
+hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, uint32_t nseg, unsigned long long* pre,
+                              unsigned long long* tsum, fb_pkt_out* out, fb_dns_out* dns, hipStream_t s);
 hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);

@@ -6,7 +6,7 @@
 // 1183-1249), then parses and upserts it one at a time.  Here the reader appends frames into the
 // current batch of a ring of page-locked (pinned) batches; a full batch is submitted as one
 // pipeline step -- H2D of frames + offsets on a copy stream, then parse + classify + session-table
-// upsert (fb_process_dev) on the context's compute stream, then the batch stats (and the DNS side
+// upsert (fb_process_seg_dev) on the context's compute stream, then the batch stats (and the DNS side
 // records, if any) back -- while the reader fills the next batch.  When every batch is in flight
 // the reader waits for the oldest one instead of dropping packets.  The session table stays in
 // HBM (read with fb_flow_export), so per frame only its bytes and offset cross PCIe.
@@ -33,8 +33,9 @@ struct RingSlot {
     fb_batch_stats* h_stats = nullptr;
     uint8_t* d_frames = nullptr;
     uint32_t* d_offsets = nullptr;
-    fb_pkt_out* d_out = nullptr;
-    fb_dns_out* d_dns = nullptr;
+    fb_pkt_out* d_out = nullptr;   // segmented records (ceil(max_packets / 64) * 64 slots)
+    uint32_t* d_seg = nullptr;     // segment counts
+    fb_dns_out* d_dns = nullptr;   // the batch's DNS side records, compacted
     fb_batch_stats* d_stats = nullptr;
     hipEvent_t ev_h2d = nullptr, ev_done = nullptr;
     uint32_t n = 0;
@@ -72,6 +73,7 @@ void free_slot(RingSlot& s) {
     (void)hipFree(s.d_frames);
     (void)hipFree(s.d_offsets);
     (void)hipFree(s.d_out);
+    (void)hipFree(s.d_seg);
     (void)hipFree(s.d_dns);
     (void)hipFree(s.d_stats);
     if (s.ev_h2d) (void)hipEventDestroy(s.ev_h2d);
@@ -81,13 +83,15 @@ void free_slot(RingSlot& s) {
 
 bool alloc_slot(RingSlot& s, const fb_ring_config& c) {
     const uint64_t np = c.max_packets;
+    const uint64_t nseg = (np + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
     return hipHostMalloc((void**)&s.h_frames, std::max<uint64_t>(c.max_bytes, 1), hipHostMallocDefault) == hipSuccess &&
            hipHostMalloc((void**)&s.h_offsets, (np + 1) * 4, hipHostMallocDefault) == hipSuccess &&
            hipHostMalloc((void**)&s.h_dns, np * sizeof(fb_dns_out), hipHostMallocDefault) == hipSuccess &&
            hipHostMalloc((void**)&s.h_stats, sizeof(fb_batch_stats), hipHostMallocDefault) == hipSuccess &&
            hipMalloc((void**)&s.d_frames, std::max<uint64_t>(c.max_bytes, 1)) == hipSuccess &&
            hipMalloc((void**)&s.d_offsets, (np + 1) * 4) == hipSuccess &&
-           hipMalloc((void**)&s.d_out, np * sizeof(fb_pkt_out)) == hipSuccess &&
+           hipMalloc((void**)&s.d_out, nseg * FB_SEG_FRAMES * sizeof(fb_pkt_out)) == hipSuccess &&
+           hipMalloc((void**)&s.d_seg, nseg * 4) == hipSuccess &&
            hipMalloc((void**)&s.d_dns, np * sizeof(fb_dns_out)) == hipSuccess &&
            hipMalloc((void**)&s.d_stats, sizeof(fb_batch_stats)) == hipSuccess &&
            hipEventCreateWithFlags(&s.ev_h2d, hipEventDisableTiming) == hipSuccess &&
@@ -138,9 +142,7 @@ int complete(fb_ring* r, RingSlot& s) {
     }
     s.n = 0;
     s.bytes = 0;
-    if (st.error)
-        return set_err((st.error & 4u) ? FB_ERR_TABLE_FULL : FB_ERR_INTERNAL, "ring batch error word %llu",
-                       (unsigned long long)st.error);
+    if (st.error) return ctx_report_error(r->ctx, st.error);
     return FB_OK;
 }
 
@@ -155,11 +157,14 @@ int submit(fb_ring* r) {
         HIP_TRY(hipMemcpyAsync(s.d_offsets, s.h_offsets, (uint64_t)(s.n + 1) * 4, hipMemcpyHostToDevice, r->copy));
         HIP_TRY(hipEventRecord(s.ev_h2d, r->copy));
         HIP_TRY(hipStreamWaitEvent(r->compute, s.ev_h2d, 0));
+        // segmented parse (+ session upsert), then only the DNS side records compacted for the
+        // read-back: no kernel of the step waits on another workgroup
         rc = (r->cfg.flags & FB_RING_NO_FLOW)
-                 ? fb_parse_classify_dev(r->ctx, s.d_frames, s.bytes, s.d_offsets, s.n, s.d_out, s.d_dns, nullptr,
-                                         s.d_stats, r->compute)
-                 : fb_process_dev(r->ctx, s.d_frames, s.bytes, s.d_offsets, s.n, s.d_out, s.d_dns, nullptr,
-                                  s.d_stats, r->compute);
+                 ? fb_parse_classify_seg_dev(r->ctx, s.d_frames, s.bytes, s.d_offsets, s.n, s.d_out, s.d_seg, nullptr,
+                                             s.d_stats, r->compute)
+                 : fb_process_seg_dev(r->ctx, s.d_frames, s.bytes, s.d_offsets, s.n, s.d_out, s.d_seg, nullptr,
+                                      s.d_stats, r->compute);
+        if (!rc) rc = fb_seg_compact_dev(r->ctx, s.d_out, s.d_seg, s.n, nullptr, s.d_dns, r->compute);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(s.h_stats, s.d_stats, sizeof(fb_batch_stats), hipMemcpyDeviceToHost, r->compute));
         HIP_TRY(hipEventRecord(s.ev_done, r->compute));

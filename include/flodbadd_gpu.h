@@ -153,9 +153,9 @@ typedef struct fb_batch_stats {
     uint64_t n_drop;           /* parse_packet_pcap -> None                                   */
     uint64_t n_filtered;       /* rejected by the session filter                              */
     uint64_t bad_offsets;      /* frames with invalid offsets (counted in n_drop too)         */
-    uint64_t error;            /* nonzero = failure bits: 1|2 bounded spin expired (FB_ERR_INTERNAL),
-                                  4 flow-table partition full (FB_ERR_TABLE_FULL), 8 more records
-                                  than the update scratch of the last parse launch holds     */
+    uint64_t error;            /* nonzero = failure bits: 4 flow-table partition full
+                                  (FB_ERR_TABLE_FULL), 8 more records than the update scratch of
+                                  the last parse launch holds (FB_ERR_INTERNAL)               */
     uint64_t reserved[3];
 } fb_batch_stats; /* 128 bytes */
 
@@ -250,6 +250,10 @@ int fb_set_filter(fb_ctx* ctx, uint32_t filter);                 /* set_filter, 
 int fb_set_service_bitmap(fb_ctx* ctx, const uint8_t* bitmap);   /* CloudModel update, port_vulns.rs:350-380 */
 int fb_set_lan_v6(fb_ctx* ctx, const fb_lan_v6* nets, uint32_t n); /* init_local_cache, ip.rs:164 */
 int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
+/* Profiling hook (the reference's PACKET_STATS timing role, src/packets.rs:28-83): when `event`
+ * (from fb_event_create, caller-owned; NULL clears) is set, fb_process_dev / fb_process_seg_dev
+ * record it on their stream between the parse and the session-table update. */
+int fb_set_stage_event(fb_ctx* ctx, void* event);
 
 /*
  * Device-resident parse + classify (parse_packet_pcap + the per-packet part of
@@ -259,6 +263,8 @@ int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
  *   d_dns   : >= n fb_dns_out, class-DNS records, packet order
  *   d_class : n bytes, fb_class of every frame
  *   d_stats : one fb_batch_stats (overwritten, not accumulated)
+ * Runs the segmented kernel into context scratch, then fb_seg_compact_dev's compaction: no
+ * kernel waits on another workgroup, so the call is safe on a GPU shared with other work.
  */
 int fb_parse_classify_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                           const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out,
@@ -331,7 +337,7 @@ int fb_parse_classify_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t fra
  * once.  `batches` is a HOST array of `count` (1..FB_MAX_SEG_BATCHES) descriptors holding DEVICE
  * pointers; each batch follows the fb_parse_classify_seg_dev rules.  Asynchronous.
  */
-#define FB_MAX_SEG_BATCHES 12u
+#define FB_MAX_SEG_BATCHES 32u
 typedef struct fb_seg_batch {
     const uint8_t* d_frames;
     uint64_t frames_bytes;     /* < 4 GiB */
@@ -344,6 +350,14 @@ typedef struct fb_seg_batch {
     fb_batch_stats* d_stats;   /* required */
 } fb_seg_batch;                /* 64 bytes */
 int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, uint32_t count, void* stream);
+
+/* Dense records from a segmented batch of n frames (d_seg_out / d_seg of the calls above): the
+ * SESSION records into d_out and the DNS side records into d_dns, batch-wide packet order, as
+ * fb_parse_classify_dev lays them out (either may be NULL).  The counts are those of the
+ * segments (= n_session / n_dns of the batch's stats).  DEVICE pointers, asynchronous; one
+ * compaction at a time per context (it uses context scratch). */
+int fb_seg_compact_dev(fb_ctx* ctx, const fb_pkt_out* d_seg_out, const uint32_t* d_seg, uint32_t n,
+                       fb_pkt_out* d_out, fb_dns_out* d_dns, void* stream);
 
 /* fb_process_parsed_dev with segmented output (same segment layout; no DNS records). */
 int fb_process_parsed_seg_dev(fb_ctx* ctx, const fb_parsed_pkt* d_in, uint32_t n,

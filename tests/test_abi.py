@@ -86,3 +86,11 @@ def test_flow_hash_is_deterministic_and_host_side():
     assert h1 == h2 and h1 != 0
     k[0]["dst_port"] = 81
     assert lib.fb_flow_hash(N.ptr(k)) != h1
+
+
+def test_header_constants_match_python():
+    import re
+    hdr = open(os.path.join(ROOT, "include", "flodbadd_gpu.h")).read()
+    for name in ("FB_MAX_SEG_BATCHES", "FB_SEG_FRAMES", "FB_ABI_VERSION"):
+        m = re.search(r"#define %s (\d+)u" % name, hdr)
+        assert m and int(m.group(1)) == getattr(N, name), name

@@ -2,7 +2,7 @@
 # GPU box: one rocprofv3 --pmc pass over ubench_ws (counters given in $PMC), summary via sqlite.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); mkdir -p gpurun_out/pmc; export TMPDIR=/tmp
-V=${V:-8_1_4}; TAG=${TAG:-a}
+V=${V:-8_3}; TAG=${TAG:-a}
 cd "$R"
 timeout -s KILL 120 rocprofv3 --pmc $PMC -d $R/gpurun_out/pmc/$TAG -o run -- $R/tools/ubench_ws_$V 2 1048576 8 20 > $R/gpurun_out/pmc/$TAG.log 2>&1
 rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 $R/gpurun_out/pmc/$TAG.log; exit 1; }

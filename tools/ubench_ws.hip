@@ -1,13 +1,9 @@
-// ubench_ws.hip -- timing + per-tick stamps of the role-specialised parse kernel (tooling, not
+// ubench_ws.hip -- timing + per-wave stamps of the segmented parse kernel (tooling, not
 // product).  Includes the product kernel source and times, interleaved in one process:
-//   ws            the product kernel (k_parse_ws<false>)
-//   ws_no_lb      look-back replaced by a fixed prefix (wrong output, timing only)
-//   ws_no_store   storer waves idle
-//   ws_no_lb_st   both
 //   read / copy   plain streaming read of the frame buffer / read frames + write 56 B per frame
-// then one stamped run: per tick, quantiles over blocks of the tick length and of each role's
-// busy time (loader: tick start -> classify + prefetch issued; look-back: -> prefix published;
-// storers: -> last store issued).
+//   seg           the product kernel (k_parse_seg<false>)
+//   seg_no_store, seg_no_classify, seg_no_classify_no_store   ablations (timing only)
+// then one stamped run: per-wave prologue / exit quantiles, by XCD and by dispatch third.
 //   build: tools/build_ubench_ws.sh ; run: tools/ubench_ws [config_id] [n] [rotate] [iters]
 #include "../flodbadd_amd/csrc/fb_parse.hip"
 
@@ -83,23 +79,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dcfg, sizeof(hc)));
     CK(hipMemcpy(dcfg, &hc, sizeof(hc), hipMemcpyHostToDevice));
 
-    const uint32_t units = (n + fbk::kWsUnit - 1) / fbk::kWsUnit;
-    const size_t swords = fbk::scratch_words(units);
-    unsigned long long* status;
-    CK(hipMalloc(&status, swords * 8));
-    CK(hipMemset(status, 0, swords * 8));
+    unsigned long long* tick;
+    CK(hipMalloc(&tick, fbk::kTickWords * 8));
+    CK(hipMemset(tick, 0, fbk::kTickWords * 8));
     uint32_t* err;
     CK(hipMalloc(&err, 16));
     CK(hipMemset(err, 0, 16));
-    int bpc = 0;
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (fbk::k_parse_ws<false>), fbk::kWsThreads, 0));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
-    const uint32_t grid = std::min<uint32_t>(units, (uint32_t)(std::max(bpc, 1) * prop.multiProcessorCount));
-    unsigned long long* dbg;
-    const size_t dbg_words = (size_t)grid * fbk::kWsDbgUnits * 4;
-    CK(hipMalloc(&dbg, dbg_words * 8));
-    CK(hipMemset(dbg, 0, dbg_words * 8));
     unsigned* sink;
     CK(hipMalloc(&sink, 16));
     struct Buf { uint8_t* fr; uint32_t* off; fb_pkt_out* out; fb_dns_out* dns; fb_batch_stats* st; };
@@ -115,35 +102,31 @@ int main(int argc, char** argv) {
     }
     hipStream_t s;
     CK(hipStreamCreate(&s));
-    uint32_t epoch = 0;
-    auto params = [&](int r) {
+    uint32_t launch = 0;
+    auto params = [&]() {
         fbk::ParseParams p;
-        p.frames = bufs[r].fr; p.offsets = bufs[r].off; p.out = bufs[r].out; p.dns = bufs[r].dns;
-        p.cls = nullptr; p.stats = bufs[r].st; p.cfg = dcfg;
-        p.tagg = status; p.wstat = status + units; p.rsum = p.wstat + 2ull * fbk::stat_slots(units); p.tick = reinterpret_cast<uint32_t*>(p.rsum + fbk::rsum_words(units)); p.seg = nullptr;
-        p.frames_bytes = (uint32_t)bytes; p.n = n; p.num_tiles = units; p.parsed = nullptr;
-        if (++epoch > 255) { CK(hipStreamSynchronize(s)); CK(hipMemset(status, 0, swords * 8)); CK(hipMemset(err, 0, 16)); epoch = 1; }
-        p.epoch = epoch;
-        p.error = err + (epoch & 1u); p.error_next = err + ((epoch & 1u) ^ 1u); p.dbg = dbg;
+        memset(&p, 0, sizeof(p));
+        p.cfg = dcfg;
+        p.tick = tick;
+        ++launch;
+        p.error = err + (launch & 1u); p.error_next = err + ((launch & 1u) ^ 1u); p.dbg = nullptr;
         return p;
     };
-    auto sb1 = [&](const fbk::ParseParams& p) {  // one-batch launch descriptor of k_parse_seg
+    auto sb1 = [&](int r, uint32_t* seg) {  // one-batch launch descriptor of k_parse_seg
         fbk::SegBatches sb;
         memset(&sb, 0, sizeof(sb));
         sb.count = 1;
-        sb.b[0].frames = p.frames; sb.b[0].offsets = p.offsets; sb.b[0].out = p.out; sb.b[0].seg = p.seg;
-        sb.b[0].cls = p.cls; sb.b[0].stats = p.stats; sb.b[0].n = p.n; sb.b[0].frames_bytes = p.frames_bytes;
-        sb.total_segs = (p.n + 63u) / 64u;
+        sb.b[0].frames = bufs[r].fr; sb.b[0].offsets = bufs[r].off; sb.b[0].out = bufs[r].out; sb.b[0].seg = seg;
+        sb.b[0].cls = nullptr; sb.b[0].stats = bufs[r].st; sb.b[0].n = n; sb.b[0].frames_bytes = (uint32_t)bytes;
+        sb.total_segs = (n + 63u) / 64u;
         return sb;
     };
     uint64_t caps = 0;
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;
-    printf("{\"blocks_per_cu_api\": %d, \"cus\": %d, \"units\": %u, \"grid\": %u, \"unit_frames\": %u, \"threads\": %d}\n", bpc,
-           prop.multiProcessorCount, units, grid, fbk::kWsUnit, fbk::kWsThreads);
-    const char* names[] = {"ws", "ws_no_lb", "ws_no_store", "ws_no_lb_st", "read", "copy", "seg", "seg_no_store",
-                           "seg_no_classify", "seg_no_classify_no_store"};
-    const int NV = 10;
+    printf("{\"cus\": %d}\n", prop.multiProcessorCount);
+    const char* names[] = {"read", "copy", "seg", "seg_no_store", "seg_no_classify", "seg_no_classify_no_store"};
+    const int NV = 6;
     int sbpc = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&sbpc, (fbk::k_parse_seg<false>), fbk::kSegThreads, 0));
     const uint32_t nseg = (n + 63) / 64;
@@ -163,19 +146,12 @@ int main(int argc, char** argv) {
                 if (it == 0) CK(hipEventRecord(e0, s));
                 const int r = (it + 100) % R;
                 switch (v) {
-                case 0: hipLaunchKernelGGL((fbk::k_parse_ws<false, 0>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
-                case 1: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoLookback>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
-                case 2: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
-                case 3: hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kNoLookback | fbk::kNoStore>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(r)); break;
-                case 4: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
-                case 6: case 7: case 8: case 9: {
-                    fbk::ParseParams pp = params(r); pp.seg = dseg; pp.dns = nullptr;
-                    if (v == 6) hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
-                    if (v == 7) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
-                    if (v == 8) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
-                    if (v == 9) hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoLookback | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
-                } break;
-                case 5: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+                case 0: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
+                case 1: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
+                case 2: hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
+                case 3: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
+                case 4: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoClassify>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
+                case 5: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoClassify | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
                 }
             }
             CK(hipEventRecord(e1, s));
@@ -188,7 +164,7 @@ int main(int argc, char** argv) {
         }
     }
     for (int v = 0; v < NV; ++v) {
-        const double gbs = v == 4 ? bytes / (best[v] * 1e3) : (v == 5 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
+        const double gbs = v == 0 ? bytes / (best[v] * 1e3) : (v == 1 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
         printf("{\"variant\": \"%s\", \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n", names[v],
                sum[v] / rounds, best[v], n / (best[v] * 1e3), gbs);
     }
@@ -198,8 +174,8 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&sd, sw * 8));
         CK(hipMemset(sd, 0, sw * 8));
         for (int w = 0; w < 3; ++w) {
-            fbk::ParseParams pp = params(w % R); pp.seg = dseg; pp.dns = nullptr; pp.dbg = sd;
-            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(pp));
+            fbk::ParseParams pp = params(); pp.dbg = sd;
+            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(w % R, dseg));
         }
         CK(hipStreamSynchronize(s));
         std::vector<unsigned long long> st2(sw);
@@ -247,49 +223,7 @@ int main(int argc, char** argv) {
         }
         CK(hipFree(sd));
     }
-    // stamped run
-    CK(hipMemset(dbg, 0, dbg_words * 8));
-    for (int w = 0; w < 3; ++w)
-        hipLaunchKernelGGL((fbk::k_parse_ws<false, fbk::kStamps>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(w % R));
-    CK(hipStreamSynchronize(s));
-    std::vector<unsigned long long> st(dbg_words);
-    CK(hipMemcpy(st.data(), dbg, dbg_words * 8, hipMemcpyDeviceToHost));
-    unsigned long long t0 = ~0ull;
-    for (uint32_t b = 0; b < grid; ++b) t0 = std::min(t0, st[(b * fbk::kWsDbgUnits + fbk::kWsDbgUnits - 1) * 4 + 3]);
-    const uint32_t Kmax = (units + grid - 1) / grid;
-    auto q = [](std::vector<double> v, double fr) {
-        if (v.empty()) return 0.0;
-        std::sort(v.begin(), v.end());
-        return v[(size_t)(fr * (v.size() - 1))];
-    };
-    // per unit k of a block: start (loader wave 0 begins it), staged, INC published, stored
-    {
-        std::vector<double> en, lx, bx, sx;
-        for (uint32_t b = 0; b < grid; ++b) {
-            const unsigned long long* r0 = &st[(b * fbk::kWsDbgUnits + fbk::kWsDbgUnits - 1) * 4];
-            en.push_back((r0[3] - t0) * 0.01); lx.push_back((r0[0] - t0) * 0.01);
-            bx.push_back((r0[1] - t0) * 0.01); sx.push_back((r0[2] - t0) * 0.01);
-        }
-        printf("{\"block\": 1, \"entry_us\": [%.2f, %.2f, %.2f], \"loader_exit\": [%.2f, %.2f, %.2f], \"lb_exit\": [%.2f, %.2f, %.2f], \"storer_exit\": [%.2f, %.2f, %.2f]}\n",
-               q(en, 0), q(en, .5), q(en, 1), q(lx, 0), q(lx, .5), q(lx, 1), q(bx, 0), q(bx, .5), q(bx, 1), q(sx, 0), q(sx, .5), q(sx, 1));
-    }
-    for (uint32_t k = 0; k < std::min<uint32_t>(Kmax, fbk::kWsDbgUnits - 1); ++k) {
-        std::vector<double> start, ld, lb, sto, done;
-        for (uint32_t b = 0; b < grid; ++b) {
-            const unsigned long long* r0 = &st[(b * fbk::kWsDbgUnits + k) * 4];
-            if (!r0[3] || !r0[0] || !r0[1] || !r0[2]) continue;
-            start.push_back((r0[3] - t0) * 0.01);
-            ld.push_back(((double)r0[0] - (double)r0[3]) * 0.01);
-            lb.push_back(((double)r0[1] - (double)r0[0]) * 0.01);
-            sto.push_back(((double)r0[2] - (double)r0[1]) * 0.01);
-            done.push_back((r0[2] - t0) * 0.01);
-        }
-        printf("{\"unit\": %u, \"start_us\": [%.2f, %.2f, %.2f], \"staged_after\": [%.2f, %.2f, %.2f], "
-               "\"inc_after_staged\": [%.2f, %.2f, %.2f], \"stored_after_inc\": [%.2f, %.2f, %.2f], \"stored_at\": [%.2f, %.2f, %.2f]}\n",
-               k, q(start, 0), q(start, .5), q(start, 1), q(ld, 0), q(ld, .5), q(ld, 1), q(lb, 0), q(lb, .5), q(lb, 1),
-               q(sto, 0), q(sto, .5), q(sto, 1), q(done, 0), q(done, .5), q(done, 1));
-    }
-    hipLaunchKernelGGL((fbk::k_parse_ws<false, 0>), dim3(grid), dim3(fbk::kWsThreads), 0, s, params(0));
+    hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(0, dseg));
     CK(hipStreamSynchronize(s));
     unsigned errw[2] = {0, 0};
     CK(hipMemcpy(errw, err, 8, hipMemcpyDeviceToHost));
