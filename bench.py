@@ -88,6 +88,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
             d[t] = (d_fr.ptr.value, nbytes, d_off.ptr.value, n, 0, d_out.ptr.value, d_seg.ptr.value, 0, d_st.ptr.value)
         return d
 
+    keep = []  # descriptor arrays referenced by address
+
     def plan(k):
         """Launch descriptors of k steps, built before the timed region."""
         if bpl == 1:
@@ -95,7 +97,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         assert mode == "seg" and not flow and rotate >= bpl, (mode, flow, rotate, bpl)
         out, first = [], 0
         for c in plan_launches(k, bpl):
-            out.append((descriptors(first, c), c))
+            d = descriptors(first, c)
+            keep.append(d)
+            out.append((d.ctypes.data, c))
             first += c
         return out
 
@@ -106,7 +110,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
                 step(i)
             return k
         for d, c in launches:
-            rc = lib.fb_parse_classify_seg_batches_dev(ctx, d.ctypes.data, c, stream.ptr)
+            rc = lib.fb_parse_classify_seg_batches_dev(ctx, d, c, stream.ptr)
             if rc != 0:
                 raise RuntimeError(lib.fb_last_error().decode())
         return len(launches)
@@ -163,8 +167,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     ev0.record(stream)
     n_launch = run_timed()
     ev1.record(stream)
-    stream.sync()
+    ev1.wait_spin()  # poll the completion (a blocking wait adds its wake-up latency to the region)
     t1 = time.perf_counter()
+    stream.sync()
     if dist:
         dist.barrier()
     elapsed = t1 - t0
@@ -212,6 +217,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         for x in b:
             x.free()
     return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage,
+                host_us=round((t1 - t0) * 1e6 - ev_ms * 1e3, 1),
                 launches=n_launch, stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
@@ -643,9 +649,11 @@ def main():
                                   "batch-wide compaction (fb_parse_classify_dev)"),
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, bpl),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, args.steps / main_r["launches"]),
                          "algo_bytes_per_launch": int(algo_per_launch),
-                         "kernel_ms_per_launch": round(per_launch_s * 1e3, 5)},
+                         "kernel_ms_per_launch": round(per_launch_s * 1e3, 5),
+                         "launches": main_r["launches"],
+                         "timed_region_host_us_outside_kernels": main_r["host_us"]},
             "cpu_baseline": cpu,
             "batch_stats": main_r["stats"],
         }

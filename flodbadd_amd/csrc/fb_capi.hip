@@ -47,8 +47,10 @@ struct fb_ctx {
     // dense output (fb_parse_classify_dev & co., fb_seg_compact_dev): segment counts + their scan
     uint32_t* d_cseg = nullptr;            // [cseg_cap] segment counts (dense pass 1)
     unsigned long long* d_cpre = nullptr;  // [cseg_cap] batch-wide offset of every segment
-    unsigned long long* d_ctsum = nullptr; // [seg_scan_tiles(cseg_cap)] scan tile sums
-    uint64_t cseg_cap = 0;                 // segments
+    unsigned long long* d_cstatus = nullptr;  // [seg_scan_tiles(cseg_cap)] scan look-back words
+    uint32_t* d_cticket = nullptr;            // scan ticket counter
+    uint32_t scan_epoch = 0;                  // epoch of the last scan (0: status needs zeroing)
+    uint64_t cseg_cap = 0;                    // segments
     hipEvent_t stage_event = nullptr;  // fb_set_stage_event (caller-owned): recorded between the
                                        // parse and the update of fb_process[_seg]_dev
     // flow table
@@ -211,16 +213,35 @@ static int ensure_compact_scratch(fb_ctx* c, uint64_t n, hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_cseg);
     hipFree(c->d_cpre);
-    hipFree(c->d_ctsum);
+    hipFree(c->d_cstatus);
+    hipFree(c->d_cticket);
     c->d_cseg = nullptr;
     c->d_cpre = nullptr;
-    c->d_ctsum = nullptr;
+    c->d_cstatus = nullptr;
+    c->d_cticket = nullptr;
     c->cseg_cap = 0;
+    c->scan_epoch = 0;
     const uint64_t want = std::max<uint64_t>(nseg, 1024);
     if (hipMalloc(&c->d_cseg, want * 4ull) != hipSuccess || hipMalloc(&c->d_cpre, want * 8ull) != hipSuccess ||
-        hipMalloc(&c->d_ctsum, seg_scan_tiles((uint32_t)want) * 8ull) != hipSuccess)
+        hipMalloc(&c->d_cstatus, seg_scan_tiles((uint32_t)want) * 8ull) != hipSuccess ||
+        hipMalloc(&c->d_cticket, 4) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "dense-output scratch (%llu segments)", (unsigned long long)want);
+    HIP_TRY(hipMemsetAsync(c->d_cticket, 0, 4, s));
     c->cseg_cap = want;
+    return FB_OK;
+}
+
+// The next scan's scratch: a fresh epoch (the status words are zeroed, stream-ordered, when the
+// 8-bit epoch wraps).
+static int scan_scratch(fb_ctx* c, hipStream_t s, SegScanScratch& sc) {
+    if (c->scan_epoch == 0u || c->scan_epoch >= 255u) {
+        HIP_TRY(hipMemsetAsync(c->d_cstatus, 0, seg_scan_tiles((uint32_t)c->cseg_cap) * 8ull, s));
+        c->scan_epoch = 0u;
+    }
+    sc.status = c->d_cstatus;
+    sc.ticket = c->d_cticket;
+    sc.epoch = ++c->scan_epoch;
+    sc.err = c->d_error + (c->epoch & 1u);
     return FB_OK;
 }
 
@@ -333,7 +354,8 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_tick);
     hipFree(c->d_cseg);
     hipFree(c->d_cpre);
-    hipFree(c->d_ctsum);
+    hipFree(c->d_cstatus);
+    hipFree(c->d_cticket);
     hipFree(c->d_error);
     hipFree(c->d_table);
     hipFree(c->d_entries);
@@ -537,8 +559,11 @@ int fb_seg_compact_dev(fb_ctx* c, const fb_pkt_out* d_seg_out, const uint32_t* d
     hipStream_t s = (hipStream_t)stream;
     int rc = ensure_compact_scratch(c, n, s);
     if (rc) return rc;
-    HIP_TRY(launch_seg_compact(d_seg_out, d_seg, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES, c->d_cpre, c->d_ctsum,
-                               d_out, d_dns, s));
+    SegScanScratch sc;
+    rc = scan_scratch(c, s, sc);
+    if (rc) return rc;
+    HIP_TRY(launch_seg_compact(d_seg_out, d_seg, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES, c->d_cpre, sc, d_out, d_dns,
+                               s));
     return FB_OK;
 }
 
@@ -559,7 +584,10 @@ static int parse_dense(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
                     s, false, SegPass::kCount);
     if (rc || (!d_out && !d_dns)) return rc;
     const uint32_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
-    HIP_TRY(launch_seg_scan(c->d_cseg, nseg, c->d_cpre, c->d_ctsum, s));
+    SegScanScratch sc;
+    rc = scan_scratch(c, s, sc);
+    if (rc) return rc;
+    HIP_TRY(launch_seg_scan(c->d_cseg, nseg, c->d_cpre, sc, s));
     return launch_seg(c, one_batch(d_frames, frames_bytes, d_offsets, n, nullptr, nullptr, nullptr, nullptr), n, d_in, s,
                       false, SegPass::kDenseOut, d_out, d_dns);
 }
@@ -1007,6 +1035,12 @@ int fb_event_elapsed_ms(float* ms, void* a, void* b) {
     if (!ms) return set_err(FB_ERR_INVAL, "NULL");
     HIP_TRY(hipEventSynchronize((hipEvent_t)b));
     HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+    return FB_OK;
+}
+int fb_event_query(void* ev) {
+    const hipError_t e = hipEventQuery((hipEvent_t)ev);
+    if (e == hipErrorNotReady) return 1;
+    HIP_TRY(e);
     return FB_OK;
 }
 int fb_set_device(int d) { HIP_TRY(hipSetDevice(d)); return FB_OK; }

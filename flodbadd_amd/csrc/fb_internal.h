@@ -229,12 +229,19 @@ hipError_t occupancy_parse_seg(int* blocks_per_cu);
 uint32_t parse_seg_block_threads();
 // Exclusive scan of segment count words into pre[nseg] (u64 n_session | n_dns << 32), and the
 // dense copy of a segmented batch (fb_seg_compact_dev); out / dns may each be NULL.
-// tsum: scratch of seg_scan_tiles(nseg) words.
+// The scan's look-back scratch: seg_scan_tiles(nseg) epoch-tagged status words (zeroed whenever
+// the 8-bit epoch wraps) and a ticket counter (zero between calls).
+struct SegScanScratch {
+    unsigned long long* status;
+    uint32_t* ticket;
+    uint32_t epoch;  // 1..255, a new one per call
+    uint32_t* err;   // error word: bit 2 if a look-back spin ever expired
+};
 uint32_t seg_scan_tiles(uint32_t nseg);
-hipError_t launch_seg_scan(const uint32_t* seg, uint32_t nseg, unsigned long long* pre, unsigned long long* tsum,
+hipError_t launch_seg_scan(const uint32_t* seg, uint32_t nseg, unsigned long long* pre, const SegScanScratch& sc,
                            hipStream_t s);
 hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, uint32_t nseg, unsigned long long* pre,
-                              unsigned long long* tsum, fb_pkt_out* out, fb_dns_out* dns, hipStream_t s);
+                              const SegScanScratch& sc, fb_pkt_out* out, fb_dns_out* dns, hipStream_t s);
 hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);

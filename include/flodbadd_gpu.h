@@ -155,7 +155,8 @@ typedef struct fb_batch_stats {
     uint64_t bad_offsets;      /* frames with invalid offsets (counted in n_drop too)         */
     uint64_t error;            /* nonzero = failure bits: 4 flow-table partition full
                                   (FB_ERR_TABLE_FULL), 8 more records than the update scratch of
-                                  the last parse launch holds (FB_ERR_INTERNAL)               */
+                                  the last parse launch holds, 2 the dense path's offset scan
+                                  waited too long (FB_ERR_INTERNAL; not expected)            */
     uint64_t reserved[3];
 } fb_batch_stats; /* 128 bytes */
 
@@ -555,6 +556,8 @@ int fb_event_create(void** ev);
 int fb_event_destroy(void* ev);
 int fb_event_record(void* ev, void* stream);
 int fb_event_elapsed_ms(float* ms, void* ev_start, void* ev_stop); /* syncs ev_stop */
+int fb_event_query(void* ev); /* FB_OK once the event completed, 1 while pending: a capture loop
+                                 polls it instead of blocking (no wake-up latency)          */
 int fb_device_count(int* n);
 int fb_set_device(int device);
 
