@@ -58,7 +58,9 @@ struct fb_ctx {
     uint64_t table_cap = 0;
     uint32_t flow_parts = 0;        // partitions of kFlowSlots slots
     uint32_t flow_shift = 64;       // 64 - log2(flow_parts)
-    FlowEntry* d_entries = nullptr; // update scratch, flow_recs entries
+    uint32_t* d_entries = nullptr;  // update scratch: flow_recs bucketed record slots
+    FlowEntry* d_comb = nullptr;    // k_flow_combine entries (2 units each), comb_cap of them
+    uint32_t comb_cap = 0;
     uint32_t* d_rows = nullptr;     // [flow_chunks][flow_parts]
     uint32_t* d_cols = nullptr;     // [flow_parts][flow_chunks]
     uint64_t flow_recs = 0;         // scratch capacity (multiple of kFlowChunk)
@@ -154,6 +156,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     if (recs <= c->flow_recs) return FB_OK;
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_entries);
+    hipFree(c->d_comb);
     hipFree(c->d_rows);
     hipFree(c->d_cols);
     hipFree(c->d_rec_flow);
@@ -166,12 +169,18 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     c->part_recs = nullptr;
     c->d_ent_slot = nullptr;
     c->d_entries = nullptr;
+    c->d_comb = nullptr;
+    c->comb_cap = 0;
     c->d_rows = c->d_cols = nullptr;
     c->d_rec_flow = c->d_hot = c->d_comb_ctl = c->d_agg_slot = nullptr;
     c->last_recs = nullptr;  // its rec_flow is gone
     c->flow_recs = 0;
     const uint64_t chunks = recs / kFlowChunk;
-    if (hipMalloc(&c->d_entries, recs * sizeof(FlowEntry)) != hipSuccess ||
+    // combined entries: at most one per two records of the hot groups; a quarter of the batch's
+    // records is room for any skew we measured (past it a hot group just stays plain)
+    const uint64_t comb = recs / 4 + 256;
+    if (hipMalloc(&c->d_entries, recs * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_comb, comb * 2ull * sizeof(FlowEntry)) != hipSuccess ||
         hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess || hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
@@ -181,6 +190,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     HIP_TRY(hipMemsetAsync(c->d_comb_ctl, 0, 8, s));
     c->flow_recs = recs;
+    c->comb_cap = (uint32_t)comb;
     return FB_OK;
 }
 
@@ -359,6 +369,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_error);
     hipFree(c->d_table);
     hipFree(c->d_entries);
+    hipFree(c->d_comb);
     hipFree(c->d_rows);
     hipFree(c->d_cols);
     hipFree(c->d_partials);
@@ -734,6 +745,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.stats = d_stats;
     p.table = c->d_table;
     p.entries = c->d_entries;
+    p.comb = c->d_comb;
+    p.comb_cap = c->comb_cap;
     p.rows = c->d_rows;
     p.cols = c->d_cols;
     p.partials = c->d_partials;

@@ -10,18 +10,24 @@
 // atomics/s = 1.73 ms per 10M-record batch on MI355X (profiles/r01_c4_kernel_stats.csv).
 // Instead the table is split into P partitions of kFlowSlots slots (fb_internal.h) and a batch
 // is applied in three launches:
-//   K1 k_flow_bucket    one workgroup per chunk of kFlowChunk records: LDS histogram of the
-//                       records' partitions, exclusive scan, then a counting-sort scatter of
-//                       64-B FlowEntry items into the chunk's region of `entries` (partition-
-//                       major inside the chunk); row b of `rows` = (start, count) per partition.
-//   K1c k_flow_combine  the hot (chunk, partition) groups K1 listed are reduced per key in place
-//                       (skewed popularity: one hot flow would otherwise run through one CU).
+//   K1 k_flow_bucket    one workgroup per chunk of kFlowChunk record slots: LDS histogram of the
+//                       records' partitions (handed over by the fused parse, else hashed here),
+//                       exclusive scan, then a counting-sort scatter of each record's SLOT INDEX
+//                       (4 B) into the chunk's region of `entries` (partition-major inside the
+//                       chunk); row b of `rows` = (start, count) per partition.
+//   K1c k_flow_combine  the hot (chunk, partition) groups K1 listed are reduced per key (skewed
+//                       popularity: one hot flow would otherwise run through one CU); a key met
+//                       more than once becomes one combined entry in `comb`, its index word
+//                       kIdxCombined | id.
 //   K1t k_flow_transpose rows[chunk][part] -> cols[part][chunk] (so K2 reads its column
 //                       contiguously).
-//   K2 k_flow_apply     one workgroup per partition: loads the partition's 64-KiB slice into
-//                       LDS, gathers its entries from every chunk, finds/inserts each key in
-//                       the slice, adds the counters and reduces the ordered state with LDS
-//                       atomics, folds the ordered state once per slot, writes the slice back.
+//   K2 k_flow_apply     one workgroup per partition: loads the partition's slot heads into LDS,
+//                       gathers its entries' records (or combined entries) from every chunk,
+//                       finds/inserts each key in the slice, adds the counters and reduces the
+//                       ordered state with LDS atomics, folds the ordered state once per slot,
+//                       writes the slice back.
+// K1 writing 4-B indices instead of 64-B entries (records gathered by K2 itself) cut K1 from 437
+// to 140 us per C4 batch; K2 gathers 56-B records instead of 64-B entries and pipelines them.
 // Counters are integer sums, so results are bit-exact whatever the order (the order-dependent
 // history state is reduced to min/max/or, see K2); new_sessions counts
 // the keys inserted (each key is inserted once), updated_sessions the remaining records.
@@ -85,6 +91,24 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
 #endif
 constexpr uint32_t kCombMin = FB_COMB_MIN;
 
+// Record slot `rec` of the batch as the four uint4 of a plain FlowEntry (fb_internal.h): key words,
+// key word 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char |
+// tcp_flags << 8 | has_flags << 16, the low word of the key's hash.  Records are 56 B, so only 8-B
+// aligned at odd slots: loaded through ld_u4 / ld_u2.
+__device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, uint4 (&e)[4]) {
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(recs + rec);
+    const uint4 a = ld_u4(r), b = ld_u4(r + 4), c = ld_u4(r + 8);
+    const uint2 m = ld_u2(r + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
+    const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+    const uint32_t meta = (m.x >> 8) & 0xFFu;
+    const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
+    const uint32_t hinfo = ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
+    e[0] = a;
+    e[1] = b;
+    e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
+    e[3] = make_uint4(m.y, rec, hinfo, (uint32_t)flow_hash_words(key));
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1: bucket one chunk of records by partition (counting sort in LDS).
 __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams P) {
@@ -98,21 +122,47 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     const uint32_t cnt = min(kFlowChunk, n - base);
     const fb_pkt_out* R = P.recs + base;
     for (uint32_t j = threadIdx.x; j < P.parts; j += kFlowK1Threads) hist[j] = 0u;
-    __syncthreads();
-    if (P.rec_part) {  // partitions from the parse of this batch: 4 B per record instead of 40
-        for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads)
-            if (slot_valid(P, base + k)) atomicAdd(&hist[P.rec_part[base + k]], 1u);
-    } else {
-        for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
-            if (!slot_valid(P, base + k)) continue;
-            const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
-            const uint4 a = ld_u4(r);
-            const uint4 b = ld_u4(r + 4);
-            const uint2 c = ld_u2(r + 8);
-            const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-            atomicAdd(&hist[part_of(flow_hash_words(key), P.part_shift)], 1u);
+    // every thread owns the chunk's slots threadIdx.x + j * kFlowK1Threads; their partitions stay in
+    // registers from the histogram pass to the scatter pass, and each pass issues all its loads
+    // before the first LDS atomic (a loop of load -> atomic iterations waits a full memory round
+    // trip per record)
+    constexpr uint32_t kPer = kFlowChunk / kFlowK1Threads;
+    static_assert(kFlowChunk % kFlowK1Threads == 0, "whole records per thread");
+    uint32_t pv[kPer];  // partition of each owned slot, ~0u: no record
+    if (P.rec_part) {   // partitions from the parse of this batch (fb_process_seg_dev): 4 B per record
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t k = threadIdx.x + j * kFlowK1Threads;
+            pv[j] = k < cnt && slot_valid(P, base + k) ? P.rec_part[base + k] : ~0u;
+        }
+    } else {            // hashed here, four records' key loads in flight at a time
+        constexpr uint32_t kG = 4;
+#pragma unroll
+        for (uint32_t j0 = 0; j0 < kPer; j0 += kG) {
+            uint4 a[kG], b[kG];
+            uint2 c[kG];
+            bool ok[kG];
+#pragma unroll
+            for (uint32_t u = 0; u < kG; ++u) {
+                const uint32_t k = threadIdx.x + (j0 + u) * kFlowK1Threads;
+                ok[u] = k < cnt && slot_valid(P, base + k);
+                const uint32_t* r = reinterpret_cast<const uint32_t*>(R + (ok[u] ? k : 0u));
+                a[u] = ld_u4(r);
+                b[u] = ld_u4(r + 4);
+                c[u] = ld_u2(r + 8);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kG; ++u) {
+                const uint32_t key[10] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w, c[u].x,
+                                          c[u].y & 0xFFFFu};
+                pv[j0 + u] = ok[u] ? part_of(flow_hash_words(key), P.part_shift) : ~0u;
+            }
         }
     }
+    __syncthreads();  // hist zeroed
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j)
+        if (pv[j] != ~0u) atomicAdd(&hist[pv[j]], 1u);
     __syncthreads();
     // exclusive scan of hist[0..parts): each thread owns E consecutive partitions
     const uint32_t E = (P.parts + kFlowK1Threads - 1u) / kFlowK1Threads;
@@ -134,27 +184,15 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         run += c;
     }
     __syncthreads();
-    FlowEntry* out = P.entries + base;
-    for (uint32_t k = threadIdx.x; k < cnt; k += kFlowK1Threads) {
-        if (!slot_valid(P, base + k)) continue;
-        const uint32_t* r = reinterpret_cast<const uint32_t*>(R + k);
-        const uint4 a = ld_u4(r);
-        const uint4 b = ld_u4(r + 4);
-        const uint4 c = ld_u4(r + 8);   // key 8,9 | packet_length | ip_packet_length
-        const uint2 m = ld_u2(r + 12);  // flags | meta | hist_char, pkt_index
-        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-        const unsigned long long fh = flow_hash_words(key);
-        const uint32_t d = atomicAdd(&hist[part_of(fh, P.part_shift)], 1u);
-        const uint32_t meta = (m.x >> 8) & 0xFFu;
-        const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-        const uint32_t hinfo =
-            ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
-        uint4* e = reinterpret_cast<uint4*>(out + d);
-        e[0] = a;
-        e[1] = b;
-        e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
-        e[3] = make_uint4(m.y, base + k, hinfo, (uint32_t)fh);  // low hash word: K2's home slot + tag filter
-        if (P.rec_flow) P.rec_flow[base + k] = base + d;  // the record's entry (coalesced; K2 fills ent_slot)
+    // scatter: entry position -> the record's slot index (4 B); K2 gathers the record itself
+    uint32_t* out = P.entries + base;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        if (pv[j] == ~0u) continue;
+        const uint32_t k = threadIdx.x + j * kFlowK1Threads;
+        const uint32_t d = atomicAdd(&hist[pv[j]], 1u);
+        out[d] = base + k;
+        if (P.rec_flow) P.rec_flow[base + k] = base + d;  // the record's entry (K2 fills ent_slot)
     }
 }
 
@@ -207,10 +245,7 @@ constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 #define FB_K2_CPT 2
 #endif
 constexpr uint32_t kK2Cpt = FB_K2_CPT;
-#ifndef FB_K2_EPT
-#define FB_K2_EPT 4
-#endif
-constexpr uint32_t kK2Ept = FB_K2_EPT;  // entries gathered per thread before they are applied  // bucketing chunks per K2 thread and round (C4: 640 chunks, one round)
+// (kK2Cpt: bucketing chunks per K2 thread and round; C4: 640 chunks, one round)
 // scratch words
 constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
 
@@ -479,7 +514,8 @@ struct CombLds {
 __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
     const uint32_t n_hot = min(P.ctl[0], P.hot_cap);
-    uint4* E = reinterpret_cast<uint4*>(P.entries);
+    uint32_t* E = P.entries;
+    uint4* CE = reinterpret_cast<uint4*>(P.comb);
     for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
         const uint32_t grp = P.hot[h], chunk = grp >> 13, part = grp & 8191u;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
@@ -496,26 +532,27 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         __syncthreads();
         // reduce per key (a key the table cannot take stays a plain entry)
         for (uint32_t k = threadIdx.x; k < cnt; k += kCombThreads) {
-            const uint4* e = E + (s0 + k) * 4u;
-            const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-            const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
+            uint4 e[4];
+            rec_entry(P.recs, E[s0 + k], e);
+            const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                      e[2].y & 0xFFFFu};
             uint32_t j;
-            if (lds_upsert<6, kCombSlots>(L.tab, key, e3.w, j) < 0) continue;
-            const uint32_t orig = (e2.y >> 16) & 1u, rec = e3.y;
+            if (lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0) continue;
+            const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
             uint32_t* f = L.f + j * kCombF;
-            atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e2.z);
-            atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e2.w);
+            atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
+            atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e[2].w);
             atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
             atomicAdd(f + kCfRecs, 1u);
-            f[kCfHash] = e3.w;  // every lane of the key stores the same word
+            f[kCfHash] = e[3].w;  // every lane of the key stores the same word
             atomicMin(f + kCfFirst, rec);
             atomicMax(f + kCfLast, rec);
-            if (e3.z & 0x10000u) {
+            if (e[3].z & 0x10000u) {
                 atomicAdd(f + kCfHcnt, 1u);
-                const uint32_t b = hist_bit(e3.z & 0xFFu);
+                const uint32_t b = hist_bit(e[3].z & 0xFFu);
                 if (b < 16u) atomicOr(f + kCfMask, 1u << b);
                 if (b < 4u) atomicMin(f + kCfChar + b, rec);
-                if ((e3.z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec);
+                if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec);
             }
         }
         __syncthreads();
@@ -528,30 +565,30 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         uint32_t rank = block_excl_scan(nc, L.wsum, n_comb);
         if (n_comb == 0u) continue;  // uniform across the block; the table is re-initialised above
         if (threadIdx.x == 0) L.base = atomicAdd(P.ctl + 1, n_comb);
+        __syncthreads();
+        const uint32_t id0 = L.base;
+        if (id0 + n_comb > P.comb_cap) continue;  // no room for its combined entries: the group stays plain
 #pragma unroll
         for (uint32_t u = 0; u < kPer; ++u) {
             uint32_t* f = L.f + (threadIdx.x * kPer + u) * kCombF;
             if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
         }
         __syncthreads();
-        const uint32_t id0 = L.base;
-        // pack the remaining plain entries to the front, tile by tile (a tile is loaded before any
-        // of its stores, and stores land below the next tile)
+        // pack the remaining plain entries (record indices) to the front, tile by tile (a tile is
+        // loaded before any of its stores, and stores land below the next tile)
         uint32_t cursor = 0u;
         for (uint32_t t = 0; t < cnt; t += kCombThreads) {
             const uint32_t k = t + threadIdx.x;
-            uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
-            uint32_t keep = 0u;
+            uint32_t keep = 0u, rec = 0u;
             if (k < cnt) {
-                const uint4* e = E + (s0 + k) * 4u;
-                q0 = e[0];
-                q1 = e[1];
-                q2 = e[2];
-                q3 = e[3];
-                const uint32_t key[10] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y & 0xFFFFu};
-                const uint32_t j = lds_find<6, kCombSlots>(L.tab, key, q3.w);
+                rec = E[s0 + k];
+                uint4 e[4];
+                rec_entry(P.recs, rec, e);
+                const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                          e[2].y & 0xFFFFu};
+                const uint32_t j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
                 if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) {
-                    if (P.rec_flow) P.rec_flow[q3.y] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                    if (P.rec_flow) P.rec_flow[rec] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
                 } else {
                     keep = 1u;
                 }
@@ -559,34 +596,32 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint32_t kept;
             const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
             if (keep) {
-                if (P.rec_flow) P.rec_flow[q3.y] = (uint32_t)(s0 + cursor + pos);  // the entry moved
-                uint4* o = E + (s0 + cursor + pos) * 4u;
-                o[0] = q0;
-                o[1] = q1;
-                o[2] = q2;
-                o[3] = q3;
+                if (P.rec_flow) P.rec_flow[rec] = (uint32_t)(s0 + cursor + pos);  // the entry moved
+                E[s0 + cursor + pos] = rec;
             }
             cursor += kept;
         }
-        // the combined entries behind them
+        // the combined entries (two units each in P.comb) and their index words behind the kept ones
 #pragma unroll
         for (uint32_t u = 0; u < kPer; ++u) {
             const uint32_t j = threadIdx.x * kPer + u;
             const uint32_t* f = L.f + j * kCombF;
             if (f[kCfRecs] < 2u) continue;
+            const uint32_t id = id0 + f[kCfId];
             const unsigned long long* tw = L.tab + j * 6;
             const unsigned long long* by = L.bytes + j * 4;
-            uint4* o = E + (s0 + cursor + 2u * f[kCfId]) * 4u;
+            uint4* o = CE + (size_t)id * 8u;
             o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
             o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
             o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
-            o[3] = make_uint4(id0 + f[kCfId], f[kCfEnd], f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
+            o[3] = make_uint4(id, f[kCfEnd], f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
             o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
             o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
             o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
             o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], 0u);
+            E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
-        if (threadIdx.x == 0) *rowp = (row & 0xFFFFu) | ((cursor + 2u * n_comb) << 16);
+        if (threadIdx.x == 0) *rowp = (row & 0xFFFFu) | ((cursor + n_comb) << 16);
         __syncthreads();  // the table is re-initialised for the next group
     }
 }
@@ -621,7 +656,8 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
         }
         __syncthreads();
-        const uint4* E = reinterpret_cast<const uint4*>(P.entries);
+        const uint32_t* E = P.entries;
+        const uint4* CE = reinterpret_cast<const uint4*>(P.comb);
         for (uint32_t g0 = 0; g0 < chunks; g0 += kK2Cpt * kFlowK2Threads) {
             // kK2Cpt consecutive chunks per thread: one round for batches up to kK2Cpt x 512 chunks
             uint32_t v[kK2Cpt], mine = 0u;
@@ -641,48 +677,85 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 pre += v[c] >> 16;
             }
             __syncthreads();
-            for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += kK2Ept * kFlowK2Threads) {
-                uint4 q[kK2Ept][4];
-                uint32_t ix[kK2Ept];
-                uint32_t ne = 0u;
-#pragma unroll
-                for (uint32_t u = 0; u < kK2Ept; ++u) {
-                    const uint32_t e = e0 + u * kFlowK2Threads;
-                    if (e < tot) {
-                        uint32_t lo = 0u, hi = kK2Cpt * kFlowK2Threads - 1u;  // largest j with sp[j] <= e
-                        while (lo < hi) {
-                            const uint32_t mid = (lo + hi + 1u) >> 1;
-                            if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
-                        }
-                        const uint32_t idx = ss[lo] + (e - sp[lo]);
-                        ix[u] = idx;
-                        q[u][0] = E[(size_t)idx * 4u];
-                        q[u][1] = E[(size_t)idx * 4u + 1u];
-                        q[u][2] = E[(size_t)idx * 4u + 2u];
-                        q[u][3] = E[(size_t)idx * 4u + 3u];
-                        ne = u + 1u;
-                    }
+            // Entries of this round, software-pipelined per thread (entries e, e+S, e+2S, ... of
+            // thread e: consecutive lanes read consecutive index words): the index word of entry
+            // e+2S and the record (or combined entry) of e+S are in flight while entry e is applied
+            // (each entry otherwise waits two dependent memory round trips: its index, then its
+            // record).  Contiguous per-thread runs with a forward walk instead of the per-entry
+            // binary search measured slower (C4 K2 672 -> 808 us).
+            constexpr uint32_t S = kFlowK2Threads;
+            auto locate = [&](uint32_t e) {  // entry position of round entry e: largest j with sp[j] <= e
+                uint32_t lo = 0u, hi = kK2Cpt * kFlowK2Threads - 1u;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1u) >> 1;
+                    if (sp[mid] <= e) lo = mid; else hi = mid - 1u;
                 }
-#pragma unroll
-                for (uint32_t u = 0; u < kK2Ept; ++u) {
-                    if (u >= ne || (q[u][2].y & kEntTail)) continue;  // second unit of a combined entry
-                    if (q[u][2].y & kEntCombined) {
-                        const uint4* t = E + ((size_t)ix[u] + 1u) * 4u;
-                        const uint4 t3 = t[3];
-                        const int r = apply_combined(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3], t[0], t[1],
-                                                     t[2], t3, part * kFlowSlots, P.agg_slot, P.error);
-                        if (r >= 0) {
-                            n_new += r == 1;
-                            n_upd += t3.z - (r == 1 ? 1u : 0u);
-                        }
-                    } else {
-                        const int r = apply_entry(slice, scr, q[u][0], q[u][1], q[u][2], q[u][3],
-                                                  part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix[u],
-                                                  P.error);
+                return ss[lo] + (e - sp[lo]);
+            };
+            auto gather = [&](uint32_t v, uint4 (&r)[4]) {  // raw words only; decoded when applied
+                if (v & kIdxCombined) {  // a k_flow_combine entry: head unit (the tail is read when applied)
+                    const uint4* c = CE + (size_t)(v & ~kIdxCombined) * 8u;
+                    r[0] = c[0];
+                    r[1] = c[1];
+                    r[2] = c[2];
+                    r[3] = c[3];
+                } else {  // a record slot of the batch (56 B, 8-B aligned at odd slots)
+                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + v);
+                    r[0] = ld_u4(q);
+                    r[1] = ld_u4(q + 4);
+                    r[2] = ld_u4(q + 8);
+                    const uint2 m = ld_u2(q + 12);
+                    r[3] = make_uint4(m.x, m.y, 0u, 0u);
+                }
+            };
+            uint32_t e = threadIdx.x, ix0 = 0u, v0 = 0u, ix1 = 0u, v1 = 0u;
+            uint4 r0[4], r1[4];
+            if (e < tot) {
+                ix0 = locate(e);
+                v0 = E[ix0];
+            }
+            if (e + S < tot) {
+                ix1 = locate(e + S);
+                v1 = E[ix1];
+            }
+            if (e < tot) gather(v0, r0);
+            for (; e < tot; e += S) {
+                uint32_t ix2 = 0u, v2 = 0u;
+                if (e + 2u * S < tot) {
+                    ix2 = locate(e + 2u * S);
+                    v2 = E[ix2];
+                }
+                if (e + S < tot) gather(v1, r1);
+                if (v0 & kIdxCombined) {
+                    const uint4* t = CE + (size_t)(v0 & ~kIdxCombined) * 8u + 4u;
+                    const uint4 t3 = t[3];
+                    const int r = apply_combined(slice, scr, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
+                                                 part * kFlowSlots, P.agg_slot, P.error);
+                    if (r >= 0) {
                         n_new += r == 1;
-                        n_upd += r == 0;
+                        n_upd += t3.z - (r == 1 ? 1u : 0u);
                     }
+                } else {
+                    // the record as a plain FlowEntry (layout: fb_internal.h; rec_entry above)
+                    const uint4 a = r0[0], b2 = r0[1], c = r0[2];
+                    const uint32_t mx = r0[3].x, my = r0[3].y;
+                    const uint32_t key[10] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w, c.x, c.y & 0xFFFFu};
+                    const uint32_t meta = (mx >> 8) & 0xFFu;
+                    const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
+                    const uint32_t hinfo =
+                        ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
+                    const int r = apply_entry(slice, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
+                                              make_uint4(my, v0, hinfo, (uint32_t)flow_hash_words(key)),
+                                              part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix0, P.error);
+                    n_new += r == 1;
+                    n_upd += r == 0;
                 }
+#pragma unroll
+                for (uint32_t w = 0; w < 4u; ++w) r0[w] = r1[w];
+                ix0 = ix1;
+                v0 = v1;
+                ix1 = ix2;
+                v1 = v2;
             }
             __syncthreads();
         }

@@ -169,6 +169,7 @@ static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the originator)
 constexpr uint32_t kEntTail = 1u << 18;
 constexpr uint32_t kRecFlowCombined = 0x80000000u;  // rec_flow value: combined id, slot in agg_slot
+constexpr uint32_t kIdxCombined = 0x80000000u;      // entries[] value: combined id (record slots < 2^27)
 
 // fb_flow_hash of a 40-B session_key (10 words, word 9 = protocol | family << 8) and the
 // partition it falls in (top bits).
@@ -197,7 +198,10 @@ struct FlowParams {
     uint32_t n_slots;
     fb_batch_stats* stats;      // n_session read from here; new/updated accumulated
     FlowSlot* table;
-    FlowEntry* entries;         // [max_recs]
+    uint32_t* entries;          // [max_recs] bucketed by partition: the record slot of each entry,
+                                // or kIdxCombined | id of a k_flow_combine entry in `comb`
+    FlowEntry* comb;            // [2 * comb_cap] combined entries (head + tail unit each)
+    uint32_t comb_cap;
     uint32_t* rows;             // [chunks][parts]  start | count << 16, per bucketing chunk
     uint32_t* cols;             // [parts][chunk_stride] the same, transposed
     unsigned long long* partials;  // 2 per partition: new, updated

@@ -7,7 +7,7 @@ mkdir -p flodbadd_amd/build
 for v in $VARIANTS; do
   name=${v%%:*}; flags=$(echo "${v#*:}" | tr ',' ' ')
   objs=""
-  for s in fb_parse fb_flow fb_hist fb_capi fb_ring fb_enrich fb_dns; do
+  for s in fb_parse fb_compact fb_flow fb_hist fb_capi fb_ring fb_enrich fb_dns; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -Iinclude -c flodbadd_amd/csrc/$s.hip \
       -o flodbadd_amd/build/var_${name}_$s.o &
     objs="$objs flodbadd_amd/build/var_${name}_$s.o"
