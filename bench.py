@@ -383,7 +383,7 @@ def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
                      "(compute stream) + stats D2H per batch, table kept in HBM" % slots)
 
 
-def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device, shard_first):
+def c5_flow_reduce(N, lib, ctx, frames, offs, dist, group, device, shard_first):
     """BASELINE config C5's exchange after the timed region: this rank's shard through the fused
     parse + classify + flow-table kernel, then the global per-flow counter merge
     (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce SUM over RCCL)."""
@@ -405,7 +405,7 @@ def c5_flow_reduce(N, lib, ctx, frames, offs, dist_nccl, device, shard_first):
     got = C.c_uint64()
     t0 = time.perf_counter()
     N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
-    merged = global_flow_table(dist_nccl, flows[: got.value], device=device, shard_first=shard_first)
+    merged = global_flow_table(dist, flows[: got.value], device=device, group=group, shard_first=shard_first)
     el = time.perf_counter() - t0
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
@@ -605,16 +605,16 @@ def main():
         try:
             import torch
             import torch.distributed as tdist
-            dev = torch.device("cuda", device)
-            torch.cuda.set_device(dev)
-            g = tdist.new_group(backend="nccl")
-
-            class _D:  # torch.distributed bound to the RCCL group
-                ReduceOp = tdist.ReduceOp
-                get_world_size = staticmethod(lambda group=None: tdist.get_world_size(g))
-                all_gather = staticmethod(lambda a, b, group=None: tdist.all_gather(a, b, group=g))
-                all_reduce = staticmethod(lambda t, op, group=None: tdist.all_reduce(t, op=op, group=g))
-            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], _D, dev, rank * n)
+            # RCCL over xGMI (one GPU per rank); FB_C5_BACKEND=gloo exercises the same exchange with
+            # CPU tensors when the ranks share one GPU (rehearsal on a one-GPU box)
+            backend = os.environ.get("FB_C5_BACKEND", "nccl")
+            dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
+            if backend == "nccl":
+                torch.cuda.set_device(dev)
+            g = tdist.new_group(backend=backend)
+            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], tdist, g, dev,
+                                                     rank * n)
+            extra["c5_flow_reduce"]["backend"] = "rccl" if backend == "nccl" else backend
         except Exception as e:  # the exchange is reported, never allowed to break the bench line
             extra["c5_flow_reduce"] = {"error": repr(e)[:300]}
 
