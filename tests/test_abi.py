@@ -94,3 +94,13 @@ def test_header_constants_match_python():
     for name in ("FB_MAX_SEG_BATCHES", "FB_SEG_FRAMES", "FB_ABI_VERSION"):
         m = re.search(r"#define %s (\d+)u" % name, hdr)
         assert m and int(m.group(1)) == getattr(N, name), name
+
+
+def test_bench_launch_plan():
+    """bench.plan_launches: k steps in ceil(k / bpl) launches of near-equal size."""
+    import bench
+    for bpl in (1, 8, 12, 32):
+        for k in list(range(0, 70)) + [200, 1000]:
+            p = bench.plan_launches(k, bpl)
+            assert sum(p) == k and all(1 <= c <= bpl for c in p)
+            assert len(p) == -(-k // bpl) and (not p or max(p) - min(p) <= 1)
