@@ -937,6 +937,7 @@ int fb_dns_parse_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, 
                      const fb_batch_stats* d_stats, fb_dns_msg* d_msgs, char* d_names, fb_ip* d_addrs, void* stream) {
     if (!c || (n && (!d_dns || !d_msgs || !d_names || !d_addrs || !d_frames)))
         return set_err(FB_ERR_INVAL, "bad arguments");
+    if (reinterpret_cast<uintptr_t>(d_names) & 3u) return set_err(FB_ERR_INVAL, "d_names must be 4-byte aligned");
     DeviceGuard g(c->device);
     HIP_TRY(launch_dns_parse(d_frames, frames_bytes, d_dns, n, d_stats, d_msgs, d_names, d_addrs, (hipStream_t)stream));
     return FB_OK;

@@ -20,15 +20,56 @@
 
 namespace fbk {
 
-__device__ __forceinline__ uint32_t be16at(const uint8_t* m, uint32_t i) { return ((uint32_t)m[i] << 8) | m[i + 1]; }
+// Bytes of one message.  The parse is a chain of dependent byte reads (label lengths, pointers),
+// so serving it from LDS instead of HBM is what sets its speed.  MsgLds: the whole message is in
+// the wavefront's LDS copy (row = the dword holding its first byte, mis = that byte's offset in
+// it).  MsgMixed: the first `staged` bytes from LDS, the rest from HBM by a range-checked buffer
+// load (a plain pointer there lets the compiler fold both sides into one generic flat load per
+// byte, which waits on both counters).  ascii(a, b): no byte of [a, b) has its top bit set.
+struct MsgLds {
+    const uint32_t* row;
+    uint32_t mis;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+        return reinterpret_cast<const uint8_t*>(row)[i + mis];
+    }
+    __device__ __forceinline__ bool ascii(uint32_t a, uint32_t b) const {  // a dword per step
+        const uint32_t p0 = a + mis, p1 = b + mis;
+        uint32_t bad = 0u;
+        for (uint32_t q = p0 & ~3u; q < p1; q += 4u) {
+            uint32_t m = 0x80808080u;
+            if (q < p0) m &= 0xFFFFFFFFu << (8u * (p0 - q));
+            if (q + 4u > p1) m &= 0xFFFFFFFFu >> (8u * (q + 4u - p1));
+            bad |= row[q >> 2] & m;
+        }
+        return bad == 0u;
+    }
+};
+struct MsgMixed {
+    const uint8_t* s;          // LDS copy of bytes [0, staged)
+    __amdgpu_buffer_rsrc_t g;  // the frame buffer
+    uint32_t off;              // the message's byte offset in it
+    uint32_t staged;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+        return i < staged ? (uint32_t)s[i] : (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(g, off + i, 0, 0);
+    }
+    __device__ __forceinline__ bool ascii(uint32_t a, uint32_t b) const {
+        for (uint32_t k = a; k < b; ++k)
+            if ((*this)(k) >= 0x80u) return false;
+        return true;
+    }
+};
+
+template <class M>
+__device__ __forceinline__ uint32_t be16at(const M& m, uint32_t i) { return (m(i) << 8) | m(i + 1u); }
 
 // Name::scan over the slice m[start..limit) with pointers into m[0..len); *blen = byte_len().
-__device__ uint32_t dns_name_scan(const uint8_t* m, uint32_t len, uint32_t start, uint32_t limit, uint32_t* blen) {
+template <class M>
+__device__ uint32_t dns_name_scan(const M& m, uint32_t len, uint32_t start, uint32_t limit, uint32_t* blen) {
     uint32_t base = start, lim = limit, pos = 0u;
     if (lim <= base) return FB_DNS_UNEXPECTED_EOF;
     uint32_t largest = len;
     int32_t ret = -1;
-    uint32_t byte = m[base];
+    uint32_t byte = m(base);
     while (byte != 0u) {
         if ((byte & 0xC0u) == 0xC0u) {
             if (lim - base < pos + 2u) return FB_DNS_UNEXPECTED_EOF;
@@ -43,33 +84,55 @@ __device__ uint32_t dns_name_scan(const uint8_t* m, uint32_t len, uint32_t start
         } else if ((byte & 0xC0u) == 0u) {
             const uint32_t end = pos + byte + 1u;
             if (lim - base < end) return FB_DNS_UNEXPECTED_EOF;
-            for (uint32_t k = pos + 1u; k < end; ++k)
-                if (m[base + k] >= 0x80u) return FB_DNS_LABEL_NOT_ASCII;
+            if (!m.ascii(base + pos + 1u, base + end)) return FB_DNS_LABEL_NOT_ASCII;
             pos = end;
             if (lim - base <= pos) return FB_DNS_UNEXPECTED_EOF;
         } else {
             return FB_DNS_UNKNOWN_LABEL_FORMAT;
         }
-        byte = m[base + pos];
+        byte = m(base + pos);
     }
     *blen = ret >= 0 ? (uint32_t)ret + 2u : pos + 1u;
     return FB_DNS_OK;
 }
 
 // Name's Display (labels joined by '.'; a pointer met after a label writes the '.' first) of a
-// name that dns_name_scan accepted.  Writes at most cap - 1 bytes; returns the full length and
-// whether it ends with ".in-addr.arpa" / ".ip6.arpa" (checked on a 16-byte tail window).
-__device__ uint32_t dns_name_write(const uint8_t* m, uint32_t start, char* out, uint32_t cap, bool* reverse) {
+// name that dns_name_scan accepted.  Writes at most cap - 1 bytes, four at a time (out is 4-byte
+// aligned, bytes of the last dword past the name are zero); returns the full length and whether
+// it ends with ".in-addr.arpa" / ".ip6.arpa", checked on a 16-byte window of the last bytes kept
+// as four words (w0 byte 0 = the last byte), shifted by funnel shifts.
+__device__ __forceinline__ bool window_ends(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t n,
+                                            const char* sfx, uint32_t l) {
+    if (n < l) return false;
+    uint32_t e[4] = {0u, 0u, 0u, 0u}, m[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t k = 0; k < l; ++k) {  // k-th byte from the end
+        e[k >> 2] |= (uint32_t)(uint8_t)sfx[l - 1u - k] << (8u * (k & 3u));
+        m[k >> 2] |= 0xFFu << (8u * (k & 3u));
+    }
+    return ((w0 ^ e[0]) & m[0]) == 0u && ((w1 ^ e[1]) & m[1]) == 0u && ((w2 ^ e[2]) & m[2]) == 0u &&
+           ((w3 ^ e[3]) & m[3]) == 0u;
+}
+
+template <class M>
+__device__ uint32_t dns_name_write(const M& m, uint32_t start, uint32_t* out, uint32_t cap, bool* reverse) {
     uint32_t seg = start, pos = start, n = 0u;
-    uint8_t tail[16];
-    for (int k = 0; k < 16; ++k) tail[k] = 0;
-    auto put = [&](uint8_t c) {
-        if (n < cap - 1u) out[n] = (char)c;
-        tail[n & 15u] = c;
+    uint32_t w0 = 0u, w1 = 0u, w2 = 0u, w3 = 0u, pend = 0u;
+    auto put = [&](uint32_t c) {
+        w3 = __builtin_amdgcn_alignbit(w3, w2, 24u);
+        w2 = __builtin_amdgcn_alignbit(w2, w1, 24u);
+        w1 = __builtin_amdgcn_alignbit(w1, w0, 24u);
+        w0 = (w0 << 8) | c;
+        if (n < cap - 1u) {
+            pend |= c << (8u * (n & 3u));
+            if ((n & 3u) == 3u) {
+                out[n >> 2] = pend;
+                pend = 0u;
+            }
+        }
         ++n;
     };
     for (;;) {
-        const uint32_t b = m[pos];
+        const uint32_t b = m(pos);
         if (b == 0u) break;
         if ((b & 0xC0u) == 0xC0u) {
             if (pos != seg) put('.');
@@ -78,16 +141,12 @@ __device__ uint32_t dns_name_write(const uint8_t* m, uint32_t start, char* out, 
             continue;
         }
         if (pos != seg) put('.');
-        for (uint32_t k = 1u; k <= b; ++k) put(m[pos + k]);
+        for (uint32_t k = 1u; k <= b; ++k) put(m(pos + k));
         pos += b + 1u;
     }
-    auto ends = [&](const char* sfx, uint32_t l) {
-        if (n < l) return false;
-        for (uint32_t k = 0; k < l; ++k)
-            if (tail[(n - l + k) & 15u] != (uint8_t)sfx[k]) return false;
-        return true;
-    };
-    *reverse = ends(".in-addr.arpa", 13u) || ends(".ip6.arpa", 9u);
+    const uint32_t nw = min(n, cap - 1u);
+    if (nw & 3u) out[nw >> 2] = pend;
+    *reverse = window_ends(w0, w1, w2, w3, n, ".in-addr.arpa", 13u) || window_ends(w0, w1, w2, w3, n, ".ip6.arpa", 9u);
     return n;
 }
 
@@ -99,7 +158,8 @@ __device__ __forceinline__ bool dns_type_ok(uint32_t t) {
 }
 
 // One resource record at *off (parse_record); A / AAAA of the answer section are collected.
-__device__ uint32_t dns_record(const uint8_t* m, uint32_t len, uint32_t* off, bool answer, fb_ip* addrs,
+template <class M>
+__device__ uint32_t dns_record(const M& m, uint32_t len, uint32_t* off, bool answer, fb_ip* addrs,
                                uint32_t* n_addrs, uint32_t* flags) {
     uint32_t bl;
     uint32_t st = dns_name_scan(m, len, *off, len, &bl);
@@ -125,8 +185,8 @@ __device__ uint32_t dns_record(const uint8_t* m, uint32_t len, uint32_t* off, bo
                     a.family = v6 ? 10u : 2u;
                     a.reserved[0] = a.reserved[1] = a.reserved[2] = 0u;
                     for (int k = 0; k < 4; ++k)
-                        a.addr[k] = (v6 || k == 0) ? ((uint32_t)m[o + 4 * k] << 24 | (uint32_t)m[o + 4 * k + 1] << 16 |
-                                                      (uint32_t)m[o + 4 * k + 2] << 8 | m[o + 4 * k + 3])
+                        a.addr[k] = (v6 || k == 0) ? (m(o + 4 * k) << 24 | m(o + 4 * k + 1) << 16 |
+                                                      m(o + 4 * k + 2) << 8 | m(o + 4 * k + 3))
                                                    : 0u;
                     ++*n_addrs;
                 } else {
@@ -159,7 +219,7 @@ __device__ uint32_t dns_record(const uint8_t* m, uint32_t len, uint32_t* off, bo
             if (rdlen < 1u) return FB_DNS_WRONG_RDATA_LENGTH;
             uint32_t p = 0u;
             while (p < rdlen) {
-                const uint32_t l = m[o + p];
+                const uint32_t l = m(o + p);
                 p += 1u;
                 if (rdlen < l + p) return FB_DNS_WRONG_RDATA_LENGTH;
                 p += l;
@@ -174,15 +234,12 @@ __device__ uint32_t dns_record(const uint8_t* m, uint32_t len, uint32_t* off, bo
     return FB_DNS_OK;
 }
 
-__global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigned long long frames_bytes,
-                                                  const fb_dns_out* dns, uint32_t n, const fb_batch_stats* stats,
-                                                  fb_dns_msg* msgs, char* names, fb_ip* addrs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t cnt = stats ? (uint32_t)min((unsigned long long)n, stats->n_dns) : n;
-    if (i >= cnt) return;
-    const fb_dns_out d = dns[i];
+// Packet::parse of one message and the fields the resolver keeps (first question's name, A / AAAA
+// answers); the record's *out.
+template <class M>
+__device__ void dns_message(const M& m, uint32_t len, uint32_t pkt_index, fb_ip* A, uint32_t* nm, fb_dns_msg* out) {
     fb_dns_msg r;
-    r.pkt_index = d.pkt_index;
+    r.pkt_index = pkt_index;
     r.id = 0;
     r.flags = 0;
     r.questions = r.answers = 0;
@@ -190,11 +247,6 @@ __global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigne
     r.n_addrs = 0;
     r.reserved = 0;
     uint32_t st = FB_DNS_OK, flags = 0u, na = 0u;
-    const unsigned long long lim = (unsigned long long)d.payload_offset + d.payload_length;
-    const uint32_t len = lim <= frames_bytes ? d.payload_length : 0u;
-    const uint8_t* m = frames + d.payload_offset;
-    fb_ip* A = addrs + (size_t)i * FB_DNS_MAX_ADDRS;
-    char* name = names + (size_t)i * FB_DNS_MAX_NAME;
     if (len < 12u) {
         st = FB_DNS_HEADER_TOO_SHORT;
     } else {
@@ -202,7 +254,7 @@ __global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigne
         const uint32_t qd = be16at(m, 4u), an = be16at(m, 6u), ns = be16at(m, 8u), ar = be16at(m, 10u);
         r.questions = (uint16_t)qd;
         r.answers = (uint16_t)an;
-        if ((m[2] & 0x80u) == 0u) flags |= FB_DNS_QUERY;
+        if ((m(2u) & 0x80u) == 0u) flags |= FB_DNS_QUERY;
         uint32_t off = 12u, q0 = 0u;
         for (uint32_t q = 0; q < qd && !st; ++q) {
             uint32_t bl;
@@ -219,7 +271,7 @@ __global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigne
         for (uint32_t k = 0; k < an + ns && !st; ++k) st = dns_record(m, len, &off, k < an, A, &na, &flags);
         bool opt = false;
         for (uint32_t k = 0; k < ar && !st; ++k) {
-            if (off + 3u <= len && m[off] == 0u && m[off + 1u] == 0u && m[off + 2u] == 41u) {
+            if (off + 3u <= len && m(off) == 0u && m(off + 1u) == 0u && m(off + 2u) == 41u) {
                 off += 1u;  // the OPT record's root name
                 if (opt) { st = FB_DNS_ADDITIONAL_OPT; break; }
                 opt = true;
@@ -234,7 +286,7 @@ __global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigne
         }
         if (!st && qd > 0u) {
             bool rev = false;
-            const uint32_t nl = dns_name_write(m, q0, name, FB_DNS_MAX_NAME, &rev);
+            const uint32_t nl = dns_name_write(m, q0, nm, FB_DNS_MAX_NAME, &rev);
             flags |= FB_DNS_HAS_QUESTION | (rev ? FB_DNS_REVERSE : 0u) | (nl > FB_DNS_MAX_NAME - 1u ? FB_DNS_NAME_TRUNCATED : 0u);
             r.name_len = (uint16_t)min(nl, FB_DNS_MAX_NAME - 1u);
         }
@@ -242,7 +294,57 @@ __global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigne
     r.status = (uint8_t)st;
     r.flags = (uint8_t)(st ? 0u : flags);
     r.n_addrs = (uint8_t)(st ? 0u : na);
-    msgs[i] = r;
+    *out = r;
+}
+
+// One wavefront (workgroup) per 64 messages.  The messages are first copied into LDS, one message
+// per step of the wave with coalesced dword loads (range-checked buffer loads, so nothing is read
+// past the frame buffer; only the dwords the message covers), up to kStage bytes each; each lane
+// then parses its own message from LDS (17 KiB per wavefront: 9 per CU).
+constexpr uint32_t kStage = 256;  // staged bytes per message (longer ones continue from HBM)
+__global__ __launch_bounds__(64) void k_dns_parse(const uint8_t* frames, unsigned long long frames_bytes,
+                                                  const fb_dns_out* dns, uint32_t n, const fb_batch_stats* stats,
+                                                  fb_dns_msg* msgs, char* names, fb_ip* addrs) {
+    __shared__ uint32_t s_msg[64][kStage / 4 + 1];  // +1 dword of row padding (lanes read different rows)
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i0 = blockIdx.x * 64u, i = i0 + lane;
+    const uint32_t cnt = stats ? (uint32_t)min((unsigned long long)n, stats->n_dns) : n;
+    if (i0 >= cnt) return;  // uniform
+    const bool live = i < cnt;
+    const fb_dns_out d = dns[live ? i : i0];
+    const unsigned long long lim = (unsigned long long)d.payload_offset + d.payload_length;
+    const uint32_t len = (live && lim <= frames_bytes) ? d.payload_length : 0u;
+    const uint32_t fb = (uint32_t)min(frames_bytes, (unsigned long long)0xFFFFFFFFull);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void*)frames, (short)0, (int)fb, 0x00020000);
+    const uint32_t base = d.payload_offset & ~3u;
+    // copy message j's dwords [base_j, base_j + kStage) with the whole wave (lane = dword), 32
+    // messages' loads in flight before their LDS writes (a load-then-write per message would wait
+    // out one HBM round trip per message); dwords past the message read as 0 (out-of-range offset)
+    for (uint32_t j0 = 0; j0 < 64u; j0 += 32u) {
+        uint32_t v[32];
+#pragma unroll
+        for (uint32_t u = 0; u < 32u; ++u) {
+            const uint32_t bj = __builtin_amdgcn_readlane(base, (int)(j0 + u)), lj = __builtin_amdgcn_readlane(len, (int)(j0 + u));
+            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rf, 4u * lane < lj + 4u ? bj + 4u * lane : 0xFFFFFFF0u, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 32u; ++u) s_msg[j0 + u][lane] = v[u];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!live) return;
+    const uint32_t mis = d.payload_offset & 3u;
+    fb_ip* A = addrs + (size_t)i * FB_DNS_MAX_ADDRS;
+    uint32_t* nm = reinterpret_cast<uint32_t*>(names + (size_t)i * FB_DNS_MAX_NAME);  // 4-B aligned (fb_dns_parse_dev)
+    // the copy starts at the dword holding the first byte: kStage - mis message bytes are staged;
+    // when every live lane's message is whole in LDS the wave runs the LDS-only parse (no
+    // per-byte range branch, dword-wide label checks)
+    if (__all(len <= kStage - mis)) {
+        dns_message(MsgLds{s_msg[lane], mis}, len, d.pkt_index, A, nm, msgs + i);
+    } else {
+        dns_message(MsgMixed{reinterpret_cast<const uint8_t*>(s_msg[lane]) + mis, rf, d.payload_offset, kStage - mis},
+                    len, d.pkt_index, A, nm, msgs + i);
+    }
 }
 
 hipError_t launch_dns_parse(const uint8_t* frames, unsigned long long frames_bytes, const fb_dns_out* dns, uint32_t n,

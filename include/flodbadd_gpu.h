@@ -480,6 +480,7 @@ typedef struct fb_dns_msg {
  * DnsPacket::parse does, keeping what process_dns_packet uses: id, query bit, the first
  * question's name, the A / AAAA answers in order.  n = d_dns entries; with d_stats non-NULL only
  * the first d_stats->n_dns (read on the device) are parsed.  d_names: n * FB_DNS_MAX_NAME bytes,
+ * 4-byte aligned (the name is written a dword at a time; bytes past name_len are unspecified),
  * d_addrs: n * FB_DNS_MAX_ADDRS fb_ip.  DEVICE pointers, asynchronous.  The ordered bookkeeping
  * (pending queries by id, resolutions) stays on the host: a few operations per DNS packet. */
 int fb_dns_parse_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes, const fb_dns_out* d_dns,

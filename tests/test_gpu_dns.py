@@ -72,6 +72,62 @@ def test_dns_parse_vs_oracle():
     assert len(seen) >= 7  # the mutations reach most rejection rules
 
 
+def test_dns_long_messages_across_the_stage():
+    """Messages longer than the kernel's LDS stage (256 B): answers, names and pointers on both
+    sides of the boundary, at every byte alignment of the payload (the stage starts at the dword
+    holding the first byte), plus their mutations."""
+    long = [G.response(9, "long.example", [("A", "192.0.2.%d" % i) for i in range(30)]),
+            G.response(10, "mixed.example", [("AAAA", "2001:db8::%x" % i) for i in range(9)] +
+                       [("CNAME", "tail-%d.mixed.example" % i) for i in range(6)] + [("A", "198.51.100.1")]),
+            G.header(11, True, qd=1, an=2) + G.question("txt.example", 16) +
+            G.rr(b"\xc0\x0c", 16, b"\xff" + b"t" * 255) + G.rr(b"\xc0\x0c", 1, bytes([203, 0, 113, 5]))]
+    rnd = random.Random(5)
+    msgs = []
+    for k in range(1200):
+        m = bytearray(long[k % len(long)])
+        if k >= len(long) * 4 and rnd.random() < 0.7:
+            i = rnd.randrange(len(m))
+            m[i] = rnd.randrange(256) if rnd.random() < 0.5 else m[i]
+            if rnd.random() < 0.3:
+                m = m[: rnd.randrange(200, len(m) + 1)]
+        msgs.append(bytes(m))
+    assert max(len(m) for m in msgs) > 400
+    for pad in range(4):  # a pad message shifts every following payload by pad bytes
+        batch = [b"\0" * (12 + pad)] + msgs
+        g_msgs, g_names, g_addrs = _run(batch)
+        for i, m in enumerate(batch):
+            r, nm, ad = coracle.dns_parse(m, i)
+            assert g_msgs[i].tobytes() == r.tobytes(), (pad, i, m.hex())
+            assert bytes(g_names[i][: len(nm)]) == nm
+            assert g_addrs[i][: len(ad)].tobytes() == ad.tobytes()
+
+
+def test_dns_names_alignment_checked():
+    """d_names is written a dword at a time: a misaligned pointer is refused up front."""
+    from flodbadd_amd import dns as D
+    lib = N.gpu_lib()
+    msg = G.query(1, "www.example.com")
+    rec = np.zeros(1, dtype=N.DNS_OUT_DTYPE)
+    rec[0] = (0, 0, len(msg), 17, 2, 0)
+    d_fr = N.DeviceBuffer(len(msg)).upload(np.frombuffer(msg, dtype=np.uint8))
+    d_dns = N.DeviceBuffer(rec.nbytes).upload(rec)
+    d_msg = N.DeviceBuffer(N.DNS_MSG_DTYPE.itemsize)
+    d_names = N.DeviceBuffer(2 * N.FB_DNS_MAX_NAME)
+    d_addrs = N.DeviceBuffer(N.FB_DNS_MAX_ADDRS * N.FB_IP_DTYPE.itemsize)
+    try:
+        rc = lib.fb_dns_parse_dev(D._ctx(), d_fr.ptr, len(msg), d_dns.ptr, 1, None, d_msg.ptr, d_names.ptr.value + 2,
+                                  d_addrs.ptr, None)
+        assert rc == N.FB_ERR_INVAL and b"aligned" in lib.fb_last_error()
+        N.check(lib.fb_dns_parse_dev(D._ctx(), d_fr.ptr, len(msg), d_dns.ptr, 1, None, d_msg.ptr, d_names.ptr.value + 4,
+                                     d_addrs.ptr, None))
+        m = d_msg.download(np.zeros(1, dtype=N.DNS_MSG_DTYPE))
+        nm = d_names.download(np.zeros(2 * N.FB_DNS_MAX_NAME, dtype=np.uint8))
+        assert int(m[0]["status"]) == 0 and bytes(nm[4: 4 + int(m[0]["name_len"])]) == b"www.example.com"
+    finally:
+        for b in (d_fr, d_dns, d_msg, d_names, d_addrs):
+            b.free()
+
+
 def test_dns_end_to_end_from_frames(gpu_capture):
     """UDP and DNS-over-TCP frames -> parse_classify (DNS side records) -> GPU parse -> resolver,
     equal to the resolver run on the oracle's parses of the same payloads."""
