@@ -647,10 +647,15 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         constexpr uint32_t kHead16 = kSlotWords * 8u / 16u;  // 6 uint4 per slot head
         FlowSlot* T = P.table + (size_t)part * kFlowSlots;
         const uint4* g = reinterpret_cast<const uint4*>(T);
+#ifndef FB_K2_NO_SLICEIO  // ablation (timing only): no slice load / write-back
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
             slice4[j] = g[(size_t)sl * (sizeof(FlowSlot) / 16u) + w];
         }
+#else
+        for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) slice4[j] = make_uint4(0, 0, 0, 0);
+        (void)g;
+#endif
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
             const uint32_t w = j % kScrU32;
             scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
@@ -700,7 +705,11 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     r[2] = c[2];
                     r[3] = c[3];
                 } else {  // a record slot of the batch (56 B, 8-B aligned at odd slots)
+#ifdef FB_K2_LOCAL_GATHER  // ablation (timing only): gather from a cache-resident window
+                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (v & 0xFFFFu));
+#else
                     const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + v);
+#endif
                     r[0] = ld_u4(q);
                     r[1] = ld_u4(q + 4);
                     r[2] = ld_u4(q + 8);
@@ -759,13 +768,17 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             }
             __syncthreads();
         }
+#ifndef FB_K2_NO_FINISH  // ablation (timing only): no ordered-field fold
         for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads)
             finish_slot(T + j, scr + (size_t)j * kScrU32, P.recs, P.batch);
+#endif
+#ifndef FB_K2_NO_SLICEIO
         uint4* gw = reinterpret_cast<uint4*>(T);
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
             gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
         }
+#endif
     }
     n_new = block_sum(n_new, sh);
     n_upd = block_sum(n_upd, sh);
