@@ -141,7 +141,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
     if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
         raise RuntimeError("bad batch stats: %s" % st)
-    if flow and int(st[0]["new_sessions"]) + int(st[0]["updated_sessions"]) != int(st[0]["n_session"]):
+    # FB_BENCH_ABLATION: timing-only library variants (tools/build_variants.sh) skip the table check
+    if flow and int(st[0]["new_sessions"]) + int(st[0]["updated_sessions"]) != int(st[0]["n_session"]) \
+            and not os.environ.get("FB_BENCH_ABLATION"):
         raise RuntimeError("flow upsert lost records: %s" % st)
     ev0, ev1 = N.Event(), N.Event()
     launches = plan(steps)
@@ -187,7 +189,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         # after warmup every session exists: the timed steps are all updates
         same = [k for k in st.dtype.names if k not in ("new_sessions", "updated_sessions")]
         assert all(int(st2[0][k]) == int(st[0][k]) for k in same), (st, st2)
-        assert int(st2[0]["updated_sessions"]) + int(st2[0]["new_sessions"]) == int(st2[0]["n_session"])
+        assert int(st2[0]["updated_sessions"]) + int(st2[0]["new_sessions"]) == int(st2[0]["n_session"]) \
+        or os.environ.get("FB_BENCH_ABLATION")
         # the parse stage as it runs inside the fused call (for fb_process_seg_dev: the
         # partition-writing instance of k_parse_seg), the update the rest of the step
         parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps

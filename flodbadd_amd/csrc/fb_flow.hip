@@ -353,14 +353,39 @@ __device__ __forceinline__ uint32_t lds_find(const unsigned long long* tab, cons
     return ~0u;
 }
 
+// Lookup while other lanes may be inserting (tags read with acquire, so a published tag's key
+// words are visible); a slot being inserted (tag 1) is probed past.  ~0u: not (yet) present --
+// the caller then takes lds_upsert, which waits on such a slot.  Steady-state batches mostly
+// update existing flows, so this branch-light loop is the common path and the upsert with its
+// claim / spin states the rare one (it costs ~40 scalar mask instructions per probe even when
+// nothing spins).
+template <uint32_t kStride, uint32_t kSlots>
+__device__ __forceinline__ uint32_t lds_lookup(unsigned long long* tab, const uint32_t key[10], uint32_t h32) {
+    const uint32_t want32 = h32 | 2u;
+    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
+    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
+    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
+    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
+    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
+    uint32_t i = h32 & (kSlots - 1u);
+    for (uint32_t probe = 0; probe < kSlots; ++probe) {
+        unsigned long long* s = tab + (size_t)i * kStride;
+        const unsigned long long t = lds_ld(s);
+        if (t == 0ull) break;
+        if ((uint32_t)t == want32 && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) return i;
+        i = (i + 1u) & (kSlots - 1u);
+    }
+    return ~0u;
+}
+
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
 __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
                                            const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* ent_slot,
                                            uint32_t idx, uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    uint32_t i;
-    const int result = lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
+    uint32_t i = lds_lookup<kSlotWords, kFlowSlots>(slice, key, e3.w);
+    const int result = i != ~0u ? 0 : lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
     if (result < 0) {
         atomicOr(err, result == -2 ? 2u : 4u);  // spin expired / partition full
         return -1;
@@ -398,8 +423,8 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
                                               const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
                                               uint32_t* err) {
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    uint32_t i;
-    const int result = lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
+    uint32_t i = lds_lookup<kSlotWords, kFlowSlots>(slice, key, e3.w);
+    const int result = i != ~0u ? 0 : lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
     if (result < 0) {
         atomicOr(err, result == -2 ? 2u : 4u);
         return -1;
@@ -440,43 +465,38 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     return result;
 }
 
-// Fold one slot's batch scratch into its ordered fields in HBM (after every entry was applied).
-__device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, const fb_pkt_out* recs, uint32_t batch) {
+// Fold one slot's batch scratch into its ordered fields (after every entry was applied).  o0, o1 =
+// the slot's ordered fields as loaded with the slice (first_seen, last_seen | end_seen, hist_len,
+// hist_state); the three record words it needs (first / last / end packet) are loaded together.
+__device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, const fb_pkt_out* recs, uint32_t batch,
+                                            const uint4 o0, const uint4 o1) {
     const uint32_t first = q[kScFirst];
     if (first == ~0u) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
     auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
         return ld_u2(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
     };
-    const uint32_t flags = q[kScMask];
-    unsigned long long end_seen;
-    uint32_t state, len;
-    if (flags & (1u << 16)) {  // new flow: start_time = its first packet, end_time None
-        g->first_seen = hi | rec_word(first).y;
-        end_seen = FB_SEEN_NONE;
-        state = 0u;
-        len = 0u;
-    } else {
-        end_seen = g->end_seen;
-        state = g->hist_state;
-        len = g->hist_len;
-    }
-    g->last_seen = hi | rec_word(q[kScLast]).y;
+    const uint32_t flags = q[kScMask], last = q[kScLast], end = q[kScEnd];
+    const bool fresh = (flags & (1u << 16)) != 0u;  // new flow: start_time = its first packet, end_time None
+    const uint2 wf = rec_word(first), wl = rec_word(last), we = rec_word(end != ~0u ? end : last);
+    const unsigned long long first_seen = fresh ? hi | wf.y : (o0.x | (unsigned long long)o0.y << 32);
+    unsigned long long end_seen = fresh ? FB_SEEN_NONE : (o1.x | (unsigned long long)o1.y << 32);
+    const uint32_t state = fresh ? 0u : o1.w, len = fresh ? 0u : o1.z;
+    const unsigned long long last_seen = hi | wl.y;
     const uint32_t mask = state & 0xFFFFu;
     uint32_t cs = state >> 16;
-    const uint32_t end = q[kScEnd];
     if (end != ~0u && end_seen == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
-        const uint2 w = rec_word(end);
-        uint32_t m = mask | (1u << hist_bit((w.x >> 16) & 0xFFu));
+        uint32_t m = mask | (1u << hist_bit((we.x >> 16) & 0xFFu));
 #pragma unroll
         for (uint32_t b = 0; b < 4u; ++b) m |= q[kScChar + b] <= end ? 1u << b : 0u;
         cs = conn_state_of(m) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
-        end_seen = hi | w.y;
+        end_seen = hi | we.y;
     }
-    g->end_seen = end_seen;
-    g->hist_len = len + q[kScCount];
-    g->hist_state = (mask | (flags & 0xFFFFu)) | (cs << 16);
+    uint4* t = reinterpret_cast<uint4*>(g) + 6;  // bytes 96..127: the ordered fields
+    t[0] = make_uint4((uint32_t)first_seen, (uint32_t)(first_seen >> 32), (uint32_t)last_seen, (uint32_t)(last_seen >> 32));
+    t[1] = make_uint4((uint32_t)end_seen, (uint32_t)(end_seen >> 32), len + q[kScCount], (mask | (flags & 0xFFFFu)) | (cs << 16));
 }
+static_assert(offsetof(FlowSlot, first_seen) == 96 && offsetof(FlowSlot, hist_state) == 124, "ordered fields at 96..127");
 
 // ---------------------------------------------------------------------------------------------
 // K1c: combine the records of one key inside the hot (chunk, partition) groups K1 listed.
@@ -639,14 +659,24 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
     const uint32_t* col = P.cols + (size_t)part * P.chunk_stride;
 
-    uint32_t mine = 0u;
-    for (uint32_t b = threadIdx.x; b < chunks; b += kFlowK2Threads) mine += col[b] >> 16;
+    // the first round's group rows (kept for it) and the rows past it: the partition's total
+    uint32_t v0[kK2Cpt], mine = 0u;
+#pragma unroll
+    for (uint32_t c = 0; c < kK2Cpt; ++c) {
+        const uint32_t b = threadIdx.x * kK2Cpt + c;
+        v0[c] = b < chunks ? col[b] : 0u;
+        mine += v0[c] >> 16;
+    }
+    for (uint32_t b = kK2Cpt * kFlowK2Threads + threadIdx.x; b < chunks; b += kFlowK2Threads) mine += col[b] >> 16;
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
     if (total != 0ull) {
         constexpr uint32_t kHead16 = kSlotWords * 8u / 16u;  // 6 uint4 per slot head
         FlowSlot* T = P.table + (size_t)part * kFlowSlots;
         const uint4* g = reinterpret_cast<const uint4*>(T);
+        // slot tid's ordered fields, for finish_slot (in flight with the slice load)
+        static_assert(kFlowSlots == kFlowK2Threads, "one slot per thread in the fold");
+        const uint4 ord0 = g[(size_t)threadIdx.x * 8u + 6u], ord1 = g[(size_t)threadIdx.x * 8u + 7u];
 #ifndef FB_K2_NO_SLICEIO  // ablation (timing only): no slice load / write-back
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
@@ -669,7 +699,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
 #pragma unroll
             for (uint32_t c = 0; c < kK2Cpt; ++c) {
                 const uint32_t b = g0 + threadIdx.x * kK2Cpt + c;
-                v[c] = b < chunks ? col[b] : 0u;
+                v[c] = g0 == 0u ? v0[c] : (b < chunks ? col[b] : 0u);
                 mine += v[c] >> 16;
             }
             uint32_t tot;
@@ -769,8 +799,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             __syncthreads();
         }
 #ifndef FB_K2_NO_FINISH  // ablation (timing only): no ordered-field fold
-        for (uint32_t j = threadIdx.x; j < kFlowSlots; j += kFlowK2Threads)
-            finish_slot(T + j, scr + (size_t)j * kScrU32, P.recs, P.batch);
+        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.recs, P.batch, ord0, ord1);
 #endif
 #ifndef FB_K2_NO_SLICEIO
         uint4* gw = reinterpret_cast<uint4*>(T);
