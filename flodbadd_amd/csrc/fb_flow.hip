@@ -370,9 +370,14 @@ __device__ __forceinline__ uint32_t lds_lookup(unsigned long long* tab, const ui
     uint32_t i = h32 & (kSlots - 1u);
     for (uint32_t probe = 0; probe < kSlots; ++probe) {
         unsigned long long* s = tab + (size_t)i * kStride;
-        const unsigned long long t = lds_ld(s);
+        // the tag, then the key words, issued together (one wait): a wave's LDS reads are served
+        // in order and a publisher writes the key before its release store of the tag, so a
+        // published tag read first implies its key words; the compare is branch-free
+        const unsigned long long t = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
+        const unsigned long long a = s[1], b = s[2], c = s[3], d = s[4], e = s[5];
         if (t == 0ull) break;
-        if ((uint32_t)t == want32 && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) return i;
+        if (((uint32_t)t == want32) & (a == kw0) & (b == kw1) & (c == kw2) & (d == kw3) & (e == kw4)) return i;
         i = (i + 1u) & (kSlots - 1u);
     }
     return ~0u;
@@ -556,8 +561,8 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             rec_entry(P.recs, E[s0 + k], e);
             const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                       e[2].y & 0xFFFFu};
-            uint32_t j;
-            if (lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0) continue;
+            uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
+            if (j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0) continue;
             const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
             uint32_t* f = L.f + j * kCombF;
             atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
