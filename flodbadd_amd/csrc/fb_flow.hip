@@ -253,24 +253,33 @@ __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character).
-__device__ __forceinline__ uint32_t hist_bit(uint32_t c) {
-    switch (c) {
-        case 'S': return 0u;
-        case 's': return 1u;
-        case 'H': return 2u;
-        case 'h': return 3u;
-        case 'F': return 4u;
-        case 'f': return 5u;
-        case 'R': return 6u;
-        case 'r': return 7u;
-        case '>': return 8u;
-        case '<': return 9u;
-        case 'A': return 10u;
-        case 'a': return 11u;
-        case '-': return 12u;
-        default: return 16u;
+// FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character), branch-free (a
+// switch here compiled to a divergent compare tree of ~100 scalar mask instructions per entry):
+// c & 31 tells the classes apart (S H F R A and > < -), c >= 96 marks the responder's lower-case
+// letter (bit + 1), and the result is checked against the table "SsHhFfRr><Aa-".
+constexpr unsigned long long hist_nibbles(uint32_t half) {
+    const char cs[8] = {'S', 'H', 'F', 'R', '>', '<', 'A', '-'};
+    const uint32_t bs[8] = {0u, 2u, 4u, 6u, 8u, 9u, 10u, 12u};
+    unsigned long long v = ~0ull;
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t k = (uint32_t)cs[j] & 31u;
+        if ((k >> 4) == half) v = (v & ~(15ull << (4u * (k & 15u)))) | ((unsigned long long)bs[j] << (4u * (k & 15u)));
     }
+    return v;
+}
+constexpr unsigned long long hist_chars(uint32_t half) {
+    const char t[13] = {'S', 's', 'H', 'h', 'F', 'f', 'R', 'r', '>', '<', 'A', 'a', '-'};
+    unsigned long long v = 0ull;
+    for (uint32_t j = 8u * half; j < 8u * half + 8u && j < 13u; ++j) v |= (unsigned long long)(uint8_t)t[j] << (8u * (j & 7u));
+    return v;
+}
+__device__ __forceinline__ uint32_t hist_bit(uint32_t c) {
+    constexpr unsigned long long kN0 = hist_nibbles(0), kN1 = hist_nibbles(1), kC0 = hist_chars(0), kC1 = hist_chars(1);
+    const uint32_t k = c & 31u;
+    const uint32_t nib = (uint32_t)(((k < 16u ? kN0 : kN1) >> (4u * (k & 15u))) & 15u);
+    const uint32_t b = nib + (c >= 96u ? 1u : 0u);
+    const uint32_t want = (uint32_t)(((b < 8u ? kC0 : kC1) >> (8u * (b & 7u))) & 0xFFu);
+    return (nib != 15u && b < 13u && want == c) ? b : 16u;
 }
 
 // determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
