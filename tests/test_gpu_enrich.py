@@ -19,15 +19,15 @@ from test_enrich_oracle import TSV
 pytestmark = pytest.mark.gpu
 
 
-def _random_tables(seed):
+def _random_tables(seed, n4=3000, n6=1500):
     rnd = random.Random(seed)
     rows = []
-    for _ in range(3000):  # v4, mostly disjoint with some overlaps and duplicates
+    for _ in range(n4):  # v4, mostly disjoint with some overlaps and duplicates
         a = rnd.randrange(1 << 32)
         b = min((1 << 32) - 1, a + rnd.choice([0, 1, 255, 4095, 65535, 1 << 20]))
         rows.append("%s\t%s\t%d\tC%d\tO%d" % (ipaddress.IPv4Address(a), ipaddress.IPv4Address(b), rnd.randrange(1, 70000),
                                                rnd.randrange(9), rnd.randrange(99)))
-    for _ in range(1500):
+    for _ in range(n6):
         a = rnd.randrange(1 << 128)
         b = min((1 << 128) - 1, a + rnd.choice([0, 1, 1 << 64, 1 << 80, 1 << 100]))
         rows.append("%s\t%s\t%d\tC\tO" % (ipaddress.IPv6Address(a), ipaddress.IPv6Address(b), rnd.randrange(1, 70000)))
@@ -94,9 +94,12 @@ def test_ip_lookup_random_tables(gpu_capture, seed):
     assert (ga >= 0).sum() > 100 and (gl != 0).sum() > 100
 
 
-def test_flow_enrich_vs_oracle(gpu_capture):
+@pytest.mark.parametrize("n4,n6", [(3000, 1500), (60000, 6000)])
+def test_flow_enrich_vs_oracle(gpu_capture, n4, n6):
+    """The kernel keeps the top 12 (v4) / 10 (v6) levels of each search in LDS: the small tables
+    fit those trees, the large ones also probe the tables in memory below them."""
     from flodbadd_amd.capture import lan_v6_table, own_ip_table
-    v4, v6, recs, cidrs, names = _random_tables(7)
+    v4, v6, recs, cidrs, names = _random_tables(7, n4, n6)
     gpu_capture.clear_all_sessions()
     gpu_capture.set_asn_tables(v4, v6)
     gpu_capture.set_blacklists(cidrs)
