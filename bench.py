@@ -494,7 +494,7 @@ def main():
     ap.add_argument("--no-single-launch", action="store_true", help="skip timing one batch per launch")
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
-                         "default = the rotated batches (C2 8, C3 4), 1 for C4")
+                         "default = the rotated batches (C2 32, C3 12), 1 for C4")
     ap.add_argument("--zipf", type=float, default=None,
                     help="profiling: the main run with Zipf(s) flow popularity instead of uniform")
     args = ap.parse_args()
@@ -572,8 +572,7 @@ def main():
                                             unit="Mpackets/s", ms_per_step=round(r1["elapsed"] * 1e3 / st_1, 4),
                                             roofline_achieved_GBs=round(r1["algo_bytes"] / pl1 / 1e9, 1),
                                             roofline_frac=round(r1["algo_bytes"] / pl1 / 1e9 / HBM_PEAK_GBS, 4))
-    # N > 1: the scaling line needs only the headline path; the dense layout's persistent
-    # look-back kernel also needs all its workgroups resident on the device
+    # N > 1: the scaling line needs only the headline path (the other layout is timed at N = 1)
     if not args.no_other_mode and world == 1:
         other = "dense" if args.mode == "seg" else "seg"
         st_o = max(args.steps // 2, 10)
