@@ -130,10 +130,31 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     static_assert(kFlowChunk % kFlowK1Threads == 0, "whole records per thread");
     uint32_t pv[kPer];  // partition of each owned slot, ~0u: no record
     if (P.rec_part) {   // partitions from the parse of this batch (fb_process_seg_dev): 4 B per record
+        // every slot's segment count word (one per wave: 64 consecutive slots) and partition word
+        // loaded unconditionally, then masked: a load that waited on the validity test would put
+        // two dependent round trips per slot in sequence (K1 142 -> DESIGN)
+        // (the null test of P.seg outside the loops: inside, the compiler waited for each load
+        // at the join of its branch)
+        uint32_t sw[kPer];
+        if (P.seg) {
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; ++j) {
+                const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
+                sw[j] = P.seg[(base + k) >> 6];
+                pv[j] = P.rec_part[base + k];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; ++j) {
+                const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
+                sw[j] = 0xFFFFu;
+                pv[j] = P.rec_part[base + k];
+            }
+        }
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t k = threadIdx.x + j * kFlowK1Threads;
-            pv[j] = k < cnt && slot_valid(P, base + k) ? P.rec_part[base + k] : ~0u;
+            if (!(k < cnt && ((base + k) & 63u) < (sw[j] & 0xFFFFu))) pv[j] = ~0u;
         }
     } else {            // hashed here, four records' key loads in flight at a time
         constexpr uint32_t kG = 4;
