@@ -837,10 +837,16 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.recs, P.batch, ord0, ord1);
 #endif
 #ifndef FB_K2_NO_SLICEIO
+        // only the slots this batch touched (inserted or updated) changed; the others' heads are
+        // not written back (a 96-B head alone is a partial line)
         uint4* gw = reinterpret_cast<uint4*>(T);
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
+#ifdef FB_NO_ORDERED  // (the ablation keeps no scratch: every head is written)
             gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
+#else
+            if (scr[(size_t)sl * kScrU32 + kScFirst] != ~0u) gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
+#endif
         }
 #endif
     }
