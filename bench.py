@@ -52,7 +52,7 @@ def plan_launches(k, bpl):
 
 
 def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1,
-               synth_kw=None):
+               synth_kw=None, pipelined=False, stage_extras=True):
     """Time `steps` steps (one step = one batch through the hot path).  mode "seg":
     fb_parse_classify_seg_dev (records compacted per 64-frame wavefront segment, no
     cross-workgroup dependency); mode "dense": fb_parse_classify_dev (the same kernel + the
@@ -62,7 +62,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     bpl > 1 (mode "seg", no flow): consecutive steps share launches of up to bpl batches
     (fb_parse_classify_seg_batches_dev; each batch its own outputs and stats), split evenly by
     plan_launches.  Batch i uses buffer set i % rotate, so rotate >= bpl keeps the batches of a
-    launch distinct."""
+    launch distinct.  pipelined (flow, mode "seg"): fb_process_seg_async_dev -- each batch's table
+    update on the context's own stream while the next batch is parsed (rotate >= 2 buffer sets),
+    joined (fb_flow_join) inside the timed region."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n, **(synth_kw or {}))
     nbytes = frames.nbytes
@@ -119,9 +121,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
         if mode == "seg" and flow:
             # fb_process_seg_dev: parse + session upsert in one call (the parse also hands each
-            # record's table partition to the update's histogram pass)
-            rc = lib.fb_process_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None, d_st.ptr,
-                                        stream.ptr)
+            # record's table partition to the update's histogram pass); pipelined: the async form
+            fn = lib.fb_process_seg_async_dev if pipelined else lib.fb_process_seg_dev
+            rc = fn(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None, d_st.ptr, stream.ptr)
         elif mode == "seg":
             rc = lib.fb_parse_classify_seg_dev(ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr, None,
                                                d_st.ptr, stream.ptr)
@@ -137,6 +139,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     if flow:
         N.check(lib.fb_flow_clear(ctx, stream.ptr))
     run_steps(warmup, plan(warmup))
+    if pipelined:
+        N.check(lib.fb_flow_join(ctx, stream.ptr))
     stream.sync()
     st = bufs[0][4].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
     if int(st[0]["error"]) or int(st[0]["n_session"]) + int(st[0]["n_dns"]) + int(st[0]["n_drop"]) != n:
@@ -147,7 +151,13 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         raise RuntimeError("flow upsert lost records: %s" % st)
     ev0, ev1 = N.Event(), N.Event()
     launches = plan(steps)
-    if flow:
+    if flow and pipelined:
+        def run_timed():
+            for i in range(steps):
+                step(i)
+            N.check(lib.fb_flow_join(ctx, stream.ptr))  # the last update is part of the region
+            return steps
+    elif flow:
         # per step: start, the stage event (recorded by the library between parse and update), end
         evs = [(N.Event(), N.Event(), N.Event()) for _ in range(steps)]
 
@@ -192,10 +202,15 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         assert int(st2[0]["updated_sessions"]) + int(st2[0]["new_sessions"]) == int(st2[0]["n_session"]) \
         or os.environ.get("FB_BENCH_ABLATION")
         # the parse stage as it runs inside the fused call (for fb_process_seg_dev: the
-        # partition-writing instance of k_parse_seg), the update the rest of the step
-        parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps
-        flow_ms = sum(b.elapsed_ms(c) for _, b, c in evs) / steps
-        stage = dict(parse_ms=parse_ms, flow_ms=flow_ms)
+        # partition-writing instance of k_parse_seg), the update the rest of the step (the
+        # pipelined form overlaps them: no split)
+        if pipelined:
+            stage = dict(parse_ms=None, flow_ms=None)
+        else:
+            parse_ms = sum(a.elapsed_ms(b) for a, b, _ in evs) / steps
+            flow_ms = sum(b.elapsed_ms(c) for _, b, c in evs) / steps
+            stage = dict(parse_ms=parse_ms, flow_ms=flow_ms)
+    if flow and stage_extras:
         # ordered per-flow history of the last update (fb_flow_history_dev: keys + stable radix sort)
         slots = n if mode == "dense" else (n + 63) // 64 * 64
         d_h, d_s, d_n = N.DeviceBuffer(slots), N.DeviceBuffer(4 * slots), N.DeviceBuffer(4)
@@ -214,7 +229,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         stage["flows"] = int(cnt.value)
         stage.update(enrich_timing(N, lib, ctx, int(cnt.value), stream))
         stage.update(dns_timing(N, lib, ctx, stream))
-    else:
+    if not flow:
         assert st2.tobytes() == st.tobytes()
     for b in bufs:
         for x in b:
@@ -495,6 +510,8 @@ def main():
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
                          "default = the rotated batches (C2 32, C3 12), 1 for C4")
+    ap.add_argument("--c4-sync", action="store_true",
+                    help="C4: time fb_process_seg_dev (one stream) instead of the pipelined fb_process_seg_async_dev")
     ap.add_argument("--zipf", type=float, default=None,
                     help="profiling: the main run with Zipf(s) flow popularity instead of uniform")
     args = ap.parse_args()
@@ -528,12 +545,15 @@ def main():
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
     # C2: 32 distinct batches (4 GB, far past the 256 MB Infinity Cache), so any K <= 32 steps is
     # one launch and longer runs are near-equal launches of up to 32 batches (plan_launches)
-    rotate = args.rotate or (32 if args.config == 2 else (12 if args.config == 3 else 1))
+    # C4 (segmented): the pipelined fused call, each batch's table update overlapping the next
+    # batch's parse, on two rotating buffer sets; --c4-sync times fb_process_seg_dev instead
+    pipe = args.config == 4 and args.mode == "seg" and not args.c4_sync
+    rotate = args.rotate or (32 if args.config == 2 else (12 if args.config == 3 else (2 if pipe else 1)))
     bpl = min(args.batches_per_launch or rotate, rotate, MAX_SEG_BATCHES) \
         if (args.mode == "seg" and args.config != 4) else 1
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
                         flow=args.config == 4, mode=args.mode, bpl=bpl,
-                        synth_kw=dict(zipf=1, zipf_s=args.zipf) if args.zipf else None)
+                        synth_kw=dict(zipf=1, zipf_s=args.zipf) if args.zipf else None, pipelined=pipe)
     # the dominant kernel's launches: algorithmic bytes per launch / average launch duration
     per_launch_s = main_r["ev_ms"] / 1e3 / main_r["launches"]
     algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
@@ -543,9 +563,19 @@ def main():
     extra = {}
     if main_r["stage"]:
         sg = main_r["stage"]
-        extra["c4_stages"] = dict(parse_ms=round(sg["parse_ms"], 4), flow_update_ms=round(sg["flow_ms"], 4),
+        split = sg
+        if pipe:  # the stage split and the one-stream rate from fb_process_seg_dev, fewer steps
+            st_s = max(args.steps // 2, 10)
+            rs = run_config(N, lib, ctx, 4, n, st_s, max(args.warmup // 2, 2), 1, rank, world, dist, flow=True,
+                            mode=args.mode, stage_extras=False)
+            split = rs["stage"]
+            extra["c4_sync"] = dict(value=round(world * n * st_s / rs["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                                    ms_per_step=round(rs["elapsed"] * 1e3 / st_s, 4),
+                                    note="fb_process_seg_dev: parse then update on one stream, no overlap")
+        extra["c4_stages"] = dict(parse_ms=round(split["parse_ms"], 4), flow_update_ms=round(split["flow_ms"], 4),
                                   stages_note="split by the stage event fb_process%s_dev records between its "
-                                              "parse and its update" % ("_seg" if args.mode == "seg" else ""),
+                                              "parse and its update%s" % ("_seg" if args.mode == "seg" else "",
+                                                                          " (one-stream run)" if pipe else ""),
                                   history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
                                   enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
                                   enrich_tables=sg["enrich_tables"],
@@ -553,8 +583,8 @@ def main():
                                   dns_payload_GBs=sg["dns_payload_GBs"], dns_ok=sg["dns_ok"],
                                   dns_workload="1M port-53 payloads (synth.dns_workload), device-resident",
                                   flows_in_table=sg["flows"],
-                                  parse_GBs=round(main_r["algo_bytes"] / sg["parse_ms"] / 1e6, 1),
-                                  flow_Mrec_s=round(main_r["stats"]["n_session"] / sg["flow_ms"] / 1e3, 1))
+                                  parse_GBs=round(main_r["algo_bytes"] / split["parse_ms"] / 1e6, 1),
+                                  flow_Mrec_s=round(main_r["stats"]["n_session"] / split["flow_ms"] / 1e3, 1))
     if args.config == 4 and not args.no_other_mode:  # C4 also with Zipf(1.1) flow popularity
         rz = run_config(N, lib, ctx, 4, n, max(args.steps // 2, 5), max(args.warmup // 2, 2), rotate, rank, world,
                         dist, flow=True, mode=args.mode, synth_kw=dict(zipf=1, zipf_s=1.1))
@@ -625,6 +655,18 @@ def main():
         cpu = cpu_baseline(main_r["frames"], main_r["offs"], args.cpu_seconds)
 
     lib.fb_destroy(ctx)
+    if bpl > 1:
+        output_desc = ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
+                       "%d batches per launch, each with its own outputs and stats)" % bpl)
+    elif args.mode == "seg" and args.config == 4:
+        output_desc = ("per-64-frame wavefront-compacted segments + session-table upsert " +
+                       ("(fb_process_seg_async_dev: each batch's update overlaps the next batch's parse, "
+                        "2 rotating buffer sets)" if pipe else "(fb_process_seg_dev)"))
+    elif args.mode == "seg":
+        output_desc = "per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)"
+    else:
+        output_desc = ("batch-wide compaction (fb_process_dev)" if args.config == 4 else
+                       "batch-wide compaction (fb_parse_classify_dev)")
     if rank == 0:
         line = {
             "metric": "Mpackets/s device-resident header parse + 5-tuple classify, 64B & IMIX frames",
@@ -641,14 +683,7 @@ def main():
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.config] + (" (Zipf(%g) flow popularity)" % args.zipf if args.zipf else ""), "frames_per_gpu_per_step": n,
                        "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
-                       "output": (("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
-                                   "%d batches per launch, each with its own outputs and stats)" % bpl) if bpl > 1 else
-                                  ("per-64-frame wavefront-compacted segments + session-table upsert "
-                                   "(fb_process_seg_dev)" if args.config == 4 else
-                                   "per-64-frame wavefront-compacted segments (fb_parse_classify_seg_dev)")
-                                  if args.mode == "seg" else
-                                  "batch-wide compaction (fb_process_dev)" if args.config == 4 else
-                                  "batch-wide compaction (fb_parse_classify_dev)"),
+                       "output": output_desc,
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, args.steps / main_r["launches"]),

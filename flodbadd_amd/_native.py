@@ -160,6 +160,8 @@ GPU_SYMBOLS = [
     ("fb_parse_classify_seg_batches_dev", _I, [_P, _P, _U32, _P]),
     ("fb_flow_update_seg_dev", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fb_process_seg_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_process_seg_async_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
+    ("fb_flow_join", _I, [_P, _P]),
     ("fb_flow_history_dev", _I, [_P, _P, _P, _P, _P]),
     ("fb_set_asn_tables", _I, [_P, _P, _U32, _P, _U32]),
     ("fb_set_blacklists", _I, [_P, _P, _U32]),

@@ -43,7 +43,8 @@ struct fb_ctx {
     bool need_reset = true;       // zero the tick + error words before the next launch
     uint32_t epoch = 0;           // parse launches so far: its parity picks the launch's error word
     uint32_t seg_grid = 0;        // streaming segmented kernel: co-resident blocks
-    uint32_t* d_error = nullptr;  // [2] error words, indexed by launch parity
+    uint32_t* d_error = nullptr;  // [4] error words, indexed by launch & 3 (a launch clears the next one's;
+                                  // a pipelined update still writes the one two launches back)
     // dense output (fb_parse_classify_dev & co., fb_seg_compact_dev): segment counts + their scan
     uint32_t* d_cseg = nullptr;            // [cseg_cap] segment counts (dense pass 1)
     unsigned long long* d_cpre = nullptr;  // [cseg_cap] batch-wide offset of every segment
@@ -72,7 +73,16 @@ struct fb_ctx {
     uint32_t* d_rec_flow = nullptr;       // [flow_recs] entry position per record slot
     uint32_t* d_ent_slot = nullptr;       // [flow_recs] table slot per entry
     uint32_t* d_rec_part = nullptr;       // [flow_recs] partition per record slot (fb_process_seg_dev)
-    const fb_pkt_out* part_recs = nullptr;  // the records d_rec_part was written for (one update)
+    const fb_pkt_out* part_recs = nullptr;  // the records part_buf was written for (one update)
+    uint32_t* part_buf = nullptr;           // the partition buffer the last fused parse wrote
+    uint32_t* part_target = nullptr;        // the buffer the next fused parse writes (null: d_rec_part)
+    // fb_process_seg_async_dev: updates on the context's own stream, one batch behind the parses
+    hipStream_t upd = nullptr;
+    hipEvent_t ev_parsed = nullptr;
+    hipEvent_t ev_upd[2] = {nullptr, nullptr};  // after the update of async batch k (k & 1)
+    uint64_t async_k = 0;                       // async batches issued
+    uint32_t* d_rec_part2 = nullptr;            // partitions of the odd async batches
+    const void* async_prev[3] = {nullptr, nullptr, nullptr};  // the last async batch's records, counts, stats
     uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* d_comb_ctl = nullptr;       // [2] its counters
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
@@ -116,6 +126,19 @@ int fbk::ctx_report_error(fb_ctx* c, uint64_t e) {
     return set_err(FB_ERR_INTERNAL, "device error word %llu", (unsigned long long)e);
 }
 
+// Entry points that read or write the table or the update scratch first order their stream after
+// the last pipelined update (fb_process_seg_async_dev runs updates on the context's own stream);
+// host code that frees or rewrites that scratch waits for it.
+static int join_updates(fb_ctx* c, hipStream_t s) {
+    if (c->async_k == 0) return FB_OK;
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[(c->async_k - 1u) & 1u], 0));
+    return FB_OK;
+}
+static int drain_updates(fb_ctx* c) {
+    if (c->async_k && c->upd) HIP_TRY(hipStreamSynchronize(c->upd));
+    return FB_OK;
+}
+
 namespace fbk {
 bool build_blacklist_tables(const fb_cidr* nets, uint32_t n, std::vector<uint32_t>& p4,
                             std::vector<unsigned long long>& m4, std::vector<uint4>& p6,
@@ -154,6 +177,8 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     recs = std::max<uint64_t>(recs, kFlowChunk);
     recs = (recs + kFlowChunk - 1) / kFlowChunk * kFlowChunk;
     if (recs <= c->flow_recs) return FB_OK;
+    int rc = drain_updates(c);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_entries);
     hipFree(c->d_comb);
@@ -162,11 +187,13 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_rec_flow);
     hipFree(c->d_ent_slot);
     hipFree(c->d_rec_part);
+    hipFree(c->d_rec_part2);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
-    c->d_rec_part = nullptr;
+    c->d_rec_part = c->d_rec_part2 = nullptr;
     c->part_recs = nullptr;
+    c->part_buf = nullptr;
     c->d_ent_slot = nullptr;
     c->d_entries = nullptr;
     c->d_comb = nullptr;
@@ -210,6 +237,8 @@ static int upload_cfg(fb_ctx* c, hipStream_t s) {
 // non-blocking stream that does not synchronise with the null stream.
 static int reset_launch_scratch(fb_ctx* c, hipStream_t s) {
     if (!c->need_reset) return FB_OK;
+    const int rc = drain_updates(c);  // a pipelined update may still write an error word
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->d_tick, 0, kTickWords * 8ull, s));
     HIP_TRY(hipMemsetAsync(c->d_error, 0, 16, s));
     c->need_reset = false;
@@ -251,7 +280,7 @@ static int scan_scratch(fb_ctx* c, hipStream_t s, SegScanScratch& sc) {
     sc.status = c->d_cstatus;
     sc.ticket = c->d_cticket;
     sc.epoch = ++c->scan_epoch;
-    sc.err = c->d_error + (c->epoch & 1u);
+    sc.err = c->d_error + (c->epoch & 3u);
     return FB_OK;
 }
 
@@ -377,9 +406,14 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_rec_flow);
     hipFree(c->d_ent_slot);
     hipFree(c->d_rec_part);
+    hipFree(c->d_rec_part2);
     hipFree(c->d_hot);
     hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
+    if (c->upd) hipStreamDestroy(c->upd);
+    if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
+    for (hipEvent_t e : c->ev_upd)
+        if (e) hipEventDestroy(e);
     hipFree(c->d_asn4);
     hipFree(c->d_asn6);
     hipFree(c->d_bl4_pos);
@@ -442,6 +476,9 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
                       bool want_parts = false, SegPass pass = SegPass::kSegments, fb_pkt_out* dense_out = nullptr,
                       fb_dns_out* dense_dns = nullptr) {
     int rc = reset_launch_scratch(c, s);
+    // a fused parse rewrites d_rec_part, which a pipelined update may still read (the pipelined
+    // call itself writes its own slot's buffer and orders that wait itself)
+    if (!rc && want_parts && !c->part_target) rc = join_updates(c, s);
     if (!rc) rc = upload_cfg(c, s);
     if (!rc) rc = ensure_flow_scratch(c, n_max, s);
     if (rc) return rc;
@@ -453,15 +490,17 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
     p.dense_dns = dense_dns;
     p.parsed = parsed;
     p.n = parsed ? sb.b[0].n : 0u;
-    p.rec_part = (want_parts && sb.count == 1u && c->d_table) ? c->d_rec_part : nullptr;
+    p.rec_part = (want_parts && sb.count == 1u && c->d_table) ? (c->part_target ? c->part_target : c->d_rec_part)
+                                                              : nullptr;
     p.part_shift = c->flow_shift;
     c->part_recs = p.rec_part ? sb.b[0].out : nullptr;
+    c->part_buf = p.rec_part;
     p.cfg = c->d_cfg;
     p.tick = c->d_tick;
     // dense pass 2 belongs to pass 1's launch: same error word, no new parity
     const uint32_t launch = pass == SegPass::kDenseOut ? c->epoch : ++c->epoch;
-    p.error = c->d_error + (launch & 1u);
-    p.error_next = c->d_error + ((launch & 1u) ^ 1u);
+    p.error = c->d_error + (launch & 3u);
+    p.error_next = c->d_error + ((launch + 1u) & 3u);
     p.dbg = nullptr;
     const uint32_t waves = parse_seg_block_threads() / 64u;
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (sb.total_segs + waves - 1) / waves));
@@ -653,7 +692,7 @@ static int ensure_staging(fb_ctx* c, uint64_t n, uint64_t bytes) {
 
 static int check_error_word(fb_ctx* c, hipStream_t s) {
     uint32_t e = 0;
-    HIP_TRY(hipMemcpyAsync(&e, c->d_error + (c->epoch & 1u), 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&e, c->d_error + (c->epoch & 3u), 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (e) return ctx_report_error(c, e);
     return FB_OK;
@@ -734,7 +773,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
                        fb_batch_stats* d_stats, hipStream_t s) {
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     DeviceGuard g(c->device);
-    int rc = ensure_flow_scratch(c, n_slots, s);
+    int rc = join_updates(c, s);
+    if (!rc) rc = ensure_flow_scratch(c, n_slots, s);
     if (rc) return rc;
     // record slots of the batch: at most last_n records (dense) / n_slots slots (segmented)
     const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_slots + kFlowChunk - 1) / kFlowChunk);
@@ -750,7 +790,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.rows = c->d_rows;
     p.cols = c->d_cols;
     p.partials = c->d_partials;
-    p.error = c->d_error + (c->epoch & 1u);
+    p.error = c->d_error + (c->epoch & 3u);
     p.max_recs = (uint32_t)std::min<uint64_t>((uint64_t)chunks * kFlowChunk, c->flow_recs);
     p.parts = c->flow_parts;
     p.part_shift = c->flow_shift;
@@ -765,10 +805,10 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ctl = c->d_comb_ctl;
     p.agg_slot = c->d_agg_slot;
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
-    p.rec_part = (d_seg && c->part_recs == d_recs) ? c->d_rec_part : nullptr;  // written by this batch's parse
+    p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
     c->part_recs = nullptr;
     HIP_TRY(launch_flow_update(p, chunks, s));
-    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 1u), s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), s));
     ++c->flow_batch;
     c->last_recs = d_recs;
     c->last_seg = d_seg;
@@ -804,6 +844,66 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
     return rc;
 }
 
+// Pipelined fb_process_seg_dev: the parse of batch k runs on `stream`, its table update on the
+// context's update stream after it, and `stream` waits only for the update of batch k-2 (which
+// read the partition buffer and the records this call's slot reuses) -- so the parse of one batch
+// overlaps the update of the one before.  Async batch k writes partition buffer k & 1.
+int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                             uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class,
+                             fb_batch_stats* d_stats, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->upd) {
+        if (hipStreamCreateWithFlags(&c->upd, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_parsed, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_upd[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_upd[1], hipEventDisableTiming) != hipSuccess)
+            return set_err(FB_ERR_HIP, "update stream / events");
+    }
+    const uint32_t slot = (uint32_t)(c->async_k & 1u);
+    int rc = ensure_flow_scratch(c, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES, s);
+    if (rc) return rc;
+    if (!c->d_rec_part2 && hipMalloc(&c->d_rec_part2, c->flow_recs * 4ull) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "second partition buffer");
+    // the same slot's previous batch (k-2): its update must be done before this parse rewrites the
+    // slot's partition buffer; before any async batch, the last synchronous update is on `s` already
+    if (c->async_k >= 2) HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[slot], 0));
+    // a batch that reuses the previous batch's records, counts or stats buffer waits for its
+    // update too (no overlap: rotate two buffer sets to get it)
+    if (c->async_k >= 1 && (d_out == c->async_prev[0] || d_seg == c->async_prev[1] || d_stats == c->async_prev[2]))
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[slot ^ 1u], 0));
+    c->part_target = slot ? c->d_rec_part2 : c->d_rec_part;
+    const uint32_t grid_full = c->seg_grid;
+    static const int grid_div = [] { const char* e = getenv("FB_ASYNC_PARSE_GRID_DIV"); return e ? atoi(e) : 1; }();
+    if (grid_div > 1) c->seg_grid = std::max<uint32_t>(1u, grid_full / (uint32_t)grid_div);  // experiment knob
+    rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
+    c->seg_grid = grid_full;
+    c->part_target = nullptr;
+    if (rc == FB_OK && c->stage_event) rc = hipEventRecord(c->stage_event, s) == hipSuccess
+                                                ? FB_OK : set_err(FB_ERR_HIP, "stage event record failed");
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev_parsed, s));
+    HIP_TRY(hipStreamWaitEvent(c->upd, c->ev_parsed, 0));
+    rc = n == 0 ? empty_update(c) : fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, c->upd);
+    c->part_recs = nullptr;
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev_upd[slot], c->upd));
+    c->async_prev[0] = d_out;
+    c->async_prev[1] = d_seg;
+    c->async_prev[2] = d_stats;
+    ++c->async_k;
+    return FB_OK;
+}
+
+int fb_flow_join(fb_ctx* c, void* stream) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    DeviceGuard g(c->device);
+    return join_updates(c, (hipStream_t)stream);
+}
+
 int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
                    uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns, uint8_t* d_class,
                    fb_batch_stats* d_stats, void* stream) {
@@ -822,6 +922,8 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
+    int jr = join_updates(c, s);
+    if (jr) return jr;
     const uint32_t n = c->last_recs ? c->last_slots : 0u;
     if (n && (!d_hist || !d_hist_slot)) return set_err(FB_ERR_INVAL, "d_hist and d_hist_slot are required");
     if (n > c->hist_cap) {
@@ -926,7 +1028,8 @@ int fb_flow_enrich_dev(fb_ctx* c, uint32_t new_only, fb_flow_enrich* d_out, uint
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
     if (!c->d_table || (new_only && c->flow_batch == 0)) return FB_OK;
-    int rc = upload_cfg(c, s);
+    int rc = join_updates(c, s);
+    if (!rc) rc = upload_cfg(c, s);
     if (rc) return rc;
     HIP_TRY(launch_flow_enrich(enrich_tables(c), c->d_cfg, c->d_table, c->table_cap, new_only ? 1u : 0u,
                                c->flow_batch - 1u, d_out, cap, (unsigned long long*)d_n, s));
@@ -950,6 +1053,8 @@ int fb_flow_count(fb_ctx* c, uint64_t* n_flows, void* stream) {
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     unsigned long long h = 0;
+    const int rc = join_updates(c, s);
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->d_n, 0, 8, s));
     HIP_TRY(launch_flow_count(c->d_table, c->table_cap, c->d_n, s));
     HIP_TRY(hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s));
@@ -964,6 +1069,8 @@ int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
     if (!c->d_table) return FB_OK;
+    const int rc = join_updates(c, s);
+    if (rc) return rc;
     HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s));
     return FB_OK;
 }
@@ -997,6 +1104,8 @@ int fb_flow_clear(fb_ctx* c, void* stream) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return FB_OK;
     DeviceGuard g(c->device);
+    const int rc = join_updates(c, (hipStream_t)stream);
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->d_table, 0, c->table_cap * sizeof(FlowSlot), (hipStream_t)stream));
     c->flow_batch = 0;
     c->last_recs = nullptr;

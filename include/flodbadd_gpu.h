@@ -375,6 +375,21 @@ int fb_flow_update_seg_dev(fb_ctx* ctx, const fb_pkt_out* d_out, const uint32_t*
 int fb_process_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                        const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
                        uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+/* Pipelined fb_process_seg_dev for a stream of batches (continuous capture): the parse of this
+ * batch is ordered on `stream`, its table update runs on the context's own update stream after
+ * it, and `stream` waits only for the update of the batch two calls back -- so each parse overlaps
+ * the previous batch's update.  Same results as fb_process_seg_dev over the same batches.  The
+ * parse's outputs (records, segment counts, stats' parse fields) are ordered on `stream` as usual;
+ * the update's (new/updated sessions in d_stats, the table) only after fb_flow_join(ctx, stream).
+ * d_out / d_seg / d_stats are read by the update until the call two batches later has been issued
+ * (rotate two buffer sets: reusing the previous batch's buffers is allowed but waits for its
+ * update, i.e. does not overlap).  Every other entry point that reads or writes the table (update,
+ * export, count, clear, history, enrichment, the fused calls) joins the update stream itself. */
+int fb_process_seg_async_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
+                             const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
+                             uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
+/* Order `stream` after every table update fb_process_seg_async_dev has issued. */
+int fb_flow_join(fb_ctx* ctx, void* stream);
 
 /*
  * History characters of the LAST flow update on this context, grouped per flow: a stable sort of

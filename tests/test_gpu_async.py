@@ -1,0 +1,110 @@
+"""fb_process_seg_async_dev (the pipelined fused call: each batch's table update on the context's
+own stream, overlapping the next batch's parse) gives the same table, the same per-batch stats and
+the same last-update history as fb_process_seg_dev over the same batches -- with two rotating
+buffer sets (overlap), with one buffer set reused every batch (the call waits for the previous
+update), mixed with synchronous calls, and with table reads issued without an explicit join."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from flodbadd_amd.capture import FlodbaddGpuCapture
+from flodbadd_amd.sessions import SessionFilter
+from test_gpu_parity import rows_sorted
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches():
+    b = [synth.generate(4, 60000, first=k * 60000, zipf=1, zipf_s=1.1) for k in range(4)]
+    b.append(synth.generate(4, 90000, first=400000))  # uniform flows, a larger batch
+    return b
+
+
+def _keyed_history(cap, n_slots, flows):
+    """{40-B key: the last update's characters} (slots are placement, so keyed by the flow key)."""
+    by_slot = {int(r["slot"]): r.tobytes()[:40] for r in flows}
+    return {by_slot[s]: h for s, h in cap.flow_history(n_slots).items()}
+
+
+def _run(batches, modes, n_sets):
+    """Process `batches` with modes[i] in {"sync", "async"}; buffer set i % n_sets per batch."""
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 18)
+    stream = N.Stream()
+    keep = []
+    try:
+        nmax = max(len(o) - 1 for _, o in batches)
+        nseg = (nmax + 63) // 64
+        sets = [(N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize))
+                for _ in range(n_sets)]
+        stats = []
+        for i, ((frames, offs), mode) in enumerate(zip(batches, modes)):
+            d_fr = N.DeviceBuffer(frames.nbytes).upload(frames)
+            d_off = N.DeviceBuffer(offs.nbytes).upload(offs)
+            keep += [d_fr, d_off]
+            d_out, d_seg, d_st = sets[i % n_sets]
+            fn = lib.fb_process_seg_async_dev if mode == "async" else lib.fb_process_seg_dev
+            N.check(fn(cap.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, len(offs) - 1, d_out.ptr, d_seg.ptr, None,
+                       d_st.ptr, stream.ptr))
+            if n_sets >= len(batches) or i == len(batches) - 1:
+                stats.append(d_st)
+        N.check(lib.fb_flow_join(cap.ctx, stream.ptr))
+        stream.sync()
+        st = [s.download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr).tobytes() for s in stats]
+        flows = cap.export_flows()  # joins the update stream itself (a no-op after the join above)
+        n_last = (len(batches[-1][1]) - 1 + 63) // 64 * 64
+        hist = _keyed_history(cap, n_last, flows)
+        cnt = C.c_uint64()
+        N.check(lib.fb_flow_count(cap.ctx, C.byref(cnt), None))
+        return rows_sorted(flows), st, hist, int(cnt.value)
+    finally:
+        for b in keep:
+            b.free()
+        cap.close()
+
+
+@pytest.fixture(scope="module")
+def reference():
+    b = _batches()
+    return b, _run(b, ["sync"] * len(b), len(b))
+
+
+@pytest.mark.parametrize("modes,n_sets", [
+    (["async"] * 5, 5),                                 # every batch its own buffers: per-batch stats compared
+    (["async"] * 5, 2),                                 # two rotating sets: parse k+1 overlaps update k
+    (["async"] * 5, 1),                                 # one set: each call waits for the previous update
+    (["async", "async", "sync", "async", "async"], 2),  # a synchronous call in between joins first
+], ids=["own-buffers", "two-sets", "one-set", "mixed"])
+def test_async_equals_sync(reference, modes, n_sets):
+    batches, (ref_rows, ref_stats, ref_hist, ref_cnt) = reference
+    rows, st, hist, cnt = _run(batches, modes, n_sets)
+    assert cnt == ref_cnt and rows == ref_rows
+    assert st == (ref_stats if n_sets >= len(batches) else ref_stats[-1:])
+    assert hist == ref_hist
+
+
+def test_async_table_reads_join(reference):
+    """Export / count right after async calls, with no explicit fb_flow_join: the entry points
+    join the update stream themselves."""
+    batches, (ref_rows, _, _, ref_cnt) = reference
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 18)
+    keep = []
+    try:
+        nseg = (max(len(o) - 1 for _, o in batches) + 63) // 64
+        for i, (frames, offs) in enumerate(batches):
+            bufs = [N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+                    N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize)]
+            keep += bufs
+            d_fr, d_off, d_out, d_seg, d_st = bufs
+            N.check(lib.fb_process_seg_async_dev(cap.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, len(offs) - 1, d_out.ptr,
+                                                 d_seg.ptr, None, d_st.ptr, None))
+        assert cap.flow_count() == ref_cnt
+        assert rows_sorted(cap.export_flows()) == ref_rows
+    finally:
+        for b in keep:
+            b.free()
+        cap.close()
