@@ -43,6 +43,9 @@ struct fb_ctx {
     bool need_reset = true;       // zero the tick + error words before the next launch
     uint32_t epoch = 0;           // parse launches so far: its parity picks the launch's error word
     uint32_t seg_grid = 0;        // streaming segmented kernel: co-resident blocks
+    uint32_t seg_grid_async = 0;  // ... in the pipelined call: one block per CU, so the previous
+                                  // batch's table update keeps the rest of each CU (C4: 9,700 ->
+                                  // 10,200-10,300 Mpackets/s against 9,840-9,990 at the full grid)
     uint32_t* d_error = nullptr;  // [4] error words, indexed by launch & 3 (a launch clears the next one's;
                                   // a pipelined update still writes the one two launches back)
     // dense output (fb_parse_classify_dev & co., fb_seg_compact_dev): segment counts + their scan
@@ -341,6 +344,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         int sb = 0;
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
+        c->seg_grid_async = std::min<uint32_t>((uint32_t)prop.multiProcessorCount, c->seg_grid);
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -877,8 +881,7 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
         HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[slot ^ 1u], 0));
     c->part_target = slot ? c->d_rec_part2 : c->d_rec_part;
     const uint32_t grid_full = c->seg_grid;
-    static const int grid_div = [] { const char* e = getenv("FB_ASYNC_PARSE_GRID_DIV"); return e ? atoi(e) : 1; }();
-    if (grid_div > 1) c->seg_grid = std::max<uint32_t>(1u, grid_full / (uint32_t)grid_div);  // experiment knob
+    c->seg_grid = c->seg_grid_async;
     rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
     c->seg_grid = grid_full;
     c->part_target = nullptr;
