@@ -371,7 +371,7 @@ int fb_flow_update_seg_dev(fb_ctx* ctx, const fb_pkt_out* d_out, const uint32_t*
 /* fb_parse_classify_seg_dev followed by fb_flow_update_seg_dev on the same stream, with the same
  * results.  Prefer it when the records are only needed for the table: its parse also writes each
  * session record's table partition to context scratch, and its update's bucketing pass reads
- * those instead of re-reading and hashing the records (C4: 1.50 -> 1.44 ms per 10M frames). */
+ * those instead of re-reading and hashing the records (DESIGN.md §4 has the C4 timings). */
 int fb_process_seg_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                        const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out, uint32_t* d_seg,
                        uint8_t* d_class, fb_batch_stats* d_stats, void* stream);
