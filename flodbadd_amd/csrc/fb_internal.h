@@ -122,7 +122,10 @@ struct SegBatches {
 //   6 counters in fb_flow_rec order, then the ordered state: first / last / end positions
 //   ((update call << 32) | pkt_index, FB_SEEN_NONE), hist_len, hist_mask | conn_state << 16 |
 //   end_mask << 24.
-constexpr uint32_t kFlowSlots = 512;             // slots per partition: 64 KiB LDS slice
+#ifndef FB_FLOW_SLOTS
+#define FB_FLOW_SLOTS 512
+#endif
+constexpr uint32_t kFlowSlots = FB_FLOW_SLOTS;   // slots per partition: 64 KiB LDS slice
 constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
 #ifndef FB_FLOW_CHUNK
 #define FB_FLOW_CHUNK 16384
