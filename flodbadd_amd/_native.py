@@ -198,6 +198,7 @@ GPU_SYMBOLS = [
     ("fb_event_record", _I, [_P, _P]),
     ("fb_event_elapsed_ms", _I, [C.POINTER(C.c_float), _P, _P]),
     ("fb_event_query", _I, [_P]),
+    ("fb_event_spin", _I, [_P]),
     ("fb_device_count", _I, [C.POINTER(C.c_int)]),
     ("fb_set_device", _I, [_I]),
 ]
@@ -323,14 +324,8 @@ class Event:
         check(gpu_lib().fb_event_record(self.ptr, stream.ptr if isinstance(stream, Stream) else stream))
 
     def wait_spin(self):
-        """Poll until the event completed (no blocking wait, no wake-up latency)."""
-        q = gpu_lib().fb_event_query
-        while True:
-            rc = q(self.ptr)
-            if rc == 0:
-                return
-            if rc < 0:
-                check(rc)
+        """Poll until the event completed (no blocking wait, no wake-up latency), in C."""
+        check(gpu_lib().fb_event_spin(self.ptr))
 
     def elapsed_ms(self, end):
         ms = C.c_float()

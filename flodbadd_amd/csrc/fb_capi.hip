@@ -1169,6 +1169,14 @@ int fb_event_query(void* ev) {
     HIP_TRY(e);
     return FB_OK;
 }
+// Busy-wait (no blocking sync, no wake-up latency) until the event completed.
+int fb_event_spin(void* ev) {
+    for (;;) {
+        const hipError_t e = hipEventQuery((hipEvent_t)ev);
+        if (e == hipSuccess) return FB_OK;
+        if (e != hipErrorNotReady) HIP_TRY(e);
+    }
+}
 int fb_set_device(int d) { HIP_TRY(hipSetDevice(d)); return FB_OK; }
 
 }  // extern "C"

@@ -574,6 +574,8 @@ int fb_event_record(void* ev, void* stream);
 int fb_event_elapsed_ms(float* ms, void* ev_start, void* ev_stop); /* syncs ev_stop */
 int fb_event_query(void* ev); /* FB_OK once the event completed, 1 while pending: a capture loop
                                  polls it instead of blocking (no wake-up latency)          */
+/* Busy-wait until the event completed: the polled completion without a call per poll. */
+int fb_event_spin(void* ev);
 int fb_device_count(int* n);
 int fb_set_device(int device);
 
