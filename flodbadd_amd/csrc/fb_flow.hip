@@ -703,15 +703,15 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         mine += v0[c] >> 16;
     }
     for (uint32_t b = kK2Cpt * kFlowK2Threads + threadIdx.x; b < chunks; b += kFlowK2Threads) mine += col[b] >> 16;
-    const unsigned long long total = block_sum(mine, sh);
-    unsigned long long n_new = 0ull, n_upd = 0ull;
-    if (total != 0ull) {
-        constexpr uint32_t kHead16 = kSlotWords * 8u / 16u;  // 6 uint4 per slot head
-        FlowSlot* T = P.table + (size_t)part * kFlowSlots;
-        const uint4* g = reinterpret_cast<const uint4*>(T);
-        // slot tid's ordered fields, for finish_slot (in flight with the slice load)
-        static_assert(kFlowSlots == kFlowK2Threads, "one slot per thread in the fold");
-        const uint4 ord0 = g[(size_t)threadIdx.x * 8u + 6u], ord1 = g[(size_t)threadIdx.x * 8u + 7u];
+    constexpr uint32_t kHead16 = kSlotWords * 8u / 16u;  // 6 uint4 per slot head
+    FlowSlot* T = P.table + (size_t)part * kFlowSlots;
+    const uint4* g = reinterpret_cast<const uint4*>(T);
+    // the slice heads into LDS and slot tid's ordered fields (for finish_slot) into registers
+    static_assert(kFlowSlots == kFlowK2Threads, "one slot per thread in the fold");
+    uint4 ord0, ord1;
+    auto load_slice = [&]() {
+        ord0 = g[(size_t)threadIdx.x * 8u + 6u];
+        ord1 = g[(size_t)threadIdx.x * 8u + 7u];
 #ifndef FB_K2_NO_SLICEIO  // ablation (timing only): no slice load / write-back
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
@@ -719,8 +719,20 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         }
 #else
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) slice4[j] = make_uint4(0, 0, 0, 0);
-        (void)g;
 #endif
+    };
+    // a batch with >= 32 record slots per partition touches nearly every partition: the slice
+    // load is issued with the group rows, before the partition's total is known (one round trip
+    // less per workgroup); sparser batches load it only for a partition with entries
+#ifndef FB_K2_PREFETCH
+#define FB_K2_PREFETCH 1
+#endif
+    const bool dense = FB_K2_PREFETCH && n >= 32u * P.parts;
+    if (dense) load_slice();
+    const unsigned long long total = block_sum(mine, sh);
+    unsigned long long n_new = 0ull, n_upd = 0ull;
+    if (total != 0ull) {
+        if (!dense) load_slice();
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
             const uint32_t w = j % kScrU32;
             scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
