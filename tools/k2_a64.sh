@@ -1,6 +1,7 @@
 #!/bin/bash
 # Experiment (GPU box): K2 with 64-B-aligned record slots (variant a64: records expanded first)
-# against the product library, kernel trace of the one-stream C4 bench.
+# against the product library, kernel trace of the one-stream C4 bench.  (The FB_K2_ALIGNED64
+# experiment code in fb_flow.hip was reverted after the measurement)
 cd "${GRAFT_REPO_ROOT}"; R=$(pwd); mkdir -p gpurun_out/a64; export TMPDIR=/tmp
 for v in base a64; do
   rm -rf gpurun_out/a64/$v; cd /tmp
