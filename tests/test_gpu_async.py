@@ -108,3 +108,44 @@ def test_async_table_reads_join(reference):
         for b in keep:
             b.free()
         cap.close()
+
+
+def test_async_empty_batch_and_table_full():
+    """An empty batch through the pipelined call counts as an update call (as in the synchronous
+    one); a batch that overflows a partition reports TABLE_FULL in its stats after the join, and
+    the context recovers for the next call."""
+    import framegen as fg
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512)
+    mk = lambda k: fg.tcp_frame("10.1.%d.%d" % (k >> 8, k & 255), 40000, "8.8.8.8", 443, fg.ACK, 10)
+    stream = N.Stream()
+    keep = []
+
+    def issue(frames, offs):
+        n = len(offs) - 1
+        nseg = max((n + 63) // 64, 1)
+        b = [N.DeviceBuffer(max(frames.nbytes, 1)), N.DeviceBuffer(offs.nbytes).upload(offs),
+             N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize)]
+        if frames.nbytes:
+            b[0].upload(frames)
+        keep.extend(b)
+        N.check(lib.fb_process_seg_async_dev(cap.ctx, b[0].ptr, frames.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr, None,
+                                             b[4].ptr, stream.ptr))
+        return b[4]
+
+    try:
+        issue(*fg.pack([mk(k) for k in range(300)]))
+        issue(*fg.pack([]))
+        st_full = issue(*fg.pack([mk(k) for k in range(600)]))
+        N.check(lib.fb_flow_join(cap.ctx, stream.ptr))
+        stream.sync()
+        st = st_full.download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)
+        assert int(st[0]["error"]) & 4  # partition full
+        # the host-side error path resets the launch scratch; the table still answers
+        cap.clear_all_sessions()
+        g = cap.process_frames(*fg.pack([mk(k) for k in range(200)]))
+        assert len(g.records) == 200 and cap.flow_count() == 200
+    finally:
+        for b in keep:
+            b.free()
+        cap.close()
