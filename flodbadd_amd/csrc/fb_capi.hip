@@ -91,6 +91,7 @@ struct fb_ctx {
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
     // the last update, for fb_flow_history_dev
     const fb_pkt_out* last_recs = nullptr;
+    const uint32_t* last_part = nullptr;  // the fused parse's per-record words of the last update
     const uint32_t* last_seg = nullptr;
     const fb_batch_stats* last_stats = nullptr;
     uint32_t last_slots = 0;
@@ -204,6 +205,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     c->d_rows = c->d_cols = nullptr;
     c->d_rec_flow = c->d_hot = c->d_comb_ctl = c->d_agg_slot = nullptr;
     c->last_recs = nullptr;  // its rec_flow is gone
+    c->last_part = nullptr;
     c->flow_recs = 0;
     const uint64_t chunks = recs / kFlowChunk;
     // combined entries: at most one per two records of the hot groups; a quarter of the batch's
@@ -770,6 +772,7 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
 static int empty_update(fb_ctx* c) {
     ++c->flow_batch;
     c->last_recs = nullptr;
+    c->last_part = nullptr;
     return FB_OK;
 }
 
@@ -815,6 +818,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), s));
     ++c->flow_batch;
     c->last_recs = d_recs;
+    c->last_part = p.rec_part;
     c->last_seg = d_seg;
     c->last_stats = d_stats;
     c->last_slots = p.max_recs < n_slots ? p.max_recs : n_slots;
@@ -959,6 +963,7 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     p.keys = c->d_hkeys;
     p.vals = c->d_hvals;
     p.n_hist = d_n_hist;
+    p.rec_part = c->last_part;
     HIP_TRY(launch_flow_history(p, c->d_htemp, c->htemp_bytes, d_hist_slot, d_hist, s));
     return FB_OK;
 }
@@ -1112,6 +1117,7 @@ int fb_flow_clear(fb_ctx* c, void* stream) {
     HIP_TRY(hipMemsetAsync(c->d_table, 0, c->table_cap * sizeof(FlowSlot), (hipStream_t)stream));
     c->flow_batch = 0;
     c->last_recs = nullptr;
+    c->last_part = nullptr;
     return FB_OK;
 }
 

@@ -141,14 +141,14 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
             for (uint32_t j = 0; j < kPer; ++j) {
                 const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
                 sw[j] = P.seg[(base + k) >> 6];
-                pv[j] = P.rec_part[base + k];
+                pv[j] = P.rec_part[base + k] & kRecPartMask;
             }
         } else {
 #pragma unroll
             for (uint32_t j = 0; j < kPer; ++j) {
                 const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
                 sw[j] = 0xFFFFu;
-                pv[j] = P.rec_part[base + k];
+                pv[j] = P.rec_part[base + k] & kRecPartMask;
             }
         }
 #pragma unroll

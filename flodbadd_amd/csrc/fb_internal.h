@@ -225,6 +225,11 @@ struct FlowParams {
                                 // segmented parse of the same batch (fb_process_seg_dev); K1's
                                 // histogram pass then reads 4 B per record instead of the record
 };
+// The fused parse's per-record word: the table partition (< kFlowMaxParts) in the low 16 bits,
+// the record's history character in bits 16-23 and FB_META_HAS_FLAGS in bit 24 -- so the history
+// keys kernel reads 4 B per record slot instead of the record.
+constexpr uint32_t kRecPartMask = 0xFFFFu;
+static_assert(kFlowMaxParts <= kRecPartMask + 1u, "partition ids fit the low half");
 
 // Launchers (fb_parse.hip / fb_compact.hip / fb_flow.hip).
 // Which k_parse_seg instance: the segmented output; dense pass 1 (segment counts, classes, stats);
@@ -271,6 +276,7 @@ struct HistParams {
     uint32_t* keys;             // [n_slots] scratch
     uint8_t* vals;              // [n_slots] scratch
     uint32_t* n_hist;           // device u32: keyed records
+    const uint32_t* rec_part;   // non-null: the fused parse's per-record words of this update
 };
 hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes);
 hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_bytes, uint32_t* hist_slot,

@@ -620,7 +620,10 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                         P.rec_part + (size_t)ls * 64u, (short)0, 256, 0x00020000);
                     const uint32_t key[10] = {kk.w[0], kk.w[1], kk.w[2], kk.w[3], kk.w[4],
                                               kk.w[5], kk.w[6], kk.w[7], kk.w[8], kk.w[9] & 0xFFFFu};
-                    __builtin_amdgcn_raw_buffer_store_b32(part_of(flow_hash_words(key), P.part_shift), r_part,
+                    // partition | history char << 16 | has_flags << 24 (kRecPart*, fb_internal.h)
+                    const uint32_t pw = part_of(flow_hash_words(key), P.part_shift) | (kk.w[12] & 0x00FF0000u) |
+                                        ((kk.w[12] & 0x100u) << 16);
+                    __builtin_amdgcn_raw_buffer_store_b32(pw, r_part,
                                                           is_s ? (uint32_t)__popcll(m_sess & lmask) * 4u : kOob, 0, 0);
                 }
             }
