@@ -260,7 +260,10 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
 // `history.contains(c)` only ask which characters are present).
 constexpr uint32_t kSlotWords = 12;  // u64 words of a slot kept in LDS: tag, key[5], counters[6]
 constexpr uint32_t kScrU32 = 10;     // per-slot batch scratch, u32 words
-constexpr uint32_t kK2Lds = kFlowSlots * (kSlotWords * 8 + kScrU32 * 4);
+#ifndef FB_K2_TAGS
+#define FB_K2_TAGS 1
+#endif
+constexpr uint32_t kK2Lds = kFlowSlots * (kSlotWords * 8 + kScrU32 * 4 + (FB_K2_TAGS ? 4 : 0));
 constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 #ifndef FB_K2_CPT
 #define FB_K2_CPT 2
@@ -413,14 +416,120 @@ __device__ __forceinline__ uint32_t lds_lookup(unsigned long long* tab, const ui
     return ~0u;
 }
 
+// K2's probe over a tag array: tags[i] = the low word of slot i's tag (0 empty, 1 being inserted,
+// h32 | 2), kept beside the slot heads.  A lookup reads the 8 tags of the probe's 32-B group with
+// two LDS reads, compares them in registers, and reads a slot's key words only on a tag match; it
+// stops at the group's first empty slot.  At the steady-state load (C4: 1.45M flows in 2^21
+// slots, 0.69) a linear probe's length has a long tail and a wave runs its loop as often as its
+// longest lane needs: 8 slots per step cut that from ~a dozen steps of six 8-B slot reads to
+// one or two group reads.
+__device__ __forceinline__ uint32_t k2_lookup(const uint32_t* tags, const unsigned long long* tab,
+                                              const uint32_t key[10], uint32_t h32) {
+    const uint32_t want = h32 | 2u;
+    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
+    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
+    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
+    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
+    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
+    const uint32_t start = h32 & (kFlowSlots - 1u);
+    uint32_t grp = start >> 3, live = 0xFFu & (0xFFu << (start & 7u));  // group positions at or past the home slot
+    for (uint32_t n = 0; n < kFlowSlots / 8u; ++n) {
+        // (re)read every step: other lanes publish tags; a wave's LDS reads are served in order and
+        // a publisher writes the key words before its release store of the tag
+        asm volatile("" ::: "memory");
+        const uint4* tg = reinterpret_cast<const uint4*>(tags + grp * 8u);
+        const uint4 a = tg[0], b = tg[1];
+        asm volatile("" ::: "memory");
+        const uint32_t t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t match = 0u, empty = 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            match |= (t[j] == want ? 1u : 0u) << j;
+            empty |= (t[j] == 0u ? 1u : 0u) << j;
+        }
+        empty &= live;
+        match &= live & (empty ? (empty & (0u - empty)) - 1u : 0xFFu);  // before the first empty
+        while (match) {
+            const uint32_t i = grp * 8u + (uint32_t)__builtin_ctz(match);
+            const unsigned long long* s = tab + (size_t)i * kSlotWords;
+            if ((s[1] == kw0) & (s[2] == kw1) & (s[3] == kw2) & (s[4] == kw3) & (s[5] == kw4)) return i;
+            match &= match - 1u;
+        }
+        if (empty) break;
+        grp = (grp + 1u) & (kFlowSlots / 8u - 1u);
+        live = 0xFFu;
+    }
+    return ~0u;  // absent, being inserted, or past a full table: the caller takes k2_upsert
+}
+
+// Find or insert through the tag array (claim: CAS of the slot's tag 0 -> 1, then the key words
+// and the 64-bit slot tag, then the release store of h32 | 2).  Same results as lds_upsert.
+__device__ __forceinline__ int k2_upsert(uint32_t* tags, unsigned long long* tab, const uint32_t key[10],
+                                         uint32_t h32, uint32_t& slot) {
+    const uint32_t want = h32 | 2u;
+    const unsigned long long kw0 = (unsigned long long)key[0] | ((unsigned long long)key[1] << 32);
+    const unsigned long long kw1 = (unsigned long long)key[2] | ((unsigned long long)key[3] << 32);
+    const unsigned long long kw2 = (unsigned long long)key[4] | ((unsigned long long)key[5] << 32);
+    const unsigned long long kw3 = (unsigned long long)key[6] | ((unsigned long long)key[7] << 32);
+    const unsigned long long kw4 = (unsigned long long)key[8] | ((unsigned long long)key[9] << 32);
+    uint32_t i = h32 & (kFlowSlots - 1u);
+    int result = -1;
+    for (uint32_t probe = 0; probe < kFlowSlots; ++probe) {
+        unsigned long long* s = tab + (size_t)i * kSlotWords;
+        uint32_t t = __hip_atomic_load(tags + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t == 0u) {
+            const uint32_t old = atomicCAS(tags + i, 0u, 1u);
+            if (old == 0u) {
+                s[1] = kw0;
+                s[2] = kw1;
+                s[3] = kw2;
+                s[4] = kw3;
+                s[5] = kw4;
+                s[0] = flow_hash_words(key) | 2ull;
+                __hip_atomic_store(tags + i, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                result = 1;
+                break;
+            }
+            t = old;
+        }
+        uint32_t spins = 0u;
+        while (t == 1u) {  // another lane of this workgroup is publishing the slot's key
+            __builtin_amdgcn_s_sleep(1);
+            t = __hip_atomic_load(tags + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (++spins > (1u << 22)) return -2;
+        }
+        if (t == want && s[1] == kw0 && s[2] == kw1 && s[3] == kw2 && s[4] == kw3 && s[5] == kw4) {
+            result = 0;
+            break;
+        }
+        i = (i + 1u) & (kFlowSlots - 1u);
+    }
+    slot = i;
+    return result;
+}
+
+// K2's find-or-insert: lookup first (steady-state batches mostly update existing flows), then the
+// claiming upsert.
+__device__ __forceinline__ int k2_find_insert(unsigned long long* slice, uint32_t* tags, const uint32_t key[10],
+                                              uint32_t h32, uint32_t& i) {
+#if FB_K2_TAGS
+    i = k2_lookup(tags, slice, key, h32);
+    return i != ~0u ? 0 : k2_upsert(tags, slice, key, h32, i);
+#else
+    (void)tags;
+    i = lds_lookup<kSlotWords, kFlowSlots>(slice, key, h32);
+    return i != ~0u ? 0 : lds_upsert<kSlotWords, kFlowSlots>(slice, key, h32, i);
+#endif
+}
+
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
-__device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
+__device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* tags, uint32_t* scr, const uint4 e0, const uint4 e1,
                                            const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* ent_slot,
                                            uint32_t idx, uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    uint32_t i = lds_lookup<kSlotWords, kFlowSlots>(slice, key, e3.w);
-    const int result = i != ~0u ? 0 : lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
+    uint32_t i;
+    const int result = k2_find_insert(slice, tags, key, e3.w, i);
     if (result < 0) {
         atomicOr(err, result == -2 ? 2u : 4u);  // spin expired / partition full
         return -1;
@@ -453,13 +562,13 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
 
 // A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
 // the group's partial sums / minima / maxima.  Its records' rec_flow point at agg_slot[id].
-__device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* scr, const uint4 e0, const uint4 e1,
+__device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr, const uint4 e0, const uint4 e1,
                                               const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
                                               const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
                                               uint32_t* err) {
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
-    uint32_t i = lds_lookup<kSlotWords, kFlowSlots>(slice, key, e3.w);
-    const int result = i != ~0u ? 0 : lds_upsert<kSlotWords, kFlowSlots>(slice, key, e3.w, i);
+    uint32_t i;
+    const int result = k2_find_insert(slice, tags, key, e3.w, i);
     if (result < 0) {
         atomicOr(err, result == -2 ? 2u : 4u);
         return -1;
@@ -689,6 +798,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     __shared__ unsigned long long sh[kFlowK2Threads / 64];
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
     uint32_t* scr = reinterpret_cast<uint32_t*>(slice + (size_t)kFlowSlots * kSlotWords);
+    uint32_t* tags = scr + (size_t)kFlowSlots * kScrU32;  // FB_K2_TAGS: the slots' probe tags
     const uint32_t part = blockIdx.x;
     const uint32_t n = batch_records(P);
     const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
@@ -709,10 +819,12 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     // the slice heads into LDS and slot tid's ordered fields (for finish_slot) into registers
     static_assert(kFlowSlots == kFlowK2Threads, "one slot per thread in the fold");
     uint4 ord0, ord1;
+    uint32_t tag0 = 0u;  // slot tid's tag, low word
     auto load_slice = [&]() {
         ord0 = g[(size_t)threadIdx.x * 8u + 6u];
         ord1 = g[(size_t)threadIdx.x * 8u + 7u];
-#ifndef FB_K2_NO_SLICEIO  // ablation (timing only): no slice load / write-back
+#ifndef FB_K2_NO_SLICEIO
+        if (FB_K2_TAGS) tag0 = reinterpret_cast<const uint32_t*>(g + (size_t)threadIdx.x * 8u)[0];  // ablation (timing only): no slice load / write-back
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
             slice4[j] = g[(size_t)sl * (sizeof(FlowSlot) / 16u) + w];
@@ -737,6 +849,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             const uint32_t w = j % kScrU32;
             scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
         }
+        if (FB_K2_TAGS) tags[threadIdx.x] = tag0;
         __syncthreads();
         const uint32_t* E = P.entries;
         const uint4* CE = reinterpret_cast<const uint4*>(P.comb);
@@ -815,7 +928,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 if (v0 & kIdxCombined) {
                     const uint4* t = CE + (size_t)(v0 & ~kIdxCombined) * 8u + 4u;
                     const uint4 t3 = t[3];
-                    const int r = apply_combined(slice, scr, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
+                    const int r = apply_combined(slice, tags, scr, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
                                                  part * kFlowSlots, P.agg_slot, P.error);
                     if (r >= 0) {
                         n_new += r == 1;
@@ -830,7 +943,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
                     const uint32_t hinfo =
                         ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
-                    const int r = apply_entry(slice, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
+                    const int r = apply_entry(slice, tags, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
                                               make_uint4(my, v0, hinfo, (uint32_t)flow_hash_words(key)),
                                               part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix0, P.error);
                     n_new += r == 1;

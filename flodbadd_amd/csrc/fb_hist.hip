@@ -59,6 +59,25 @@ __global__ __launch_bounds__(256) void k_hist_keys(const HistParams P) {
     }
 }
 
+#ifndef FB_HIST_RADIX_BITS
+#define FB_HIST_RADIX_BITS 0  // 0: rocPRIM's gfx950 default (8 bits per onesweep pass)
+#endif
+#ifndef FB_HIST_SORT_BLOCK
+#define FB_HIST_SORT_BLOCK 1024
+#endif
+#ifndef FB_HIST_SORT_IPT
+#define FB_HIST_SORT_IPT 8
+#endif
+#if FB_HIST_RADIX_BITS
+using HistSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
+                                        rocprim::kernel_config<FB_HIST_SORT_BLOCK, FB_HIST_SORT_IPT>,
+                                        FB_HIST_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+#else
+using HistSortConfig = rocprim::default_config;
+#endif
+
 static uint32_t key_bits(uint32_t sentinel) {
     uint32_t b = 1u;
     while (b < 32u && (1ull << b) <= sentinel) ++b;
@@ -66,7 +85,7 @@ static uint32_t key_bits(uint32_t sentinel) {
 }
 
 hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes) {
-    return rocprim::radix_sort_pairs(nullptr, *bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+    return rocprim::radix_sort_pairs<HistSortConfig>(nullptr, *bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const uint8_t*)nullptr, (uint8_t*)nullptr, (size_t)n_slots, 0u,
                                      key_bits(sentinel));
 }
@@ -80,7 +99,7 @@ hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_byte
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = temp_bytes;
-    return rocprim::radix_sort_pairs(temp, tb, (const uint32_t*)p.keys, hist_slot, (const uint8_t*)p.vals, hist,
+    return rocprim::radix_sort_pairs<HistSortConfig>(temp, tb, (const uint32_t*)p.keys, hist_slot, (const uint8_t*)p.vals, hist,
                                      (size_t)p.n_slots, 0u, key_bits(p.sentinel), s);
 }
 
