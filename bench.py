@@ -551,9 +551,10 @@ def main():
     rotate = args.rotate or (32 if args.config == 2 else (12 if args.config == 3 else (2 if pipe else 1)))
     bpl = min(args.batches_per_launch or rotate, rotate, MAX_SEG_BATCHES) \
         if (args.mode == "seg" and args.config != 4) else 1
+    main_kw = dict(zipf=1, zipf_s=args.zipf) if args.zipf else None
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
                         flow=args.config == 4, mode=args.mode, bpl=bpl,
-                        synth_kw=dict(zipf=1, zipf_s=args.zipf) if args.zipf else None, pipelined=pipe)
+                        synth_kw=main_kw, pipelined=pipe)
     # the dominant kernel's launches: algorithmic bytes per launch / average launch duration
     per_launch_s = main_r["ev_ms"] / 1e3 / main_r["launches"]
     algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
@@ -567,7 +568,7 @@ def main():
         if pipe:  # the stage split and the one-stream rate from fb_process_seg_dev, fewer steps
             st_s = max(args.steps // 2, 10)
             rs = run_config(N, lib, ctx, 4, n, st_s, max(args.warmup // 2, 2), 1, rank, world, dist, flow=True,
-                            mode=args.mode, stage_extras=False)
+                            mode=args.mode, synth_kw=main_kw, stage_extras=False)
             split = rs["stage"]
             extra["c4_sync"] = dict(value=round(world * n * st_s / rs["elapsed"] / 1e6, 2), unit="Mpackets/s",
                                     ms_per_step=round(rs["elapsed"] * 1e3 / st_s, 4),

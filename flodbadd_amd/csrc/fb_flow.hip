@@ -667,10 +667,20 @@ constexpr uint32_t kCombGrid = FB_COMB_GRID;
 static_assert(kCombSlots % kCombThreads == 0, "each thread numbers kCombSlots / kCombThreads keys");
 constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
                    kCfRecs = 10, kCfId = 11, kCfHash = 12, kCombF = 13;  // u32 fields of a key (kCfChar..+3)
+// The reduce pass keeps each record's key slot (u8; 0xFF: none or slot 255) for the group's first
+// kCombJc records, so the pack pass finds them without gathering the 56-B records again: K1c is
+// bound by those random record reads (under Zipf(1.1) ~4.6M records per C4 batch sit in hot
+// groups), not by its same-key LDS atomics (folding a hot key's lanes with wave reductions first
+// measured slower: 318 -> 348-358 us).  C4 Zipf(1.1): K1c 371 -> 317 us.
+#ifndef FB_COMB_JC
+#define FB_COMB_JC 4096
+#endif
+constexpr uint32_t kCombJc = FB_COMB_JC;
 struct CombLds {
     unsigned long long tab[kCombSlots * 6];    // tag + key words (lds_upsert layout)
     unsigned long long bytes[kCombSlots * 4];  // outbound, inbound, orig ip, resp ip
     uint32_t f[kCombSlots * kCombF];
+    uint8_t jc[kCombJc > 0 ? kCombJc : 1];     // the reduce pass's key slot per record
     uint32_t wsum[kCombThreads / 64];
     uint32_t base;
 };
@@ -701,7 +711,9 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                       e[2].y & 0xFFFFu};
             uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
-            if (j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0) continue;
+            const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
+            if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
+            if (no_slot) continue;
             const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
             uint32_t* f = L.f + j * kCombF;
             atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
@@ -746,11 +758,14 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint32_t keep = 0u, rec = 0u;
             if (k < cnt) {
                 rec = E[s0 + k];
-                uint4 e[4];
-                rec_entry(P.recs, rec, e);
-                const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
-                                          e[2].y & 0xFFFFu};
-                const uint32_t j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
+                uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
+                if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
+                    uint4 e[4];
+                    rec_entry(P.recs, rec, e);
+                    const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                              e[2].y & 0xFFFFu};
+                    j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
+                }
                 if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) {
                     if (P.rec_flow) P.rec_flow[rec] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
                 } else {
