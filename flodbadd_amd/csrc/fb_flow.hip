@@ -698,11 +698,17 @@ struct CombLds {
     uint8_t jc[kCombJc > 0 ? kCombJc : 1];     // the reduce pass's key slot per record
     uint32_t wsum[kCombThreads / 64];
     uint32_t base;
+    uint32_t pool_next, pool_end;  // this workgroup's reserved combined-entry ids
 };
 
 __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
     const uint32_t n_hot = min(P.ctl[0], P.hot_cap);
+    // combined-entry ids: a workgroup reserves them `pool` at a time (one returned atomic per group on
+    // one address serialised ~19K of them per Zipf C4 batch); the reservations leave most of comb_cap
+    // (a quarter of the batch's records) to spare
+    const uint32_t pool = max(1u, min(32u, P.comb_cap / (4u * gridDim.x)));
+    if (threadIdx.x == 0) L.pool_next = L.pool_end = 0u;  // published by the group loop's first barrier
     uint32_t* E = P.entries;
     uint4* CE = reinterpret_cast<uint4*>(P.comb);
     for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
@@ -755,7 +761,17 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         uint32_t n_comb;
         uint32_t rank = block_excl_scan(nc, L.wsum, n_comb);
         if (n_comb == 0u) continue;  // uniform across the block; the table is re-initialised above
-        if (threadIdx.x == 0) L.base = atomicAdd(P.ctl + 1, n_comb);
+        if (threadIdx.x == 0) {
+            uint32_t nx = L.pool_next, en = L.pool_end;
+            if (en - nx < n_comb) {
+                const uint32_t g = max(n_comb, pool);
+                nx = atomicAdd(P.ctl + 1, g);
+                en = nx + g;
+            }
+            L.base = nx;
+            L.pool_next = nx + n_comb;
+            L.pool_end = en;
+        }
         __syncthreads();
         const uint32_t id0 = L.base;
         if (id0 + n_comb > P.comb_cap) continue;  // no room for its combined entries: the group stays plain
