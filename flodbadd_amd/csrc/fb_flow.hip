@@ -677,7 +677,10 @@ static_assert(offsetof(FlowSlot, first_seen) == 96 && offsetof(FlowSlot, hist_st
 // Zipf update 1.39 ms, against 1.74 ms at 512 keys x 512 / >= 24 (fixed cost per group: table
 // init, barriers, the id atomic) and 1.50 ms at >= 48 with 512 keys (tools/sweep_flow.sh, ZIPF=1.1).
 constexpr uint32_t kCombSlots = FB_COMB_SLOTS;  // keys past a full table stay plain entries
-constexpr uint32_t kCombThreads = 256;
+#ifndef FB_COMB_THREADS
+#define FB_COMB_THREADS 256
+#endif
+constexpr uint32_t kCombThreads = FB_COMB_THREADS;
 constexpr uint32_t kCombGrid = FB_COMB_GRID;
 static_assert(kCombSlots % kCombThreads == 0, "each thread numbers kCombSlots / kCombThreads keys");
 constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
