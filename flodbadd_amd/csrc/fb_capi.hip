@@ -55,6 +55,13 @@ struct fb_ctx {
     uint32_t* d_cticket = nullptr;            // scan ticket counter
     uint32_t scan_epoch = 0;                  // epoch of the last scan (0: status needs zeroing)
     uint64_t cseg_cap = 0;                    // segments
+    // single-pass dense output (k_parse_dense): per-tile look-back words, epoch, grid, and the
+    // look-back's polls before it computes a late predecessor's sums itself (FB_DENSE_STEAL_POLLS
+    // at fb_create; tests set 0 to force that path)
+    unsigned long long* d_dstatus = nullptr;  // [cseg_cap / parse_dense_tile_segs() + 1]
+    uint32_t dense_epoch = 0;                 // epoch of the last launch (0: status needs zeroing)
+    uint32_t dense_grid = 0;
+    uint32_t steal_polls = 1u << 12;
     hipEvent_t stage_event = nullptr;  // fb_set_stage_event (caller-owned): recorded between the
                                        // parse and the update of fb_process[_seg]_dev
     // flow table
@@ -250,6 +257,8 @@ static int reset_launch_scratch(fb_ctx* c, hipStream_t s) {
     return FB_OK;
 }
 
+static uint64_t dense_status_words(uint64_t nseg) { return nseg / parse_dense_tile_segs() + 1; }
+
 // Scan scratch of the dense entry points, for batches of up to `n` frames (grown, never shrunk).
 static int ensure_compact_scratch(fb_ctx* c, uint64_t n, hipStream_t s) {
     const uint64_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
@@ -259,16 +268,20 @@ static int ensure_compact_scratch(fb_ctx* c, uint64_t n, hipStream_t s) {
     hipFree(c->d_cpre);
     hipFree(c->d_cstatus);
     hipFree(c->d_cticket);
+    hipFree(c->d_dstatus);
     c->d_cseg = nullptr;
     c->d_cpre = nullptr;
     c->d_cstatus = nullptr;
     c->d_cticket = nullptr;
+    c->d_dstatus = nullptr;
     c->cseg_cap = 0;
     c->scan_epoch = 0;
+    c->dense_epoch = 0;
     const uint64_t want = std::max<uint64_t>(nseg, 1024);
     if (hipMalloc(&c->d_cseg, want * 4ull) != hipSuccess || hipMalloc(&c->d_cpre, want * 8ull) != hipSuccess ||
         hipMalloc(&c->d_cstatus, seg_scan_tiles((uint32_t)want) * 8ull) != hipSuccess ||
-        hipMalloc(&c->d_cticket, 4) != hipSuccess)
+        hipMalloc(&c->d_cticket, 4) != hipSuccess ||
+        hipMalloc(&c->d_dstatus, dense_status_words(want) * 8ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "dense-output scratch (%llu segments)", (unsigned long long)want);
     HIP_TRY(hipMemsetAsync(c->d_cticket, 0, 4, s));
     c->cseg_cap = want;
@@ -347,6 +360,10 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
         c->seg_grid_async = std::min<uint32_t>((uint32_t)prop.multiProcessorCount, c->seg_grid);
+        int db = 0;
+        if (occupancy_parse_dense(&db) != hipSuccess || db < 1) db = 1;
+        c->dense_grid = std::min<uint32_t>((uint32_t)(db * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
+        if (const char* e = getenv("FB_DENSE_STEAL_POLLS")) c->steal_polls = (uint32_t)strtoul(e, nullptr, 10);
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -401,6 +418,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_cpre);
     hipFree(c->d_cstatus);
     hipFree(c->d_cticket);
+    hipFree(c->d_dstatus);
     hipFree(c->d_error);
     hipFree(c->d_table);
     hipFree(c->d_entries);
@@ -627,6 +645,51 @@ int fb_seg_compact_dev(fb_ctx* c, const fb_pkt_out* d_seg_out, const uint32_t* d
 // segment (classes and batch stats too), the scan turns the counts into batch-wide offsets, pass 2
 // parses again and stores each record at its offset -- at C2 the frames are still in the Infinity
 // Cache for pass 2.  No kernel of the path waits on another workgroup.
+// Frame batches take the single-pass kernel (k_parse_dense: tiles ordered by ticket, decoupled
+// look-back, records kept in registers until the tile's offset is known); parsed-packet batches
+// (and FB_DENSE_TWO_PASS builds, for A/B timing) the two passes below.
+static int parse_dense_single(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
+                              uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns, uint8_t* d_class,
+                              fb_batch_stats* d_stats, hipStream_t s) {
+    int rc = reset_launch_scratch(c, s);
+    if (!rc) rc = upload_cfg(c, s);
+    if (!rc) rc = ensure_flow_scratch(c, n, s);
+    if (!rc) rc = ensure_compact_scratch(c, n, s);
+    if (rc) return rc;
+    const uint32_t nseg = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES;
+    if (c->dense_epoch == 0u || c->dense_epoch >= 255u) {
+        HIP_TRY(hipMemsetAsync(c->d_dstatus, 0, dense_status_words(c->cseg_cap) * 8ull, s));
+        c->dense_epoch = 0u;
+    }
+    c->last_n = n;
+    c->part_recs = nullptr;
+    c->part_buf = nullptr;
+    ParseParams p;
+    memset(&p, 0, sizeof(p));
+    p.cfg = c->d_cfg;
+    p.tick = c->d_tick;
+    const uint32_t launch = ++c->epoch;
+    p.error = c->d_error + (launch & 3u);
+    p.error_next = c->d_error + ((launch + 1u) & 3u);
+    p.dense_out = d_out;
+    p.dense_dns = d_dns;
+    p.dstatus = c->d_dstatus;
+    p.steal_polls = c->steal_polls;
+    p.dep = ++c->dense_epoch;
+    p.ntiles = (nseg + parse_dense_tile_segs() - 1) / parse_dense_tile_segs();
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->dense_grid, p.ntiles));
+    SegBatch b;
+    memset(&b, 0, sizeof(b));
+    b.frames = d_frames;
+    b.offsets = d_offsets;
+    b.cls = d_class;
+    b.stats = d_stats;
+    b.n = n;
+    b.frames_bytes = (uint32_t)frames_bytes;
+    HIP_TRY(launch_parse_dense(p, b, grid, s));
+    return FB_OK;
+}
+
 static int parse_dense(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets,
                        const fb_parsed_pkt* d_in, uint32_t n, fb_pkt_out* d_out, fb_dns_out* d_dns, uint8_t* d_class,
                        fb_batch_stats* d_stats, hipStream_t s) {
@@ -634,6 +697,9 @@ static int parse_dense(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
         HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(fb_batch_stats), s));
         return FB_OK;
     }
+#ifndef FB_DENSE_TWO_PASS
+    if (!d_in) return parse_dense_single(c, d_frames, frames_bytes, d_offsets, n, d_out, d_dns, d_class, d_stats, s);
+#endif
     int rc = ensure_compact_scratch(c, n, s);
     if (rc) return rc;
     rc = launch_seg(c, one_batch(d_frames, frames_bytes, d_offsets, n, nullptr, c->d_cseg, d_class, d_stats), n, d_in,

@@ -77,6 +77,8 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
 // Record slots of the batch: dense -> n_session of the parse launch (read on the device);
 // segmented -> every slot of every segment (invalid slots are skipped by slot_valid).
 __device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
+    // dense records whose look-back expired (error bit 2: offsets not trusted) never reach the table
+    if (!P.seg && (__hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return 0u;
     const unsigned long long n = P.seg ? (unsigned long long)P.n_slots : P.stats->n_session;
     return (uint32_t)min(n, (unsigned long long)P.max_recs);
 }

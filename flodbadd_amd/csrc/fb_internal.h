@@ -44,6 +44,13 @@ struct ParseParams {
     const unsigned long long* pre;  // dense pass 2: per segment n_session | n_dns << 32 before it
     fb_pkt_out* dense_out;        // dense pass 2: batch-wide SESSION records (or nullptr)
     fb_dns_out* dense_dns;        // dense pass 2: batch-wide DNS records (or nullptr)
+    // k_parse_dense (single-pass dense output): per-tile look-back words, the launch's 8-bit
+    // epoch, the number of tiles, and the polls a look-back waits for a predecessor's word before
+    // computing that tile's sums itself
+    unsigned long long* dstatus;
+    uint32_t dep;
+    uint32_t ntiles;
+    uint32_t steal_polls;
 };
 // 16 / 8 bytes at a 4-B aligned address: 56-B records (fb_pkt_out, fb_parsed_pkt) are only 8-B
 // aligned at odd indices, so a uint4 dereference there would claim an alignment the data lacks
@@ -239,6 +246,12 @@ hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t
                             SegPass pass = SegPass::kSegments);
 hipError_t occupancy_parse_seg(int* blocks_per_cu);
 uint32_t parse_seg_block_threads();
+// Single-pass dense output of one frame batch (k_parse_dense): records, DNS records, classes and
+// stats, tiles of parse_dense_tile_segs() segments (P.dstatus / dep / ntiles / steal_polls set by
+// the caller).
+hipError_t launch_parse_dense(const ParseParams& p, const SegBatch& b, uint32_t grid, hipStream_t s);
+hipError_t occupancy_parse_dense(int* blocks_per_cu);
+uint32_t parse_dense_tile_segs();
 // Exclusive scan of segment count words into pre[nseg] (u64 n_session | n_dns << 32), and the
 // dense copy of a segmented batch (fb_seg_compact_dev); out / dns may each be NULL.
 // The scan's look-back scratch: seg_scan_tiles(nseg) epoch-tagged status words (zeroed whenever

@@ -701,6 +701,301 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     sstamp(15);
 }
 
+// ============================================================================================
+// k_parse_dense -- single-pass batch-wide (dense) output of one frame batch.
+//
+// The batch is cut into tiles of kDnTileSegs 64-frame segments; block b runs tiles b, b + G,
+// b + 2G ... (G = grid).  Per tile it parses and classifies the frames with the records kept in
+// registers (kDnSegs segments per wave), publishes the tile's (n_session, n_dns) in an
+// epoch-tagged status word, looks back over its predecessors' words for the tile's batch-wide
+// offset (decoupled look-back by wave 0, a 64-tile window per step), and stores the records and
+// DNS records at their final positions.  Classes and batch stats as in k_parse_seg.  Replaces
+// pass 1 + scan + pass 2 of the two-pass dense path (fb_compact.hip): the same outputs from one
+// read of the headers.
+//
+// Forward progress without assuming every workgroup is resident (a GPU shared with other work
+// may not run all of them at once -- the failure round 1's look-back kernel had): a
+// look-back that has waited kDnSteal polls for a predecessor's word computes that tile's sums
+// itself (count-only classification of its frames, the same deterministic result the owner
+// will publish), CASes them in as the tile's aggregate if the word is still unpublished, and
+// walks on.  So a look-back never depends on a workgroup that is not running; in the normal case
+// nothing is recomputed.  A ticket counter ordering the tiles instead was measured first: its
+// same-address atomics (~1,500 per 1M frames) cost 16 us per batch.
+// ============================================================================================
+#ifndef FB_DN_SEGS
+#define FB_DN_SEGS 2
+#endif
+#ifndef FB_DN_BPC
+#define FB_DN_BPC 2
+#endif
+constexpr int kDnWaves = 8;
+constexpr int kDnSegs = FB_DN_SEGS;  // segments per wave per tile (records held in registers)
+constexpr uint32_t kDnTileSegs = kDnWaves * kDnSegs;
+constexpr int kDnThreads = 64 * kDnWaves;
+// tile status word [epoch:8 | P:1 | A:1 | n_dns:27 | n_session:27]: A = the tile's own sums are
+// published, P = its inclusive prefix is (k_seg_scan's format)
+constexpr unsigned long long kDnA = 1ull << 54, kDnP = 1ull << 55, kDn27 = (1ull << 27) - 1ull;
+__device__ __forceinline__ unsigned long long dn_word(uint32_t ep, unsigned long long flag, unsigned long long pair) {
+    return ((unsigned long long)ep << 56) | flag | (pair & kDn27) | (((pair >> 32) & kDn27) << 27);
+}
+__device__ __forceinline__ unsigned long long dn_pair(unsigned long long w) {
+    return (w & kDn27) | (((w >> 27) & kDn27) << 32);
+}
+
+__global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_dense(const ParseParams P,
+                                                                                      const SegBatch B) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t nt = P.ntiles, ep = P.dep, n = B.n;
+    __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
+    __shared__ unsigned long long s_stage[kDnWaves][64 * 7];
+    __shared__ unsigned long long s_wsum[2][kDnWaves];  // per wave n_session | n_dns << 32, by tile parity
+    __shared__ unsigned long long s_excl;                // the tile's batch-wide offset (same packing)
+    __shared__ uint32_t s_acc[11];                       // the block's stats counters; wave arrivals
+    const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
+    const unsigned long long lmask = (1ull << lane) - 1ull;
+    unsigned long long* stage = s_stage[wave];
+    constexpr uint32_t kOob = 0x80000000u;
+    uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
+    if (tid <= 10u) s_acc[tid] = 0u;
+    {
+        constexpr uint32_t kCfg16 = kCfgLdsBytes / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
+        for (uint32_t k = tid; k < kCfg16; k += kDnThreads) s_cfg4[k] = src[k];
+        constexpr uint32_t kLanOff = offsetof(DevConfig, lan_v6) / 16, kOwnOff = offsetof(DevConfig, own) / 16;
+        const uint32_t nl = P.cfg->n_lan_v6 * (sizeof(LanV6) / 16), no = P.cfg->n_own * (sizeof(fb_ip) / 16);
+        for (uint32_t k = tid; k < nl; k += kDnThreads) s_cfg4[kLanOff + k] = src[kLanOff + k];
+        for (uint32_t k = tid; k < no; k += kDnThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
+        if (b == 0u && tid == 0u) *P.error_next = 0u;
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t r_fr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)B.frames, (short)0, (int)B.frames_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)n : 0, 0x00020000);
+    // (n_session, n_dns) of tile j, computed by the calling wave (the look-back's fallback)
+    auto tile_pair = [&](uint32_t j) {
+        unsigned long long acc = 0ull;
+        for (uint32_t sgi = 0; sgi < kDnTileSegs; ++sgi) {
+            const uint32_t i = (j * kDnTileSegs + sgi) * 64u + lane;
+            const bool valid = i < n;
+            const uint2 q = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
+            Hdr h;
+            load_headers1(r_fr, q.x, h);
+            Pkt k;
+            process_frame(r_fr, cfg, cfg, h, valid ? q.x : 1u, valid ? q.y : 0u, B.frames_bytes, i, k);
+            acc += (unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_SESSION)) |
+                   ((unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_DNS)) << 32);
+        }
+        return acc;
+    };
+    uint32_t par = 0u;
+    for (uint32_t t = b; t < nt; t += G) {
+        const uint32_t sg0 = t * kDnTileSegs + wave * (uint32_t)kDnSegs;
+        uint2 q[kDnSegs];
+        Hdr h[kDnSegs];
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) {
+            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
+            q[j] = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
+        }
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, q[j].x, h[j]);
+        Pkt kk[kDnSegs];
+        uint32_t cs[kDnSegs], cd[kDnSegs], rs[kDnSegs], rd[kDnSegs];
+        bool ss[kDnSegs], sd[kDnSegs];
+        unsigned long long ws = 0ull;
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) {
+            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
+            const bool valid = i < n;
+            process_frame(r_fr, cfg, cfg, h[j], valid ? q[j].x : 1u, valid ? q[j].y : 0u, B.frames_bytes, i, kk[j]);
+            const bool is_s = valid && kk[j].cls == FB_CLASS_SESSION;
+            const bool is_d = valid && kk[j].cls == FB_CLASS_DNS;
+            const bool is_f = valid && kk[j].cls == FB_CLASS_FILTERED;
+            const bool counted = is_s || is_f;
+            const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+            cs[j] = (uint32_t)__popcll(m_sess);
+            cd[j] = (uint32_t)__popcll(m_dns);
+            rs[j] = (uint32_t)__popcll(m_sess & lmask);
+            rd[j] = (uint32_t)__popcll(m_dns & lmask);
+            ss[j] = is_s;
+            sd[j] = is_d;
+            ws += (unsigned long long)cs[j] | ((unsigned long long)cd[j] << 32);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk[j].cls, r_cls, valid ? i : kOob, 0, 0);
+            a_s += cs[j];
+            a_d += cd[j];
+            a_f += __popcll(__ballot(is_f));
+            a_t += __popcll(__ballot(counted && kk[j].tcp));
+            a_4 += __popcll(__ballot(counted && kk[j].v4));
+            a_b += __popcll(__ballot(valid && kk[j].bad));
+            a_n += __popcll(__ballot(valid));
+        }
+        if (lane == 0u) s_wsum[par][wave] = ws;
+        lds_barrier();
+        if (wave == 0u) {
+            unsigned long long agg = 0ull;
+#pragma unroll
+            for (int k = 0; k < kDnWaves; ++k) agg += s_wsum[par][k];
+            unsigned long long excl = 0ull;
+            if (t == 0u) {
+                if (lane == 0u) __hip_atomic_store(P.dstatus, dn_word(ep, kDnP, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (lane == 0u)
+                    __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnA, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int64_t jt = (int64_t)t;  // window: tiles jt-1-lane
+                for (;;) {
+                    const int64_t idx = jt - 1 - (int64_t)lane;
+                    auto probe = [&]() {
+                        return idx >= 0 ? __hip_atomic_load(P.dstatus + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : dn_word(ep, kDnP, 0ull);
+                    };
+                    auto ready = [&](unsigned long long x) { return (uint32_t)(x >> 56) == ep && (x & (kDnA | kDnP)); };
+                    unsigned long long v = probe();
+                    for (uint32_t spins = 0u;; ++spins) {
+                        unsigned long long late = __ballot(!ready(v));
+                        if (late == 0ull) break;
+                        if (spins >= P.steal_polls) {
+                            // the owners of these tiles may not be running: compute their sums here
+                            while (late) {
+                                const uint32_t l = (uint32_t)__builtin_ctzll(late);
+                                late &= late - 1ull;
+                                const uint32_t j = (uint32_t)(jt - 1 - (int64_t)l);
+                                const unsigned long long w = dn_word(ep, kDnA, tile_pair(j));
+                                if (lane == l) {
+                                    atomicCAS(P.dstatus + j, v, w);  // unless the owner published meanwhile
+                                    v = w;
+                                }
+                            }
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        if (!ready(v)) v = probe();
+                    }
+                    const unsigned long long pm = __ballot((v & kDnP) != 0ull);
+                    const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;  // nearest inclusive
+                    unsigned long long part = lane <= stop ? dn_pair(v) : 0ull;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                    excl += part;
+                    if (pm) break;
+                    jt -= 64;
+                }
+                if (lane == 0u)
+                    __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnP, excl + agg), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0u) s_excl = excl;
+        }
+        lds_barrier();
+        unsigned long long base = s_excl;
+#pragma unroll
+        for (int k = 0; k < kDnWaves; ++k) base += (uint32_t)k < wave ? s_wsum[par][k] : 0ull;
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) {
+            // the segment's records at record bs of the batch (56 bs is 16-B aligned when bs is even;
+            // otherwise its first 8-B word goes alone and the 16-B body stays aligned), DNS at bd
+            if (ss[j]) {
+                unsigned long long* dd = stage + (size_t)rs[j] * 7;
+#pragma unroll
+                for (int w = 0; w < 7; ++w)
+                    dd[w] = (unsigned long long)kk[j].w[2 * w] | ((unsigned long long)kk[j].w[2 * w + 1] << 32);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t bs = (uint32_t)base, bd = (uint32_t)(base >> 32);
+            const uint32_t words = cs[j] * 7u, head = cs[j] ? (bs & 1u) : 0u, body = (words - head) >> 1;
+            const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint8_t*>(P.dense_out) + (size_t)bs * 56u, (short)0, P.dense_out ? (int)(words * 8u) : 0,
+                0x00020000);
+            const __amdgpu_buffer_rsrc_t r_dns = __builtin_amdgcn_make_buffer_rsrc(
+                P.dense_dns + bd, (short)0, P.dense_dns ? (int)(cd[j] * 16u) : 0, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t cc = lane + 64u * k;
+                const uint32_t src = head + 2u * min(cc, 223u - head);
+                const unsigned long long x = stage[src], y = stage[src + 1u];
+                const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? head * 8u + cc * 16u : kOob, 0, FB_ST_AUX);
+            }
+            {   // lane 0: the head word (odd base), lane 1: the tail word (odd body remainder)
+                const bool h1 = head && lane == 0u, t1 = ((words - head) & 1u) && lane == 1u;
+                const uint32_t w = lane == 0u ? 0u : (words ? words - 1u : 0u);
+                const unsigned long long x = stage[w];
+                const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(v, r_out, (h1 || t1) ? w * 8u : kOob, 0, FB_ST_AUX);
+            }
+            {
+                const u32x4 v = {kk[j].w[0], kk[j].w[1], kk[j].w[2], kk[j].w[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r_dns, sd[j] ? 16u * rd[j] : kOob, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
+            base += (unsigned long long)cs[j] | ((unsigned long long)cd[j] << 32);
+        }
+        par ^= 1u;
+    }
+    // batch stats: as k_parse_seg (one batch): wave counters into LDS, the block's last wave adds
+    // the block's into the five packed device words; the block completing a word writes its fields
+    {
+        const uint32_t a_tot = a_s + a_f;
+        const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
+        if (lane < 10u) {
+            uint32_t v = 0u;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
+            __hip_atomic_fetch_add(&s_acc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t arrived = 0u;
+        if (lane == 0u) arrived = __hip_atomic_fetch_add(&s_acc[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        arrived = __shfl(arrived, 0, 64);
+        if (arrived == (uint32_t)kDnWaves - 1u && lane < 5u) {
+            asm volatile("" ::: "memory");
+            const uint32_t j = lane;
+            const unsigned long long lo = s_acc[2u * j], hi = s_acc[2u * j + 1u];
+            unsigned long long* word = P.tick + j;
+            const unsigned long long add = (1ull << 54) | (hi << 27) | lo;
+            const unsigned long long old = __hip_atomic_fetch_add(word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((old >> 54) == (unsigned long long)G - 1u) {
+                const unsigned long long tot = old + add, m27 = (1ull << 27) - 1ull;
+                const unsigned long long f_lo = tot & m27, f_hi = (tot >> 27) & m27;
+                __hip_atomic_store(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fb_batch_stats* S = B.stats;
+                if (S) {
+                    if (j == 0u) {
+                        S->n_session = f_lo;
+                        S->n_filtered = f_hi;
+                        S->new_sessions = 0ull;
+                        S->updated_sessions = 0ull;
+                        S->error = __hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        S->reserved[0] = S->reserved[1] = S->reserved[2] = 0ull;
+                    } else if (j == 1u) {
+                        S->n_dns = f_lo;
+                        S->bad_offsets = f_hi;
+                    } else if (j == 2u) {
+                        S->tcp_processed = f_lo;
+                        S->udp_processed = f_hi;
+                    } else if (j == 3u) {
+                        S->ipv4_processed = f_lo;
+                        S->ipv6_processed = f_hi;
+                    } else {
+                        S->total_processed = f_lo;
+                        S->n_drop = f_hi;
+                    }
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_parse_dense(const ParseParams& p, const SegBatch& b, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_parse_dense, dim3(grid), dim3(kDnThreads), 0, s, p, b);
+    return hipGetLastError();
+}
+hipError_t occupancy_parse_dense(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_parse_dense, kDnThreads, 0);
+}
+uint32_t parse_dense_tile_segs() { return kDnTileSegs; }
+
 hipError_t launch_parse_seg(const ParseParams& p, const SegBatches& sb, uint32_t grid, hipStream_t s, SegPass pass) {
     const dim3 g(grid), t(kSegThreads);
     if (pass == SegPass::kCount) {
