@@ -728,7 +728,13 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 #ifndef FB_DN_BPC
 #define FB_DN_BPC 2
 #endif
-constexpr int kDnWaves = 8;
+#ifndef FB_DN_WAVES
+#define FB_DN_WAVES 8
+#endif
+#ifndef FB_DN_SLEEP
+#define FB_DN_SLEEP 1
+#endif
+constexpr int kDnWaves = FB_DN_WAVES;
 constexpr int kDnSegs = FB_DN_SEGS;  // segments per wave per tile (records held in registers)
 constexpr uint32_t kDnTileSegs = kDnWaves * kDnSegs;
 constexpr int kDnThreads = 64 * kDnWaves;
@@ -759,6 +765,22 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
     constexpr uint32_t kOob = 0x80000000u;
     uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
     if (tid <= 10u) s_acc[tid] = 0u;
+    const __amdgpu_buffer_rsrc_t r_fr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)B.frames, (short)0, (int)B.frames_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)n : 0, 0x00020000);
+    uint32_t par = 0u;
+    // the offsets of the wave's segments of tile t (the next tile's are loaded while this one runs,
+    // so a tile waits for one round trip before its headers arrive, not two)
+    uint2 q[kDnSegs];
+    auto load_offsets = [&](uint32_t t, uint2 (&qq)[kDnSegs]) {
+        const uint32_t sg0 = min(t, nt - 1u) * kDnTileSegs + wave * (uint32_t)kDnSegs;
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) {
+            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
+            qq[j] = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
+        }
+    };
+    if (b < nt) load_offsets(b, q);  // in flight with the configuration copy
     {
         constexpr uint32_t kCfg16 = kCfgLdsBytes / 16;
         const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
@@ -769,10 +791,7 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
         for (uint32_t k = tid; k < no; k += kDnThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
         if (b == 0u && tid == 0u) *P.error_next = 0u;
     }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t r_fr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)B.frames, (short)0, (int)B.frames_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)n : 0, 0x00020000);
+    lds_barrier();  // configuration in LDS (the offsets loads stay in flight)
     // (n_session, n_dns) of tile j, computed by the calling wave (the look-back's fallback)
     auto tile_pair = [&](uint32_t j) {
         unsigned long long acc = 0ull;
@@ -789,18 +808,13 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
         }
         return acc;
     };
-    uint32_t par = 0u;
     for (uint32_t t = b; t < nt; t += G) {
         const uint32_t sg0 = t * kDnTileSegs + wave * (uint32_t)kDnSegs;
-        uint2 q[kDnSegs];
         Hdr h[kDnSegs];
 #pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) {
-            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
-            q[j] = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
-        }
-#pragma unroll
         for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, q[j].x, h[j]);
+        uint2 qn[kDnSegs];
+        load_offsets(t + G, qn);
         Pkt kk[kDnSegs];
         uint32_t cs[kDnSegs], cd[kDnSegs], rs[kDnSegs], rd[kDnSegs];
         bool ss[kDnSegs], sd[kDnSegs];
@@ -869,7 +883,7 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
                             }
                             break;
                         }
-                        __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
                         if (!ready(v)) v = probe();
                     }
                     const unsigned long long pm = __ballot((v & kDnP) != 0ull);
@@ -932,6 +946,8 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
             base += (unsigned long long)cs[j] | ((unsigned long long)cd[j] << 32);
         }
         par ^= 1u;
+#pragma unroll
+        for (int j = 0; j < kDnSegs; ++j) q[j] = qn[j];
     }
     // batch stats: as k_parse_seg (one batch): wave counters into LDS, the block's last wave adds
     // the block's into the five packed device words; the block completing a word writes its fields
