@@ -4,7 +4,8 @@
 // fb_parse_classify_dev / fb_process_parsed_dev / fb_process_dev promise the reference's
 // emission order with no gaps: class-SESSION records packed in packet order, DNS side records
 // likewise (what a caller iterating frames one by one through parse_packet_pcap +
-// process_parsed_packet, src/capture.rs:1036-1061, would see).  They run k_parse_seg twice
+// process_parsed_packet, src/capture.rs:1036-1061, would see).  Frame batches take the
+// single-pass k_parse_dense (fb_parse.hip); parsed-packet batches run k_parse_seg twice
 // (fb_capi.hip parse_dense): pass 1 counts each 64-frame segment (and writes classes + stats),
 // k_seg_scan (one pass, decoupled look-back) turns the counts into batch-wide offsets, pass 2
 // re-parses (the frames of a 1M-frame batch are still in the Infinity Cache) and stores every
