@@ -7,7 +7,8 @@ per-flow count (BASELINE config C5):
   1. every rank exports its flow table (canonical key + 6 integer counters, fb_flow_export);
   2. all-gather of the keys (keys << packets);
   3. every rank sorts the union by the derived Ord of Session (src/sessions.rs:23-30: protocol,
-     src_ip [V4 < V6, then octets], src_port, dst_ip, dst_port) -> an identical dense flow_id;
+     src_ip [V4 < V6, then octets], src_port, dst_ip, dst_port) -> an identical dense flow_id
+     (an LSD sort of the keys' Ord columns on the collective's device);
   4. each rank scatters its counters into a dense int64[F][6];
   5. all_reduce(SUM) -- over RCCL/xGMI with device tensors ("nccl" backend), gloo on the CPU.
 Integer sums are order independent, so the result is bit-identical to a single-GPU table.
@@ -56,87 +57,113 @@ def _conn_state(m):
     return np.select([S & H & F & f, S & ~h & ~r, R | r, S & H & ~F & ~f], [1, 2, 3, 4], 5).astype(np.uint8)
 
 
+def _ord_sort(cols):
+    """Permutation sorting the rows of [T,12] int64 Ord columns lexicographically (column 0
+    primary): one stable sort per column, least significant first (LSD), all on cols' device."""
+    import torch
+    perm = torch.arange(cols.shape[0], device=cols.device)
+    for c in range(cols.shape[1] - 1, -1, -1):
+        _, o = torch.sort(cols[perm, c], stable=True)
+        perm = perm[o]
+    return perm
+
+
 def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
     """All ranks' flow tables merged into one table sorted by Session's derived Ord, identical
     on every rank.  `dist` is torch.distributed (initialised); `device` is the torch device of
     the collective tensors (a cuda device for RCCL, None/cpu for gloo); `shard_first` is the
-    global index of this rank's first packet (shard_range)."""
+    global index of this rank's first packet (shard_range).  Everything between the upload of
+    the exported records and the download of the merged columns runs as torch ops on `device`:
+    the keys' Ord columns, their all-gather, an LSD sort of the union, dense ids from adjacent
+    differences, the scatters and the all-reduces."""
     import torch
+    dev = torch.device("cpu") if device is None else torch.device(device)
     flows = np.ascontiguousarray(flows, dtype=FLOW_REC_DTYPE)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     assert world < 16, "hist_mask OR uses 4-bit fields"
-    kw = _key_words(flows).astype(np.int64)  # u32 words widened (exact)
-    n = torch.tensor([len(flows)], dtype=torch.int64, device=device)
+    nl = len(flows)
+    raw = torch.from_numpy(flows.view(np.uint8).reshape(nl, FLOW_REC_DTYPE.itemsize)).to(dev)
+    w32 = raw.view(torch.int32).to(torch.int64) & 0xFFFFFFFF  # [nl, 32] u32 words, widened
+    w64 = raw.view(torch.int64)                                # [nl, 16] u64 words (as int64 bits)
+    ports, pf = w32[:, 8], w32[:, 9]
+    # key columns in the derived Ord's priority: protocol, family (V4 < V6), src words, src port,
+    # dst words, dst port (src/sessions.rs:23-30; IpAddr octets big-endian = the words' order)
+    mine = torch.stack([pf & 0xFF, (pf >> 8) & 0xFF, w32[:, 0], w32[:, 1], w32[:, 2], w32[:, 3], ports & 0xFFFF,
+                        w32[:, 4], w32[:, 5], w32[:, 6], w32[:, 7], ports >> 16], dim=1)
+    n = torch.tensor([nl], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(x.item()) for x in sizes]
     m = max(sizes + [1])
-    pad = torch.zeros((m, 10), dtype=torch.int64, device=device)
-    if len(flows):
-        pad[: len(flows)] = torch.from_numpy(kw).to(device)
+    pad = torch.zeros((m, 12), dtype=torch.int64, device=dev)
+    pad[:nl] = mine
     gathered = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(gathered, pad, group=group)
-    allk = np.concatenate([g[:s].cpu().numpy() for g, s in zip(gathered, sizes)]).astype(np.uint32)
-    # unique keys, dense ids in derived-Ord order
-    uniq = np.unique(allk.view(np.dtype((np.void, 40))).ravel()).view(np.uint32).reshape(-1, 10)
-    order = sort_keys(uniq)
-    uniq = uniq[order]
-    F = len(uniq)
-    ukey = uniq.view(np.dtype((np.void, 40))).ravel()
-    mine = _key_words(flows).view(np.dtype((np.void, 40))).ravel()
-    # position of each local key in the (void-sorted) unique array, then in the Ord order
-    vsort = np.argsort(ukey)
-    idx = vsort[np.searchsorted(ukey[vsort], mine)] if len(flows) else np.zeros(0, dtype=np.int64)
+    allc = torch.cat([g[:sz] for g, sz in zip(gathered, sizes)])
+    # dense ids in Ord order: sort the union, a new id wherever a row differs from the one before
+    perm = _ord_sort(allc)
+    srt = allc[perm]
+    first = torch.ones(srt.shape[0], dtype=torch.bool, device=dev)
+    if srt.shape[0] > 1:
+        first[1:] = (srt[1:] != srt[:-1]).any(dim=1)
+    ids = torch.cumsum(first.to(torch.int64), 0) - 1
+    inv = torch.empty_like(ids)
+    inv[perm] = ids
+    uniq = srt[first]
+    F = int(uniq.shape[0])
+    start = sum(sizes[:rank])
+    idx = inv[start:start + nl]
 
     def reduce(cols, fill, op):
-        a = np.full((F, len(cols)), fill, dtype=np.int64)
-        if len(flows):
-            a[idx] = np.stack(cols, axis=1)
-        t = torch.from_numpy(a).to(device)
+        t = torch.full((F, len(cols)), fill, dtype=torch.int64, device=dev)
+        if nl:
+            t[idx] = torch.stack(cols, dim=1)
         dist.all_reduce(t, op=op, group=group)
-        return t.cpu().numpy()
+        return t
 
     def glob(pos):  # rank-local position -> global ((call << 32) | global packet index)
-        pos = pos.astype(np.uint64)
-        return ((pos >> np.uint64(32)) << np.uint64(32)) | ((pos & np.uint64(0xFFFFFFFF)) + np.uint64(shard_first))
+        return ((pos >> 32) << 32) | ((pos & 0xFFFFFFFF) + shard_first)
 
-    big = np.iinfo(np.int64).max
-    mask = flows["hist_mask"].astype(np.int64)
-    spread = np.zeros(len(flows), dtype=np.int64)
+    big = torch.iinfo(torch.int64).max
+    counters, first_seen, last_seen, end_seen = w64[:, 5:11], w64[:, 11], w64[:, 12], w64[:, 13]
+    hist_len, state = w32[:, 28], w32[:, 29]
+    mask, end_mask = state & 0xFFFF, (state >> 24) & 0xFF
+    spread = torch.zeros(nl, dtype=torch.int64, device=dev)
     for b in range(13):
         spread |= ((mask >> b) & 1) << (4 * b)
-    ended = flows["end_seen"] != np.uint64(FB_SEEN_NONE)
-    end = np.where(ended, glob(flows["end_seen"]).astype(np.int64), big)
-    sums = reduce([flows[c].astype(np.int64) for c in COUNTERS] + [flows["hist_len"].astype(np.int64), spread],
-                  0, dist.ReduceOp.SUM)
-    mins = reduce([glob(flows["first_seen"]).astype(np.int64), end], big, dist.ReduceOp.MIN)
-    last = reduce([glob(flows["last_seen"]).astype(np.int64)], -1, dist.ReduceOp.MAX)
+    ended = end_seen != -1  # FB_SEEN_NONE
+    end = torch.where(ended, glob(end_seen), torch.full_like(end_seen, big))
+    sums = reduce([counters[:, j] for j in range(6)] + [hist_len, spread], 0, dist.ReduceOp.SUM)
+    mins = reduce([glob(first_seen), end], big, dist.ReduceOp.MIN)
+    last = reduce([glob(last_seen)], -1, dist.ReduceOp.MAX)
     # conn_state: the ending rank's end_mask | the conn_state characters of the ranks before it
     gend = mins[:, 1]
-    my_end = np.full(F, big, dtype=np.int64)
-    my_end[idx] = end
-    is_end_rank = (my_end == gend) & (gend != big)
-    end_rank = reduce([np.where(is_end_rank[idx], rank, 0)], 0, dist.ReduceOp.SUM)[:, 0]
+    is_end = (end == gend[idx]) & (gend[idx] != big)
+    end_rank = reduce([torch.where(is_end, rank, 0)], 0, dist.ReduceOp.SUM)[:, 0]
     # ranks before the ending one add their S s H h F f R r bits, the ending rank its end_mask
-    before = np.where(rank < end_rank[idx], mask & 0xFF, 0) | \
-        np.where(is_end_rank[idx], flows["end_mask"].astype(np.int64), 0)
-    bits = np.zeros(len(flows), dtype=np.int64)
+    before = torch.where(rank < end_rank[idx], mask & 0xFF, 0) | torch.where(is_end, end_mask, 0)
+    bits = torch.zeros(nl, dtype=torch.int64, device=dev)
     for b in range(8):
         bits |= ((before >> b) & 1) << (4 * b)
     emask_sum = reduce([bits], 0, dist.ReduceOp.SUM)[:, 0]
-    emask = np.zeros(F, dtype=np.int64)
-    hmask = np.zeros(F, dtype=np.int64)
+    hmask = torch.zeros(F, dtype=torch.int64, device=dev)
+    emask = torch.zeros(F, dtype=torch.int64, device=dev)
     for b in range(13):
-        hmask |= (((sums[:, 7] >> (4 * b)) & 15) > 0).astype(np.int64) << b
+        hmask |= (((sums[:, 7] >> (4 * b)) & 15) > 0).to(torch.int64) << b
         if b < 8:
-            emask |= (((emask_sum >> (4 * b)) & 15) > 0).astype(np.int64) << b
+            emask |= (((emask_sum >> (4 * b)) & 15) > 0).to(torch.int64) << b
 
+    # one download of the merged columns, then the records
+    u, sums, mins, last, hmask, emask = (x.cpu().numpy() for x in (uniq, sums, mins, last, hmask, emask))
+    gend = mins[:, 1]
+    has_end = gend != np.iinfo(np.int64).max
     out = np.zeros(F, dtype=FLOW_REC_DTYPE)
-    out.view(np.uint8).reshape(F, FLOW_REC_DTYPE.itemsize)[:, :40] = uniq.view(np.uint8).reshape(F, 40)
+    out["protocol"], out["family"] = u[:, 0], u[:, 1]
+    out["src_ip"], out["src_port"] = u[:, 2:6], u[:, 6]
+    out["dst_ip"], out["dst_port"] = u[:, 7:11], u[:, 11]
     for j, c in enumerate(COUNTERS):
         out[c] = sums[:, j].astype(np.uint64)
-    has_end = gend != big
     out["hist_len"] = sums[:, 6].astype(np.uint32)
     out["hist_mask"] = hmask.astype(np.uint16)
     out["first_seen"] = mins[:, 0].astype(np.uint64)

@@ -1,0 +1,34 @@
+"""Time the C5 merge (flodbadd_amd.distributed.global_flow_table) over RCCL at world size 1 on the
+device: the C4 10M-frame table (1.45M flows) exported, then merged (union, Ord sort, dense ids,
+all-reduces)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from flodbadd_amd import synth  # noqa: E402
+from flodbadd_amd.capture import FlodbaddGpuCapture  # noqa: E402
+from flodbadd_amd.distributed import global_flow_table  # noqa: E402
+from flodbadd_amd.sessions import SessionFilter  # noqa: E402
+
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29541")
+dev = torch.device("cuda", 0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+for n in (1 << 20, 10 << 20):
+    frames, offs = synth.generate(4, n, first=1)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 21)
+    cap.process_frames(frames, offs)
+    flows = cap.export_flows()
+    for rep in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        merged = global_flow_table(dist, flows, device=dev)
+        torch.cuda.synchronize()
+        print("frames %d flows %d: merge %.1f ms" % (n, len(merged), (time.perf_counter() - t0) * 1e3))
+    cap.close()
+dist.destroy_process_group()
