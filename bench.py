@@ -419,17 +419,28 @@ def c5_flow_reduce(N, lib, ctx, frames, offs, dist, group, device, shard_first):
     flow_ms = ev0.elapsed_ms(ev1)
     cnt = C.c_uint64()
     N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
-    flows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
-    got = C.c_uint64()
     t0 = time.perf_counter()
-    N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
-    merged = global_flow_table(dist, flows[: got.value], device=device, group=group, shard_first=shard_first)
+    if device.type == "cuda":  # RCCL: the table is exported straight into a device tensor
+        import torch
+        flows = torch.empty((max(cnt.value, 1), N.FLOW_REC_DTYPE.itemsize), dtype=torch.uint8, device=device)
+        d_n = torch.zeros(1, dtype=torch.int64, device=device)
+        N.check(lib.fb_flow_export_dev(ctx, C.c_void_p(flows.data_ptr()), cnt.value, C.c_void_p(d_n.data_ptr()), None))
+        torch.cuda.synchronize(device)
+        local = int(d_n.item())
+        merged = global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first)
+    else:
+        flows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
+        got = C.c_uint64()
+        N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
+        local = int(got.value)
+        merged = global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first)
     el = time.perf_counter() - t0
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
-    return dict(local_flows=int(got.value), global_flows=int(len(merged)), flow_update_ms=round(flow_ms, 3),
+    return dict(local_flows=local, global_flows=int(len(merged)), flow_update_ms=round(flow_ms, 3),
                 export_merge_ms=round(el * 1e3, 3),
-                note="per-rank fused parse+flow upsert of the rank's shard, then export + RCCL all-gather/all-reduce")
+                note="per-rank fused parse+flow upsert of the rank's shard, then the table exported (to a device "
+                     "tensor with RCCL) and merged: all-gather of keys, device sort -> dense ids, all-reduces")
 
 
 def cpu_baseline(frames, offs, seconds):

@@ -21,7 +21,7 @@ batch (C5), since the earlier ranks' packets then all precede the end packet.
 """
 import numpy as np
 
-from ._native import FB_SEEN_NONE, FLOW_REC_DTYPE
+from ._native import FLOW_REC_DTYPE
 
 COUNTERS = ("outbound_bytes", "inbound_bytes", "orig_pkts", "resp_pkts", "orig_ip_bytes", "resp_ip_bytes")
 
@@ -51,10 +51,20 @@ def sort_keys(words):
 
 
 def _conn_state(m):
-    """determine_conn_state (src/packets.rs:539-559) over FB_HIST_CHARS bits (vectorised)."""
-    b = lambda k: (m >> k) & 1 == 1
+    """determine_conn_state (src/packets.rs:539-559) over FB_HIST_CHARS bits (vectorised, torch)."""
+    import torch
+    b = lambda k: ((m >> k) & 1) == 1
     S, H, h, F, f, R, r = b(0), b(2), b(3), b(4), b(5), b(6), b(7)
-    return np.select([S & H & F & f, S & ~h & ~r, R | r, S & H & ~F & ~f], [1, 2, 3, 4], 5).astype(np.uint8)
+    c = torch.full_like(m, 5)
+    c = torch.where(S & H & ~F & ~f, torch.full_like(m, 4), c)
+    c = torch.where(R | r, torch.full_like(m, 3), c)
+    c = torch.where(S & ~h & ~r, torch.full_like(m, 2), c)
+    return torch.where(S & H & F & f, torch.full_like(m, 1), c)  # np.select order: first match wins
+
+
+def _hi32(x):
+    """x (int64 holding a u32) << 32 without leaving int64: sign-extend bit 31 first."""
+    return ((x ^ 0x80000000) - 0x80000000) << 32
 
 
 def _ord_sort(cols):
@@ -78,12 +88,15 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
     differences, the scatters and the all-reduces."""
     import torch
     dev = torch.device("cpu") if device is None else torch.device(device)
-    flows = np.ascontiguousarray(flows, dtype=FLOW_REC_DTYPE)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     assert world < 16, "hist_mask OR uses 4-bit fields"
-    nl = len(flows)
-    raw = torch.from_numpy(flows.view(np.uint8).reshape(nl, FLOW_REC_DTYPE.itemsize)).to(dev)
+    if isinstance(flows, torch.Tensor):  # [n, 128] uint8 on `dev` (fb_flow_export_dev)
+        raw = flows.to(dev).reshape(-1, FLOW_REC_DTYPE.itemsize)
+    else:
+        flows = np.ascontiguousarray(flows, dtype=FLOW_REC_DTYPE)
+        raw = torch.from_numpy(flows.view(np.uint8).reshape(len(flows), FLOW_REC_DTYPE.itemsize)).to(dev)
+    nl = int(raw.shape[0])
     w32 = raw.view(torch.int32).to(torch.int64) & 0xFFFFFFFF  # [nl, 32] u32 words, widened
     w64 = raw.view(torch.int64)                                # [nl, 16] u64 words (as int64 bits)
     ports, pf = w32[:, 8], w32[:, 9]
@@ -154,21 +167,18 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
         if b < 8:
             emask |= (((emask_sum >> (4 * b)) & 15) > 0).to(torch.int64) << b
 
-    # one download of the merged columns, then the records
-    u, sums, mins, last, hmask, emask = (x.cpu().numpy() for x in (uniq, sums, mins, last, hmask, emask))
-    gend = mins[:, 1]
-    has_end = gend != np.iinfo(np.int64).max
-    out = np.zeros(F, dtype=FLOW_REC_DTYPE)
-    out["protocol"], out["family"] = u[:, 0], u[:, 1]
-    out["src_ip"], out["src_port"] = u[:, 2:6], u[:, 6]
-    out["dst_ip"], out["dst_port"] = u[:, 7:11], u[:, 11]
-    for j, c in enumerate(COUNTERS):
-        out[c] = sums[:, j].astype(np.uint64)
-    out["hist_len"] = sums[:, 6].astype(np.uint32)
-    out["hist_mask"] = hmask.astype(np.uint16)
-    out["first_seen"] = mins[:, 0].astype(np.uint64)
-    out["last_seen"] = last[:, 0].astype(np.uint64)
-    out["end_seen"] = np.where(has_end, gend.astype(np.uint64), np.uint64(FB_SEEN_NONE))
-    out["end_mask"] = np.where(has_end, emask, 0).astype(np.uint8)
-    out["conn_state"] = np.where(has_end, _conn_state(emask), 0).astype(np.uint8)
-    return out
+    # the merged records assembled as fb_flow_rec words on the device, one download
+    has_end = gend != big
+    w = torch.zeros((F, 16), dtype=torch.int64, device=dev)
+    kw = [uniq[:, 2], uniq[:, 3], uniq[:, 4], uniq[:, 5], uniq[:, 7], uniq[:, 8], uniq[:, 9], uniq[:, 10],
+          uniq[:, 6] | (uniq[:, 11] << 16), uniq[:, 0] | (uniq[:, 1] << 8)]
+    for j in range(5):
+        w[:, j] = kw[2 * j] | _hi32(kw[2 * j + 1])
+    w[:, 5:11] = sums[:, 0:6]
+    w[:, 11] = mins[:, 0]
+    w[:, 12] = last[:, 0]
+    w[:, 13] = torch.where(has_end, gend, torch.full_like(gend, -1))  # FB_SEEN_NONE
+    em = torch.where(has_end, emask, 0)
+    cs = torch.where(has_end, _conn_state(emask), 0)
+    w[:, 14] = sums[:, 6] | _hi32(hmask | (cs << 16) | (em << 24))
+    return w.cpu().numpy().view(FLOW_REC_DTYPE).reshape(F)

@@ -1,6 +1,6 @@
 """Time the C5 merge (flodbadd_amd.distributed.global_flow_table) over RCCL at world size 1 on the
-device: the C4 10M-frame table (1.45M flows) exported, then merged (union, Ord sort, dense ids,
-all-reduces)."""
+device: the C4 10M-frame table (1.45M flows) exported into a device tensor (fb_flow_export_dev),
+then merged (union, Ord sort, dense ids, all-reduces, records assembled on the device)."""
 import os
 import sys
 import time
@@ -23,7 +23,15 @@ for n in (1 << 20, 10 << 20):
     frames, offs = synth.generate(4, n, first=1)
     cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 21)
     cap.process_frames(frames, offs)
-    flows = cap.export_flows()
+    import ctypes as C
+    from flodbadd_amd import _native as N
+    cnt = C.c_uint64()
+    N.check(N.gpu_lib().fb_flow_count(cap.ctx, C.byref(cnt), None))
+    flows = torch.empty((cnt.value, N.FLOW_REC_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(1, dtype=torch.int64, device=dev)
+    N.check(N.gpu_lib().fb_flow_export_dev(cap.ctx, C.c_void_p(flows.data_ptr()), cnt.value,
+                                           C.c_void_p(d_n.data_ptr()), None))
+    torch.cuda.synchronize()
     for rep in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
