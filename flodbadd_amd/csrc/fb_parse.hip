@@ -738,6 +738,10 @@ constexpr int kDnWaves = FB_DN_WAVES;
 constexpr int kDnSegs = FB_DN_SEGS;  // segments per wave per tile (records held in registers)
 constexpr uint32_t kDnTileSegs = kDnWaves * kDnSegs;
 constexpr int kDnThreads = 64 * kDnWaves;
+#ifndef FB_DN_LB
+#define FB_DN_LB 1
+#endif
+constexpr int kDnLb = FB_DN_LB;  // look-back: status words per lane per step
 // tile status word [epoch:8 | P:1 | A:1 | n_dns:27 | n_session:27]: A = the tile's own sums are
 // published, P = its inclusive prefix is (k_seg_scan's format)
 constexpr unsigned long long kDnA = 1ull << 54, kDnP = 1ull << 55, kDn27 = (1ull << 27) - 1ull;
@@ -852,53 +856,91 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
 #pragma unroll
             for (int k = 0; k < kDnWaves; ++k) agg += s_wsum[par][k];
             unsigned long long excl = 0ull;
+#ifdef FB_DN_FAKE_LB
+            if (false) {
+#else
             if (t == 0u) {
+#endif
                 if (lane == 0u) __hip_atomic_store(P.dstatus, dn_word(ep, kDnP, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
+            } else
+#ifdef FB_DN_FAKE_LB
+            if (false)
+#endif
+            {
                 if (lane == 0u)
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnA, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                int64_t jt = (int64_t)t;  // window: tiles jt-1-lane
+                // window of 64 x kDnLb tiles per step: lane l holds tiles jt-1-(l*kDnLb+k), k < kDnLb.
+                // A step waits only for the words in front of the nearest published inclusive prefix
+                // (P) it can see -- words behind it are not needed -- and walks on when there is none.
+                int64_t jt = (int64_t)t;
+                auto ready = [&](unsigned long long x) { return (uint32_t)(x >> 56) == ep && (x & (kDnA | kDnP)); };
                 for (;;) {
-                    const int64_t idx = jt - 1 - (int64_t)lane;
-                    auto probe = [&]() {
+                    auto probe = [&](int k) {
+                        const int64_t idx = jt - 1 - (int64_t)(lane * (uint32_t)kDnLb + (uint32_t)k);
                         return idx >= 0 ? __hip_atomic_load(P.dstatus + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                         : dn_word(ep, kDnP, 0ull);
                     };
-                    auto ready = [&](unsigned long long x) { return (uint32_t)(x >> 56) == ep && (x & (kDnA | kDnP)); };
-                    unsigned long long v = probe();
+                    unsigned long long v[kDnLb];
+#pragma unroll
+                    for (int k = 0; k < kDnLb; ++k) v[k] = probe(k);
+                    uint32_t sl = 64u, kp = 0u;  // the nearest P: its lane and word (sl 64: none)
                     for (uint32_t spins = 0u;; ++spins) {
-                        unsigned long long late = __ballot(!ready(v));
+                        uint32_t kpl = kDnLb;
+#pragma unroll
+                        for (int k = kDnLb - 1; k >= 0; --k) kpl = (ready(v[k]) && (v[k] & kDnP)) ? (uint32_t)k : kpl;
+                        const unsigned long long pm = __ballot(kpl < (uint32_t)kDnLb);
+                        sl = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+                        kp = pm ? (uint32_t)__shfl((int)kpl, (int)sl, 64) : 0u;
+                        uint32_t need = 0u;  // unpublished words in front of it
+#pragma unroll
+                        for (int k = 0; k < kDnLb; ++k)
+                            need |= ((lane < sl || (lane == sl && (uint32_t)k < kp)) && !ready(v[k])) ? 1u << k : 0u;
+                        unsigned long long late = __ballot(need != 0u);
                         if (late == 0ull) break;
                         if (spins >= P.steal_polls) {
                             // the owners of these tiles may not be running: compute their sums here
                             while (late) {
                                 const uint32_t l = (uint32_t)__builtin_ctzll(late);
                                 late &= late - 1ull;
-                                const uint32_t j = (uint32_t)(jt - 1 - (int64_t)l);
-                                const unsigned long long w = dn_word(ep, kDnA, tile_pair(j));
-                                if (lane == l) {
-                                    atomicCAS(P.dstatus + j, v, w);  // unless the owner published meanwhile
-                                    v = w;
+                                uint32_t nk = (uint32_t)__shfl((int)need, (int)l, 64);
+                                while (nk) {
+                                    const uint32_t kk = (uint32_t)__builtin_ctz(nk);
+                                    nk &= nk - 1u;
+                                    const uint32_t j = (uint32_t)(jt - 1 - (int64_t)(l * (uint32_t)kDnLb + kk));
+                                    const unsigned long long w = dn_word(ep, kDnA, tile_pair(j));
+#pragma unroll
+                                    for (int k = 0; k < kDnLb; ++k) {
+                                        if (lane == l && (uint32_t)k == kk) {
+                                            atomicCAS(P.dstatus + j, v[k], w);  // unless the owner published meanwhile
+                                            v[k] = w;
+                                        }
+                                    }
                                 }
                             }
                             break;
                         }
                         __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
-                        if (!ready(v)) v = probe();
+#pragma unroll
+                        for (int k = 0; k < kDnLb; ++k)
+                            if (!ready(v[k])) v[k] = probe(k);
                     }
-                    const unsigned long long pm = __ballot((v & kDnP) != 0ull);
-                    const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;  // nearest inclusive
-                    unsigned long long part = lane <= stop ? dn_pair(v) : 0ull;
+                    unsigned long long part = 0ull;
+#pragma unroll
+                    for (int k = 0; k < kDnLb; ++k)
+                        part += (lane < sl || (lane == sl && (uint32_t)k <= kp)) ? dn_pair(v[k]) : 0ull;
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
                     excl += part;
-                    if (pm) break;
-                    jt -= 64;
+                    if (sl < 64u) break;
+                    jt -= 64 * kDnLb;
                 }
                 if (lane == 0u)
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnP, excl + agg), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
+#ifdef FB_DN_FAKE_LB  // timing-only ablation: no look-back wait, each tile at a disjoint fake offset
+            excl = (unsigned long long)t * (kDnTileSegs * 64u) * 0x100000001ull;
+#endif
             if (lane == 0u) s_excl = excl;
         }
         lds_barrier();
