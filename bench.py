@@ -401,11 +401,15 @@ def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
                      "(compute stream) + stats D2H per batch, table kept in HBM" % slots)
 
 
-def c5_flow_reduce(N, lib, ctx, frames, offs, dist, group, device, shard_first):
-    """BASELINE config C5's exchange after the timed region: this rank's shard through the fused
-    parse + classify + flow-table kernel, then the global per-flow counter merge
-    (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce SUM over RCCL)."""
+def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
+    """BASELINE config C5 after the timed region: rank r's shard of a world x per_rank frame batch
+    (C4 mix, flow pool 2^20; packets [r * per_rank, (r+1) * per_rank)) through the fused parse +
+    classify + session-table kernels, then the global per-flow counter merge
+    (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce over RCCL)."""
+    from flodbadd_amd import synth
     from flodbadd_amd.distributed import global_flow_table
+    shard_first = rank * per_rank
+    frames, offs = synth.generate(4, per_rank, first=shard_first)
     n = len(offs) - 1
     N.check(lib.fb_flow_clear(ctx, None))
     d_fr = N.DeviceBuffer(frames.nbytes).upload(frames)
@@ -413,6 +417,9 @@ def c5_flow_reduce(N, lib, ctx, frames, offs, dist, group, device, shard_first):
     d_out = N.DeviceBuffer(n * N.PKT_OUT_DTYPE.itemsize)
     d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
     ev0, ev1 = N.Event(), N.Event()
+    # once untimed (grows the context's update scratch to the shard), then the timed update
+    N.check(lib.fb_process_dev(ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, None, None, d_st.ptr, None))
+    N.check(lib.fb_flow_clear(ctx, None))
     ev0.record(None)
     N.check(lib.fb_process_dev(ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, None, None, d_st.ptr, None))
     ev1.record(None)
@@ -437,7 +444,14 @@ def c5_flow_reduce(N, lib, ctx, frames, offs, dist, group, device, shard_first):
     el = time.perf_counter() - t0
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
-    return dict(local_flows=local, global_flows=int(len(merged)), flow_update_ms=round(flow_ms, 3),
+    t = np.array([flow_ms], dtype=np.float64)
+    if world > 1:  # the slowest rank's update: the aggregate rate of the concurrent shards
+        import torch
+        tt = torch.tensor(t, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        t = tt.cpu().numpy()
+    return dict(frames_per_rank=n, total_frames=n * world, local_flows=local, global_flows=int(len(merged)),
+                flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3),
                 note="per-rank fused parse+flow upsert of the rank's shard, then the table exported (to a device "
                      "tensor with RCCL) and merged: all-gather of keys, device sort -> dense ids, all-reduces")
@@ -514,6 +528,8 @@ def main():
     ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C3) measurement")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (pinned H2D/D2H) measurement")
     ap.add_argument("--no-flow-reduce", action="store_true", help="N>1: skip the C5 global flow-counter exchange")
+    ap.add_argument("--c5-frames", type=int, default=10 * (1 << 20),
+                    help="N>1: frames per rank of the C5 shard (BASELINE configs[4]: 80M over 8 GPUs)")
     ap.add_argument("--mode", choices=["seg", "dense"], default="seg",
                     help="output layout: per-wavefront segments (default) or one batch-wide compaction")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
@@ -656,8 +672,7 @@ def main():
             if backend == "nccl":
                 torch.cuda.set_device(dev)
             g = tdist.new_group(backend=backend)
-            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, main_r["frames"], main_r["offs"], tdist, g, dev,
-                                                     rank * n)
+            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, args.c5_frames, rank, world, tdist, g, dev)
             extra["c5_flow_reduce"]["backend"] = "rccl" if backend == "nccl" else backend
         except Exception as e:  # the exchange is reported, never allowed to break the bench line
             extra["c5_flow_reduce"] = {"error": repr(e)[:300]}

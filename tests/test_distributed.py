@@ -41,6 +41,9 @@ def _worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         flows, first = _rank_flows(rank, world)
+        if rank == 1:  # the device-tensor input form (fb_flow_export_dev records), on the CPU here
+            import torch
+            flows = torch.from_numpy(flows.view(np.uint8).reshape(len(flows), N.FLOW_REC_DTYPE.itemsize).copy())
         merged = global_flow_table(dist, flows, shard_first=first)
         np.save(os.path.join(outdir, "r%d.npy" % rank), merged.view(np.uint8))
     finally:
