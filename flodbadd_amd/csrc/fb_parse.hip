@@ -812,11 +812,16 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
         }
         return acc;
     };
-    for (uint32_t t = b; t < nt; t += G) {
-        const uint32_t sg0 = t * kDnTileSegs + wave * (uint32_t)kDnSegs;
-        Hdr h[kDnSegs];
+    // the current tile's headers: loaded here for the first tile, then during the previous tile's
+    // look-back and stores (issued right after its first barrier), so a tile starts on headers
+    // that are already in registers
+    Hdr h[kDnSegs];
+    if (b < nt) {
 #pragma unroll
         for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, q[j].x, h[j]);
+    }
+    for (uint32_t t = b; t < nt; t += G) {
+        const uint32_t sg0 = t * kDnTileSegs + wave * (uint32_t)kDnSegs;
         uint2 qn[kDnSegs];
         load_offsets(t + G, qn);
         Pkt kk[kDnSegs];
@@ -851,6 +856,10 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
         }
         if (lane == 0u) s_wsum[par][wave] = ws;
         lds_barrier();
+        if (t + G < nt) {  // the next tile's headers, in flight through the look-back and the stores
+#pragma unroll
+            for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, qn[j].x, h[j]);
+        }
         if (wave == 0u) {
             unsigned long long agg = 0ull;
 #pragma unroll
