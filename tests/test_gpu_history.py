@@ -180,7 +180,7 @@ def test_history_combine_table_overflow():
     groups = {}
     for i in range(len(recs)):
         h = lib.fb_flow_hash(N.ptr(recs[i: i + 1]))
-        groups.setdefault((i // 16384, h >> 59), []).append(recs[i: i + 1].tobytes()[:40])
+        groups.setdefault((i // 20480, h >> 59), []).append(recs[i: i + 1].tobytes()[:40])
     assert max(len(set(v)) for v in groups.values() if len(v) >= 2048) > 256
     gf = _run(batches, capacity=1 << 14)
     assert (gf["hist_len"] > 10000).sum() == 1
