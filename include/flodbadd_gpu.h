@@ -264,8 +264,10 @@ int fb_set_stage_event(fb_ctx* ctx, void* event);
  *   d_dns   : >= n fb_dns_out, class-DNS records, packet order
  *   d_class : n bytes, fb_class of every frame
  *   d_stats : one fb_batch_stats (overwritten, not accumulated)
- * Runs the segmented kernel into context scratch, then fb_seg_compact_dev's compaction: no
- * kernel waits on another workgroup, so the call is safe on a GPU shared with other work.
+ * One pass (k_parse_dense): 1,024-frame tiles whose batch-wide offsets come from a decoupled
+ * look-back; a look-back that finds a predecessor tile unpublished for long computes that tile's
+ * counts itself instead of waiting on it, so the call never depends on every workgroup being
+ * resident and is safe on a GPU shared with other work.
  */
 int fb_parse_classify_dev(fb_ctx* ctx, const uint8_t* d_frames, uint64_t frames_bytes,
                           const uint32_t* d_offsets, uint32_t n, fb_pkt_out* d_out,
