@@ -536,7 +536,7 @@ def main():
     ap.add_argument("--no-single-launch", action="store_true", help="skip timing one batch per launch")
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
-                         "default = the rotated batches (C2 32, C3 12), 1 for C4")
+                         "default = the rotated batches (C2 / C3 32), 1 for C4")
     ap.add_argument("--c4-sync", action="store_true",
                     help="C4: time fb_process_seg_dev (one stream) instead of the pipelined fb_process_seg_async_dev")
     ap.add_argument("--zipf", type=float, default=None,
@@ -570,12 +570,12 @@ def main():
     ctx = C.c_void_p(ctx)
 
     n = args.packets or (10 * (1 << 20) if args.config == 4 else 1 << 20)
-    # C2: 32 distinct batches (4 GB, far past the 256 MB Infinity Cache), so any K <= 32 steps is
-    # one launch and longer runs are near-equal launches of up to 32 batches (plan_launches)
+    # C2 / C3: 32 distinct batches (4 / 12 GB, far past the 256 MB Infinity Cache), so any K <= 32
+    # steps is one launch and longer runs are near-equal launches of up to 32 batches (plan_launches)
     # C4 (segmented): the pipelined fused call, each batch's table update overlapping the next
     # batch's parse, on two rotating buffer sets; --c4-sync times fb_process_seg_dev instead
     pipe = args.config == 4 and args.mode == "seg" and not args.c4_sync
-    rotate = args.rotate or (32 if args.config == 2 else (12 if args.config == 3 else (2 if pipe else 1)))
+    rotate = args.rotate or (32 if args.config in (2, 3) else (2 if pipe else 1))
     bpl = min(args.batches_per_launch or rotate, rotate, MAX_SEG_BATCHES) \
         if (args.mode == "seg" and args.config != 4) else 1
     main_kw = dict(zipf=1, zipf_s=args.zipf) if args.zipf else None
@@ -643,8 +643,8 @@ def main():
                                       roofline_frac=round(ro["algo_bytes"] / plo / 1e9 / HBM_PEAK_GBS, 4))
     if not args.no_imix and args.config == 2:
         steps3 = max(args.steps // 2, 10)
-        bpl3 = 12 if args.mode == "seg" and bpl > 1 else 1
-        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 12, rank, world, dist,
+        bpl3 = 32 if args.mode == "seg" and bpl > 1 else 1
+        r3 = run_config(N, lib, ctx, 3, 1 << 20, steps3, max(args.warmup // 2, 2), 32, rank, world, dist,
                         mode=args.mode, bpl=bpl3)
         pl3 = r3["ev_ms"] / 1e3 / r3["launches"]
         algo3 = r3["algo_bytes"] * steps3 / r3["launches"]
