@@ -315,6 +315,9 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #ifndef FB_SEG_DEPTH
 #define FB_SEG_DEPTH 1
 #endif
+#ifndef FB_SEG_PRIO
+#define FB_SEG_PRIO 0
+#endif
 constexpr int kSegWaves = FB_SEG_WAVES;
 constexpr int kSegDepth = FB_SEG_DEPTH;  // segments of header loads in flight per wave
 constexpr int kSegThreads = 64 * kSegWaves;
@@ -544,8 +547,14 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             if constexpr ((FLAGS & kDense) != 0u) pw = PARSED ? ppre : X.p;
             // prefetch: headers of this set's next segment (offsets already here), offsets of the
             // one after
+#if FB_SEG_PRIO  // experiment: the next segment's loads issued at raised wave priority
+            __builtin_amdgcn_s_setprio(FB_SEG_PRIO);
+#endif
             if constexpr (!PARSED) fetch(X, g_next, g_after);
             else load_parsed(g_next);
+#if FB_SEG_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             if constexpr ((FLAGS & kCountOnly) != 0u) {
                 // dense pass 1: the count word and the class only
                 const __amdgpu_buffer_rsrc_t r_seg =
