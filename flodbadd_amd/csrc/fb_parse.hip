@@ -1,6 +1,6 @@
-// fb_parse.hip -- gfx950 parse + classify kernel k_parse_seg (streaming, per-wavefront
-// compaction into 64-frame output segments).  Batch-wide (dense) output is the same launch
-// followed by the segment compaction of fb_compact.hip.
+// fb_parse.hip -- gfx950 parse + classify kernels: k_parse_seg (streaming, per-wavefront
+// compaction into 64-frame output segments; also the two passes of the parsed-packet dense path)
+// and k_parse_dense (single-pass batch-wide output of a frame batch, decoupled look-back).
 //
 // One wavefront lane per frame.  Replaces, per frame:
 //   parse_packet_pcap                 src/packets.rs:603-802 (pnet_packet 0.35.0 decode)
