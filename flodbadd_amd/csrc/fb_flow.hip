@@ -286,7 +286,7 @@ constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 #define FB_K2_CPT 2
 #endif
 constexpr uint32_t kK2Cpt = FB_K2_CPT;
-// (kK2Cpt: bucketing chunks per K2 thread and round; C4: 640 chunks, one round)
+// (kK2Cpt: bucketing chunks per K2 thread and round; C4: 512 chunks, one round)
 // scratch words
 constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
 
