@@ -359,7 +359,10 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         int sb = 0;
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
-        c->seg_grid_async = std::min<uint32_t>((uint32_t)prop.multiProcessorCount, c->seg_grid);
+#ifndef FB_ASYNC_BPC
+#define FB_ASYNC_BPC 1
+#endif
+        c->seg_grid_async = std::min<uint32_t>((uint32_t)(FB_ASYNC_BPC * prop.multiProcessorCount), c->seg_grid);
         int db = 0;
         if (occupancy_parse_dense(&db) != hipSuccess || db < 1) db = 1;
         c->dense_grid = std::min<uint32_t>((uint32_t)(db * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
