@@ -465,13 +465,51 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                      "tensor with RCCL) and merged: all-gather of keys, device sort -> dense ids, all-reduces")
 
 
+def usable_cores():
+    """Host cores this process may use: the CPU affinity set, capped by the cgroup CPU quota (the
+    GPU box's CPU share) and by OMP_NUM_THREADS when the harness sets it to that share.  Returns
+    (cores, how it was decided)."""
+    aff = len(os.sched_getaffinity(0))
+    n, why = aff, "sched_getaffinity %d" % aff
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+            why += ", cgroup cpu.max quota %d" % quota
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < n:
+        why += ", OMP_NUM_THREADS %s (the box's CPU share for one GPU)" % omp
+        n = int(omp)
+    return n, why
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        return ""
+
+
+def _timed_passes(fn, budget):
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget:
+            return passes, el
+
+
 def cpu_baseline(frames, offs, seconds):
     """The oracle (C restatement of src/packets.rs parse + classify) on the same batch, repeated
     for about `seconds` of wall time: a bounded sample of the same workload.  SURVEY.md 8d asks for
     (i) one thread, like the reference's one processor task per interface (src/capture.rs:1027),
     and (ii) all host cores: the main object is (ii) (orc_parse_classify_mt, contiguous ranges in
-    parallel, compacted in packet order; `cores` = the threads used: OMP_NUM_THREADS, 16 on the
-    GPU box), with (i) beside it."""
+    parallel, compacted in packet order; `cores` = usable_cores()), with (i) beside it."""
     from oracle import coracle
     cfg = coracle.make_cfg(1)  # FlodbaddCapture::new() default filter: GlobalOnly
     n = len(offs) - 1
@@ -480,34 +518,49 @@ def cpu_baseline(frames, offs, seconds):
     st = np.zeros(1, dtype=coracle.STATS_DTYPE)
     no, nd = C.c_uint32(), C.c_uint32()
     L = coracle.lib()
-    threads = int(os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 1, 16))
+    threads, why = usable_cores()
 
-    def run(t, budget):
-        passes, t0 = 0, time.perf_counter()
-        while True:
-            if t == 1:
-                L.orc_parse_classify(C.byref(cfg), frames.ctypes.data, frames.nbytes, offs.ctypes.data, n,
-                                     out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), None, st.ctypes.data)
-            else:
-                L.orc_parse_classify_mt(C.byref(cfg), frames.ctypes.data, frames.nbytes, offs.ctypes.data, n,
-                                        out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), st.ctypes.data, t)
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= budget:
-                return passes, el
-    p1, e1 = run(1, seconds / 2)
-    pm, em = run(threads, seconds / 2)
-    cpu_model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
-    except OSError:
-        pass
+    def run(t):
+        if t == 1:
+            L.orc_parse_classify(C.byref(cfg), frames.ctypes.data, frames.nbytes, offs.ctypes.data, n,
+                                 out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), None, st.ctypes.data)
+        else:
+            L.orc_parse_classify_mt(C.byref(cfg), frames.ctypes.data, frames.nbytes, offs.ctypes.data, n,
+                                    out.ctypes.data, C.byref(no), dns.ctypes.data, C.byref(nd), st.ctypes.data, t)
+    p1, e1 = _timed_passes(lambda: run(1), seconds / 2)
+    pm, em = _timed_passes(lambda: run(threads), seconds / 2)
     return dict(value=round(pm * n / em / 1e6, 3), unit="Mpackets/s", cores=threads, kind="port",
+                cores_rule=why,
                 sample="%d passes over the %d-frame batch (%.1f s, %d threads, C restatement oracle/oracle.c, %s)"
-                       % (pm, n, em, threads, cpu_model),
+                       % (pm, n, em, threads, _cpu_model()),
                 single_thread=dict(value=round(p1 * n / e1 / 1e6, 3), cores=1,
                                    sample="%d passes (%.1f s, 1 thread)" % (p1, e1)))
+
+
+def cpu_baseline_c4(frames, offs, seconds):
+    """C4 CPU baseline: parse + classify + the session-table upsert (orc_pipeline_mt: ranges
+    parsed in parallel, then every thread upserts the keys it owns, in packet order, into its own
+    table; orc_pipeline for one thread) on a bounded sample: the first 2M frames of the C4 batch,
+    each pass into fresh tables (the GPU's timed steps update a warm table: the CPU passes after
+    the first do the same, tables are cleared only between the two thread counts)."""
+    from oracle import coracle
+    cfg = coracle.make_cfg(1)
+    m = min(len(offs) - 1, 1 << 21)
+    o = np.ascontiguousarray(offs[: m + 1])
+    threads, why = usable_cores()
+    L = coracle.lib()
+    scratch = np.zeros(m, dtype=coracle.PKT_OUT_DTYPE)
+    st = np.zeros(1, dtype=coracle.STATS_DTYPE)
+    one = coracle.Flows()
+    p1, e1 = _timed_passes(lambda: L.orc_pipeline(C.byref(cfg), one.h, frames.ctypes.data, frames.nbytes,
+                                                  o.ctypes.data, m, scratch.ctypes.data, st.ctypes.data), seconds / 2)
+    tabs = [coracle.Flows() for _ in range(threads)]
+    pm, em = _timed_passes(lambda: coracle.pipeline_mt(cfg, frames, o, threads, tabs), seconds / 2)
+    return dict(value=round(pm * m / em / 1e6, 3), unit="Mpackets/s", cores=threads, kind="port", cores_rule=why,
+                sample="%d passes over the first %d frames of the C4 batch, parse + classify + session upsert "
+                       "(%.1f s, %d threads, oracle/oracle.c orc_pipeline_mt, %s)" % (pm, m, em, threads, _cpu_model()),
+                single_thread=dict(value=round(p1 * m / e1 / 1e6, 3), cores=1,
+                                   sample="%d passes (%.1f s, 1 thread, orc_pipeline)" % (p1, e1)))
 
 
 def load_traffic(config_id, bpl=1):
@@ -523,6 +576,64 @@ def load_traffic(config_id, bpl=1):
         return None
 
 
+def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pipe, synth_kw=None):
+    """The C4 step's parse / update split: for the pipelined line a one-stream fb_process_seg_dev run
+    (fewer steps) whose stage event splits each step; plus the side timings the C4 main run took
+    (history, enrichment, DNS parse)."""
+    extra = {}
+    sg = main_r["stage"]
+    split = sg
+    if pipe:  # the stage split and the one-stream rate from fb_process_seg_dev, fewer steps
+        st_s = max(steps // 2, 10)
+        rs = run_config(N, lib, ctx, 4, n, st_s, max(warmup // 2, 2), 1, rank, world, dist, flow=True,
+                        mode=mode, synth_kw=synth_kw, stage_extras=False)
+        split = rs["stage"]
+        extra["c4_sync"] = dict(value=round(world * n * st_s / rs["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                                ms_per_step=round(rs["elapsed"] * 1e3 / st_s, 4),
+                                note="fb_process_seg_dev: parse then update on one stream, no overlap")
+    extra["c4_stages"] = dict(parse_ms=round(split["parse_ms"], 4), flow_update_ms=round(split["flow_ms"], 4),
+                              stages_note="split by the stage event fb_process%s_dev records between its "
+                                          "parse and its update%s" % ("_seg" if mode == "seg" else "",
+                                                                      " (one-stream run)" if pipe else ""),
+                              history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
+                              enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
+                              enrich_tables=sg["enrich_tables"],
+                              dns_parse_ms=sg["dns_parse_ms"], dns_Mmsgs_s=sg["dns_Mmsgs_s"],
+                              dns_payload_GBs=sg["dns_payload_GBs"], dns_ok=sg["dns_ok"],
+                              dns_workload="1M port-53 payloads (synth.dns_workload), device-resident",
+                              flows_in_table=sg["flows"],
+                              parse_GBs=round(main_r["algo_bytes"] / split["parse_ms"] / 1e6, 1),
+                              flow_Mrec_s=round(main_r["stats"]["n_session"] / split["flow_ms"] / 1e3, 1))
+    return extra
+
+
+def c4_algo_bytes(r):
+    """Algorithmic bytes of one C4 step: the parse's (header windows, offsets,
+    records written) + the update's: every SESSION record read once (56 B) and every flow's 128-B
+    table slot read and written once."""
+    return r["algo_bytes"] + 56 * r["stats"]["n_session"] + 2 * 128 * r["stage"]["flows"]
+
+
+def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
+    """BASELINE configs[3] (C4) as an extra of the default run, so the driver times it: 10,485,760
+    IMIX frames per step through the pipelined fused call (fb_process_seg_async_dev, two rotating
+    buffer sets, joined inside the timed region), its parse / update split, the step's algorithmic
+    bytes against HBM peak, and the CPU parse + upsert baseline beside it."""
+    n = 10 * (1 << 20)
+    r = run_config(N, lib, ctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg", pipelined=True)
+    out = dict(value=round(world * n * steps / r["elapsed"] / 1e6, 2), unit="Mpackets/s",
+               ms_per_step=round(r["elapsed"] * 1e3 / steps, 4), steps=steps, warmup=warmup,
+               workload=WORKLOADS[4], output="fb_process_seg_async_dev (pipelined parse + session upsert)")
+    ach = c4_algo_bytes(r) * steps / (r["ev_ms"] / 1e3) / 1e9
+    out["roofline"] = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                           frac=round(ach / HBM_PEAK_GBS, 4), algo_bytes_per_step=int(c4_algo_bytes(r)),
+                           note="whole step (parse + update, overlapped) over its algorithmic bytes")
+    out.update(c4_split(N, lib, ctx, r, n, steps, warmup, rank, world, dist, "seg", True))
+    if rank == 0 and world == 1 and cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline_c4(r["frames"], r["offs"], cpu_seconds)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -534,6 +645,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C3) measurement")
+    ap.add_argument("--no-c4", action="store_true", help="config 2: skip the C4 (parse + session table) extra")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (pinned H2D/D2H) measurement")
     ap.add_argument("--no-flow-reduce", action="store_true", help="N>1: skip the C5 global flow-counter exchange")
     ap.add_argument("--c5-frames", type=int, default=10 * (1 << 20),
@@ -598,29 +710,8 @@ def main():
 
     extra = {}
     if main_r["stage"]:
-        sg = main_r["stage"]
-        split = sg
-        if pipe:  # the stage split and the one-stream rate from fb_process_seg_dev, fewer steps
-            st_s = max(args.steps // 2, 10)
-            rs = run_config(N, lib, ctx, 4, n, st_s, max(args.warmup // 2, 2), 1, rank, world, dist, flow=True,
-                            mode=args.mode, synth_kw=main_kw, stage_extras=False)
-            split = rs["stage"]
-            extra["c4_sync"] = dict(value=round(world * n * st_s / rs["elapsed"] / 1e6, 2), unit="Mpackets/s",
-                                    ms_per_step=round(rs["elapsed"] * 1e3 / st_s, 4),
-                                    note="fb_process_seg_dev: parse then update on one stream, no overlap")
-        extra["c4_stages"] = dict(parse_ms=round(split["parse_ms"], 4), flow_update_ms=round(split["flow_ms"], 4),
-                                  stages_note="split by the stage event fb_process%s_dev records between its "
-                                              "parse and its update%s" % ("_seg" if args.mode == "seg" else "",
-                                                                          " (one-stream run)" if pipe else ""),
-                                  history_ms=round(sg["history_ms"], 4), history_chars=sg["history_chars"],
-                                  enrich_ms=sg["enrich_ms"], enrich_Mflows_s=sg["enrich_Mflows_s"],
-                                  enrich_tables=sg["enrich_tables"],
-                                  dns_parse_ms=sg["dns_parse_ms"], dns_Mmsgs_s=sg["dns_Mmsgs_s"],
-                                  dns_payload_GBs=sg["dns_payload_GBs"], dns_ok=sg["dns_ok"],
-                                  dns_workload="1M port-53 payloads (synth.dns_workload), device-resident",
-                                  flows_in_table=sg["flows"],
-                                  parse_GBs=round(main_r["algo_bytes"] / split["parse_ms"] / 1e6, 1),
-                                  flow_Mrec_s=round(main_r["stats"]["n_session"] / split["flow_ms"] / 1e3, 1))
+        extra.update(c4_split(N, lib, ctx, main_r, n, args.steps, args.warmup, rank, world, dist, args.mode, pipe,
+                              main_kw))
     if args.config == 4 and not args.no_other_mode:  # C4 also with Zipf(1.1) flow popularity
         rz = run_config(N, lib, ctx, 4, n, max(args.steps // 2, 5), max(args.warmup // 2, 2), rotate, rank, world,
                         dist, flow=True, mode=args.mode, synth_kw=dict(zipf=1, zipf_s=1.1))
@@ -662,6 +753,9 @@ def main():
                                 roofline_frac=round(algo3 / pl3 / 1e9 / HBM_PEAK_GBS, 4),
                                 batches_per_launch=bpl3, algo_bytes_per_batch=r3["algo_bytes"])
 
+    if args.config == 2 and not args.no_c4:  # BASELINE configs[3] in the default (driver-timed) run
+        extra["c4"] = c4_line(N, lib, ctx, max(args.steps // 10, 20), 5, rank, world, dist,
+                              0 if args.no_cpu_baseline else args.cpu_seconds / 2)
     if not args.no_host and rank == 0 and args.config == 2:
         extra["host_inclusive_c2"] = host_inclusive(N, lib, ctx, main_r["frames"], main_r["offs"])
         try:

@@ -12,7 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 GPU_LIB_PATH = os.environ.get("FLODBADD_GPU_LIB") or os.path.join(PKG, "libflodbadd_gpu.so")  # override: tools/
 SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
 
-FB_ABI_VERSION = 2
+FB_ABI_VERSION = 3
 FB_MAX_BATCH_PACKETS = (1 << 27) - 1
 FB_MAX_LAN_V6 = 64
 FB_MAX_OWN_IPS = 64
@@ -45,7 +45,9 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
     ("outbound_bytes", "<u8"), ("inbound_bytes", "<u8"), ("orig_pkts", "<u8"), ("resp_pkts", "<u8"),
     ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8"),
     ("first_seen", "<u8"), ("last_seen", "<u8"), ("end_seen", "<u8"), ("hist_len", "<u4"),
-    ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("reserved1", "<u4")])
+    ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("session_flags", "<u4")])
+# fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst at insert)
+SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST = 1, 2, 4, 8
 # fb_flow_rec positions: (update call << 32) | pkt_index; FB_SEEN_NONE = None
 FB_SEEN_NONE = (1 << 64) - 1
 FB_HIST_CHARS = "SsHhFfRr><Aa-"
@@ -171,6 +173,8 @@ GPU_SYMBOLS = [
     ("fb_flow_count", _I, [_P, _PU64, _P]),
     ("fb_flow_export", _I, [_P, _P, _U64, _PU64, _P]),
     ("fb_flow_export_dev", _I, [_P, _P, _U64, _P, _P]),
+    ("fb_flow_export_sessions", _I, [_P, _U32, _P, _U64, _PU64, _P]),
+    ("fb_flow_export_sessions_dev", _I, [_P, _U32, _P, _U64, _P, _P]),
     ("fb_flow_clear", _I, [_P, _P]),
     ("fb_flow_hash", _U64, [_P]),
     ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),

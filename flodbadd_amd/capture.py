@@ -222,16 +222,19 @@ class FlodbaddGpuCapture:
         N.check(N.gpu_lib().fb_flow_count(self.ctx, C.byref(n), None))
         return n.value
 
-    def export_flows(self):
+    def export_flows(self, session_filter=SessionFilter.All):
+        """fb_flow_export_sessions: every flow (All), or those passing the filter evaluated now."""
         cnt = self.flow_count()
         out = np.zeros(max(cnt, 1), dtype=N.FLOW_REC_DTYPE)
         n = C.c_uint64(0)
-        N.check(N.gpu_lib().fb_flow_export(self.ctx, N.ptr(out), cnt, C.byref(n), None))
+        N.check(N.gpu_lib().fb_flow_export_sessions(self.ctx, int(session_filter), N.ptr(out), cnt, C.byref(n), None))
         return out[: n.value]
 
-    def get_sessions(self, is_lan=None):
-        """Sessions sorted by the derived Ord of Session (integer counters + derived f64s)."""
-        return flows_to_sessions(self.export_flows(), is_lan, self.histories if self.track_history else None)
+    def get_sessions(self):
+        """get_sessions (src/capture.rs:1578-1612): the sessions that pass the CURRENT filter,
+        is_local_session! evaluated at query time on the GPU (capture.rs:1603-1608), sorted by the
+        derived Ord of Session (integer counters + derived f64s)."""
+        return flows_to_sessions(self.export_flows(self.filter), self.histories if self.track_history else None)
 
     # ---- new-session enrichment (src/packets.rs:429-485) -------------------------------------
     def set_asn_tables(self, v4, v6):

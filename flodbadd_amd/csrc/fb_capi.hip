@@ -93,6 +93,7 @@ struct fb_ctx {
     uint64_t async_k = 0;                       // async batches issued
     uint32_t* d_rec_part2 = nullptr;            // partitions of the odd async batches
     const void* async_prev[3] = {nullptr, nullptr, nullptr};  // the last async batch's records, counts, stats
+    uint32_t upd_word[2] = {4u, 4u};            // error word (launch & 3) of the async update in slot k & 1 (4: none)
     uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* d_comb_ctl = nullptr;       // [2] its counters
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
@@ -134,7 +135,8 @@ int fbk::ctx_device(const fb_ctx* c) { return c->device; }
 int fbk::ctx_report_error(fb_ctx* c, uint64_t e) {
     c->need_reset = true;
     if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full (error word %llu)", (unsigned long long)e);
-    return set_err(FB_ERR_INTERNAL, "device error word %llu", (unsigned long long)e);
+    return set_err(FB_ERR_INTERNAL, "device error word %llu (2: offset scan expired, 8: update scratch "
+                   "overflow, 16: table-update spin expired)", (unsigned long long)e);
 }
 
 // Entry points that read or write the table or the update scratch first order their stream after
@@ -143,6 +145,16 @@ int fbk::ctx_report_error(fb_ctx* c, uint64_t e) {
 static int join_updates(fb_ctx* c, hipStream_t s) {
     if (c->async_k == 0) return FB_OK;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[(c->async_k - 1u) & 1u], 0));
+    return FB_OK;
+}
+// A parse launch zeroes the error word of the launch after it ((launch + 1) & 3).  A pipelined
+// update still in flight may own that word (it sets bits there and copies it into its stats at
+// the end): the stream waits for that update first, so no failure bit of it is lost.
+static int guard_next_error_word(fb_ctx* c, hipStream_t s) {
+    if (c->async_k == 0) return FB_OK;
+    const uint32_t z = (c->epoch + 2u) & 3u;
+    for (uint32_t k = 0; k < 2; ++k)
+        if (c->upd_word[k] == z) HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[k], 0));
     return FB_OK;
 }
 static int drain_updates(fb_ctx* c) {
@@ -524,6 +536,10 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
     c->part_buf = p.rec_part;
     p.cfg = c->d_cfg;
     p.tick = c->d_tick;
+    if (pass != SegPass::kDenseOut) {
+        rc = guard_next_error_word(c, s);
+        if (rc) return rc;
+    }
     // dense pass 2 belongs to pass 1's launch: same error word, no new parity
     const uint32_t launch = pass == SegPass::kDenseOut ? c->epoch : ++c->epoch;
     p.error = c->d_error + (launch & 3u);
@@ -671,6 +687,8 @@ static int parse_dense_single(fb_ctx* c, const uint8_t* d_frames, uint64_t frame
     memset(&p, 0, sizeof(p));
     p.cfg = c->d_cfg;
     p.tick = c->d_tick;
+    rc = guard_next_error_word(c, s);
+    if (rc) return rc;
     const uint32_t launch = ++c->epoch;
     p.error = c->d_error + (launch & 3u);
     p.error_next = c->d_error + ((launch + 1u) & 3u);
@@ -967,6 +985,7 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     c->part_recs = nullptr;
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_upd[slot], c->upd));
+    c->upd_word[slot] = c->epoch & 3u;  // the word flow_update handed this update
     c->async_prev[0] = d_out;
     c->async_prev[1] = d_seg;
     c->async_prev[2] = d_stats;
@@ -1140,26 +1159,33 @@ int fb_flow_count(fb_ctx* c, uint64_t* n_flows, void* stream) {
     return FB_OK;
 }
 
-int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n, void* stream) {
-    if (!c || !d_n || (cap && !d_out)) return set_err(FB_ERR_INVAL, "bad arguments");
+int fb_flow_export_sessions_dev(fb_ctx* c, uint32_t filter, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n,
+                                void* stream) {
+    if (!c || !d_n || (cap && !d_out) || filter > FB_FILTER_ALL) return set_err(FB_ERR_INVAL, "bad arguments");
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
     if (!c->d_table) return FB_OK;
-    const int rc = join_updates(c, s);
+    int rc = join_updates(c, s);
+    if (!rc && filter != FB_FILTER_ALL) rc = upload_cfg(c, s);  // the LAN configuration as of now
     if (rc) return rc;
-    HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s));
+    HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s, filter, c->d_cfg));
     return FB_OK;
 }
 
-int fb_flow_export(fb_ctx* c, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream) {
-    if (!c || !n || (cap && !out)) return set_err(FB_ERR_INVAL, "bad arguments");
+int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n, void* stream) {
+    return fb_flow_export_sessions_dev(c, FB_FILTER_ALL, d_out, cap, d_n, stream);
+}
+
+int fb_flow_export_sessions(fb_ctx* c, uint32_t filter, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream) {
+    if (!c || !n || (cap && !out) || filter > FB_FILTER_ALL) return set_err(FB_ERR_INVAL, "bad arguments");
     *n = 0;
     if (!c->d_table || cap == 0) return FB_OK;
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     uint64_t total = 0;
     int rc = fb_flow_count(c, &total, stream);
+    if (!rc && filter != FB_FILTER_ALL) rc = upload_cfg(c, s);
     if (rc) return rc;
     const uint64_t m = std::min(total, cap);
     if (m == 0) return FB_OK;
@@ -1167,14 +1193,20 @@ int fb_flow_export(fb_ctx* c, fb_flow_rec* out, uint64_t cap, uint64_t* n, void*
     if (hipMalloc(&d_out, m * sizeof(fb_flow_rec)) != hipSuccess) return set_err(FB_ERR_NOMEM, "export buffer");
     unsigned long long h = 0;
     hipError_t e = hipMemsetAsync(c->d_n, 0, 8, s);
-    if (e == hipSuccess) e = launch_flow_export(c->d_table, c->table_cap, d_out, m, c->d_n, s);
+    if (e == hipSuccess) e = launch_flow_export(c->d_table, c->table_cap, d_out, m, c->d_n, s, filter, c->d_cfg);
     if (e == hipSuccess) e = hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, m * sizeof(fb_flow_rec), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint64_t got = std::min<uint64_t>(h, m);
+    if (e == hipSuccess && got) e = hipMemcpyAsync(out, d_out, got * sizeof(fb_flow_rec), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     hipFree(d_out);
     if (e != hipSuccess) return set_err(FB_ERR_HIP, "flow export: %s", hipGetErrorString(e));
-    *n = std::min<uint64_t>(h, m);
+    *n = got;
     return FB_OK;
+}
+
+int fb_flow_export(fb_ctx* c, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream) {
+    return fb_flow_export_sessions(c, FB_FILTER_ALL, out, cap, n, stream);
 }
 
 int fb_flow_clear(fb_ctx* c, void* stream) {

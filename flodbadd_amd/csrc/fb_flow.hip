@@ -77,7 +77,8 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
 // Record slots of the batch: dense -> n_session of the parse launch (read on the device);
 // segmented -> every slot of every segment (invalid slots are skipped by slot_valid).
 __device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
-    // dense records whose look-back expired (error bit 2: offsets not trusted) never reach the table
+    // dense records whose offset scan expired (error bit 2, set only by k_seg_scan, which completes
+    // before K1 starts: every workgroup of K1 / K1c / K2 reads the same value) never reach the table
     if (!P.seg && (__hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return 0u;
     const unsigned long long n = P.seg ? (unsigned long long)P.n_slots : P.stats->n_session;
     return (uint32_t)min(n, (unsigned long long)P.max_recs);
@@ -95,7 +96,7 @@ constexpr uint32_t kCombMin = FB_COMB_MIN;
 
 // Record slot `rec` of the batch as the four uint4 of a plain FlowEntry (fb_internal.h): key words,
 // key word 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char |
-// tcp_flags << 8 | has_flags << 16, the low word of the key's hash.  Records are 56 B, so only 8-B
+// tcp_flags << 8 | has_flags << 16 | session flags << 20, the low word of the key's hash.  Records are 56 B, so only 8-B
 // aligned at odd slots: loaded through ld_u4 / ld_u2.
 __device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, uint4 (&e)[4]) {
     const uint32_t* r = reinterpret_cast<const uint32_t*>(recs + rec);
@@ -104,7 +105,8 @@ __device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, 
     const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
     const uint32_t meta = (m.x >> 8) & 0xFFu;
     const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-    const uint32_t hinfo = ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
+    const uint32_t hinfo = ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
+                           ((meta >> 3) & 0xFu) << 20;  // FB_META_LOCAL_SRC .. SELF_DST -> fb_session_flags
     e[0] = a;
     e[1] = b;
     e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
@@ -548,7 +550,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     uint32_t i;
     const int result = k2_find_insert(slice, tags, key, e3.w, i);
     if (result < 0) {
-        atomicOr(err, result == -2 ? 2u : 4u);  // spin expired / partition full
+        atomicOr(err, result == -2 ? 16u : 4u);  // spin expired / partition full
         return -1;
     }
     unsigned long long* s = slice + (size_t)i * kSlotWords;
@@ -566,7 +568,9 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     const uint32_t rec = e3.y;
     atomicMin(q + kScFirst, rec);
     atomicMax(q + kScLast, rec);
-    if (result == 1) atomicOr(q + kScMask, 1u << 16);  // inserted by this batch
+    // inserted by this batch: bit 16, and the session flags the reference stores at insert
+    // (is_local_src/dst, is_self_src/dst of the canonical key, src/packets.rs:429-435) in bits 20-23
+    if (result == 1) atomicOr(q + kScMask, (1u << 16) | (e3.z & 0x00F00000u));
     if (e3.z & 0x10000u) {                              // Some(flags): history.push(map_tcp_flags(..))
         atomicAdd(q + kScCount, 1u);
         const uint32_t b = hist_bit(e3.z & 0xFFu);
@@ -587,7 +591,7 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     uint32_t i;
     const int result = k2_find_insert(slice, tags, key, e3.w, i);
     if (result < 0) {
-        atomicOr(err, result == -2 ? 2u : 4u);
+        atomicOr(err, result == -2 ? 16u : 4u);
         return -1;
     }
     unsigned long long* s = slice + (size_t)i * kSlotWords;
@@ -613,7 +617,7 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     atomicMin(q + kScFirst, e2.z);
     atomicMax(q + kScLast, e2.w);
     const uint32_t hc = e3.z & 0xFFFFu;
-    const uint32_t m = (e3.z >> 16) | (result == 1 ? 1u << 16 : 0u);
+    const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) : 0u);
     if (m) atomicOr(q + kScMask, m);
     if (hc) {
         atomicAdd(q + kScCount, hc);
@@ -642,7 +646,8 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
     const uint2 wf = rec_word(first), wl = rec_word(last), we = rec_word(end != ~0u ? end : last);
     const unsigned long long first_seen = fresh ? hi | wf.y : (o0.x | (unsigned long long)o0.y << 32);
     unsigned long long end_seen = fresh ? FB_SEEN_NONE : (o1.x | (unsigned long long)o1.y << 32);
-    const uint32_t state = fresh ? 0u : o1.w, len = fresh ? 0u : o1.z;
+    // hist_state: hist_mask 0-12 | conn_state 16-19 | session flags 20-23 | end_mask 24-31
+    const uint32_t state = fresh ? (flags & 0x00F00000u) : o1.w, len = fresh ? 0u : o1.z;
     const unsigned long long last_seen = hi | wl.y;
     const uint32_t mask = state & 0xFFFFu;
     uint32_t cs = state >> 16;
@@ -650,7 +655,7 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, cons
         uint32_t m = mask | (1u << hist_bit((we.x >> 16) & 0xFFu));
 #pragma unroll
         for (uint32_t b = 0; b < 4u; ++b) m |= q[kScChar + b] <= end ? 1u << b : 0u;
-        cs = conn_state_of(m) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
+        cs = conn_state_of(m) | (cs & 0xF0u) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
         end_seen = hi | we.y;
     }
     uint4* t = reinterpret_cast<uint4*>(g) + 6;  // bytes 96..127: the ordered fields
@@ -686,7 +691,7 @@ constexpr uint32_t kCombThreads = FB_COMB_THREADS;
 constexpr uint32_t kCombGrid = FB_COMB_GRID;
 static_assert(kCombSlots % kCombThreads == 0, "each thread numbers kCombSlots / kCombThreads keys");
 constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
-                   kCfRecs = 10, kCfId = 11, kCfHash = 12, kCombF = 13;  // u32 fields of a key (kCfChar..+3)
+                   kCfRecs = 10, kCfId = 11, kCfHash = 12, kCfMeta = 13, kCombF = 14;  // u32 fields of a key (kCfChar..+3)
 // The reduce pass keeps each record's key slot (u8; 0xFF: none or slot 255) for the group's first
 // kCombJc records, so the pack pass finds them without gathering the 56-B records again: K1c is
 // bound by those random record reads (under Zipf(1.1) ~4.6M records per C4 batch sit in hot
@@ -747,6 +752,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
             atomicAdd(f + kCfRecs, 1u);
             f[kCfHash] = e[3].w;  // every lane of the key stores the same word
+            f[kCfMeta] = (e[3].z >> 20) & 0xFu;  // session flags: a function of the key and the configuration
             atomicMin(f + kCfFirst, rec);
             atomicMax(f + kCfLast, rec);
             if (e[3].z & 0x10000u) {
@@ -833,7 +839,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
             o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
             o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
-            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], 0u);
+            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta]);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
         if (threadIdx.x == 0) *rowp = (row & 0xFFFFu) | ((cursor + n_comb) << 16);
@@ -992,8 +998,8 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     const uint32_t key[10] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w, c.x, c.y & 0xFFFFu};
                     const uint32_t meta = (mx >> 8) & 0xFFu;
                     const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-                    const uint32_t hinfo =
-                        ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u);
+                    const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) |
+                                           ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0xFu) << 20;
                     const int r = apply_entry(slice, tags, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
                                               make_uint4(my, v0, hinfo, (uint32_t)flow_hash_words(key)),
                                               part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix0, P.error);
@@ -1051,15 +1057,25 @@ __global__ __launch_bounds__(256) void k_flow_finish(fb_batch_stats* S, const un
     }
 }
 
+// is_local_session! (src/sessions.rs:660-666) of a slot's key under the current configuration.
+__device__ __forceinline__ bool slot_local(const DevConfig* cfg, const FlowSlot& t) {
+    const uint32_t fam = (t.key[9] >> 8) & 0xFFu;
+    if (fam == 2u) return lan_v4(t.key[0]) && lan_v4(t.key[4]);
+    const uint32_t s[4] = {t.key[0], t.key[1], t.key[2], t.key[3]}, d[4] = {t.key[4], t.key[5], t.key[6], t.key[7]};
+    return lan_v6(cfg, cfg, s) && lan_v6(cfg, cfg, d);
+}
+
 __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned long long cap,
                                                      fb_flow_rec* out, unsigned long long out_cap,
-                                                     unsigned long long* d_n) {
+                                                     unsigned long long* d_n, uint32_t filter, const DevConfig* cfg) {
     __shared__ unsigned long long sh[4];
     __shared__ unsigned long long s_base;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < cap; base += stride) {
         const unsigned long long i = base + threadIdx.x;
-        const bool occ = i < cap && T[i].tag >= 2ull;
+        bool occ = i < cap && T[i].tag >= 2ull;
+        // get_sessions' read-time filter (src/capture.rs:1603-1608): is_lan_ip evaluated now
+        if (occ && filter != FB_FILTER_ALL) occ = slot_local(cfg, T[i]) == (filter == FB_FILTER_LOCAL_ONLY);
         const unsigned long long m = __ballot(occ);
         const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
         if (lane == 0u) sh[wave] = __popcll(m);
@@ -1085,10 +1101,10 @@ __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned
             r.end_seen = T[i].end_seen;
             r.hist_len = T[i].hist_len;
             r.hist_mask = (uint16_t)(T[i].hist_state & 0xFFFFu);
-            r.conn_state = (uint8_t)(T[i].hist_state >> 16);
+            r.conn_state = (uint8_t)((T[i].hist_state >> 16) & 0xFu);
             r.end_mask = (uint8_t)(T[i].hist_state >> 24);
             r.slot = (uint32_t)i;
-            r.reserved1 = 0u;
+            r.session_flags = (T[i].hist_state >> 20) & 0xFu;
             out[pos] = r;
         }
         __syncthreads();
@@ -1132,11 +1148,13 @@ hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* p
     return hipGetLastError();
 }
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,
-                              unsigned long long out_cap, unsigned long long* d_n, hipStream_t s) {
+                              unsigned long long out_cap, unsigned long long* d_n, hipStream_t s, uint32_t filter,
+                              const DevConfig* cfg) {
     unsigned long long g = (cap + 255ull) / 256ull;
     if (g > 1024ull) g = 1024ull;
     if (g == 0ull) g = 1ull;
-    hipLaunchKernelGGL(k_flow_export, dim3((uint32_t)g), dim3(256), 0, s, table, cap, out, out_cap, d_n);
+    if (!cfg) filter = FB_FILTER_ALL;
+    hipLaunchKernelGGL(k_flow_export, dim3((uint32_t)g), dim3(256), 0, s, table, cap, out, out_cap, d_n, filter, cfg);
     return hipGetLastError();
 }
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap, unsigned long long* d_n,

@@ -128,7 +128,7 @@ struct SegBatches {
 //   Slot (128 B): tag (0 empty, 1 being inserted [LDS only], else hash | 2), 40-B key,
 //   6 counters in fb_flow_rec order, then the ordered state: first / last / end positions
 //   ((update call << 32) | pkt_index, FB_SEEN_NONE), hist_len, hist_mask | conn_state << 16 |
-//   end_mask << 24.
+//   session flags << 20 | end_mask << 24.
 #ifndef FB_FLOW_SLOTS
 #define FB_FLOW_SLOTS 512
 #endif
@@ -156,7 +156,8 @@ struct FlowSlot {
                                 // orig_ip_bytes, resp_ip_bytes
     unsigned long long first_seen, last_seen, end_seen;
     uint32_t hist_len;
-    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | conn_state << 16 | end_mask << 24
+    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | conn_state << 16 (4 bits) |
+                                // session flags << 20 (fb_session_flags, set at insert) | end_mask << 24
 };
 static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
@@ -272,9 +273,11 @@ hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, ui
 hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
                               uint32_t nblk, uint32_t* error, hipStream_t s);
+// filter: fb_filter evaluated per flow at export time against `cfg` (is_local_session!,
+// src/sessions.rs:660-672); FB_FILTER_ALL (cfg may be null) exports every flow.
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,
                               unsigned long long out_cap, unsigned long long* d_n,
-                              hipStream_t s);
+                              hipStream_t s, uint32_t filter = FB_FILTER_ALL, const DevConfig* cfg = nullptr);
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
                              unsigned long long* d_n, hipStream_t s);
 

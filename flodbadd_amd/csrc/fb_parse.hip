@@ -439,10 +439,14 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     auto load_parsed = [&](uint32_t sg) {
         if constexpr ((FLAGS & kDense) != 0u) ppre = load_pre(sg);
         // 56-B records are only 8-B aligned at odd indices: byte-offset buffer loads (a uint4
-        // dereference there would claim 16-B alignment the data does not have)
-        const __amdgpu_buffer_rsrc_t rp =
-            __builtin_amdgcn_make_buffer_rsrc((void*)P.parsed, (short)0, (int)(P.n * 56u), 0x00020000);
-        const uint32_t o = min(sg * 64u + lane, P.n - 1u) * 56u;
+        // dereference there would claim 16-B alignment the data does not have).  The resource
+        // covers this segment's records only (base in 64-bit arithmetic): a batch-wide byte range
+        // or offset would overflow 32 bits past 76.7M records.
+        const uint32_t sc = min(sg, (P.n - 1u) >> 6);  // segments past the end clamp to the last one
+        const uint32_t left = P.n - sc * 64u;
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(P.parsed + (size_t)sc * 64u), (short)0, (int)(min(left, 64u) * 56u), 0x00020000);
+        const uint32_t o = min(lane, left - 1u) * 56u;
         const u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rp, o, 0, 0);
         const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rp, o + 16u, 0, 0);
         const u32x4 x2 = __builtin_amdgcn_raw_buffer_load_b128(rp, o + 32u, 0, 0);

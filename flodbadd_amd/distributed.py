@@ -149,7 +149,9 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
     end = torch.where(ended, glob(end_seen), torch.full_like(end_seen, big))
     sums = reduce([counters[:, j] for j in range(6)] + [hist_len, spread], 0, dist.ReduceOp.SUM)
     mins = reduce([glob(first_seen), end], big, dist.ReduceOp.MIN)
-    last = reduce([glob(last_seen)], -1, dist.ReduceOp.MAX)
+    # session_flags (stored at insert) are a function of the key and the configuration, the same on
+    # every rank that holds the flow: MAX keeps them
+    last = reduce([glob(last_seen), w32[:, 31]], -1, dist.ReduceOp.MAX)
     # conn_state: the ending rank's end_mask | the conn_state characters of the ranks before it
     gend = mins[:, 1]
     is_end = (end == gend[idx]) & (gend[idx] != big)
@@ -181,4 +183,5 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
     em = torch.where(has_end, emask, 0)
     cs = torch.where(has_end, _conn_state(emask), 0)
     w[:, 14] = sums[:, 6] | _hi32(hmask | (cs << 16) | (em << 24))
+    w[:, 15] = _hi32(last[:, 1])  # slot 0, session_flags
     return w.cpu().numpy().view(FLOW_REC_DTYPE).reshape(F)

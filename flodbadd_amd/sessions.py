@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional
 
 from ._native import (CONN_STATES, FB_FILTER_ALL, FB_FILTER_GLOBAL_ONLY, FB_FILTER_LOCAL_ONLY, FB_SEEN_NONE,
-                      FLOW_REC_DTYPE,
+                      FLOW_REC_DTYPE, SESSION_LOCAL_DST, SESSION_LOCAL_SRC, SESSION_SELF_DST, SESSION_SELF_SRC,
                       META_DST_SERVICE, META_HAS_FLAGS, META_LOCAL_DST, META_LOCAL_SRC, META_ORIGINATOR,
                       META_SELF_DST, META_SELF_SRC, META_SWAP, PARSED_DTYPE, PKT_OUT_DTYPE)
 
@@ -121,11 +121,40 @@ class SessionStats:
 
 @dataclass
 class SessionInfo:
-    """Subset of src/sessions.rs:40-61 that the GPU path owns."""
+    """Subset of src/sessions.rs:40-61 that the GPU path owns.  is_local_* / is_self_* are the
+    values stored when the session was inserted (src/packets.rs:429-435, fb_flow_rec.session_flags)."""
     session: Session
     stats: SessionStats = field(default_factory=SessionStats)
     is_local_src: bool = False
     is_local_dst: bool = False
+    is_self_src: bool = False
+    is_self_dst: bool = False
+
+
+def is_lan_ip(ip, lan_v6=()):
+    """is_lan_ip, src/ip.rs:199-242: the IPv4 fast check (ip.rs:55-91), the IPv6 special ranges
+    (ip.rs:112-136) and the interface prefixes of the LAN cache (ip.rs:141-156, 164-191), given as
+    [(address, prefix_len)] like FlodbaddGpuCapture's lan_v6.  Host-side: the reference evaluates it
+    per query in is_local_session! / filter_sessions (src/sessions.rs:660-692)."""
+    ip = ipaddress.ip_address(ip)
+    if ip.version == 4:
+        v = int(ip)
+        return (v in (0, 0xFFFFFFFF) or (v >> 24) in (127, 10) or (v >> 28) == 0xE or (v >> 16) in (0xA9FE, 0xC0A8)
+                or ((v >> 24) == 172 and 16 <= ((v >> 16) & 0xFF) <= 31))
+    v = int(ip)
+    s0 = v >> 112
+    if v in (0, 1) or (s0 & 0xFFC0) == 0xFE80 or (s0 & 0xFF00) == 0xFF00 or (s0 & 0xFE00) == 0xFC00:
+        return True
+    for net, pfx in lan_v6:
+        mask = 0 if pfx == 0 else ((1 << 128) - 1) ^ ((1 << (128 - pfx)) - 1)
+        if (v & mask) == (int(ipaddress.IPv6Address(net)) & mask):
+            return True
+    return False
+
+
+def is_local_session(info, lan_v6=()):
+    """is_local_session! (src/sessions.rs:660-666): both key addresses LAN, evaluated now."""
+    return is_lan_ip(info.session.src_ip, lan_v6) and is_lan_ip(info.session.dst_ip, lan_v6)
 
 
 def records_to_packets(recs):
@@ -188,9 +217,10 @@ def histories_from_records(recs):
     return {k: (h, state.get(k)) for k, h in hist.items()}
 
 
-def flows_to_sessions(flows, is_lan=None, histories=None):
+def flows_to_sessions(flows, histories=None):
     """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session.  `histories`
-    ({table slot: str}, FlodbaddGpuCapture.histories) supplies the history strings."""
+    ({table slot: str}, FlodbaddGpuCapture.histories) supplies the history strings; the locality
+    flags come from fb_flow_rec.session_flags (stored at insert, src/packets.rs:429-435)."""
     assert flows.dtype == FLOW_REC_DTYPE
     out = []
     for r in flows:
@@ -201,25 +231,26 @@ def flows_to_sessions(flows, is_lan=None, histories=None):
                           CONN_STATES[int(r["conn_state"])], int(r["first_seen"]), int(r["last_seen"]),
                           None if end == FB_SEEN_NONE else end, int(r["hist_len"]))
         s = Session.from_key(r)
-        info = SessionInfo(s, st)
-        if is_lan is not None:
-            info.is_local_src, info.is_local_dst = is_lan(s.src_ip), is_lan(s.dst_ip)
+        f = int(r["session_flags"])
+        info = SessionInfo(s, st, bool(f & SESSION_LOCAL_SRC), bool(f & SESSION_LOCAL_DST),
+                           bool(f & SESSION_SELF_SRC), bool(f & SESSION_SELF_DST))
         out.append(info)
     out.sort(key=lambda i: i.session.sort_key())
     return out
 
 
-def filter_sessions(sessions: List[SessionInfo], flt: SessionFilter) -> List[SessionInfo]:
-    """src/sessions.rs:678-692 over SessionInfo.is_local_src/dst (set from the record meta bits)."""
+def filter_sessions(sessions: List[SessionInfo], flt: SessionFilter, lan_v6=()) -> List[SessionInfo]:
+    """src/sessions.rs:678-692: is_local_session! / is_global_session! evaluate is_lan_ip on the
+    session's addresses at call time (src/sessions.rs:660-672), not the flags stored at insert."""
     if flt == SessionFilter.LocalOnly:
-        return [s for s in sessions if s.is_local_src and s.is_local_dst]
+        return [s for s in sessions if is_local_session(s, lan_v6)]
     if flt == SessionFilter.GlobalOnly:
-        return [s for s in sessions if not (s.is_local_src and s.is_local_dst)]
+        return [s for s in sessions if not is_local_session(s, lan_v6)]
     return list(sessions)
 
 
 __all__ = ["Protocol", "SessionFilter", "Session", "SessionPacketData", "SessionStats", "SessionInfo",
            "ip_to_words", "words_to_ip", "records_to_packets", "flows_to_sessions", "filter_sessions",
-           "packets_to_parsed", "determine_conn_state", "histories_from_records",
+           "packets_to_parsed", "determine_conn_state", "histories_from_records", "is_lan_ip", "is_local_session",
            "META_HAS_FLAGS", "META_SWAP", "META_ORIGINATOR", "META_LOCAL_SRC", "META_LOCAL_DST",
            "META_SELF_SRC", "META_SELF_DST", "META_DST_SERVICE"]

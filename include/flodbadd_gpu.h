@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FB_ABI_VERSION 2u
+#define FB_ABI_VERSION 3u /* 3: fb_flow_rec.session_flags, error-word bit 16, fb_flow_export_sessions* */
 #define FB_MAX_BATCH_PACKETS ((1u << 27) - 1u)
 #define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
 #define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
@@ -153,10 +153,12 @@ typedef struct fb_batch_stats {
     uint64_t n_drop;           /* parse_packet_pcap -> None                                   */
     uint64_t n_filtered;       /* rejected by the session filter                              */
     uint64_t bad_offsets;      /* frames with invalid offsets (counted in n_drop too)         */
-    uint64_t error;            /* nonzero = failure bits: 4 flow-table partition full
-                                  (FB_ERR_TABLE_FULL), 8 more records than the update scratch of
-                                  the last parse launch holds, 2 the dense path's offset scan
-                                  waited too long (FB_ERR_INTERNAL; not expected)            */
+    uint64_t error;            /* nonzero = failure bits: 2 the two-pass dense path's offset scan
+                                  waited too long (its records are not trusted and the update
+                                  that follows skips them; FB_ERR_INTERNAL, not expected),
+                                  4 flow-table partition full (FB_ERR_TABLE_FULL), 8 more records
+                                  than the update scratch of the last parse launch holds,
+                                  16 a table-update LDS spin expired (FB_ERR_INTERNAL)       */
     uint64_t reserved[3];
 } fb_batch_stats; /* 128 bytes */
 
@@ -235,8 +237,20 @@ typedef struct fb_flow_rec {
     uint8_t end_mask;        /* 119: hist_mask & 0xFF at end_seen (the characters S s H h F f R r
                                 conn_state was decided on); 0 while end_seen is NONE              */
     uint32_t slot;           /* 120: table slot (the flow id of fb_flow_history_dev)           */
-    uint32_t reserved1;      /* 124 */
+    uint32_t session_flags;  /* 124: fb_session_flags as stored when the session was inserted
+                                (src/packets.rs:429-435: is_local_src/dst, is_self_src/dst of the
+                                canonical key under the configuration of that update call)      */
 } fb_flow_rec;               /* 128 bytes */
+
+/* fb_flow_rec.session_flags (SessionInfo.is_local_src / is_local_dst / is_self_src / is_self_dst,
+ * src/sessions.rs:40-61, set once at insert, src/packets.rs:429-435).  Same bit values as
+ * fb_enrich_bits. */
+enum fb_session_flags {
+    FB_SESSION_LOCAL_SRC = 1u,
+    FB_SESSION_LOCAL_DST = 2u,
+    FB_SESSION_SELF_SRC = 4u,
+    FB_SESSION_SELF_DST = 8u
+};
 
 typedef struct fb_ctx fb_ctx;
 
@@ -510,6 +524,15 @@ int fb_flow_export(fb_ctx* ctx, fb_flow_rec* out, uint64_t cap, uint64_t* n, voi
 /* Same, into DEVICE memory; *d_n (device u64) receives the count. Asynchronous. */
 int fb_flow_export_dev(fb_ctx* ctx, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n,
                        void* stream);
+/* get_sessions (src/capture.rs:1578-1612): the flows that pass `filter` (fb_filter) evaluated at
+ * query time, as the reference does per SessionInfo: LOCAL_ONLY keeps is_local_session! (is_lan_ip
+ * of both key addresses under the context's CURRENT LAN configuration, src/sessions.rs:660-672),
+ * GLOBAL_ONLY keeps is_global_session!, ALL keeps everything (= fb_flow_export).  Slot order.
+ * Host variant synchronous; the _dev variant asynchronous, *d_n (device u64) = flows written. */
+int fb_flow_export_sessions(fb_ctx* ctx, uint32_t filter, fb_flow_rec* out, uint64_t cap, uint64_t* n,
+                            void* stream);
+int fb_flow_export_sessions_dev(fb_ctx* ctx, uint32_t filter, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n,
+                                void* stream);
 int fb_flow_clear(fb_ctx* ctx, void* stream); /* clear_all_sessions, src/capture.rs:396 */
 /* The table's deterministic 64-bit key hash (the reference's DashMap uses SipHash with a random
  * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */

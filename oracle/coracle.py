@@ -66,6 +66,8 @@ def lib():
         L.orc_flows_history.argtypes = [P, P, C.c_char_p, U64, C.c_char_p, U64]
         L.orc_pipeline.restype = U64
         L.orc_pipeline.argtypes = [P, P, P, U64, P, U32, P, P]
+        L.orc_pipeline_mt.restype = U64
+        L.orc_pipeline_mt.argtypes = [P, P, C.c_int, P, U64, P, U32, P, P, P]
         L.orc_key_cmp.restype = C.c_int
         L.orc_key_cmp.argtypes = [P, P]
         _lib = L
@@ -214,3 +216,19 @@ class Flows:
             lib().orc_flows_free(self.h)
         except Exception:
             pass
+
+
+def pipeline_mt(cfg, frames, offsets, threads, tables=None):
+    """orc_pipeline_mt: all-cores parse + classify + session upsert.  Returns (per-thread Flows,
+    stats); the union of the tables equals the single-thread table."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    n = offsets.size - 1
+    tables = tables or [Flows() for _ in range(threads)]
+    hs = (C.c_void_p * threads)(*[t.h.value for t in tables])
+    out = np.zeros(max(n, 1), dtype=PKT_OUT_DTYPE)
+    dns = np.zeros(max(n, 1), dtype=DNS_OUT_DTYPE)
+    st = np.zeros(1, dtype=STATS_DTYPE)
+    lib().orc_pipeline_mt(C.byref(cfg), hs, threads, frames.ctypes.data, frames.nbytes, offsets.ctypes.data, n,
+                          out.ctypes.data, dns.ctypes.data, st.ctypes.data)
+    return tables, st

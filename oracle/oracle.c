@@ -441,9 +441,16 @@ static uint32_t hist_bit(char c) {
     return (c && p) ? (uint32_t)(p - FB_HIST_CHARS) : 16u;
 }
 
+static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st);
+
 void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* st) {
-    for (uint64_t i = 0; i < n; ++i) {
-        const fb_pkt_out* r = &recs[i];
+    for (uint64_t i = 0; i < n; ++i) flow_upsert(f, &recs[i], st);
+    f->batch++;
+}
+
+/* One SessionPacketData through the DashMap upsert (src/packets.rs:329-535). */
+static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
+    {
         if ((f->count + 1) * 2 > f->cap) grow(f);
         orc_flow* s = find_slot(f->slots, f->cap, &r->key);
         const uint64_t pos = ((uint64_t)f->batch << 32) | r->pkt_index; /* stands for `now` */
@@ -453,6 +460,8 @@ void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch
             s->rec.key = r->key;
             s->rec.first_seen = pos; /* start_time, src/packets.rs:352 */
             s->rec.end_seen = FB_SEEN_NONE;
+            /* is_local_src/dst, is_self_src/dst of the key, stored once at insert (src/packets.rs:429-435) */
+            s->rec.session_flags = ((uint32_t)r->meta >> 3) & 0xFu;
             f->count++;
             if (st) st->new_sessions++;
         } else if (st) {
@@ -485,7 +494,6 @@ void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch
         }
         s->rec.last_seen = pos; /* last_activity, src/packets.rs:184 */
     }
-    f->batch++;
 }
 
 uint64_t orc_flows_count(const orc_flows* f) { return f->count; }
@@ -901,4 +909,70 @@ int orc_parse_classify_mt(const orc_cfg* c, const uint8_t* frames, uint64_t fram
     if (n_dns) *n_dns = sd;
     if (st) *st = m;
     return 0;
+}
+
+/* ---------------------------------------------------------------------------------------
+ * All-cores parse + session-table baseline (SURVEY.md 8d (ii) for config C4): parse + classify in
+ * `threads` contiguous ranges (orc_parse_classify_mt), then the SESSION records are split by an
+ * owner thread taken from their key hash (a stable counting sort, so each owner sees its records
+ * in packet order) and every thread upserts its own keys into its own table.  A key's records
+ * all go to one table in batch order, so the union of the tables is exactly the single-thread
+ * table (checked in tests).  Returns the number of SESSION records.
+ * ------------------------------------------------------------------------------------- */
+uint64_t orc_pipeline_mt(const orc_cfg* c, orc_flows** tables, int threads, const uint8_t* frames, uint64_t fb,
+                         const uint32_t* offsets, uint32_t n, fb_pkt_out* scratch, fb_dns_out* dns_scratch,
+                         fb_batch_stats* st) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    uint32_t no = 0, nd = 0;
+    fb_batch_stats s;
+    orc_parse_classify_mt(c, frames, fb, offsets, n, scratch, &no, dns_scratch, &nd, &s, threads);
+    const int T = threads;
+    uint32_t* own = (uint32_t*)malloc((size_t)(no ? no : 1) * 4);
+    uint32_t* idx = (uint32_t*)malloc((size_t)(no ? no : 1) * 4);
+    uint64_t* cnt = (uint64_t*)calloc((size_t)T * T, 8); /* cnt[range * T + owner] -> scatter cursor */
+    uint64_t* beg = (uint64_t*)calloc((size_t)T + 1, 8);
+    fb_batch_stats ts[256];
+#pragma omp parallel num_threads(T)
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num();
+#else
+        const int t = 0;
+#endif
+        const uint32_t a = (uint32_t)((uint64_t)no * t / T), b = (uint32_t)((uint64_t)no * (t + 1) / T);
+        for (uint32_t i = a; i < b; ++i) {
+            own[i] = (uint32_t)((key_hash(&scratch[i].key) >> 40) % (uint64_t)T);
+            cnt[(size_t)t * T + own[i]]++;
+        }
+#pragma omp barrier
+#pragma omp single
+        {
+            uint64_t run = 0;
+            for (int o = 0; o < T; ++o) {
+                beg[o] = run;
+                for (int r = 0; r < T; ++r) {
+                    const uint64_t k = cnt[(size_t)r * T + o];
+                    cnt[(size_t)r * T + o] = run;
+                    run += k;
+                }
+            }
+            beg[T] = run;
+        }
+        for (uint32_t i = a; i < b; ++i) idx[cnt[(size_t)t * T + own[i]]++] = i;
+#pragma omp barrier
+        memset(&ts[t], 0, sizeof(ts[t]));
+        for (uint64_t k = beg[t]; k < beg[t + 1]; ++k) flow_upsert(tables[t], &scratch[idx[k]], &ts[t]);
+        tables[t]->batch++;
+    }
+    for (int t = 0; t < T; ++t) {
+        s.new_sessions += ts[t].new_sessions;
+        s.updated_sessions += ts[t].updated_sessions;
+    }
+    free(own);
+    free(idx);
+    free(cnt);
+    free(beg);
+    if (st) *st = s;
+    return no;
 }

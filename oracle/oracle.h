@@ -118,6 +118,11 @@ uint64_t orc_pipeline(const orc_cfg* cfg, orc_flows* flows, const uint8_t* frame
                       uint64_t frames_bytes, const uint32_t* offsets, uint32_t n,
                       fb_pkt_out* scratch, fb_batch_stats* stats);
 
+/* All-cores C4 baseline: parse + classify in `threads` ranges, then each thread upserts the keys
+ * it owns (by key hash) into tables[thread]; the union of the tables = the single-thread table. */
+uint64_t orc_pipeline_mt(const orc_cfg* cfg, orc_flows** tables, int threads, const uint8_t* frames,
+                         uint64_t frames_bytes, const uint32_t* offsets, uint32_t n, fb_pkt_out* scratch,
+                         fb_dns_out* dns_scratch, fb_batch_stats* st);
 /* Derived Ord comparison of two keys (protocol, src_ip, src_port, dst_ip, dst_port). */
 int orc_key_cmp(const fb_session_key* a, const fb_session_key* b);
 

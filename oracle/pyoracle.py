@@ -167,8 +167,10 @@ class SessionTable:
         key = c["key"]
         s = self.sessions.get(key)
         if s is None:
+            # is_local_src/dst and is_self_src/dst are stored once, at insert (src/packets.rs:429-435)
             s = dict(outbound_bytes=0, inbound_bytes=0, orig_pkts=0, resp_pkts=0, orig_ip_bytes=0,
-                     resp_ip_bytes=0, history="", conn_state=None)
+                     resp_ip_bytes=0, history="", conn_state=None, is_local_src=c["local_src"],
+                     is_local_dst=c["local_dst"], is_self_src=c["self_src"], is_self_dst=c["self_dst"])
             self.sessions[key] = s
             self.new += 1
         else:

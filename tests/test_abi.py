@@ -26,6 +26,16 @@ def test_header_declares_all_bound_symbols():
     assert declared == bound, (set(declared) ^ set(bound))
 
 
+def test_integration_rust_binding_declares_every_entry_point():
+    """INTEGRATION.md's Rust extern blocks bind every function of the header (a maintainer copying
+    them gets the whole ABI)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    rust = "\n".join(re.findall(r"```rust\n(.*?)```", doc, flags=re.S))
+    declared_rust = set(re.findall(r"pub fn (fb_\w+)\s*\(", rust))
+    missing = set(_declared_functions()) - declared_rust
+    assert not missing, sorted(missing)
+
+
 def test_library_exports_every_declared_symbol():
     from flodbadd_amd.build import build_gpu
     build_gpu()
