@@ -683,6 +683,7 @@ def main():
     cfg.filter = N.FB_FILTER_GLOBAL_ONLY  # FlodbaddCapture::new() default (src/capture.rs:108)
     cfg.max_batch_packets = 1 << 24
     cfg.flow_capacity = 1 << 21  # C5 exchange: the rank's shard flows (<= 2^20 in the C4/C5 pool)
+    cfg.flags = N.FB_CFG_FIXED_TABLE  # sized for the pool (1.45M flows): no growth mid-run
     N.check(lib.fb_set_device(device))
     ctx = lib.fb_create(device, C.byref(cfg))
     if not ctx:

@@ -113,7 +113,16 @@ class FbConfig(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("filter", C.c_uint32), ("service_bitmap", C.c_void_p),
                 ("lan_v6", C.c_void_p), ("n_lan_v6", C.c_uint32), ("n_own_ips", C.c_uint32),
                 ("own_ips", C.c_void_p), ("flow_capacity", C.c_uint64), ("max_batch_packets", C.c_uint32),
-                ("reserved0", C.c_uint32), ("max_batch_bytes", C.c_uint64)]
+                ("flags", C.c_uint32), ("max_batch_bytes", C.c_uint64)]
+
+
+FB_CFG_FIXED_TABLE = 1
+FB_MAX_FLOW_CAPACITY = 1 << 25
+
+
+class FlowTableInfo(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("partitions", C.c_uint64), ("generation", C.c_uint64),
+                ("flows", C.c_uint64), ("max_partition", C.c_uint64), ("reserved", C.c_uint64 * 3)]
 
 
 class FbRingConfig(C.Structure):
@@ -176,6 +185,8 @@ GPU_SYMBOLS = [
     ("fb_flow_export_sessions", _I, [_P, _U32, _P, _U64, _PU64, _P]),
     ("fb_flow_export_sessions_dev", _I, [_P, _U32, _P, _U64, _P, _P]),
     ("fb_flow_clear", _I, [_P, _P]),
+    ("fb_flow_table_info_get", _I, [_P, C.POINTER(FlowTableInfo)]),
+    ("fb_flow_slot_remap", _I, [_P, _P, _U64, _PU64]),
     ("fb_flow_hash", _U64, [_P]),
     ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),
     ("fb_ring_destroy", _I, [_P]),

@@ -51,7 +51,8 @@ def stats_dict(arr):
 
 class FlodbaddGpuCapture:
     def __init__(self, device=0, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 20,
-                 service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20, track_history=False):
+                 service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20, track_history=False,
+                 grow=True):
         lib = N.gpu_lib()
         self._keep = []
         cfg = N.FbConfig()
@@ -71,6 +72,7 @@ class FlodbaddGpuCapture:
         cfg.n_own_ips = len(ot)
         cfg.flow_capacity = int(flow_capacity)
         cfg.max_batch_packets = int(max_batch_packets)
+        cfg.flags = 0 if grow else N.FB_CFG_FIXED_TABLE  # the reference's session map is unbounded
         ctx = lib.fb_create(int(device), C.byref(cfg))
         if not ctx:
             raise N.FbError(N.FB_ERR_NODEV, lib.fb_last_error().decode(errors="replace"))
@@ -82,6 +84,7 @@ class FlodbaddGpuCapture:
         # from fb_flow_history_dev when track_history is set
         self.track_history = bool(track_history) and flow_capacity > 0
         self.histories = {}
+        self._generation = 0  # table growths seen (slots move when the table grows)
 
     # ---- configuration -------------------------------------------------------------------
     def set_filter(self, flt):
@@ -211,9 +214,34 @@ class FlodbaddGpuCapture:
         starts, ends = np.r_[0, cut], np.r_[cut, k]
         return {int(slots[a]): chars[a:b].tobytes().decode("ascii") for a, b in zip(starts, ends)}
 
+    def table_info(self):
+        """fb_flow_table_info_get: capacity, partitions, growths, flows / fullest partition as the
+        last completed update reported."""
+        t = N.FlowTableInfo()
+        N.check(N.gpu_lib().fb_flow_table_info_get(self.ctx, C.byref(t)))
+        return dict(capacity=t.capacity, partitions=t.partitions, generation=t.generation, flows=t.flows,
+                    max_partition=t.max_partition)
+
+    def _follow_growth(self):
+        """The table grew since the histories were last keyed: move them to the new slots
+        (fb_flow_slot_remap; only the last growth's map is kept, and this runs after every batch)."""
+        gen = self.table_info()["generation"]
+        if gen == self._generation:
+            return
+        assert gen == self._generation + 1, "more than one growth between two batches"
+        self._generation = gen
+        if not self.histories:
+            return
+        old_cap = max(self.histories) + 1
+        m = np.zeros(max(old_cap, 1), dtype=np.uint32)
+        n = C.c_uint64(0)
+        N.check(N.gpu_lib().fb_flow_slot_remap(self.ctx, N.ptr(m), old_cap, C.byref(n)))
+        self.histories = {int(m[k]): v for k, v in self.histories.items()}
+
     def _pull_history(self, n_slots):
         if not self.track_history:
             return
+        self._follow_growth()
         for slot, run in self.flow_history(n_slots).items():
             self.histories[slot] = self.histories.get(slot, "") + run
 

@@ -34,6 +34,19 @@ int set_err(int code, const char* fmt, ...) {
 
 }  // namespace fbk
 
+// Update scratch of one table update (K1 bucketing -> K1c -> K1t -> K2).  Two sets: the pipelined
+// call buckets batch k (on the caller's stream, right after its parse) into set k & 1 while the
+// update stream applies batch k - 1 from the other set.
+struct UpdScratch {
+    uint32_t* entries = nullptr;   // [flow_recs] bucketed record slots (or combined ids)
+    FlowEntry* comb = nullptr;     // k_flow_combine entries (2 units each), comb_cap of them
+    uint32_t* rows = nullptr;      // [flow_chunks][flow_parts]
+    uint32_t* cols = nullptr;      // [flow_parts][flow_chunks]
+    uint32_t* rec_flow = nullptr;  // [flow_recs] entry position per record slot
+    uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
+    uint32_t* ctl = nullptr;       // [2] its counters
+};
+
 struct fb_ctx {
     int device = 0;
     DevConfig* h_cfg = nullptr;  // host shadow
@@ -69,18 +82,24 @@ struct fb_ctx {
     uint64_t table_cap = 0;
     uint32_t flow_parts = 0;        // partitions of kFlowSlots slots
     uint32_t flow_shift = 64;       // 64 - log2(flow_parts)
-    uint32_t* d_entries = nullptr;  // update scratch: flow_recs bucketed record slots
-    FlowEntry* d_comb = nullptr;    // k_flow_combine entries (2 units each), comb_cap of them
+    UpdScratch us[2];               // update scratch sets (set 1: pipelined calls only, allocated lazily)
     uint32_t comb_cap = 0;
-    uint32_t* d_rows = nullptr;     // [flow_chunks][flow_parts]
-    uint32_t* d_cols = nullptr;     // [flow_parts][flow_chunks]
     uint64_t flow_recs = 0;         // scratch capacity (multiple of kFlowChunk)
     uint32_t last_n = 0;            // packets of the last parse launch (bounds its records)
-    unsigned long long* d_partials = nullptr;
+    unsigned long long* d_partials = nullptr;  // [3 * flow_parts] per-partition new / updated / occupied
+    // growth: the occupancy each update reports in host-mapped memory, updates issued
+    FlowMailbox* h_mbox = nullptr;  // pinned, host-mapped (written by k_flow_finish)
+    FlowMailbox* d_mbox = nullptr;  // its device address
+    uint64_t upd_seq = 0;           // table updates issued (the mailbox's seq counts them from 1)
+    uint64_t grown_seq = 0;         // upd_seq at the last growth (older reports describe the old geometry)
+    uint64_t clear_seq = 0;         // upd_seq at the last fb_flow_clear (older reports are void)
+    uint64_t generation = 0;        // growths so far
+    bool grow = true;               // FB_CFG_FIXED_TABLE clears it
+    uint32_t* d_remap = nullptr;    // the last growth's old -> new slot map
+    uint64_t remap_n = 0;
     unsigned long long* d_n = nullptr;
     // ordered per-flow state: update calls since create/clear, table slot of each record slot
     uint32_t flow_batch = 0;
-    uint32_t* d_rec_flow = nullptr;       // [flow_recs] entry position per record slot
     uint32_t* d_ent_slot = nullptr;       // [flow_recs] table slot per entry
     uint32_t* d_rec_part = nullptr;       // [flow_recs] partition per record slot (fb_process_seg_dev)
     const fb_pkt_out* part_recs = nullptr;  // the records part_buf was written for (one update)
@@ -94,9 +113,8 @@ struct fb_ctx {
     uint32_t* d_rec_part2 = nullptr;            // partitions of the odd async batches
     const void* async_prev[3] = {nullptr, nullptr, nullptr};  // the last async batch's records, counts, stats
     uint32_t upd_word[2] = {4u, 4u};            // error word (launch & 3) of the async update in slot k & 1 (4: none)
-    uint32_t* d_hot = nullptr;            // [flow_recs / 16 + 16] hot groups for k_flow_combine
-    uint32_t* d_comb_ctl = nullptr;       // [2] its counters
     uint32_t* d_agg_slot = nullptr;       // [flow_recs / 2 + 1] table slot per combined entry
+    uint32_t last_set = 0;                // the update scratch set of the last update (history)
     // the last update, for fb_flow_history_dev
     const fb_pkt_out* last_recs = nullptr;
     const uint32_t* last_part = nullptr;  // the fused parse's per-record words of the last update
@@ -194,6 +212,33 @@ static int upload_array(T** d, const T* h, size_t n) {
     return FB_OK;
 }
 
+static void free_upd_scratch(UpdScratch& u) {
+    hipFree(u.entries);
+    hipFree(u.comb);
+    hipFree(u.rows);
+    hipFree(u.cols);
+    hipFree(u.rec_flow);
+    hipFree(u.hot);
+    hipFree(u.ctl);
+    u = UpdScratch();
+}
+
+// One update scratch set sized for c->flow_recs records.
+static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
+    const uint64_t recs = c->flow_recs, chunks = recs / kFlowChunk;
+    if (hipMalloc(&u.entries, recs * 4ull) != hipSuccess ||
+        hipMalloc(&u.comb, (uint64_t)c->comb_cap * 2ull * sizeof(FlowEntry)) != hipSuccess ||
+        hipMalloc(&u.rec_flow, recs * 4ull) != hipSuccess ||
+        hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 8) != hipSuccess) {
+        free_upd_scratch(u);
+        return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
+    }
+    HIP_TRY(hipMemsetAsync(u.ctl, 0, 8, s));
+    return FB_OK;
+}
+
 // Session-table update scratch for batches of up to `recs` records (grown, never shrunk).
 static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     if (!c->d_table) return FB_OK;
@@ -203,46 +248,31 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     int rc = drain_updates(c);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));
-    hipFree(c->d_entries);
-    hipFree(c->d_comb);
-    hipFree(c->d_rows);
-    hipFree(c->d_cols);
-    hipFree(c->d_rec_flow);
+    const bool had_set1 = c->us[1].entries != nullptr;
+    for (UpdScratch& u : c->us) free_upd_scratch(u);
     hipFree(c->d_ent_slot);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
-    hipFree(c->d_hot);
-    hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
     c->d_rec_part = c->d_rec_part2 = nullptr;
     c->part_recs = nullptr;
     c->part_buf = nullptr;
     c->d_ent_slot = nullptr;
-    c->d_entries = nullptr;
-    c->d_comb = nullptr;
     c->comb_cap = 0;
-    c->d_rows = c->d_cols = nullptr;
-    c->d_rec_flow = c->d_hot = c->d_comb_ctl = c->d_agg_slot = nullptr;
+    c->d_agg_slot = nullptr;
     c->last_recs = nullptr;  // its rec_flow is gone
     c->last_part = nullptr;
     c->flow_recs = 0;
-    const uint64_t chunks = recs / kFlowChunk;
-    // combined entries: at most one per two records of the hot groups; a quarter of the batch's
-    // records is room for any skew we measured (past it a hot group just stays plain)
-    const uint64_t comb = recs / 4 + 256;
-    if (hipMalloc(&c->d_entries, recs * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_comb, comb * 2ull * sizeof(FlowEntry)) != hipSuccess ||
-        hipMalloc(&c->d_rec_flow, recs * 4ull) != hipSuccess || hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&c->d_comb_ctl, 8) != hipSuccess ||
+    if (hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess || hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
-    HIP_TRY(hipMemsetAsync(c->d_comb_ctl, 0, 8, s));
     c->flow_recs = recs;
-    c->comb_cap = (uint32_t)comb;
-    return FB_OK;
+    // combined entries: at most one per two records of the hot groups; a quarter of the batch's
+    // records is room for any skew we measured (past it a hot group just stays plain)
+    c->comb_cap = (uint32_t)(recs / 4 + 256);
+    rc = alloc_upd_scratch(c, c->us[0], s);
+    if (!rc && had_set1) rc = alloc_upd_scratch(c, c->us[1], s);
+    return rc;
 }
 
 static int empty_update(fb_ctx* c);
@@ -411,7 +441,11 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         c->flow_shift = 64u - lg;
         ok = hipMalloc(&c->d_table, cap * sizeof(FlowSlot)) == hipSuccess &&
              hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess &&
-             hipMalloc(&c->d_partials, 2ull * c->flow_parts * 8ull) == hipSuccess;
+             hipMalloc(&c->d_partials, 3ull * c->flow_parts * 8ull) == hipSuccess &&
+             hipHostMalloc((void**)&c->h_mbox, sizeof(FlowMailbox), hipHostMallocMapped) == hipSuccess &&
+             hipHostGetDevicePointer((void**)&c->d_mbox, c->h_mbox, 0) == hipSuccess;
+        if (ok) memset(c->h_mbox, 0, sizeof(FlowMailbox));
+        c->grow = (cfg->flags & FB_CFG_FIXED_TABLE) == 0u;
         ok = ok && ensure_flow_scratch(c, cfg->max_batch_packets, nullptr) == FB_OK;
     }
     ok = ok && upload_cfg(c, nullptr) == FB_OK;
@@ -436,18 +470,14 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_dstatus);
     hipFree(c->d_error);
     hipFree(c->d_table);
-    hipFree(c->d_entries);
-    hipFree(c->d_comb);
-    hipFree(c->d_rows);
-    hipFree(c->d_cols);
+    for (UpdScratch& u : c->us) free_upd_scratch(u);
     hipFree(c->d_partials);
+    hipFree(c->d_remap);
+    if (c->h_mbox) hipHostFree(c->h_mbox);
     hipFree(c->d_n);
-    hipFree(c->d_rec_flow);
     hipFree(c->d_ent_slot);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
-    hipFree(c->d_hot);
-    hipFree(c->d_comb_ctl);
     hipFree(c->d_agg_slot);
     if (c->upd) hipStreamDestroy(c->upd);
     if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
@@ -863,13 +893,107 @@ static int empty_update(fb_ctx* c) {
     return FB_OK;
 }
 
+// ---- table growth -------------------------------------------------------------------------------
+// Doubles the table on the device: every slot re-inserted into 2x partitions (k_flow_grow), the old
+// -> new slot map kept for fb_flow_slot_remap.  Drains the updates in flight first: growth is rare.
+static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
+    int rc = drain_updates(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t cap = c->table_cap << k;
+    FlowSlot* nw = nullptr;
+    unsigned long long* partials = nullptr;
+    if (hipMalloc(&nw, cap * sizeof(FlowSlot)) != hipSuccess) return set_err(FB_ERR_NOMEM, "grown flow table");
+    if (hipMalloc(&partials, 3ull * (cap / kFlowSlots) * 8ull) != hipSuccess) {
+        hipFree(nw);
+        return set_err(FB_ERR_NOMEM, "grown flow table partials");
+    }
+    hipFree(c->d_remap);
+    c->d_remap = nullptr;
+    c->remap_n = 0;
+    if (hipMalloc(&c->d_remap, c->table_cap * 4ull) != hipSuccess) {
+        hipFree(nw);
+        hipFree(partials);
+        return set_err(FB_ERR_NOMEM, "slot remap");
+    }
+    HIP_TRY(hipMemsetAsync(nw, 0, cap * sizeof(FlowSlot), s));
+    HIP_TRY(launch_flow_grow(c->d_table, c->flow_parts, k, c->flow_shift - k, nw, c->d_remap, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(c->d_table);
+    hipFree(c->d_partials);
+    c->d_table = nw;
+    c->d_partials = partials;
+    c->remap_n = c->table_cap;
+    c->table_cap = cap;
+    c->flow_parts <<= k;
+    c->flow_shift -= k;
+    c->grown_seq = c->upd_seq;
+    ++c->generation;
+    // scratch sized by the partition count (K1 rows / K2 columns), history sort bits: rebuilt
+    const uint64_t recs = c->flow_recs;
+    const bool had_set1 = c->us[1].entries != nullptr;
+    for (UpdScratch& u : c->us) free_upd_scratch(u);
+    c->flow_recs = 0;
+    rc = ensure_flow_scratch(c, recs, s);
+    if (!rc && had_set1) rc = alloc_upd_scratch(c, c->us[1], s);
+    hipFree(c->d_hkeys);
+    hipFree(c->d_hvals);
+    hipFree(c->d_htemp);
+    c->d_hkeys = nullptr;
+    c->d_hvals = nullptr;
+    c->d_htemp = nullptr;
+    c->hist_cap = 0;
+    c->last_recs = nullptr;  // the last update's slots moved: its history is no longer available
+    c->last_part = nullptr;
+    return rc;
+}
+
+// Before an update call: grow while the occupancy the last completed update reported, plus the new
+// flows of the updates still in flight (each estimated at the last reported update's count) and of
+// this one (twice that: arrival rates rise), spread over the partitions, plus slack for the spread
+// between partitions, would pass 7/8 of a partition, or the flows 3/4 of the table.  No device
+// wait: the report sits in host-mapped memory.  A burst beyond that estimate inside one batch can
+// still fill a partition: the update then reports error bit 4 (FB_ERR_TABLE_FULL).
+static constexpr uint64_t kGrowPart = kFlowSlots * 7u / 8u;
+static int maybe_grow(fb_ctx* c, hipStream_t s) {
+    if (!c->d_table || !c->grow || c->part_recs) return FB_OK;  // (a fused parse already bucketed for this geometry)
+    const volatile FlowMailbox* m = c->h_mbox;
+    const uint64_t seq = __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE);
+    if (seq == 0 || seq <= c->clear_seq) return FB_OK;
+    const uint64_t flows = m->flows, newf = m->new_flows;
+    const uint64_t ahead = c->upd_seq - seq + 2u;  // in flight, plus this call counted twice
+    // the smallest k (table x 2^k) that holds the projection: one growth (one slot remap) per call
+    uint32_t k = 0;
+    for (;; ++k) {
+        const uint64_t parts = (uint64_t)c->flow_parts << k;
+        if ((c->table_cap << k) > kFlowMaxCapacity || k > 5u) {
+            if (k > 0) --k;
+            break;
+        }
+        // a report from before a growth describes other partitions: only its flow count is used there
+        const uint64_t maxp = (k == 0 && seq > c->grown_seq) ? m->max_part : flows / parts + 3u * kFlowSlots / 16u;
+        const uint64_t add = (ahead * newf + parts - 1u) / parts;
+        if (maxp + add + kFlowSlots / 32u <= kGrowPart && flows + ahead * newf <= (c->table_cap << k) * 3u / 4u) break;
+    }
+    return k ? grow_table(c, s, k) : FB_OK;
+}
+
+// One table update.  `split` (the pipelined call): the bucketing kernels (K1, K1c) run on `s_bucket`
+// -- the caller's stream (possibly the null stream), right after the parse that wrote the batch's
+// partitions, into update scratch set `set` -- and the rest (K1t, K2, the stats fold) on `s` after
+// an event; otherwise everything runs on `s` with set 0.
 static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_seg, uint32_t n_slots,
-                       fb_batch_stats* d_stats, hipStream_t s) {
+                       fb_batch_stats* d_stats, hipStream_t s, bool split = false, hipStream_t s_bucket = nullptr,
+                       uint32_t set = 0) {
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     DeviceGuard g(c->device);
-    int rc = join_updates(c, s);
-    if (!rc) rc = ensure_flow_scratch(c, n_slots, s);
+    if (!split) s_bucket = s;
+    int rc = split ? FB_OK : join_updates(c, s);
+    if (!rc && !split) rc = maybe_grow(c, s);  // (skipped after a fused parse: it bucketed for this geometry)
+    if (!rc) rc = ensure_flow_scratch(c, n_slots, s_bucket);
+    if (!rc && set == 1u && !c->us[1].entries) rc = alloc_upd_scratch(c, c->us[1], s_bucket);
     if (rc) return rc;
+    const UpdScratch& u = c->us[set];
     // record slots of the batch: at most last_n records (dense) / n_slots slots (segmented)
     const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_slots + kFlowChunk - 1) / kFlowChunk);
     FlowParams p;
@@ -878,11 +1002,11 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.n_slots = n_slots;
     p.stats = d_stats;
     p.table = c->d_table;
-    p.entries = c->d_entries;
-    p.comb = c->d_comb;
+    p.entries = u.entries;
+    p.comb = u.comb;
     p.comb_cap = c->comb_cap;
-    p.rows = c->d_rows;
-    p.cols = c->d_cols;
+    p.rows = u.rows;
+    p.cols = u.cols;
     p.partials = c->d_partials;
     p.error = c->d_error + (c->epoch & 3u);
     p.max_recs = (uint32_t)std::min<uint64_t>((uint64_t)chunks * kFlowChunk, c->flow_recs);
@@ -890,20 +1014,24 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.part_shift = c->flow_shift;
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
-    p.rec_flow = c->d_rec_flow;
+    p.rec_flow = u.rec_flow;
     p.ent_slot = c->d_ent_slot;
-#ifdef FB_NO_RECFLOW  // ablation: no per-record slot for the history
-    p.rec_flow = nullptr;
-#endif
-    p.hot = c->d_hot;
-    p.ctl = c->d_comb_ctl;
+    p.hot = u.hot;
+    p.ctl = u.ctl;
     p.agg_slot = c->d_agg_slot;
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
     c->part_recs = nullptr;
-    HIP_TRY(launch_flow_update(p, chunks, s));
-    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), s));
+    HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
+    if (split) {
+        HIP_TRY(hipEventRecord(c->ev_parsed, s_bucket));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_parsed, 0));
+    }
+    HIP_TRY(launch_flow_apply(p, chunks, s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), c->d_mbox,
+                               ++c->upd_seq, s));
     ++c->flow_batch;
+    c->last_set = set;
     c->last_recs = d_recs;
     c->last_part = p.rec_part;
     c->last_seg = d_seg;
@@ -931,7 +1059,12 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
                        void* stream) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
-    int rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
+    int rc;
+    {
+        DeviceGuard g(c->device);
+        rc = maybe_grow(c, (hipStream_t)stream);  // before the parse writes partitions of this geometry
+    }
+    if (!rc) rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
     if (rc == FB_OK && c->stage_event) rc = hipEventRecord(c->stage_event, (hipStream_t)stream) == hipSuccess
                                                 ? FB_OK : set_err(FB_ERR_HIP, "stage event record failed");
     if (rc == FB_OK) rc = n == 0 ? empty_update(c) : fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, stream);
@@ -959,7 +1092,8 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
             return set_err(FB_ERR_HIP, "update stream / events");
     }
     const uint32_t slot = (uint32_t)(c->async_k & 1u);
-    int rc = ensure_flow_scratch(c, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES, s);
+    int rc = maybe_grow(c, s);  // before this batch's parse writes partitions (drains the pipeline if it grows)
+    if (!rc) rc = ensure_flow_scratch(c, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES, s);
     if (rc) return rc;
     if (!c->d_rec_part2 && hipMalloc(&c->d_rec_part2, c->flow_recs * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "second partition buffer");
@@ -979,9 +1113,11 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     if (rc == FB_OK && c->stage_event) rc = hipEventRecord(c->stage_event, s) == hipSuccess
                                                 ? FB_OK : set_err(FB_ERR_HIP, "stage event record failed");
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(c->ev_parsed, s));
-    HIP_TRY(hipStreamWaitEvent(c->upd, c->ev_parsed, 0));
-    rc = n == 0 ? empty_update(c) : fb_flow_update_seg_dev(c, d_out, d_seg, n, d_stats, c->upd);
+    // the bucketing kernels follow the parse on `stream` (into scratch set k & 1, which update k-2
+    // -- waited for above -- was the last to read); the update stream takes over after them
+    rc = n == 0 ? empty_update(c)
+                : flow_update(c, d_out, d_seg, (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES, d_stats,
+                              c->upd, true, s, slot);
     c->part_recs = nullptr;
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_upd[slot], c->upd));
@@ -1043,7 +1179,7 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     p.recs = c->last_recs;
     p.seg = c->last_seg;
     p.stats = c->last_stats;
-    p.rec_flow = c->d_rec_flow;
+    p.rec_flow = c->us[c->last_set].rec_flow;
     p.ent_slot = c->d_ent_slot;
     p.agg_slot = c->d_agg_slot;
     p.n_slots = n;
@@ -1209,6 +1345,33 @@ int fb_flow_export(fb_ctx* c, fb_flow_rec* out, uint64_t cap, uint64_t* n, void*
     return fb_flow_export_sessions(c, FB_FILTER_ALL, out, cap, n, stream);
 }
 
+int fb_flow_table_info_get(fb_ctx* c, fb_flow_table_info* info) {
+    if (!c || !info) return set_err(FB_ERR_INVAL, "bad arguments");
+    memset(info, 0, sizeof(*info));
+    if (!c->d_table) return FB_OK;
+    info->capacity = c->table_cap;
+    info->partitions = c->flow_parts;
+    info->generation = c->generation;
+    const volatile FlowMailbox* m = c->h_mbox;
+    const uint64_t seq = __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE);
+    if (seq && seq > c->clear_seq) {
+        info->flows = m->flows;
+        info->max_partition = m->max_part;
+    }
+    return FB_OK;
+}
+
+int fb_flow_slot_remap(fb_ctx* c, uint32_t* old_to_new, uint64_t cap, uint64_t* n) {
+    if (!c || !n || (cap && !old_to_new)) return set_err(FB_ERR_INVAL, "bad arguments");
+    *n = 0;
+    if (!c->d_remap || !c->remap_n) return FB_OK;
+    DeviceGuard g(c->device);
+    const uint64_t m = std::min(cap, c->remap_n);
+    if (m) HIP_TRY(hipMemcpy(old_to_new, c->d_remap, m * 4ull, hipMemcpyDeviceToHost));
+    *n = m;
+    return FB_OK;
+}
+
 int fb_flow_clear(fb_ctx* c, void* stream) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return FB_OK;
@@ -1217,6 +1380,7 @@ int fb_flow_clear(fb_ctx* c, void* stream) {
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->d_table, 0, c->table_cap * sizeof(FlowSlot), (hipStream_t)stream));
     c->flow_batch = 0;
+    c->clear_seq = c->upd_seq;
     c->last_recs = nullptr;
     c->last_part = nullptr;
     return FB_OK;

@@ -113,10 +113,34 @@ __device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, 
     e[3] = make_uint4(m.y, rec, hinfo, (uint32_t)flow_hash_words(key));
 }
 
+// K1's LDS histogram / cursors: one u32 per partition, or (more than kFlowPackedParts partitions)
+// two u16 halves per word -- a chunk holds < 2^16 records, so no half carries into the other.
+struct PartHist {
+    uint32_t* w;
+    bool packed;
+    __device__ __forceinline__ uint32_t add(uint32_t p) const {  // returns the old count / cursor
+        if (!packed) return atomicAdd(&w[p], 1u);
+        const uint32_t sh = 16u * (p & 1u);
+        return (atomicAdd(&w[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t p) const {
+        return packed ? reinterpret_cast<const uint16_t*>(w)[p] : w[p];
+    }
+    __device__ __forceinline__ void set(uint32_t p, uint32_t v) const {
+        if (packed) reinterpret_cast<uint16_t*>(w)[p] = (uint16_t)v;
+        else w[p] = v;
+    }
+};
+__host__ __device__ inline uint32_t part_hist_bytes(uint32_t parts) {
+    return parts > kFlowPackedParts ? parts * 2u : parts * 4u;
+}
+static_assert(kFlowChunk < 65536u, "packed K1 counters hold a chunk's records");
+
 // ---------------------------------------------------------------------------------------------
 // K1: bucket one chunk of records by partition (counting sort in LDS).
 __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams P) {
-    extern __shared__ uint32_t hist[];  // [P.parts]
+    extern __shared__ uint32_t hist_w[];  // part_hist_bytes(P.parts)
+    const PartHist hist{hist_w, P.parts > kFlowPackedParts};
     __shared__ uint32_t wsum[kFlowK1Threads / 64];
     const uint32_t n = batch_records(P);
     if (blockIdx.x == 0 && threadIdx.x == 0 && !P.seg && P.stats->n_session > (unsigned long long)P.max_recs)
@@ -125,7 +149,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     if (base >= n) return;
     const uint32_t cnt = min(kFlowChunk, n - base);
     const fb_pkt_out* R = P.recs + base;
-    for (uint32_t j = threadIdx.x; j < P.parts; j += kFlowK1Threads) hist[j] = 0u;
+    for (uint32_t j = threadIdx.x; j < part_hist_bytes(P.parts) / 4u; j += kFlowK1Threads) hist_w[j] = 0u;
     // every thread owns the chunk's slots threadIdx.x + j * kFlowK1Threads; their partitions stay in
     // registers from the histogram pass to the scatter pass, and each pass issues all its loads
     // before the first LDS atomic (a loop of load -> atomic iterations waits a full memory round
@@ -187,27 +211,28 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     __syncthreads();  // hist zeroed
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j)
-        if (pv[j] != ~0u) atomicAdd(&hist[pv[j]], 1u);
+        if (pv[j] != ~0u) hist.add(pv[j]);
     __syncthreads();
     // exclusive scan of hist[0..parts): each thread owns E consecutive partitions
     const uint32_t E = (P.parts + kFlowK1Threads - 1u) / kFlowK1Threads;
     const uint32_t j0 = threadIdx.x * E;
     uint32_t local = 0u;
-    for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) local += hist[j];
+    for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) local += hist.get(j);
     uint32_t total;
     uint32_t run = block_excl_scan(local, wsum, total);
     uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
     const uint32_t hot_min = max(kCombMin, 4u * ((cnt + P.parts - 1u) / P.parts));
-    static_assert(kFlowMaxParts / kFlowK1Threads <= 32u, "a thread's partitions fit the hot mask");
-    uint32_t hot = 0u, n_hot = 0u;  // this thread's hot groups (bit j - j0), handed to k_flow_combine
+    static_assert(kFlowMaxParts / kFlowK1Threads <= 64u, "a thread's partitions fit the hot mask");
+    unsigned long long hot = 0ull;  // this thread's hot groups (bit j - j0), handed to k_flow_combine
+    uint32_t n_hot = 0u;
     for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
-        const uint32_t c = hist[j];
+        const uint32_t c = hist.get(j);
         row[j] = run | (c << 16);
-        if (c >= hot_min && j - j0 < 32u) {
-            hot |= 1u << (j - j0);
+        if (c >= hot_min) {
+            hot |= 1ull << (j - j0);
             ++n_hot;
         }
-        hist[j] = run;  // becomes the scatter cursor
+        hist.set(j, run);  // becomes the scatter cursor
         run += c;
     }
     if (P.hot) {  // one list slot atomic per workgroup (one per group serialised ~19K same-address
@@ -219,8 +244,8 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
             if (threadIdx.x == 0) s_hot0 = atomicAdd(P.ctl, tot_hot);
             __syncthreads();
             h += s_hot0;
-            for (; hot; hot &= hot - 1u, ++h)
-                if (h < P.hot_cap) P.hot[h] = blockIdx.x << 13 | (j0 + (uint32_t)__builtin_ctz(hot));
+            for (; hot; hot &= hot - 1ull, ++h)
+                if (h < P.hot_cap) P.hot[h] = blockIdx.x << 16 | (j0 + (uint32_t)__builtin_ctzll(hot));
         }
     }
     __syncthreads();
@@ -230,7 +255,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     for (uint32_t j = 0; j < kPer; ++j) {
         if (pv[j] == ~0u) continue;
         const uint32_t k = threadIdx.x + j * kFlowK1Threads;
-        const uint32_t d = atomicAdd(&hist[pv[j]], 1u);
+        const uint32_t d = hist.add(pv[j]);
         out[d] = base + k;
         if (P.rec_flow) P.rec_flow[base + k] = base + d;  // the record's entry (K2 fills ent_slot)
     }
@@ -722,7 +747,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     uint32_t* E = P.entries;
     uint4* CE = reinterpret_cast<uint4*>(P.comb);
     for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
-        const uint32_t grp = P.hot[h], chunk = grp >> 13, part = grp & 8191u;
+        const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
@@ -1034,27 +1059,77 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     }
     n_new = block_sum(n_new, sh);
     n_upd = block_sum(n_upd, sh);
+    // occupied slots after the update (the host grows the table from these, k_flow_finish)
+    unsigned long long occ = total != 0ull ? (FB_K2_TAGS ? tags[threadIdx.x] >= 2u : slice[(size_t)threadIdx.x * kSlotWords] >= 2ull)
+                                           : g[(size_t)threadIdx.x * 8u].x >= 2u;
+    occ = block_sum(occ, sh);
     if (threadIdx.x == 0) {
-        P.partials[2 * part] = n_new;
-        P.partials[2 * part + 1] = n_upd;
+        P.partials[3 * part] = n_new;
+        P.partials[3 * part + 1] = n_upd;
+        P.partials[3 * part + 2] = occ;
     }
 }
 
-__global__ __launch_bounds__(256) void k_flow_finish(fb_batch_stats* S, const unsigned long long* part,
-                                                     uint32_t nblk, const uint32_t* err) {
-    __shared__ unsigned long long sh[4];
-    unsigned long long a = 0ull, b = 0ull;
+__global__ __launch_bounds__(1024) void k_flow_finish(fb_batch_stats* S, const unsigned long long* part,
+                                                      uint32_t nblk, const uint32_t* err, FlowMailbox* mbox,
+                                                      unsigned long long seq) {
+    __shared__ unsigned long long sh[16];
+    unsigned long long a = 0ull, b = 0ull, o = 0ull, m = 0ull;
     for (uint32_t i = threadIdx.x; i < nblk; i += blockDim.x) {
-        a += part[2 * i];
-        b += part[2 * i + 1];
+        a += part[3 * i];
+        b += part[3 * i + 1];
+        o += part[3 * i + 2];
+        m = max(m, part[3 * i + 2]);
     }
     a = block_sum(a, sh);
     b = block_sum(b, sh);
+    o = block_sum(o, sh);
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, k, 64));
+    if ((threadIdx.x & 63u) == 0u) sh[threadIdx.x >> 6] = m;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < blockDim.x / 64u; ++w) m = max(m, sh[w]);
         S->new_sessions += a;
         S->updated_sessions += b;
         S->error |= *err;
+        if (mbox) {  // host-mapped: the occupancy first, the sequence number last (system-scope stores)
+            __hip_atomic_store(&mbox->flows, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&mbox->max_part, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&mbox->new_flows, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&mbox->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
+}
+
+// Growth by 2^k: old partition p (one workgroup, one slot per thread) splits into new partitions
+// p * 2^k .. p * 2^k + 2^k - 1 (the next k top bits of the key's hash); each key is re-inserted from
+// its unchanged home slot (low bits of the hash) by linear probing, the claim made on an LDS array
+// per new partition.
+__global__ __launch_bounds__(kFlowSlots) void k_flow_grow(const FlowSlot* old, uint32_t new_shift, uint32_t k,
+                                                          FlowSlot* nw, uint32_t* remap) {
+    extern __shared__ uint32_t claim_w[];  // [2^k][kFlowSlots]
+    const uint32_t p = blockIdx.x, i = threadIdx.x;
+    for (uint32_t j = i; j < (kFlowSlots << k); j += kFlowSlots) claim_w[j] = 0u;
+    __syncthreads();
+    const FlowSlot& o = old[(size_t)p * kFlowSlots + i];
+    uint32_t dst = ~0u;
+    if (o.tag >= 2ull) {
+        uint32_t key[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) key[k] = o.key[k];
+        const unsigned long long h = flow_hash_words(key);
+        const uint32_t b = new_shift >= 64u ? 0u : (uint32_t)(h >> new_shift) & ((1u << k) - 1u);
+        uint32_t* claim = claim_w + b * kFlowSlots;
+        uint32_t j = (uint32_t)h & (kFlowSlots - 1u);
+        while (atomicCAS(&claim[j], 0u, 1u) != 0u) j = (j + 1u) & (kFlowSlots - 1u);  // a partition holds <= 512 keys
+        dst = ((p << k) + b) * kFlowSlots + j;
+        const uint4* src = reinterpret_cast<const uint4*>(&o);
+        uint4* d = reinterpret_cast<uint4*>(nw + dst);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = src[k];
+    }
+    remap[(size_t)p * kFlowSlots + i] = dst;
 }
 
 // is_local_session! (src/sessions.rs:660-666) of a slot's key under the current configuration.
@@ -1122,19 +1197,26 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
     if (threadIdx.x == 0 && c) atomicAdd(d_n, c);
 }
 
-hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s) {
+hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
-    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), p.parts * sizeof(uint32_t), s, p);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_flow_bucket,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)part_hist_bytes(kFlowMaxParts));
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), part_hist_bytes(p.parts), s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (p.hot) {
         hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p);
         e = hipGetLastError();
-        if (e != hipSuccess) return e;
     }
+    return e;
+}
+hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s) {
+    if (chunks == 0u) chunks = 1u;
     hipLaunchKernelGGL(k_flow_transpose, dim3((p.parts + 63u) / 64u, (chunks + 63u) / 64u), dim3(256), 0, s, p,
                        chunks);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k_flow_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2Lds);
@@ -1143,8 +1225,15 @@ hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t 
     return hipGetLastError();
 }
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials, uint32_t nblk,
-                              uint32_t* error, hipStream_t s) {
-    hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(256), 0, s, stats, partials, nblk, error);
+                              uint32_t* error, FlowMailbox* mbox, unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(1024), 0, s, stats, partials, nblk, error, mbox, seq);
+    return hipGetLastError();
+}
+hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k, uint32_t new_shift, FlowSlot* nw,
+                            uint32_t* remap, hipStream_t s) {
+    if (k < 1u || k > 5u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_flow_grow, dim3(old_parts), dim3(kFlowSlots), (kFlowSlots << k) * 4u, s, old, new_shift, k, nw,
+                       remap);
     return hipGetLastError();
 }
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,

@@ -133,7 +133,9 @@ struct SegBatches {
 #define FB_FLOW_SLOTS 512
 #endif
 constexpr uint32_t kFlowSlots = FB_FLOW_SLOTS;   // slots per partition: 64 KiB LDS slice
-constexpr uint32_t kFlowMaxParts = 8192;         // K1 histogram in LDS: capacity <= 2^22 slots
+constexpr uint32_t kFlowMaxParts = 65536;        // K1 histogram in LDS (u16 counters past 16,384
+                                                 // partitions): capacity <= 2^25 slots (4 GiB)
+constexpr uint32_t kFlowPackedParts = 16384;     // more partitions than this: K1 counts in u16 halves
 #ifndef FB_FLOW_CHUNK
 #define FB_FLOW_CHUNK 20480  // 512 chunks per 10M-record C4 batch = one wave of the 512 K1 workgroups
                              // resident at once (16,384: 640 chunks, a 128-workgroup second wave;
@@ -217,7 +219,7 @@ struct FlowParams {
     uint32_t comb_cap;
     uint32_t* rows;             // [chunks][parts]  start | count << 16, per bucketing chunk
     uint32_t* cols;             // [parts][chunk_stride] the same, transposed
-    unsigned long long* partials;  // 2 per partition: new, updated
+    unsigned long long* partials;  // 3 per partition: new, updated, occupied slots after the update
     uint32_t* error;
     uint32_t max_recs;          // scratch capacity in records
     uint32_t parts;             // P (power of two)
@@ -227,7 +229,7 @@ struct FlowParams {
     uint32_t* rec_flow;         // [max_recs] per record slot: its entry position (K1, moved by K1c)
                                 // or kRecFlowCombined | combined id (for the history)
     uint32_t* ent_slot;         // [max_recs] table slot of each plain entry (K2; coalesced writes)
-    uint32_t* hot;              // [hot_cap] (chunk << 13 | part) groups K1 hands to k_flow_combine
+    uint32_t* hot;              // [hot_cap] (chunk << 16 | part) groups K1 hands to k_flow_combine
     uint32_t* ctl;              // [2] hot groups, combined entries (reset by K1t)
     uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
     uint32_t hot_cap;
@@ -270,9 +272,26 @@ hipError_t launch_seg_scan(const uint32_t* seg, uint32_t nseg, unsigned long lon
                            hipStream_t s);
 hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, uint32_t nseg, unsigned long long* pre,
                               const SegScanScratch& sc, fb_pkt_out* out, fb_dns_out* dns, hipStream_t s);
-hipError_t launch_flow_update(const FlowParams& p, uint32_t chunks, hipStream_t s);
+// One table update = launch_flow_bucket (K1 bucketing, K1c hot-group combine) then launch_flow_apply
+// (K1t transpose, K2 apply) -- two calls so the pipelined path can put them on different streams.
+hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s);
+hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s);
+// Table occupancy after an update, written by k_flow_finish into host-mapped memory so the host can
+// decide to grow the table without waiting for the device: seq = the update's number (+1).
+struct FlowMailbox {
+    unsigned long long flows;     // occupied slots
+    unsigned long long max_part;  // fullest partition (slots of kFlowSlots)
+    unsigned long long new_flows; // keys the update inserted
+    unsigned long long seq;       // written last
+};
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials,
-                              uint32_t nblk, uint32_t* error, hipStream_t s);
+                              uint32_t nblk, uint32_t* error, FlowMailbox* mbox, unsigned long long seq,
+                              hipStream_t s);
+// Table growth by 2^k (1 <= k <= 5): every slot of `old` (old_parts partitions) re-inserted into `nw`
+// (old_parts << k partitions, zeroed): a key's new partition is k more top bits of its hash, its home
+// slot the same low bits; remap[old slot] = new slot (~0u for empty slots).
+hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k, uint32_t new_shift, FlowSlot* nw,
+                            uint32_t* remap, hipStream_t s);
 // filter: fb_filter evaluated per flow at export time against `cfg` (is_local_session!,
 // src/sessions.rs:660-672); FB_FILTER_ALL (cfg may be null) exports every flow.
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,

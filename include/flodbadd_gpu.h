@@ -42,6 +42,8 @@ extern "C" {
 #define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
 #define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
 #define FB_SERVICE_BITMAP_BYTES 8192u
+#define FB_MAX_FLOW_CAPACITY (1ull << 25) /* slots: 65,536 partitions of 512 (4 GiB of table)   */
+#define FB_CFG_FIXED_TABLE 1u             /* fb_config.flags: never grow the flow table         */
 
 /* Return codes. */
 enum fb_err {
@@ -185,12 +187,17 @@ typedef struct fb_config {
     uint32_t n_lan_v6;             /* <= FB_MAX_LAN_V6                                        */
     uint32_t n_own_ips;            /* <= FB_MAX_OWN_IPS                                       */
     const fb_ip* own_ips;          /* may be NULL when n_own_ips == 0                         */
-    uint64_t flow_capacity;        /* flow-table slots: rounded up to a power of two >= 512,
-                                      at most 2^22; 0 = no table. Stored as partitions of 512
-                                      slots chosen by the key hash: a partition fills (error
-                                      bit 4) when more than 512 of its keys exist            */
+    uint64_t flow_capacity;        /* INITIAL flow-table slots: rounded up to a power of two
+                                      >= 512, at most FB_MAX_FLOW_CAPACITY; 0 = no table.
+                                      Stored as partitions of 512 slots chosen by the key hash.
+                                      The table grows (x2, rehashed on the device, before an
+                                      update call) when the occupancy the last completed updates
+                                      reported, projected over the updates still in flight,
+                                      would fill a partition: the reference's map is unbounded
+                                      (src/packets.rs:330).  A partition that still fills inside
+                                      one batch reports error bit 4 (FB_ERR_TABLE_FULL)      */
     uint32_t max_batch_packets;    /* host-mode staging capacity (packets per call)           */
-    uint32_t reserved0;
+    uint32_t flags;                /* FB_CFG_*                                                */
     uint64_t max_batch_bytes;      /* host-mode staging capacity (frame bytes per call)       */
 } fb_config;
 
@@ -534,6 +541,21 @@ int fb_flow_export_sessions(fb_ctx* ctx, uint32_t filter, fb_flow_rec* out, uint
 int fb_flow_export_sessions_dev(fb_ctx* ctx, uint32_t filter, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n,
                                 void* stream);
 int fb_flow_clear(fb_ctx* ctx, void* stream); /* clear_all_sessions, src/capture.rs:396 */
+/* Flow-table geometry and growth.  `generation` counts the growths since fb_create: each moves
+ * flows to new slots (fb_flow_rec.slot, the history's flow ids), and fb_flow_slot_remap gives the
+ * last growth's old -> new slot map (old capacity entries, 0xFFFFFFFF = empty) so a host that keys
+ * per-flow state by slot can follow.  flows / max_partition are those the last completed update
+ * reported (no device wait).  Synchronous. */
+typedef struct fb_flow_table_info {
+    uint64_t capacity;      /* slots */
+    uint64_t partitions;    /* of 512 slots */
+    uint64_t generation;    /* growths so far */
+    uint64_t flows;         /* occupied slots after the last completed update */
+    uint64_t max_partition; /* fullest partition then */
+    uint64_t reserved[3];
+} fb_flow_table_info;
+int fb_flow_table_info_get(fb_ctx* ctx, fb_flow_table_info* info);
+int fb_flow_slot_remap(fb_ctx* ctx, uint32_t* old_to_new, uint64_t cap, uint64_t* n);
 /* The table's deterministic 64-bit key hash (the reference's DashMap uses SipHash with a random
  * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */
 uint64_t fb_flow_hash(const fb_session_key* key);

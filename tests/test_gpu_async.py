@@ -116,7 +116,7 @@ def test_async_empty_batch_and_table_full():
     the context recovers for the next call."""
     import framegen as fg
     lib = N.gpu_lib()
-    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512, grow=False)
     mk = lambda k: fg.tcp_frame("10.1.%d.%d" % (k >> 8, k & 255), 40000, "8.8.8.8", 443, fg.ACK, 10)
     stream = N.Stream()
     keep = []

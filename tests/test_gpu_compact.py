@@ -130,7 +130,7 @@ def test_table_full_then_recovers():
     context processes the next batches normally (the error words are per launch and reset)."""
     from flodbadd_amd.capture import FlodbaddGpuCapture
     from flodbadd_amd.sessions import SessionFilter
-    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512, grow=False)
     try:
         mk = lambda k: fg.tcp_frame("10.1.%d.%d" % (k >> 8, k & 255), 40000, "8.8.8.8", 443, fg.ACK, 10)
         with pytest.raises(N.FbError) as ei:

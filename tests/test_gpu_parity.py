@@ -123,10 +123,11 @@ def test_flow_table_single_flow_batch(gpu_capture):
 
 
 def test_flow_table_small_capacity_and_full():
-    """flow_capacity 512 = one partition: 300 flows fit; 600 distinct flows report TABLE_FULL."""
+    """flow_capacity 512 = one partition, growth off (FB_CFG_FIXED_TABLE): 300 flows fit; 600
+    distinct flows report TABLE_FULL."""
     from flodbadd_amd.capture import FlodbaddGpuCapture
     from flodbadd_amd.sessions import SessionFilter
-    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=512, grow=False)
     try:
         mk = lambda k: fg.tcp_frame("10.1.%d.%d" % (k >> 8, k & 255), 40000, "8.8.8.8", 443, fg.ACK, 10)
         _flows_vs_oracle(cap, [fg.pack([mk(k) for k in range(300)] * 3)])
