@@ -436,7 +436,8 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                                            None))
             torch.cuda.synchronize(device)
             local = int(d_n.item())
-            return local, global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first)
+            return local, global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first,
+                                            as_tensor=True)
         flows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
         got = C.c_uint64()
         N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
@@ -462,7 +463,8 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),
                 note="per-rank fused parse+flow upsert of the rank's shard, then the table exported (to a device "
-                     "tensor with RCCL) and merged: all-gather of keys, device sort -> dense ids, all-reduces")
+                     "tensor with RCCL) and merged: records all_to_all to their Ord-range owners, owner sort + "
+                     "merge, all-gather of the merged records (left on the device)")
 
 
 def usable_cores():

@@ -42,9 +42,12 @@ struct UpdScratch {
     FlowEntry* comb = nullptr;     // k_flow_combine entries (2 units each), comb_cap of them
     uint32_t* rows = nullptr;      // [flow_chunks][flow_parts]
     uint32_t* cols = nullptr;      // [flow_parts][flow_chunks]
-    uint32_t* rec_flow = nullptr;  // [flow_recs] entry position per record slot
+    uint32_t* rows_h = nullptr;    // [flow_chunks][flow_parts] rows before k_flow_combine (history)
+    uint32_t* cols_h = nullptr;    // [flow_parts][flow_chunks]
+    uint32_t* e_orig = nullptr;    // [flow_recs] combined groups' original entry words (history)
+    uint32_t* pos_map = nullptr;   // [flow_recs] combined groups' position map (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
-    uint32_t* ctl = nullptr;       // [2] its counters
+    uint32_t* ctl = nullptr;       // [3] its counters (FlowParams::ctl)
 };
 
 struct fb_ctx {
@@ -100,7 +103,7 @@ struct fb_ctx {
     unsigned long long* d_n = nullptr;
     // ordered per-flow state: update calls since create/clear, table slot of each record slot
     uint32_t flow_batch = 0;
-    uint32_t* d_ent_slot = nullptr;       // [flow_recs] table slot per entry
+    uint32_t* d_hword = nullptr;          // [flow_recs] K2's history word per entry
     uint32_t* d_rec_part = nullptr;       // [flow_recs] partition per record slot (fb_process_seg_dev)
     const fb_pkt_out* part_recs = nullptr;  // the records part_buf was written for (one update)
     uint32_t* part_buf = nullptr;           // the partition buffer the last fused parse wrote
@@ -121,11 +124,11 @@ struct fb_ctx {
     const uint32_t* last_seg = nullptr;
     const fb_batch_stats* last_stats = nullptr;
     uint32_t last_slots = 0;
-    uint32_t* d_hkeys = nullptr;          // [hist_cap] history sort scratch
-    uint8_t* d_hvals = nullptr;
-    void* d_htemp = nullptr;
-    size_t htemp_bytes = 0;
-    uint64_t hist_cap = 0;
+    uint32_t last_chunks = 0;
+    FlowParams last_p;                    // the last update's parameters (fb_flow_history_dev)
+    uint32_t* d_hcount = nullptr;         // [table_cap] history characters per slot of the last update
+    uint32_t* d_part_base = nullptr;      // [flow_parts + 1] history output offset per partition
+    uint32_t* d_hist_slow = nullptr;      // [flow_parts + 1] count + partitions for the general history kernel
     // enrichment tables (fb_set_asn_tables / fb_set_blacklists)
     fb_asn_range* d_asn4 = nullptr;
     fb_asn_range* d_asn6 = nullptr;
@@ -217,7 +220,10 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.comb);
     hipFree(u.rows);
     hipFree(u.cols);
-    hipFree(u.rec_flow);
+    hipFree(u.rows_h);
+    hipFree(u.cols_h);
+    hipFree(u.e_orig);
+    hipFree(u.pos_map);
     hipFree(u.hot);
     hipFree(u.ctl);
     u = UpdScratch();
@@ -228,14 +234,16 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
     const uint64_t recs = c->flow_recs, chunks = recs / kFlowChunk;
     if (hipMalloc(&u.entries, recs * 4ull) != hipSuccess ||
         hipMalloc(&u.comb, (uint64_t)c->comb_cap * 2ull * sizeof(FlowEntry)) != hipSuccess ||
-        hipMalloc(&u.rec_flow, recs * 4ull) != hipSuccess ||
+        hipMalloc(&u.rows_h, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&u.cols_h, chunks * c->flow_parts * 4ull) != hipSuccess ||
+        hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.pos_map, recs * 4ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 8) != hipSuccess) {
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess) {
         free_upd_scratch(u);
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     }
-    HIP_TRY(hipMemsetAsync(u.ctl, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(u.ctl, 0, 12, s));
     return FB_OK;
 }
 
@@ -250,20 +258,20 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
     const bool had_set1 = c->us[1].entries != nullptr;
     for (UpdScratch& u : c->us) free_upd_scratch(u);
-    hipFree(c->d_ent_slot);
+    hipFree(c->d_hword);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
     hipFree(c->d_agg_slot);
     c->d_rec_part = c->d_rec_part2 = nullptr;
     c->part_recs = nullptr;
     c->part_buf = nullptr;
-    c->d_ent_slot = nullptr;
+    c->d_hword = nullptr;
     c->comb_cap = 0;
     c->d_agg_slot = nullptr;
-    c->last_recs = nullptr;  // its rec_flow is gone
+    c->last_recs = nullptr;  // its scratch is gone
     c->last_part = nullptr;
     c->flow_recs = 0;
-    if (hipMalloc(&c->d_ent_slot, recs * 4ull) != hipSuccess || hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
+    if (hipMalloc(&c->d_hword, recs * 4ull) != hipSuccess || hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     c->flow_recs = recs;
@@ -441,7 +449,10 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         c->flow_shift = 64u - lg;
         ok = hipMalloc(&c->d_table, cap * sizeof(FlowSlot)) == hipSuccess &&
              hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess &&
-             hipMalloc(&c->d_partials, 3ull * c->flow_parts * 8ull) == hipSuccess &&
+             hipMalloc(&c->d_partials, 4ull * c->flow_parts * 8ull) == hipSuccess &&
+             hipMalloc(&c->d_hcount, cap * 4ull) == hipSuccess &&
+             hipMalloc(&c->d_part_base, (c->flow_parts + 1ull) * 4ull) == hipSuccess &&
+             hipMalloc(&c->d_hist_slow, (c->flow_parts + 1ull) * 4ull) == hipSuccess &&
              hipHostMalloc((void**)&c->h_mbox, sizeof(FlowMailbox), hipHostMallocMapped) == hipSuccess &&
              hipHostGetDevicePointer((void**)&c->d_mbox, c->h_mbox, 0) == hipSuccess;
         if (ok) memset(c->h_mbox, 0, sizeof(FlowMailbox));
@@ -475,7 +486,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_remap);
     if (c->h_mbox) hipHostFree(c->h_mbox);
     hipFree(c->d_n);
-    hipFree(c->d_ent_slot);
+    hipFree(c->d_hword);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
     hipFree(c->d_agg_slot);
@@ -489,9 +500,9 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_bl4_mask);
     hipFree(c->d_bl6_pos);
     hipFree(c->d_bl6_mask);
-    hipFree(c->d_hkeys);
-    hipFree(c->d_hvals);
-    hipFree(c->d_htemp);
+    hipFree(c->d_hcount);
+    hipFree(c->d_part_base);
+    hipFree(c->d_hist_slow);
     hipFree(c->s_frames);
     hipFree(c->s_offsets);
     hipFree(c->s_out);
@@ -574,7 +585,6 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
     const uint32_t launch = pass == SegPass::kDenseOut ? c->epoch : ++c->epoch;
     p.error = c->d_error + (launch & 3u);
     p.error_next = c->d_error + ((launch + 1u) & 3u);
-    p.dbg = nullptr;
     const uint32_t waves = parse_seg_block_threads() / 64u;
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (sb.total_segs + waves - 1) / waves));
     HIP_TRY(launch_parse_seg(p, sb, grid, s, pass));
@@ -904,7 +914,18 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     FlowSlot* nw = nullptr;
     unsigned long long* partials = nullptr;
     if (hipMalloc(&nw, cap * sizeof(FlowSlot)) != hipSuccess) return set_err(FB_ERR_NOMEM, "grown flow table");
-    if (hipMalloc(&partials, 3ull * (cap / kFlowSlots) * 8ull) != hipSuccess) {
+    uint32_t *hcount = nullptr, *part_base = nullptr, *hist_slow = nullptr;
+    auto free_new = [&]() {
+        hipFree(partials);
+        hipFree(hcount);
+        hipFree(part_base);
+        hipFree(hist_slow);
+    };
+    if (hipMalloc(&partials, 4ull * (cap / kFlowSlots) * 8ull) != hipSuccess ||
+        hipMalloc(&hcount, cap * 4ull) != hipSuccess ||
+        hipMalloc(&part_base, (cap / kFlowSlots + 1ull) * 4ull) != hipSuccess ||
+        hipMalloc(&hist_slow, (cap / kFlowSlots + 1ull) * 4ull) != hipSuccess) {
+        free_new();
         hipFree(nw);
         return set_err(FB_ERR_NOMEM, "grown flow table partials");
     }
@@ -913,7 +934,7 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     c->remap_n = 0;
     if (hipMalloc(&c->d_remap, c->table_cap * 4ull) != hipSuccess) {
         hipFree(nw);
-        hipFree(partials);
+        free_new();
         return set_err(FB_ERR_NOMEM, "slot remap");
     }
     HIP_TRY(hipMemsetAsync(nw, 0, cap * sizeof(FlowSlot), s));
@@ -921,8 +942,14 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_table);
     hipFree(c->d_partials);
+    hipFree(c->d_hcount);
+    hipFree(c->d_part_base);
+    hipFree(c->d_hist_slow);
     c->d_table = nw;
     c->d_partials = partials;
+    c->d_hcount = hcount;
+    c->d_part_base = part_base;
+    c->d_hist_slow = hist_slow;
     c->remap_n = c->table_cap;
     c->table_cap = cap;
     c->flow_parts <<= k;
@@ -936,13 +963,6 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     c->flow_recs = 0;
     rc = ensure_flow_scratch(c, recs, s);
     if (!rc && had_set1) rc = alloc_upd_scratch(c, c->us[1], s);
-    hipFree(c->d_hkeys);
-    hipFree(c->d_hvals);
-    hipFree(c->d_htemp);
-    c->d_hkeys = nullptr;
-    c->d_hvals = nullptr;
-    c->d_htemp = nullptr;
-    c->hist_cap = 0;
     c->last_recs = nullptr;  // the last update's slots moved: its history is no longer available
     c->last_part = nullptr;
     return rc;
@@ -1014,8 +1034,13 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.part_shift = c->flow_shift;
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
-    p.rec_flow = u.rec_flow;
-    p.ent_slot = c->d_ent_slot;
+    p.rows_h = u.rows_h;
+    p.cols_h = u.cols_h;
+    p.e_orig = u.e_orig;
+    p.pos_map = u.pos_map;
+    p.hcount = c->d_hcount;
+    p.part_base = c->d_part_base;
+    p.hword = c->d_hword;
     p.hot = u.hot;
     p.ctl = u.ctl;
     p.agg_slot = c->d_agg_slot;
@@ -1037,6 +1062,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     c->last_seg = d_seg;
     c->last_stats = d_stats;
     c->last_slots = p.max_recs < n_slots ? p.max_recs : n_slots;
+    c->last_chunks = chunks;
+    c->last_p = p;
     return FB_OK;
 }
 
@@ -1156,39 +1183,12 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
     int jr = join_updates(c, s);
     if (jr) return jr;
     const uint32_t n = c->last_recs ? c->last_slots : 0u;
-    if (n && (!d_hist || !d_hist_slot)) return set_err(FB_ERR_INVAL, "d_hist and d_hist_slot are required");
-    if (n > c->hist_cap) {
-        HIP_TRY(hipStreamSynchronize(s));
-        hipFree(c->d_hkeys);
-        hipFree(c->d_hvals);
-        hipFree(c->d_htemp);
-        c->d_hkeys = nullptr;
-        c->d_hvals = nullptr;
-        c->d_htemp = nullptr;
-        c->hist_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(c->flow_recs, n);
-        size_t tb = 0;
-        HIP_TRY(flow_history_temp_bytes((uint32_t)cap, (uint32_t)c->table_cap, &tb));
-        if (hipMalloc(&c->d_hkeys, cap * 4ull) != hipSuccess || hipMalloc(&c->d_hvals, cap) != hipSuccess ||
-            hipMalloc(&c->d_htemp, std::max<size_t>(tb, 16)) != hipSuccess)
-            return set_err(FB_ERR_NOMEM, "history sort scratch (%llu records)", (unsigned long long)cap);
-        c->htemp_bytes = std::max<size_t>(tb, 16);
-        c->hist_cap = cap;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_n_hist, 0, 4, s));
+        return FB_OK;
     }
-    HistParams p;
-    p.recs = c->last_recs;
-    p.seg = c->last_seg;
-    p.stats = c->last_stats;
-    p.rec_flow = c->us[c->last_set].rec_flow;
-    p.ent_slot = c->d_ent_slot;
-    p.agg_slot = c->d_agg_slot;
-    p.n_slots = n;
-    p.sentinel = (uint32_t)c->table_cap;
-    p.keys = c->d_hkeys;
-    p.vals = c->d_hvals;
-    p.n_hist = d_n_hist;
-    p.rec_part = c->last_part;
-    HIP_TRY(launch_flow_history(p, c->d_htemp, c->htemp_bytes, d_hist_slot, d_hist, s));
+    if (!d_hist || !d_hist_slot) return set_err(FB_ERR_INVAL, "d_hist and d_hist_slot are required");
+    HIP_TRY(launch_flow_history(c->last_p, c->last_chunks, d_hist_slot, d_hist, d_n_hist, c->d_hist_slow, s));
     return FB_OK;
 }
 

@@ -113,6 +113,43 @@ __device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, 
     e[3] = make_uint4(m.y, rec, hinfo, (uint32_t)flow_hash_words(key));
 }
 
+// FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character), branch-free (a
+// switch here compiled to a divergent compare tree of ~100 scalar mask instructions per entry):
+// c & 31 tells the classes apart (S H F R A and > < -), c >= 96 marks the responder's lower-case
+// letter (bit + 1), and the result is checked against the table "SsHhFfRr><Aa-".
+constexpr unsigned long long hist_nibbles(uint32_t half) {
+    const char cs[8] = {'S', 'H', 'F', 'R', '>', '<', 'A', '-'};
+    const uint32_t bs[8] = {0u, 2u, 4u, 6u, 8u, 9u, 10u, 12u};
+    unsigned long long v = ~0ull;
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t k = (uint32_t)cs[j] & 31u;
+        if ((k >> 4) == half) v = (v & ~(15ull << (4u * (k & 15u)))) | ((unsigned long long)bs[j] << (4u * (k & 15u)));
+    }
+    return v;
+}
+constexpr unsigned long long hist_chars(uint32_t half) {
+    const char t[13] = {'S', 's', 'H', 'h', 'F', 'f', 'R', 'r', '>', '<', 'A', 'a', '-'};
+    unsigned long long v = 0ull;
+    for (uint32_t j = 8u * half; j < 8u * half + 8u && j < 13u; ++j) v |= (unsigned long long)(uint8_t)t[j] << (8u * (j & 7u));
+    return v;
+}
+__device__ __forceinline__ uint32_t hist_bit(uint32_t c) {
+    constexpr unsigned long long kN0 = hist_nibbles(0), kN1 = hist_nibbles(1), kC0 = hist_chars(0), kC1 = hist_chars(1);
+    const uint32_t k = c & 31u;
+    const uint32_t nib = (uint32_t)(((k < 16u ? kN0 : kN1) >> (4u * (k & 15u))) & 15u);
+    const uint32_t b = nib + (c >= 96u ? 1u : 0u);
+    const uint32_t want = (uint32_t)(((b < 8u ? kC0 : kC1) >> (8u * (b & 7u))) & 0xFFu);
+    return (nib != 15u && b < 13u && want == c) ? b : 16u;
+}
+
+// The entry word's history code of a record: 0 without history character (not TCP), else 1 + the
+// FB_HIST_CHARS index of its map_tcp_flags character (hist_char | tcp_flags << 8 | has_flags << 16
+// as in FlowEntry word 14, or the fused parse's partition word: char << 16 | has_flags << 24).
+__device__ __forceinline__ uint32_t hist_code(uint32_t has_flags, uint32_t ch) {
+    const uint32_t b = hist_bit(ch);
+    return has_flags && b < 13u ? b + 1u : 0u;
+}
+
 // K1's LDS histogram / cursors: one u32 per partition, or (more than kFlowPackedParts partitions)
 // two u16 halves per word -- a chunk holds < 2^16 records, so no half carries into the other.
 struct PartHist {
@@ -169,19 +206,22 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
             for (uint32_t j = 0; j < kPer; ++j) {
                 const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
                 sw[j] = P.seg[(base + k) >> 6];
-                pv[j] = P.rec_part[base + k] & kRecPartMask;
+                pv[j] = P.rec_part[base + k];
             }
         } else {
 #pragma unroll
             for (uint32_t j = 0; j < kPer; ++j) {
                 const uint32_t k = min(threadIdx.x + j * kFlowK1Threads, cnt - 1u);
                 sw[j] = 0xFFFFu;
-                pv[j] = P.rec_part[base + k] & kRecPartMask;
+                pv[j] = P.rec_part[base + k];
             }
         }
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t k = threadIdx.x + j * kFlowK1Threads;
+            // partition | history code << 16 (the parse's word: partition | char << 16 | has_flags << 24)
+            const uint32_t w = pv[j];
+            pv[j] = (w & kRecPartMask) | hist_code((w >> 24) & 1u, (w >> 16) & 0xFFu) << 16;
             if (!(k < cnt && ((base + k) & 63u) < (sw[j] & 0xFFFFu))) pv[j] = ~0u;
         }
     } else {            // hashed here, four records' key loads in flight at a time
@@ -190,6 +230,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         for (uint32_t j0 = 0; j0 < kPer; j0 += kG) {
             uint4 a[kG], b[kG];
             uint2 c[kG];
+            uint32_t m[kG];
             bool ok[kG];
 #pragma unroll
             for (uint32_t u = 0; u < kG; ++u) {
@@ -199,19 +240,21 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
                 a[u] = ld_u4(r);
                 b[u] = ld_u4(r + 4);
                 c[u] = ld_u2(r + 8);
+                m[u] = r[12];  // flags | meta << 8 | hist_char << 16
             }
 #pragma unroll
             for (uint32_t u = 0; u < kG; ++u) {
                 const uint32_t key[10] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w, c[u].x,
                                           c[u].y & 0xFFFFu};
-                pv[j0 + u] = ok[u] ? part_of(flow_hash_words(key), P.part_shift) : ~0u;
+                const uint32_t code = hist_code((m[u] >> 8) & FB_META_HAS_FLAGS, (m[u] >> 16) & 0xFFu);
+                pv[j0 + u] = ok[u] ? part_of(flow_hash_words(key), P.part_shift) | code << 16 : ~0u;
             }
         }
     }
     __syncthreads();  // hist zeroed
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j)
-        if (pv[j] != ~0u) hist.add(pv[j]);
+        if (pv[j] != ~0u) hist.add(pv[j] & kRecPartMask);
     __syncthreads();
     // exclusive scan of hist[0..parts): each thread owns E consecutive partitions
     const uint32_t E = (P.parts + kFlowK1Threads - 1u) / kFlowK1Threads;
@@ -221,6 +264,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     uint32_t total;
     uint32_t run = block_excl_scan(local, wsum, total);
     uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
+    uint32_t* row_h = P.rows_h + (size_t)blockIdx.x * P.parts;
     const uint32_t hot_min = max(kCombMin, 4u * ((cnt + P.parts - 1u) / P.parts));
     static_assert(kFlowMaxParts / kFlowK1Threads <= 64u, "a thread's partitions fit the hot mask");
     unsigned long long hot = 0ull;  // this thread's hot groups (bit j - j0), handed to k_flow_combine
@@ -228,6 +272,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
         const uint32_t c = hist.get(j);
         row[j] = run | (c << 16);
+        row_h[j] = run | (c << 16);
         if (c >= hot_min) {
             hot |= 1ull << (j - j0);
             ++n_hot;
@@ -249,15 +294,15 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         }
     }
     __syncthreads();
-    // scatter: entry position -> the record's slot index (4 B); K2 gathers the record itself
+    // scatter: entry position -> the record's slot index | its history code (4 B); K2 gathers the
+    // record itself
     uint32_t* out = P.entries + base;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (pv[j] == ~0u) continue;
         const uint32_t k = threadIdx.x + j * kFlowK1Threads;
-        const uint32_t d = hist.add(pv[j]);
-        out[d] = base + k;
-        if (P.rec_flow) P.rec_flow[base + k] = base + d;  // the record's entry (K2 fills ent_slot)
+        const uint32_t d = hist.add(pv[j] & kRecPartMask);
+        out[d] = (base + k) | (pv[j] >> 16) << kEntCodeShift;
     }
 }
 
@@ -270,15 +315,21 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
     if (P.ctl && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // k_flow_combine is done with them
         P.ctl[0] = 0u;
         P.ctl[1] = 0u;
+        P.ctl[2] = 0u;
     }
-    for (uint32_t y = ty; y < 64u; y += 4u) {
-        const uint32_t c = c0 + y, p = p0 + tx;
-        tile[y][tx] = (c < chunks && p < P.parts) ? P.rows[(size_t)c * P.parts + p] : 0u;
-    }
-    __syncthreads();
-    for (uint32_t y = ty; y < 64u; y += 4u) {
-        const uint32_t p = p0 + y, c = c0 + tx;
-        if (p < P.parts && c < chunks) P.cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
+    for (int h = 0; h < 2; ++h) {  // rows -> cols (K2), rows_h -> cols_h (the history)
+        const uint32_t* rows = h ? P.rows_h : P.rows;
+        uint32_t* cols = h ? P.cols_h : P.cols;
+        for (uint32_t y = ty; y < 64u; y += 4u) {
+            const uint32_t c = c0 + y, p = p0 + tx;
+            tile[y][tx] = (c < chunks && p < P.parts) ? rows[(size_t)c * P.parts + p] : 0u;
+        }
+        __syncthreads();
+        for (uint32_t y = ty; y < 64u; y += 4u) {
+            const uint32_t p = p0 + y, c = c0 + tx;
+            if (p < P.parts && c < chunks) cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
+        }
+        __syncthreads();
     }
 }
 
@@ -319,35 +370,6 @@ constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount 
 
 __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character), branch-free (a
-// switch here compiled to a divergent compare tree of ~100 scalar mask instructions per entry):
-// c & 31 tells the classes apart (S H F R A and > < -), c >= 96 marks the responder's lower-case
-// letter (bit + 1), and the result is checked against the table "SsHhFfRr><Aa-".
-constexpr unsigned long long hist_nibbles(uint32_t half) {
-    const char cs[8] = {'S', 'H', 'F', 'R', '>', '<', 'A', '-'};
-    const uint32_t bs[8] = {0u, 2u, 4u, 6u, 8u, 9u, 10u, 12u};
-    unsigned long long v = ~0ull;
-    for (int j = 0; j < 8; ++j) {
-        const uint32_t k = (uint32_t)cs[j] & 31u;
-        if ((k >> 4) == half) v = (v & ~(15ull << (4u * (k & 15u)))) | ((unsigned long long)bs[j] << (4u * (k & 15u)));
-    }
-    return v;
-}
-constexpr unsigned long long hist_chars(uint32_t half) {
-    const char t[13] = {'S', 's', 'H', 'h', 'F', 'f', 'R', 'r', '>', '<', 'A', 'a', '-'};
-    unsigned long long v = 0ull;
-    for (uint32_t j = 8u * half; j < 8u * half + 8u && j < 13u; ++j) v |= (unsigned long long)(uint8_t)t[j] << (8u * (j & 7u));
-    return v;
-}
-__device__ __forceinline__ uint32_t hist_bit(uint32_t c) {
-    constexpr unsigned long long kN0 = hist_nibbles(0), kN1 = hist_nibbles(1), kC0 = hist_chars(0), kC1 = hist_chars(1);
-    const uint32_t k = c & 31u;
-    const uint32_t nib = (uint32_t)(((k < 16u ? kN0 : kN1) >> (4u * (k & 15u))) & 15u);
-    const uint32_t b = nib + (c >= 96u ? 1u : 0u);
-    const uint32_t want = (uint32_t)(((b < 8u ? kC0 : kC1) >> (8u * (b & 7u))) & 0xFFu);
-    return (nib != 15u && b < 13u && want == c) ? b : 16u;
 }
 
 // determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
@@ -568,8 +590,7 @@ __device__ __forceinline__ int k2_find_insert(unsigned long long* slice, uint32_
 
 // Returns 1 if the key was inserted, 0 if it existed; -1 if the partition is full/spin expired.
 __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* tags, uint32_t* scr, const uint4 e0, const uint4 e1,
-                                           const uint4 e2, const uint4 e3, uint32_t slot_base, uint32_t* ent_slot,
-                                           uint32_t idx, uint32_t* err) {
+                                           const uint4 e2, const uint4 e3, uint32_t& slot, uint32_t* err) {
     const uint32_t orig = (e2.y >> 16) & 1u;
     const uint32_t key[10] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y & 0xFFFFu};
     uint32_t i;
@@ -583,11 +604,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     atomicAdd(s + 6 + (orig ? 0 : 1), (unsigned long long)e2.z);
     atomicAdd(s + 8 + (orig ? 0 : 1), 1ull);
     atomicAdd(s + 10 + (orig ? 0 : 1), (unsigned long long)e2.w);
-    if (ent_slot) ent_slot[idx] = slot_base + i;
-#ifdef FB_NO_ORDERED  // ablation: counters only
-    (void)scr;
-    return result;
-#endif
+    slot = i;
     // ordered state into the batch scratch (see above)
     uint32_t* q = scr + (size_t)i * kScrU32;
     const uint32_t rec = e3.y;
@@ -607,7 +624,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
 }
 
 // A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
-// the group's partial sums / minima / maxima.  Its records' rec_flow point at agg_slot[id].
+// the group's partial sums / minima / maxima.  Its records' pos_map words point at agg_slot[id].
 __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr, const uint4 e0, const uint4 e1,
                                               const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
                                               const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
@@ -634,10 +651,6 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
         atomicAdd(s + 11, ri);
     }
     if (agg_slot) agg_slot[e3.x] = slot_base + i;
-#ifdef FB_NO_ORDERED
-    (void)scr;
-    return result;
-#endif
     uint32_t* q = scr + (size_t)i * kScrU32;
     atomicMin(q + kScFirst, e2.z);
     atomicMax(q + kScLast, e2.w);
@@ -749,6 +762,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
         const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
+        uint32_t* rowp_h = P.rows_h + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
         for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
@@ -763,7 +777,9 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         // reduce per key (a key the table cannot take stays a plain entry)
         for (uint32_t k = threadIdx.x; k < cnt; k += kCombThreads) {
             uint4 e[4];
-            rec_entry(P.recs, E[s0 + k], e);
+            const uint32_t w = E[s0 + k];
+            P.e_orig[s0 + k] = w;  // the group's original words stay readable for the history
+            rec_entry(P.recs, w & kEntRecMask, e);
             const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                       e[2].y & 0xFFFFu};
             uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
@@ -828,13 +844,13 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
                 if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
                     uint4 e[4];
-                    rec_entry(P.recs, rec, e);
+                    rec_entry(P.recs, rec & kEntRecMask, e);
                     const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                               e[2].y & 0xFFFFu};
                     j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
                 }
                 if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) {
-                    if (P.rec_flow) P.rec_flow[rec] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                    P.pos_map[s0 + k] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
                 } else {
                     keep = 1u;
                 }
@@ -842,7 +858,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint32_t kept;
             const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
             if (keep) {
-                if (P.rec_flow) P.rec_flow[rec] = (uint32_t)(s0 + cursor + pos);  // the entry moved
+                P.pos_map[s0 + k] = (uint32_t)(s0 + cursor + pos);  // the entry moved
                 E[s0 + cursor + pos] = rec;
             }
             cursor += kept;
@@ -867,7 +883,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta]);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
-        if (threadIdx.x == 0) *rowp = (row & 0xFFFFu) | ((cursor + n_comb) << 16);
+        if (threadIdx.x == 0) {
+            *rowp = (row & 0xFFFFu) | ((cursor + n_comb) << 16);
+            *rowp_h |= 0x8000u;  // a combined group: the history reads e_orig / pos_map here
+        }
         __syncthreads();  // the table is re-initialised for the next group
     }
 }
@@ -878,6 +897,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     __shared__ uint32_t ss[kK2Cpt * kFlowK2Threads];
     __shared__ uint32_t wsum[kFlowK2Threads / 64];
     __shared__ unsigned long long sh[kFlowK2Threads / 64];
+    __shared__ uint32_t s_hbase;
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
     uint32_t* scr = reinterpret_cast<uint32_t*>(slice + (size_t)kFlowSlots * kSlotWords);
     uint32_t* tags = scr + (size_t)kFlowSlots * kScrU32;  // FB_K2_TAGS: the slots' probe tags
@@ -905,15 +925,11 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     auto load_slice = [&]() {
         ord0 = g[(size_t)threadIdx.x * 8u + 6u];
         ord1 = g[(size_t)threadIdx.x * 8u + 7u];
-#ifndef FB_K2_NO_SLICEIO
-        if (FB_K2_TAGS) tag0 = reinterpret_cast<const uint32_t*>(g + (size_t)threadIdx.x * 8u)[0];  // ablation (timing only): no slice load / write-back
+        if (FB_K2_TAGS) tag0 = reinterpret_cast<const uint32_t*>(g + (size_t)threadIdx.x * 8u)[0];
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
             slice4[j] = g[(size_t)sl * (sizeof(FlowSlot) / 16u) + w];
         }
-#else
-        for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) slice4[j] = make_uint4(0, 0, 0, 0);
-#endif
     };
     // a batch with >= 32 record slots per partition touches nearly every partition: the slice
     // load is issued with the group rows, before the partition's total is known (one round trip
@@ -925,6 +941,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     if (dense) load_slice();
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
+    uint32_t hbase_out = 0u;
     if (total != 0ull) {
         if (!dense) load_slice();
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
@@ -932,7 +949,11 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
         }
         if (FB_K2_TAGS) tags[threadIdx.x] = tag0;
+        if (threadIdx.x == 0) s_hbase = atomicAdd(P.ctl + 2, (uint32_t)total);  // the history words' range
         __syncthreads();
+        const uint32_t hbase = s_hbase;
+        hbase_out = hbase;
+        uint32_t rbase = 0u;  // entries of the earlier rounds
         const uint32_t* E = P.entries;
         const uint4* CE = reinterpret_cast<const uint4*>(P.comb);
         for (uint32_t g0 = 0; g0 < chunks; g0 += kK2Cpt * kFlowK2Threads) {
@@ -977,11 +998,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     r[2] = c[2];
                     r[3] = c[3];
                 } else {  // a record slot of the batch (56 B, 8-B aligned at odd slots)
-#ifdef FB_K2_LOCAL_GATHER  // ablation (timing only): gather from a cache-resident window
-                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (v & 0xFFFFu));
-#else
-                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + v);
-#endif
+                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (v & kEntRecMask));
                     r[0] = ld_u4(q);
                     r[1] = ld_u4(q + 4);
                     r[2] = ld_u4(q + 8);
@@ -1025,11 +1042,14 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
                     const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) |
                                            ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0xFu) << 20;
+                    uint32_t sl = ~0u;
                     const int r = apply_entry(slice, tags, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
-                                              make_uint4(my, v0, hinfo, (uint32_t)flow_hash_words(key)),
-                                              part * kFlowSlots, P.rec_flow ? P.ent_slot : nullptr, ix0, P.error);
+                                              make_uint4(my, v0 & kEntRecMask, hinfo, (uint32_t)flow_hash_words(key)), sl,
+                                              P.error);
                     n_new += r == 1;
                     n_upd += r == 0;
+                    // the history word (layout: fb_internal.h), in this partition's entry order
+                    P.hword[hbase + rbase + e] = r < 0 ? 0u : hist_word(sl, v0);
                 }
 #pragma unroll
                 for (uint32_t w = 0; w < 4u; ++w) r0[w] = r1[w];
@@ -1038,24 +1058,17 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 ix1 = ix2;
                 v1 = v2;
             }
+            rbase += tot;
             __syncthreads();
         }
-#ifndef FB_K2_NO_FINISH  // ablation (timing only): no ordered-field fold
         finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.recs, P.batch, ord0, ord1);
-#endif
-#ifndef FB_K2_NO_SLICEIO
         // only the slots this batch touched (inserted or updated) changed; the others' heads are
         // not written back (a 96-B head alone is a partial line)
         uint4* gw = reinterpret_cast<uint4*>(T);
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
-#ifdef FB_NO_ORDERED  // (the ablation keeps no scratch: every head is written)
-            gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
-#else
             if (scr[(size_t)sl * kScrU32 + kScFirst] != ~0u) gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
-#endif
         }
-#endif
     }
     n_new = block_sum(n_new, sh);
     n_upd = block_sum(n_upd, sh);
@@ -1063,10 +1076,15 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     unsigned long long occ = total != 0ull ? (FB_K2_TAGS ? tags[threadIdx.x] >= 2u : slice[(size_t)threadIdx.x * kSlotWords] >= 2ull)
                                            : g[(size_t)threadIdx.x * 8u].x >= 2u;
     occ = block_sum(occ, sh);
+    // history characters per slot this update (the history's output offsets), and their total
+    const uint32_t hc = total != 0ull ? scr[(size_t)threadIdx.x * kScrU32 + kScCount] : 0u;
+    P.hcount[(size_t)part * kFlowSlots + threadIdx.x] = hc;
+    const unsigned long long hcs = block_sum((unsigned long long)hc, sh);
     if (threadIdx.x == 0) {
-        P.partials[3 * part] = n_new;
-        P.partials[3 * part + 1] = n_upd;
-        P.partials[3 * part + 2] = occ;
+        P.partials[4 * part] = n_new;
+        P.partials[4 * part + 1] = n_upd;
+        P.partials[4 * part + 2] = occ;
+        P.partials[4 * part + 3] = hcs | (unsigned long long)hbase_out << 32;
     }
 }
 
@@ -1076,10 +1094,10 @@ __global__ __launch_bounds__(1024) void k_flow_finish(fb_batch_stats* S, const u
     __shared__ unsigned long long sh[16];
     unsigned long long a = 0ull, b = 0ull, o = 0ull, m = 0ull;
     for (uint32_t i = threadIdx.x; i < nblk; i += blockDim.x) {
-        a += part[3 * i];
-        b += part[3 * i + 1];
-        o += part[3 * i + 2];
-        m = max(m, part[3 * i + 2]);
+        a += part[4 * i];
+        b += part[4 * i + 1];
+        o += part[4 * i + 2];
+        m = max(m, part[4 * i + 2]);
     }
     a = block_sum(a, sh);
     b = block_sum(b, sh);

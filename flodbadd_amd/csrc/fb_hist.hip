@@ -2,105 +2,485 @@
 //
 // The reference appends map_tcp_flags(..) to the flow's `history` String for every TCP packet
 // (src/packets.rs:187-198 occupied, 410-426 vacant), so a flow's history is its TCP packets'
-// characters in arrival order.  k_flow_apply (fb_flow.hip) records the table slot of every
-// record slot of the batch via `rec_flow` (entry position) and `ent_slot` / `agg_slot`; here the batch's TCP records are stably sorted by that
-// slot, which groups each flow's characters into one run while keeping packet order inside it:
-//   k_hist_keys : key[i] = rec_flow[i] for a valid record with FB_META_HAS_FLAGS, else the
-//                 sentinel (= table capacity, sorts last); value[i] = the record's hist_char;
-//                 counts the keyed records into *n_hist.
-//   radix sort  : rocPRIM's stable LSD radix sort over log2(capacity)+1 key bits, pairs
-//                 (u32 slot, u8 char) -> the caller's d_hist_slot / d_hist.
-// Bytes per record: 4 (the fused parse's per-record word -- partition, history character,
-// has_flags -- or, without it, the record's word 12, which at 56-B stride costs its sector) + 4
-// (rec_flow) read, 5 written, then the sort's passes.  C4: 160 -> 92 us with the fused word.
-#include <algorithm>
-
-#include <rocprim/device/device_radix_sort.hpp>
-
+// characters in arrival order.  fb_flow_history_dev returns the last update's characters grouped
+// per flow: a stable sort of its TCP records by table slot.  No global sort is needed: the update
+// already bucketed every record by table partition (= slot / 512), and k_flow_apply left one
+// history word per entry it applied (slot in the partition | character code | record within its
+// bucketing chunk), each partition's words contiguous and in chunk (= record) order:
+//   k_hist_scan : exclusive scan of the per-partition character counts k_flow_apply reported
+//                 (partials[4 p + 3]) -> each partition's output offset; the total -> *n_hist.
+//   k_hist_part<true> : one workgroup per partition, for a partition of one chunk round, at most
+//                 kHistCap entries, no combined group and no chunk run over kRunSort entries (the
+//                 uniform case; others are listed for the general kernel):
+//                 1. thread t sorts chunk run t by record in registers (K1's scatter leaves a run
+//                    unordered) into LDS at the run's place: the partition is then in record order;
+//                 2. wave w takes a contiguous eighth, 64 entries a step: the lanes holding one
+//                    slot find each other (a ballot per slot bit) and the lowest adds their count
+//                    to the wave's count of the slot;
+//                 3. per slot, a scan over the waves from the slot's offset (hcount scanned);
+//                 4. the walk again: a key's output position = its wave's position for the slot +
+//                    the slot's lanes below it in the step; the lowest lane moves it on.  Stable by
+//                    record without a comparison sort; the output is staged in LDS and written
+//                    coalesced.
+//   k_hist_part<false> : the listed partitions, a grid-stride loop: chunk rounds of 512 runs,
+//                 batches of at most kHistCap entries; a run k_flow_combine folded (a hot group)
+//                 is read from its original entry words (e_orig), each record's slot from the
+//                 combined entry's agg_slot or, for a record left plain, the word of its moved
+//                 entry (pos_map).  A batch is counting-sorted by slot in LDS; a record's place in
+//                 its slot's run is the number of the slot's records of the batch before it (a
+//                 scan of the slot's bucket), or -- a slot with more than kHistScan records in the
+//                 batch, or a run longer than kHistCap taken in record windows -- its index after
+//                 a bitonic sort of the batch by (slot, record).
+// Bytes per entry: its 4-B history word read; per character 5 B written (+ the count arrays).
 #include "fb_internal.h"
 
 namespace fbk {
 
-__global__ __launch_bounds__(256) void k_hist_keys(const HistParams P) {
-    __shared__ uint32_t wcnt[4];
-    const uint32_t n = P.seg ? P.n_slots : (uint32_t)min(P.stats->n_session, (unsigned long long)P.n_slots);
-    uint32_t cnt = 0u;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P.n_slots; i += stride) {
-        bool keyed = false;
-        uint32_t ch = 0u;
-        if (i < n && (!P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu))) {
-            if (P.rec_part) {  // the fused parse's word: 4 B per slot instead of the 56-B record's word 12
-                const uint32_t w = P.rec_part[i];
-                keyed = (w >> 24) & 1u;
-                ch = (w >> 16) & 0xFFu;
-            } else {
-                const uint32_t w = reinterpret_cast<const uint32_t*>(P.recs + i)[12];  // flags|meta|hist_char
-                keyed = ((w >> 8) & FB_META_HAS_FLAGS) != 0u;
-                ch = (w >> 16) & 0xFFu;
+constexpr uint32_t kHistThreads = 512;
+#ifndef FB_HIST_CAP
+#define FB_HIST_CAP 4096
+#endif
+constexpr uint32_t kHistCap = FB_HIST_CAP;  // entries per batch (8 B of LDS each)
+constexpr uint32_t kHistRuns = 512;         // chunk runs per round: one per thread
+constexpr uint32_t kHistScan = 64;          // (general) a slot with more records in a batch takes the sort
+constexpr uint32_t kRunSort = 16;           // (uniform) the longest chunk run sorted in registers
+constexpr uint32_t kHistWaves = kHistThreads / 64;
+constexpr uint32_t kHistPer = kHistCap / kHistThreads;
+static_assert(kFlowSlots == kHistThreads && kHistRuns == kHistThreads, "one slot / run per thread");
+static_assert(kHistWaves * kFlowSlots <= kHistCap, "the waves' slot counts share the keys' LDS");
+
+// History character of a code (1 + FB_HIST_CHARS index) from two packed constants: no table load.
+__device__ __forceinline__ uint8_t hist_char_of(uint32_t code) {
+    constexpr unsigned long long kLo = 0x5266466848735300ull;  // "\0SsHhFfR", byte k = code k
+    constexpr unsigned long long kHi = 0x2D61413C3E72ull;    // "r><Aa-", byte k = code 8 + k
+    return (uint8_t)(((code < 8u) ? kLo : kHi) >> (8u * (code & 7u)));
+}
+
+// Ascending bitonic network over a[0 .. N) (registers: every index is a constant once unrolled).
+template <int N>
+__device__ __forceinline__ void sort_net(uint32_t (&a)[kRunSort]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint32_t x = a[i], y = a[l], lo = min(x, y), hi = max(x, y);
+                    const bool up = (i & k) == 0;
+                    a[i] = up ? lo : hi;
+                    a[l] = up ? hi : lo;
+                }
             }
         }
-        uint32_t slot = P.sentinel;
-        if (keyed) {
-            const uint32_t v = P.rec_flow[i];  // entry position, or a k_flow_combine id
-            slot = (v & kRecFlowCombined) ? P.agg_slot[v & ~kRecFlowCombined] : P.ent_slot[v];
-        }
-        P.keys[i] = slot;
-        P.vals[i] = (uint8_t)ch;
-        cnt += keyed;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if ((threadIdx.x & 63u) == 0u) wcnt[threadIdx.x >> 6] = cnt;
-    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* partials, uint32_t parts,
+                                                    uint32_t* part_base, uint32_t* n_hist, uint32_t* slow) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
     if (threadIdx.x == 0) {
-        const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        if (t) atomicAdd(P.n_hist, t);
+        carry = 0u;
+        slow[0] = 0u;  // k_hist_part<true> lists the partitions it leaves to k_hist_part<false>
+    }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < parts; b0 += 1024u) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < parts ? (uint32_t)partials[4 * (size_t)i + 3] : 0u;
+        uint32_t x = v;
+        const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63u) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry;
+        for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+        if (i < parts) part_base[i] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023u) carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part_base[parts] = carry;
+        *n_hist = carry;
     }
 }
 
-#ifndef FB_HIST_RADIX_BITS
-#define FB_HIST_RADIX_BITS 0  // 0: rocPRIM's gfx950 default (8 bits per onesweep pass)
-#endif
-#ifndef FB_HIST_SORT_BLOCK
-#define FB_HIST_SORT_BLOCK 1024
-#endif
-#ifndef FB_HIST_SORT_IPT
-#define FB_HIST_SORT_IPT 8
-#endif
-#if FB_HIST_RADIX_BITS
-using HistSortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
-                                        rocprim::kernel_config<FB_HIST_SORT_BLOCK, FB_HIST_SORT_IPT>,
-                                        FB_HIST_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-#else
-using HistSortConfig = rocprim::default_config;
-#endif
+struct HistLds {
+    unsigned long long keys[kHistCap];  // (general) batch keys; (uniform) run-sorted keys + wave counts
+    uint32_t cursor[kFlowSlots], bcnt[kFlowSlots], boff[kFlowSlots];
+    uint32_t rs[kHistRuns];      // run r (chunk c0 + r): its first entry position
+    uint32_t rn[kHistRuns];      // its entries to read (bit 31: a combined group, e_orig)
+    uint32_t rp[kHistRuns + 1];  // exclusive prefix of rn
+    uint32_t rq[kHistRuns];      // the history word of its first applied entry
+    uint32_t wsum[kHistThreads / 64], wsum2[kHistThreads / 64];
+    uint32_t s_n;
+};
 
-static uint32_t key_bits(uint32_t sentinel) {
-    uint32_t b = 1u;
-    while (b < 32u && (1ull << b) <= sentinel) ++b;
-    return b;
+template <bool kUniform>
+__global__ __launch_bounds__(kHistThreads) void k_hist_part(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
+                                                            uint8_t* out_char, uint32_t* slow) {
+    __shared__ HistLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    // block-wide exclusive sums of one or two values per thread (tot: the sum)
+    auto block_scan2 = [&](uint32_t v, uint32_t v2, uint32_t& tot, uint32_t& ex2, uint32_t& tot2) {
+        uint32_t x = v, x2 = v2;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64), y2 = __shfl_up(x2, o, 64);
+            if (lane >= (uint32_t)o) {
+                x += y;
+                x2 += y2;
+            }
+        }
+        if (lane == 63u) {
+            L.wsum[wave] = x;
+            L.wsum2[wave] = x2;
+        }
+        __syncthreads();
+        uint32_t before = 0u, before2 = 0u;
+        tot = tot2 = 0u;
+        for (uint32_t k = 0; k < kHistThreads / 64u; ++k) {
+            const uint32_t s = L.wsum[k], s2 = L.wsum2[k];
+            if (k < wave) {
+                before += s;
+                before2 += s2;
+            }
+            tot += s;
+            tot2 += s2;
+        }
+        __syncthreads();
+        ex2 = before2 + x2 - v2;
+        return before + x - v;
+    };
+    auto block_scan = [&](uint32_t v, uint32_t& tot) {
+        uint32_t ex2, tot2;
+        return block_scan2(v, 0u, tot, ex2, tot2);
+    };
+
+    auto partition = [&](uint32_t q) {
+        // every load the first round needs, issued together: the partition's character count and
+        // history-word base, its output range, its slots' counts, the first round's group rows
+        const unsigned long long pw = P.partials[4 * (size_t)q + 3];
+        const uint32_t out_beg = P.part_base[q], out_end = P.part_base[q + 1];
+        const uint32_t hc = P.hcount[(size_t)q * kFlowSlots + tid];
+        const uint32_t* col = P.cols + (size_t)q * P.chunk_stride;
+        const uint32_t* col_h = P.cols_h + (size_t)q * P.chunk_stride;
+        uint32_t vp = tid < chunks ? col[tid] : 0u, vh = tid < chunks ? col_h[tid] : 0u;
+        const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
+        if (n_chars == 0u) return;  // uniform: no history characters in this partition
+        {
+            uint32_t t;
+            L.cursor[tid] = block_scan(hc, t);  // relative to out_beg
+            L.bcnt[tid] = 0u;
+        }
+        uint32_t carry = hbase;  // history word of the round's first applied entry
+        // round setup: the runs of chunks c0 .. c0 + 511 (tid: run tid); returns the entries read
+        auto round = [&](uint32_t c0, uint32_t nr) {
+            const uint32_t c = c0 + tid;
+            const bool comb = tid < nr && (vh & 0x8000u) != 0u;
+            const uint32_t lp = tid < nr ? vp >> 16 : 0u, lv = comb ? vh >> 16 : lp;  // applied / read entries
+            L.rs[tid] = c * kFlowChunk + (vp & 0xFFFFu);  // (k_flow_combine packs a group in place)
+            L.rn[tid] = lv | (comb ? 1u << 31 : 0u);
+            uint32_t tv, tp, ep;
+            const uint32_t ev = block_scan2(lv, lp, tv, ep, tp);
+            L.rp[tid] = ev;
+            L.rq[tid] = carry + ep;
+            if (tid == 0) L.rp[kHistRuns] = tv;
+            carry += tp;
+            __syncthreads();
+            return tv;
+        };
+        const uint32_t nr0 = min(kHistRuns, chunks);
+        const uint32_t tv0 = round(0u, nr0);
+        if constexpr (kUniform) {
+            const uint32_t len = L.rn[tid];  // bit 31 (combined) makes it > kRunSort
+            if (__syncthreads_or(len > kRunSort) || chunks > kHistRuns || tv0 > kHistCap) {  // uniform
+                if (tid == 0) slow[1u + atomicAdd(slow, 1u)] = q;
+                return;
+            }
+            uint32_t* skeys = reinterpret_cast<uint32_t*>(L.keys);  // run-sorted keys, then the output
+            uint32_t* hist = skeys + kHistCap;                        // [wave][slot] counts / positions
+            for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) hist[j] = 0u;
+            {   // 1. run tid in record order: key = record in chunk << 13 | slot << 4 | code
+                uint32_t a[kRunSort];
+                // unpredicated buffer loads (a predicated load waits alone): all in flight at once,
+                // words past the array read 0, words past the run are masked
+                const __amdgpu_buffer_rsrc_t rh =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)P.hword, (short)0, (int)(P.max_recs * 4u), 0x00020000);
+                const uint32_t vo = L.rq[tid] * 4u;
+#pragma unroll
+                for (uint32_t k = 0; k < kRunSort; ++k) a[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, vo + 4u * k, 0, 0);
+#pragma unroll
+                for (uint32_t k = 0; k < kRunSort; ++k)
+                    a[k] = k < len ? (a[k] >> 13) << 13 | (a[k] & 0x1FFu) << 4 | ((a[k] >> 9) & 15u) : ~0u;
+                uint32_t wl = len;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+                if (wl > 8u) sort_net<16>(a);
+                else if (wl > 4u) sort_net<8>(a);
+                else if (wl > 1u) sort_net<4>(a);
+                const uint32_t d = L.rp[tid];
+#pragma unroll
+                for (uint32_t k = 0; k < kRunSort; ++k)
+                    if (k < len) skeys[d + k] = a[k];
+            }
+            __syncthreads();
+            // 2-4: the waves' walks
+            const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+            const uint32_t n = tv0, per = (((n + kHistWaves - 1u) / kHistWaves) + 63u) & ~63u;
+            const uint32_t lo_w = min(wv * per, n), hi_w = min(lo_w + per, n);
+            uint32_t* hw = hist + wv * kFlowSlots;
+            uint8_t* tag = reinterpret_cast<uint8_t*>(L.bcnt) + wv * kFlowSlots;  // (bcnt, boff: unused here)
+            const unsigned long long below = (1ull << lane) - 1ull;
+            // the step's lanes holding this lane's slot: each TCP lane writes its lane number at its
+            // slot's tag and reads it back; a lane that finds another number shares its slot, and
+            // only such slots (a few per step) are resolved, one ballot each
+            auto peers = [&](uint32_t sl, bool tcp) {
+                if (tcp) tag[sl] = (uint8_t)lane;
+                __builtin_amdgcn_wave_barrier();
+                const bool lost = tcp && tag[sl] != lane;
+                unsigned long long pending = __ballot(lost), m = 1ull << lane;
+                while (pending) {  // wave-uniform
+                    const uint32_t l = (uint32_t)__builtin_ctzll(pending);
+                    const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)l);
+                    const unsigned long long pm = __ballot(tcp && sl == s);
+                    if (tcp && sl == s) m = pm;
+                    pending &= ~pm;
+                }
+                __builtin_amdgcn_wave_barrier();  // tag reads before the next step's writes
+                return m;
+            };
+            for (uint32_t e0 = lo_w; e0 < hi_w; e0 += 64u) {  // wave-uniform
+                const uint32_t e = e0 + lane, key = e < hi_w ? skeys[e] : 0u, sl = (key >> 4) & 511u;
+                const bool tcp = e < hi_w && (key & 15u) != 0u;
+                const unsigned long long m = peers(sl, tcp);
+                if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+            {
+                uint32_t run = L.cursor[tid];
+#pragma unroll
+                for (uint32_t w = 0; w < kHistWaves; ++w) {
+                    const uint32_t x = hist[w * kFlowSlots + tid];
+                    hist[w * kFlowSlots + tid] = run;
+                    run += x;
+                }
+            }
+            __syncthreads();
+            uint32_t dst[kHistPer], val[kHistPer];
+#pragma unroll
+            for (uint32_t s = 0; s < kHistPer; ++s) {
+                const uint32_t e = lo_w + s * 64u + lane;
+                dst[s] = ~0u;
+                val[s] = 0u;
+                if (lo_w + s * 64u >= hi_w) continue;  // wave-uniform
+                const uint32_t key = e < hi_w ? skeys[e] : 0u, sl = (key >> 4) & 511u;
+                const bool tcp = e < hi_w && (key & 15u) != 0u;
+                const unsigned long long m = peers(sl, tcp);
+                if (tcp) {
+                    dst[s] = hw[sl] + (uint32_t)__popcll(m & below);
+                    val[s] = sl | (uint32_t)hist_char_of(key & 15u) << 16;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
+            }
+            __syncthreads();  // every key read: stage the output in its order, one coalesced write
+#pragma unroll
+            for (uint32_t s = 0; s < kHistPer; ++s)
+                if (dst[s] < n_chars) skeys[dst[s]] = val[s];
+            __syncthreads();
+            for (uint32_t i = tid; i < n_chars; i += kHistThreads) {
+                const uint32_t v = skeys[i];
+                out_slot[out_beg + i] = q * kFlowSlots + (v & 0xFFFFu);
+                out_char[out_beg + i] = (uint8_t)(v >> 16);
+            }
+            return;
+        } else {
+            // entry e of the round (runs laid end to end): key slot << 36 | record << 4 | code, or
+            // ~0 for none (no character, outside the record window)
+            auto entry_key = [&](uint32_t e, uint32_t r0, uint32_t r1, uint32_t c0, uint32_t win_lo,
+                                 uint32_t win_hi) {
+                uint32_t lo = r0, hi = r1 - 1u;  // the run holding e: the largest r with rp[r] <= e
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1u) >> 1;
+                    if (L.rp[mid] <= e) lo = mid; else hi = mid - 1u;
+                }
+                const uint32_t k = e - L.rp[lo];
+                uint32_t slot = 0u, code, rec;
+                if (!(L.rn[lo] >> 31)) {
+                    const uint32_t w = P.hword[L.rq[lo] + k];
+                    slot = w & (kFlowSlots - 1u);
+                    code = (w >> 9) & 15u;
+                    rec = (c0 + lo) * kFlowChunk + (w >> 13);
+                } else {
+                    const uint32_t w = P.e_orig[L.rs[lo] + k];
+                    code = (w >> kEntCodeShift) & 15u;
+                    rec = w & kEntRecMask;
+                    if (code != 0u) {
+                        const uint32_t m = P.pos_map[L.rs[lo] + k];
+                        slot = ((m & kRecFlowCombined) ? P.agg_slot[m & ~kRecFlowCombined]
+                                                       : P.hword[L.rq[lo] + (m - L.rs[lo])]) &
+                               (kFlowSlots - 1u);
+                    }
+                }
+                if (code == 0u || rec < win_lo || rec >= win_hi) return ~0ull;
+                return ((unsigned long long)slot << 36) | ((unsigned long long)rec << 4) | code;
+            };
+            auto emit = [&](uint32_t dst, unsigned long long key) {
+                dst += out_beg;
+                if (dst < out_end) {  // (a table-full batch may hold fewer slot counts than characters)
+                    out_slot[dst] = q * kFlowSlots + (uint32_t)(key >> 36);
+                    out_char[dst] = hist_char_of(key & 15u);
+                }
+            };
+            // the batch's n keys in keys[0 .. n), slot buckets counted (bcnt) and placed (boff):
+            // bitonic sort by (slot, record); a key's place in its slot's run = its index - the
+            // bucket's offset
+            auto sort_emit = [&](uint32_t n) {
+                uint32_t n2 = 1u;
+                while (n2 < n) n2 <<= 1;
+                for (uint32_t i = n + tid; i < n2; i += kHistThreads) L.keys[i] = ~0ull;
+                __syncthreads();
+                for (uint32_t k = 2; k <= n2; k <<= 1) {
+                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                        for (uint32_t i = tid; i < n2 / 2u; i += kHistThreads) {
+                            const uint32_t a = 2u * i - (i & (j - 1u)), b = a + j;
+                            const unsigned long long x = L.keys[a], y = L.keys[b];
+                            if ((x > y) == ((a & k) == 0u)) {
+                                L.keys[a] = y;
+                                L.keys[b] = x;
+                            }
+                        }
+                        __syncthreads();
+                    }
+                }
+                for (uint32_t i = tid; i < n; i += kHistThreads) {
+                    const unsigned long long key = L.keys[i];
+                    const uint32_t sl = (uint32_t)(key >> 36);
+                    emit(L.cursor[sl] + (i - L.boff[sl]), key);
+                }
+            };
+            auto batch_end = [&]() {
+                __syncthreads();
+                L.cursor[tid] += L.bcnt[tid];
+                L.bcnt[tid] = 0u;
+                __syncthreads();
+            };
+            // entries [e0, e1) (<= kHistCap) of runs r0 .. r1 - 1: keys in registers, bucketed by
+            // slot; a key's place by a scan of its bucket, or a sort of the batch
+            auto batch = [&](uint32_t r0, uint32_t r1, uint32_t e0, uint32_t e1, uint32_t c0) {
+                unsigned long long kk[kHistPer];
+                uint32_t sub[kHistPer];
+#pragma unroll
+                for (uint32_t u = 0; u < kHistPer; ++u) {
+                    const uint32_t e = e0 + tid + u * kHistThreads;
+                    kk[u] = e < e1 ? entry_key(e, r0, r1, c0, 0u, ~0u) : ~0ull;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kHistPer; ++u)
+                    if (kk[u] != ~0ull) sub[u] = atomicAdd(&L.bcnt[(uint32_t)(kk[u] >> 36)], 1u);
+                __syncthreads();
+                const uint32_t c = L.bcnt[tid];
+                uint32_t n;
+                L.boff[tid] = block_scan(c, n);
+                const bool heavy = __syncthreads_or(c > kHistScan);
+                if (n == 0u) return;  // uniform (bcnt all zero)
+#pragma unroll
+                for (uint32_t u = 0; u < kHistPer; ++u)
+                    if (kk[u] != ~0ull) L.keys[L.boff[(uint32_t)(kk[u] >> 36)] + sub[u]] = kk[u];
+                __syncthreads();
+                if (heavy) {
+                    sort_emit(n);
+                } else {
+#pragma unroll
+                    for (uint32_t u = 0; u < kHistPer; ++u) {
+                        if (kk[u] == ~0ull) continue;
+                        const uint32_t sl = (uint32_t)(kk[u] >> 36), b0 = L.boff[sl], bc = L.bcnt[sl];
+                        uint32_t rank = 0u;
+                        for (uint32_t j = 0; j < bc; ++j) rank += L.keys[b0 + j] < kk[u];
+                        emit(L.cursor[sl] + rank, kk[u]);
+                    }
+                }
+                batch_end();
+            };
+            // one run longer than kHistCap, in record windows of kHistCap (each holds at most
+            // kHistCap of its entries): keys appended in LDS, then sorted
+            auto long_run = [&](uint32_t r, uint32_t c0) {
+                const uint32_t cb = (c0 + r) * kFlowChunk;
+                for (uint32_t w0 = 0; w0 < kFlowChunk; w0 += kHistCap) {
+                    if (tid == 0) L.s_n = 0u;
+                    __syncthreads();
+                    for (uint32_t e = L.rp[r] + tid; e < L.rp[r + 1u]; e += kHistThreads) {
+                        const unsigned long long key = entry_key(e, r, r + 1u, c0, cb + w0, cb + w0 + kHistCap);
+                        if (key == ~0ull) continue;
+                        L.keys[atomicAdd(&L.s_n, 1u)] = key;
+                        atomicAdd(&L.bcnt[(uint32_t)(key >> 36)], 1u);
+                    }
+                    __syncthreads();
+                    uint32_t n;
+                    L.boff[tid] = block_scan(L.bcnt[tid], n);
+                    if (n != 0u) sort_emit(n);  // uniform
+                    batch_end();
+                }
+            };
+            for (uint32_t c0 = 0; c0 < chunks; c0 += kHistRuns) {
+                const uint32_t nr = min(kHistRuns, chunks - c0);
+                if (c0 != 0u) {
+                    vp = tid < nr ? col[c0 + tid] : 0u;
+                    vh = tid < nr ? col_h[c0 + tid] : 0u;
+                    round(c0, nr);
+                }
+                // batches of whole runs up to kHistCap entries; a longer run alone, in record windows
+                uint32_t r = 0;
+                while (r < nr) {  // uniform: every thread walks the same runs
+                    if (L.rp[r + 1u] - L.rp[r] > kHistCap) {
+                        long_run(r, c0);
+                        ++r;
+                        continue;
+                    }
+                    // r1 = the largest run index with rp[r1] <= rp[r] + kHistCap (> r: run r fits)
+                    uint32_t lo = r + 1u, hi = nr;
+                    const uint32_t lim = L.rp[r] + kHistCap;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1u) >> 1;
+                        if (L.rp[mid] <= lim) lo = mid; else hi = mid - 1u;
+                    }
+                    batch(r, lo, L.rp[r], L.rp[lo], c0);
+                    r = lo;
+                }
+                __syncthreads();
+            }
+        }
+    };
+    if constexpr (kUniform) {
+        partition(blockIdx.x);
+    } else {
+        const uint32_t n = slow[0];
+        for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+            partition(slow[1u + i]);
+            __syncthreads();  // the LDS is re-initialised for the next partition
+        }
+    }
 }
 
-hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes) {
-    return rocprim::radix_sort_pairs<HistSortConfig>(nullptr, *bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (const uint8_t*)nullptr, (uint8_t*)nullptr, (size_t)n_slots, 0u,
-                                     key_bits(sentinel));
-}
-
-hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_bytes, uint32_t* hist_slot,
-                               uint8_t* hist, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(p.n_hist, 0, 4, s);
-    if (e != hipSuccess || p.n_slots == 0u) return e;
-    const uint32_t grid = std::min<uint32_t>((p.n_slots + 255u) / 256u, 2048u);
-    hipLaunchKernelGGL(k_hist_keys, dim3(grid), dim3(256), 0, s, p);
+hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* hist_slot, uint8_t* hist,
+                               uint32_t* n_hist, uint32_t* slow, hipStream_t s) {
+    if (chunks == 0u) chunks = 1u;
+    hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(1024), 0, s, p.partials, p.parts, p.part_base, n_hist, slow);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hist_part<true>, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    size_t tb = temp_bytes;
-    return rocprim::radix_sort_pairs<HistSortConfig>(temp, tb, (const uint32_t*)p.keys, hist_slot, (const uint8_t*)p.vals, hist,
-                                     (size_t)p.n_slots, 0u, key_bits(p.sentinel), s);
+    hipLaunchKernelGGL(k_hist_part<false>, dim3(min(p.parts, 1024u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
+                       hist, slow);
+    return hipGetLastError();
 }
 
 }  // namespace fbk

@@ -39,7 +39,6 @@ struct ParseParams {
     unsigned long long* tick;     // [kTickWords] packed stats words, 8 per batch of the launch
     uint32_t* error;              // this launch's error word (launch parity); set by the flow kernels
     uint32_t* error_next;         // the other parity's word, zeroed by this launch for the next one
-    unsigned long long* dbg;      // diagnostic stamps (ablation builds only; nullptr in the product)
     uint32_t* rec_part;           // one batch: partition of each SESSION record slot, or nullptr
     const unsigned long long* pre;  // dense pass 2: per segment n_session | n_dns << 32 before it
     fb_pkt_out* dense_out;        // dense pass 2: batch-wide SESSION records (or nullptr)
@@ -183,8 +182,19 @@ static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 // of S s H h (~0 none), records, 0.
 constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the originator)
 constexpr uint32_t kEntTail = 1u << 18;
-constexpr uint32_t kRecFlowCombined = 0x80000000u;  // rec_flow value: combined id, slot in agg_slot
-constexpr uint32_t kIdxCombined = 0x80000000u;      // entries[] value: combined id (record slots < 2^27)
+constexpr uint32_t kRecFlowCombined = 0x80000000u;  // pos_map value: combined id, slot in agg_slot
+// entries[] word: the record slot (< 2^27) | its history code << 27 (0: no history character --
+// not TCP --, else 1 + the character's FB_HIST_CHARS index), or kIdxCombined | a combined id
+constexpr uint32_t kIdxCombined = 0x80000000u;
+constexpr uint32_t kEntRecMask = 0x07FFFFFFu;
+constexpr uint32_t kEntCodeShift = 27;
+// K2's history word of a plain entry: its table slot within the partition (9 bits), history code
+// (4 bits, 0: none) << 9, record slot within its bucketing chunk (15 bits) << 13; 0 for an entry
+// the table could not take.
+static_assert(FB_FLOW_SLOTS == 512 && FB_FLOW_CHUNK <= 32768, "hist_word field widths");
+__device__ __forceinline__ uint32_t hist_word(uint32_t slot_local, uint32_t entry_word) {
+    return slot_local | ((entry_word >> kEntCodeShift) & 15u) << 9 | ((entry_word & kEntRecMask) % kFlowChunk) << 13;
+}
 
 // fb_flow_hash of a 40-B session_key (10 words, word 9 = protocol | family << 8) and the
 // partition it falls in (top bits).
@@ -219,20 +229,28 @@ struct FlowParams {
     uint32_t comb_cap;
     uint32_t* rows;             // [chunks][parts]  start | count << 16, per bucketing chunk
     uint32_t* cols;             // [parts][chunk_stride] the same, transposed
-    unsigned long long* partials;  // 3 per partition: new, updated, occupied slots after the update
+    unsigned long long* partials;  // 4 per partition: new, updated, occupied slots after the update,
+                                   // history characters | the partition's first hword index << 32
     uint32_t* error;
     uint32_t max_recs;          // scratch capacity in records
     uint32_t parts;             // P (power of two)
     uint32_t part_shift;        // 64 - log2(P) (64 when P == 1)
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
     uint32_t batch;             // update call number since create / clear (positions' high word)
-    uint32_t* rec_flow;         // [max_recs] per record slot: its entry position (K1, moved by K1c)
-                                // or kRecFlowCombined | combined id (for the history)
-    uint32_t* ent_slot;         // [max_recs] table slot of each plain entry (K2; coalesced writes)
+    uint32_t* rows_h;           // [chunks][parts] rows before k_flow_combine (the history reads every
+                                // record): start | count << 16, bit 15 set for a combined (hot) group
+    uint32_t* cols_h;           // [parts][chunk_stride] rows_h transposed (K1t)
+    uint32_t* e_orig;           // [max_recs] a combined group's original entry words (K1c)
+    uint32_t* pos_map;          // [max_recs] a combined group's original position -> the entry's new
+                                // position, or kRecFlowCombined | combined id
+    uint32_t* hword;            // [max_recs] K2: a hist_word per entry it applied, each partition's in
+                                // its entry order from partials[4 p + 3] >> 32 (coalesced writes)
+    uint32_t* hcount;           // [capacity] history characters each slot got this update (K2)
     uint32_t* hot;              // [hot_cap] (chunk << 16 | part) groups K1 hands to k_flow_combine
-    uint32_t* ctl;              // [2] hot groups, combined entries (reset by K1t)
+    uint32_t* ctl;              // [3] hot groups, combined entries, hword entries (reset by K1t)
     uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
     uint32_t hot_cap;
+    uint32_t* part_base;        // [parts + 1] the history's output offset per partition (history)
     const uint32_t* rec_part;   // non-null: partition of each SESSION record slot, written by the
                                 // segmented parse of the same batch (fb_process_seg_dev); K1's
                                 // histogram pass then reads 4 B per record instead of the record
@@ -300,24 +318,10 @@ hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
                              unsigned long long* d_n, hipStream_t s);
 
-// Per-flow history characters of the last update (fb_hist.hip).
-struct HistParams {
-    const fb_pkt_out* recs;     // the update's records (dense or segmented)
-    const uint32_t* seg;        // segmented: record slot i valid iff (i & 63) < (seg[i >> 6] & 0xFFFF)
-    const fb_batch_stats* stats;  // dense: n_session read here
-    const uint32_t* rec_flow;   // entry position of each record slot, or kRecFlowCombined | combined id
-    const uint32_t* ent_slot;   // table slot of each plain entry (k_flow_apply)
-    const uint32_t* agg_slot;   // table slot of each combined entry
-    uint32_t n_slots;           // record slots of the update
-    uint32_t sentinel;          // key of the records that are not sorted in (= table capacity)
-    uint32_t* keys;             // [n_slots] scratch
-    uint8_t* vals;              // [n_slots] scratch
-    uint32_t* n_hist;           // device u32: keyed records
-    const uint32_t* rec_part;   // non-null: the fused parse's per-record words of this update
-};
-hipError_t flow_history_temp_bytes(uint32_t n_slots, uint32_t sentinel, size_t* bytes);
-hipError_t launch_flow_history(const HistParams& p, void* temp, size_t temp_bytes, uint32_t* hist_slot,
-                               uint8_t* hist, hipStream_t s);
+// Per-flow history characters of the last update (fb_hist.hip): the update's FlowParams (its
+// entries, transposed original rows, combined-group maps, per-slot counts) and the outputs.
+hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* hist_slot, uint8_t* hist,
+                               uint32_t* n_hist, uint32_t* slow, hipStream_t s);
 
 // Enrichment tables (fb_set_asn_tables / fb_set_blacklists, fb_enrich.hip).  Blacklists are
 // flattened per family into disjoint elementary intervals: bl*_pos[i] = first address of

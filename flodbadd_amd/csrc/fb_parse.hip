@@ -258,11 +258,8 @@ __device__ __forceinline__ void process_frame(__amdgpu_buffer_rsrc_t r, const De
     classify_session(cfg, gcfg, proto, fam, src, dst, sport, dport, hasf, flags, plen, iplen, idx, k);
 }
 
-// Ablation switches (tools/ubench_ws.hip); the product instantiates kFlagsProduct.
+// k_parse_seg instances: kFlagsProduct = the plain segmented output, or one of
 constexpr uint32_t kFlagsProduct = 0u;
-constexpr uint32_t kNoClassify = 1u;  // every frame a SESSION record of raw header words (timing only)
-constexpr uint32_t kNoStore = 2u;     // no record / dns stores (timing only)
-constexpr uint32_t kStamps = 4u;      // per-wave s_memrealtime stamps into P.dbg
 constexpr uint32_t kPartOut = 8u;     // k_parse_seg: also the flow-table partition of each SESSION
                                       // record slot (P.rec_part), for the update that follows
 constexpr uint32_t kCountOnly = 16u;  // dense pass 1: segment counts, classes and stats, no records
@@ -315,16 +312,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #ifndef FB_SEG_DEPTH
 #define FB_SEG_DEPTH 1
 #endif
-#ifndef FB_SEG_PRIO
-#define FB_SEG_PRIO 0
-#endif
 constexpr int kSegWaves = FB_SEG_WAVES;
 constexpr int kSegDepth = FB_SEG_DEPTH;  // segments of header loads in flight per wave
 constexpr int kSegThreads = 64 * kSegWaves;
 constexpr uint32_t kSegBytes = 64u * 56u;  // one segment of output: 64 record slots
 
-// Ablations (tools/ubench_ws.hip): kNoStore drops every store, kNoClassify skips the
-// classification (each frame becomes a SESSION record of raw header words).
 template <bool PARSED, uint32_t FLAGS = kFlagsProduct, bool MULTI = false>
 __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_parse_seg(const ParseParams P,
                                                                                       const SegBatches SB) {
@@ -340,15 +332,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
     const unsigned long long lmask = (1ull << lane) - 1ull;
     unsigned long long* stage = s_stage[wave];
-    // kStamps: P.dbg[(b * kSegWaves + wave) * 16 + slot]: 0 entry, 1 prologue done, 2.. end of
-    // iteration j (j < 12), 14 stats start, 15 exit
-    auto sstamp = [&](uint32_t slot) {
-        if constexpr ((FLAGS & kStamps) != 0u)
-            if (lane == 0u && slot < 16u)
-                P.dbg[((size_t)b * kSegWaves + wave) * 16u + slot] = __builtin_amdgcn_s_memrealtime();
-    };
-    sstamp(0);
-    uint32_t iter = 0;
     uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
     uint32_t a_k = 0u;  // the batch the counters belong to
     if (tid <= kAcc) s_acc[tid] = 0u;  // published by the prologue barrier
@@ -430,11 +413,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     // stores per step: segmented 8 (+1 partition), count-only 2, dense 6
     constexpr int kStores = (FLAGS & kCountOnly) ? 2 : (FLAGS & kDense) ? 6 : ((FLAGS & kPartOut) ? 9 : 8);
     auto dropped_stores = [&]() {
-        if constexpr ((FLAGS & kNoStore) == 0u) {
 #pragma unroll
-            for (int j = 0; j < kStores; ++j)
-                __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
-        }
+        for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
     };
     auto load_parsed = [&](uint32_t sg) {
         if constexpr ((FLAGS & kDense) != 0u) ppre = load_pre(sg);
@@ -489,7 +469,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     if constexpr (!PARSED) fetch(SS[0], sg, seg_of(Ln));
     dropped_stores();
     lds_barrier();  // configuration in LDS (LDS-only barrier: the header loads stay in flight)
-    sstamp(1);
     // a wave's counters go to LDS whenever its segments move on to the next batch
     auto flush = [&]() {
         const uint32_t a_tot = a_s + a_f;
@@ -513,14 +492,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             const uint32_t i = ls * 64u + lane;
             const bool valid = i < B.n;
             Pkt kk;
-            if constexpr ((FLAGS & kNoClassify) != 0u) {
-                kk.cls = FB_CLASS_SESSION;
-                kk.tcp = kk.v4 = true;
-                kk.bad = false;
-                const uint32_t hw[14] = {X.h.A.x, X.h.A.y, X.h.A.z, X.h.A.w, X.h.B.x, X.h.B.y, X.h.B.z, X.h.B.w, X.h.C.x, X.h.C.y, X.h.C.z, X.h.C.w, X.h.A.x ^ X.h.C.w, X.c.x};
-    #pragma unroll
-                for (int j = 0; j < 14; ++j) kk.w[j] = hw[j];
-            } else if constexpr (!PARSED) {
+            if constexpr (!PARSED) {
                 process_frame(frames_rsrc(k), cfg, cfg, X.h, valid ? X.c.x : 1u, valid ? X.c.y : 0u, B.frames_bytes, i,
                               kk);
             } else {
@@ -551,14 +523,8 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             if constexpr ((FLAGS & kDense) != 0u) pw = PARSED ? ppre : X.p;
             // prefetch: headers of this set's next segment (offsets already here), offsets of the
             // one after
-#if FB_SEG_PRIO  // experiment: the next segment's loads issued at raised wave priority
-            __builtin_amdgcn_s_setprio(FB_SEG_PRIO);
-#endif
             if constexpr (!PARSED) fetch(X, g_next, g_after);
             else load_parsed(g_next);
-#if FB_SEG_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
             if constexpr ((FLAGS & kCountOnly) != 0u) {
                 // dense pass 1: the count word and the class only
                 const __amdgpu_buffer_rsrc_t r_seg =
@@ -598,7 +564,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                     __builtin_amdgcn_raw_buffer_store_b128(v, r_dns, is_d ? 16u * (uint32_t)__popcll(m_dns & lmask) : kOob,
                                                            0, 0);
                 }
-            } else if constexpr ((FLAGS & kNoStore) == 0u) {
+            } else {
             // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
                 const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
                     reinterpret_cast<uint8_t*>(B.out) + (size_t)ls * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
@@ -648,7 +614,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             a_4 += __popcll(__ballot(counted && kk.v4));
             a_b += __popcll(__ballot(valid && kk.bad));
             a_n += __popcll(__ballot(valid));
-            sstamp(2u + min(iter++, 11u));
     };
     while (sg < nseg) {
         const uint32_t La = grab();
@@ -658,7 +623,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         Ln = La;
         sg = g_next;
     }
-    sstamp(14);
     if constexpr ((FLAGS & kDense) != 0u) return;  // pass 1 of the dense call published the stats
     // ---- batch stats, no barrier and no partials read-back:
     // every wave adds its counters into LDS (per batch); the block's last wave (LDS arrival
@@ -711,7 +675,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             }
         }
     }
-    sstamp(15);
 }
 
 // ============================================================================================
@@ -878,17 +841,9 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
 #pragma unroll
             for (int k = 0; k < kDnWaves; ++k) agg += s_wsum[par][k];
             unsigned long long excl = 0ull;
-#ifdef FB_DN_FAKE_LB
-            if (false) {
-#else
             if (t == 0u) {
-#endif
                 if (lane == 0u) __hip_atomic_store(P.dstatus, dn_word(ep, kDnP, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else
-#ifdef FB_DN_FAKE_LB
-            if (false)
-#endif
-            {
+            } else {
                 if (lane == 0u)
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnA, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // window of 64 x kDnLb tiles per step: lane l holds tiles jt-1-(l*kDnLb+k), k < kDnLb.
@@ -960,9 +915,6 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnP, excl + agg), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-#ifdef FB_DN_FAKE_LB  // timing-only ablation: no look-back wait, each tile at a disjoint fake offset
-            excl = (unsigned long long)t * (kDnTileSegs * 64u) * 0x100000001ull;
-#endif
             if (lane == 0u) s_excl = excl;
         }
         lds_barrier();

@@ -1,23 +1,25 @@
-"""Multi-GPU data path: packet-index shards, and the optional global per-flow counter reduce.
+"""Multi-GPU data path: packet-index shards, and the optional global per-flow merge.
 
 SURVEY.md 8e.  Decode/classify has no cross-packet state, so a batch of N*W frames shards by
 contiguous packet-index range: rank r owns [r*N, (r+1)*N) and runs its own context with no
 data-path collective (bench.py reports "scaling": "weak").  The one real exchange is the global
-per-flow count (BASELINE config C5):
-  1. every rank exports its flow table (canonical key + 6 integer counters, fb_flow_export);
-  2. all-gather of the keys (keys << packets);
-  3. every rank sorts the union by the derived Ord of Session (src/sessions.rs:23-30: protocol,
-     src_ip [V4 < V6, then octets], src_port, dst_ip, dst_port) -> an identical dense flow_id
-     (an LSD sort of the keys' Ord columns on the collective's device);
-  4. each rank scatters its counters into a dense int64[F][6];
-  5. all_reduce(SUM) -- over RCCL/xGMI with device tensors ("nccl" backend), gloo on the CPU.
+per-flow table (BASELINE config C5), O(F) per rank:
+  1. every rank exports its flow table (fb_flow_export[_dev]: canonical key, 6 integer counters,
+     ordered state) and makes its positions global (+ its shard's first packet index);
+  2. owner ranks by ranges of Session's derived Ord (src/sessions.rs:23-30: protocol, src_ip
+     [V4 < V6, then octets], src_port, dst_ip, dst_port): W-1 splitters from an all-gathered
+     sample of keys, the same on every rank;
+  3. all_to_all of the 128-B records to their owners (RCCL over xGMI with device tensors, gloo on
+     the CPU);
+  4. each owner sorts what it received by Ord (the key's non-constant fields packed into 63-bit
+     words, one stable sort per word) and merges equal keys: integer sums, MIN first_seen and
+     end_seen, MAX last_seen, hist_len = SUM, hist_mask = OR (a SUM of per-bit 4-bit fields,
+     no rank holds a key twice), conn_state re-decided from the ending rank's end_mask OR the
+     characters of the ranks before it -- exact when every rank's table holds one update call of
+     the same global batch (C5), since the earlier ranks' packets then all precede the end packet;
+  5. all-gather of the merged records: owner ranges are Ord ranges, so rank order IS Ord order.
+Bytes per rank: ~128 B x its flows out (x (W-1)/W) and in, and 128 B x the global flows gathered.
 Integer sums are order independent, so the result is bit-identical to a single-GPU table.
-The ordered per-flow state merges the same way once positions are made global (rank r's
-pkt_index + its shard's first index): first_seen = MIN, last_seen = MAX, end_seen = MIN (the
-earliest FIN/RST), hist_len = SUM, hist_mask = OR (a SUM of per-bit 4-bit fields, since RCCL has
-no bitwise reduction).  conn_state is re-decided from the ending rank's end_mask OR the characters
-of the ranks before it -- exact when every rank's table holds one update call of the same global
-batch (C5), since the earlier ranks' packets then all precede the end packet.
 """
 import numpy as np
 
@@ -67,25 +69,94 @@ def _hi32(x):
     return ((x ^ 0x80000000) - 0x80000000) << 32
 
 
-def _ord_sort(cols):
-    """Permutation sorting the rows of [T,12] int64 Ord columns lexicographically (column 0
-    primary): one stable sort per column, least significant first (LSD), all on cols' device."""
+def _ord_fields(rows):
+    """The key's Ord fields (value, bits) of [n, 16] int64 flow records, in priority order:
+    protocol, family (V4 < V6), src words, src port, dst words, dst port (IpAddr octets big-endian =
+    the words' order)."""
     import torch
-    perm = torch.arange(cols.shape[0], device=cols.device)
-    for c in range(cols.shape[1] - 1, -1, -1):
-        _, o = torch.sort(cols[perm, c], stable=True)
+    w = rows.view(torch.int32)
+
+    def u32(j):
+        return w[:, j].to(torch.int64) & 0xFFFFFFFF
+
+    ports, pf = u32(8), u32(9)
+    return [(pf & 0xFF, 8), ((pf >> 8) & 0xFF, 8), (u32(0), 32), (u32(1), 32), (u32(2), 32), (u32(3), 32),
+            (ports & 0xFFFF, 16), (u32(4), 32), (u32(5), 32), (u32(6), 32), (u32(7), 32), (ports >> 16, 16)]
+
+
+def _pack63(fields, drop_constant):
+    """The fields' bits, most significant first, in 63-bit words (non-negative int64): comparing
+    the word lists lexicographically compares the fields.  drop_constant: fields equal on every
+    row are left out (they cannot change an order between those rows)."""
+    import torch
+    if drop_constant and fields and fields[0][0].shape[0] > 1:
+        st = torch.stack([v for v, _ in fields], dim=1)
+        keep = (st != st[:1]).any(dim=0).tolist()
+        fields = [f for f, k in zip(fields, keep) if k]
+    words, cur, used = [], None, 0
+    for v, bits in fields:
+        while bits > 0:
+            take = min(bits, 63 - used)
+            part = (v >> (bits - take)) & ((1 << take) - 1)
+            cur = part if cur is None else (cur << take) | part
+            used += take
+            bits -= take
+            v = v & ((1 << bits) - 1)
+            if used == 63:
+                words.append(cur)
+                cur, used = None, 0
+    if cur is not None:
+        words.append(cur << (63 - used))
+    return words
+
+
+def _lsd_order(words, n, device):
+    """Permutation sorting rows by the word list (word 0 most significant): one stable sort per
+    word, least significant first."""
+    import torch
+    perm = torch.arange(n, device=device)
+    for wd in reversed(words):
+        _, o = torch.sort(wd[perm], stable=True)
         perm = perm[o]
     return perm
 
 
-def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
+def _owners(dist, group, world, words, n, device, sample=1024):
+    """Owner rank of each row: the number of the W-1 Ord splitters at or below its key.  The
+    splitters are quantiles of an all-gathered sample (up to `sample` rows per rank), sorted the
+    same way on every rank."""
+    import torch
+    k = len(words)
+    take = min(n, sample)
+    idx = (torch.arange(take, device=device) * n) // max(take, 1)
+    mine = torch.zeros((sample, k), dtype=torch.int64, device=device)
+    if take:
+        mine[:take] = torch.stack([wd[idx] for wd in words], dim=1)
+    cnt = torch.tensor([take], dtype=torch.int64, device=device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine, group=group)
+    smp = torch.cat([g[:int(c.item())] for g, c in zip(got, cnts)]).cpu().numpy()
+    order = np.lexsort([smp[:, j] for j in range(k - 1, -1, -1)]) if len(smp) else np.zeros(0, np.int64)
+    spl = smp[order[[(j * len(order)) // world for j in range(1, world)]]] if len(smp) else np.zeros((0, k), np.int64)
+    owner = torch.zeros(n, dtype=torch.int64, device=device)
+    for s in spl:  # owner += (row >= splitter), lexicographic over the words
+        lt = torch.zeros(n, dtype=torch.bool, device=device)
+        for j in range(k - 1, -1, -1):
+            lt = (words[j] < int(s[j])) | ((words[j] == int(s[j])) & lt)
+        owner += (~lt).to(torch.int64)
+    return owner
+
+
+def global_flow_table(dist, flows, device=None, group=None, shard_first=0, as_tensor=False):
     """All ranks' flow tables merged into one table sorted by Session's derived Ord, identical
     on every rank.  `dist` is torch.distributed (initialised); `device` is the torch device of
     the collective tensors (a cuda device for RCCL, None/cpu for gloo); `shard_first` is the
-    global index of this rank's first packet (shard_range).  Everything between the upload of
-    the exported records and the download of the merged columns runs as torch ops on `device`:
-    the keys' Ord columns, their all-gather, an LSD sort of the union, dense ids from adjacent
-    differences, the scatters and the all-reduces."""
+    global index of this rank's first packet (shard_range).  Returns FLOW_REC_DTYPE records, or
+    with as_tensor=True the [F, 128] uint8 tensor on `device` (no download).  Everything runs as
+    torch ops on `device`: owners by Ord splitters, all_to_all of the records, the owner's sort
+    and merge, the all-gather of merged records."""
     import torch
     dev = torch.device("cpu") if device is None else torch.device(device)
     world = dist.get_world_size(group)
@@ -97,85 +168,89 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
         flows = np.ascontiguousarray(flows, dtype=FLOW_REC_DTYPE)
         raw = torch.from_numpy(flows.view(np.uint8).reshape(len(flows), FLOW_REC_DTYPE.itemsize)).to(dev)
     nl = int(raw.shape[0])
-    w32 = raw.view(torch.int32).to(torch.int64) & 0xFFFFFFFF  # [nl, 32] u32 words, widened
-    w64 = raw.view(torch.int64)                                # [nl, 16] u64 words (as int64 bits)
-    ports, pf = w32[:, 8], w32[:, 9]
-    # key columns in the derived Ord's priority: protocol, family (V4 < V6), src words, src port,
-    # dst words, dst port (src/sessions.rs:23-30; IpAddr octets big-endian = the words' order)
-    mine = torch.stack([pf & 0xFF, (pf >> 8) & 0xFF, w32[:, 0], w32[:, 1], w32[:, 2], w32[:, 3], ports & 0xFFFF,
-                        w32[:, 4], w32[:, 5], w32[:, 6], w32[:, 7], ports >> 16], dim=1)
-    n = torch.tensor([nl], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(x.item()) for x in sizes]
-    m = max(sizes + [1])
-    pad = torch.zeros((m, 12), dtype=torch.int64, device=dev)
-    pad[:nl] = mine
-    gathered = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(gathered, pad, group=group)
-    allc = torch.cat([g[:sz] for g, sz in zip(gathered, sizes)])
-    # dense ids in Ord order: sort the union, a new id wherever a row differs from the one before
-    perm = _ord_sort(allc)
-    srt = allc[perm]
-    first = torch.ones(srt.shape[0], dtype=torch.bool, device=dev)
-    if srt.shape[0] > 1:
-        first[1:] = (srt[1:] != srt[:-1]).any(dim=1)
-    ids = torch.cumsum(first.to(torch.int64), 0) - 1
-    inv = torch.empty_like(ids)
-    inv[perm] = ids
-    uniq = srt[first]
-    F = int(uniq.shape[0])
-    start = sum(sizes[:rank])
-    idx = inv[start:start + nl]
+    # [nl, 16] u64 words (as int64 bits)
+    rows = raw.contiguous().view(torch.int64) if nl else torch.zeros((0, 16), dtype=torch.int64, device=dev)
+    if shard_first:  # rank-local positions -> global ((call << 32) | global packet index)
+        rows = rows.clone()
+        for j in (11, 12, 13):
+            pos = rows[:, j]
+            g = ((pos >> 32) << 32) | ((pos & 0xFFFFFFFF) + shard_first)
+            rows[:, j] = g if j != 13 else torch.where(pos != -1, g, pos)  # end_seen NONE stays
+    # 2-3. owners by Ord range, records to their owners
+    if world > 1:
+        owner = _owners(dist, group, world, _pack63(_ord_fields(rows), False), nl, dev)
+        order = torch.sort(owner, stable=True)[1]
+        send = rows[order].contiguous()
+        send_n = torch.bincount(owner, minlength=world)
+        recv_n = torch.empty_like(send_n)
+        dist.all_to_all_single(recv_n, send_n, group=group)
+        rn = recv_n.tolist()
+        recv = torch.empty((sum(rn), 16), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, send, output_split_sizes=rn, input_split_sizes=send_n.tolist(), group=group)
+        src = torch.repeat_interleave(torch.arange(world, device=dev), recv_n)
+    else:
+        recv, src = rows, torch.zeros(nl, dtype=torch.int64, device=dev)
+    m = int(recv.shape[0])
+    # 4. sort by Ord, merge equal keys
+    words = _pack63(_ord_fields(recv), True)
+    if m > 1 and words:
+        perm = _lsd_order(words, m, dev)
+        recv, src = recv[perm], src[perm]
+        words = [wd[perm] for wd in words]
+    first = torch.ones(m, dtype=torch.bool, device=dev)
+    if m > 1:
+        first[1:] = False
+        for wd in words:
+            first[1:] |= wd[1:] != wd[:-1]
+    F = int(first.sum().item()) if m else 0
+    dup = F != m
+    gid = torch.cumsum(first.to(torch.int64), 0) - 1 if dup else None
 
-    def reduce(cols, fill, op):
-        t = torch.full((F, len(cols)), fill, dtype=torch.int64, device=dev)
-        if nl:
-            t[idx] = torch.stack(cols, dim=1)
-        dist.all_reduce(t, op=op, group=group)
-        return t
+    def seg(vals, op, fill):  # per merged key: op over its rows (identity when no key repeats)
+        if not dup:
+            return vals
+        t = torch.full((F,) + tuple(vals.shape[1:]), fill, dtype=torch.int64, device=dev)
+        if op == "sum":
+            return t.index_add_(0, gid, vals)
+        ix = gid.view(-1, *([1] * (vals.dim() - 1))).expand_as(vals)
+        return t.scatter_reduce_(0, ix, vals, reduce=op, include_self=True)
 
-    def glob(pos):  # rank-local position -> global ((call << 32) | global packet index)
-        return ((pos >> 32) << 32) | ((pos & 0xFFFFFFFF) + shard_first)
+    def at(x):  # a per-key value back at its rows
+        return x[gid] if dup else x
 
     big = torch.iinfo(torch.int64).max
-    counters, first_seen, last_seen, end_seen = w64[:, 5:11], w64[:, 11], w64[:, 12], w64[:, 13]
-    hist_len, state = w32[:, 28], w32[:, 29]
+    w32 = recv.view(torch.int32)
+    hist_len = w32[:, 28].to(torch.int64) & 0xFFFFFFFF
+    state = w32[:, 29].to(torch.int64) & 0xFFFFFFFF
+    flags = w32[:, 31].to(torch.int64) & 0xFFFFFFFF
     mask, end_mask = state & 0xFFFF, (state >> 24) & 0xFF
-    spread = torch.zeros(nl, dtype=torch.int64, device=dev)
+    end_seen = recv[:, 13]
+    end = torch.where(end_seen != -1, end_seen, torch.full_like(end_seen, big))
+    spread = torch.zeros(m, dtype=torch.int64, device=dev)
     for b in range(13):
         spread |= ((mask >> b) & 1) << (4 * b)
-    ended = end_seen != -1  # FB_SEEN_NONE
-    end = torch.where(ended, glob(end_seen), torch.full_like(end_seen, big))
-    sums = reduce([counters[:, j] for j in range(6)] + [hist_len, spread], 0, dist.ReduceOp.SUM)
-    mins = reduce([glob(first_seen), end], big, dist.ReduceOp.MIN)
-    # session_flags (stored at insert) are a function of the key and the configuration, the same on
-    # every rank that holds the flow: MAX keeps them
-    last = reduce([glob(last_seen), w32[:, 31]], -1, dist.ReduceOp.MAX)
+    sums = seg(torch.cat([recv[:, 5:11], hist_len[:, None], spread[:, None]], dim=1), "sum", 0)
+    mins = seg(torch.stack([recv[:, 11], end], dim=1), "amin", big)
+    last = seg(torch.stack([recv[:, 12], flags], dim=1), "amax", -1)
     # conn_state: the ending rank's end_mask | the conn_state characters of the ranks before it
     gend = mins[:, 1]
-    is_end = (end == gend[idx]) & (gend[idx] != big)
-    end_rank = reduce([torch.where(is_end, rank, 0)], 0, dist.ReduceOp.SUM)[:, 0]
-    # ranks before the ending one add their S s H h F f R r bits, the ending rank its end_mask
-    before = torch.where(rank < end_rank[idx], mask & 0xFF, 0) | torch.where(is_end, end_mask, 0)
-    bits = torch.zeros(nl, dtype=torch.int64, device=dev)
+    is_end = (end == at(gend)) & (at(gend) != big)
+    end_rank = seg(torch.where(is_end, src, 0), "sum", 0)
+    before = torch.where(src < at(end_rank), mask & 0xFF, 0) | torch.where(is_end, end_mask, 0)
+    bits = torch.zeros(m, dtype=torch.int64, device=dev)
     for b in range(8):
         bits |= ((before >> b) & 1) << (4 * b)
-    emask_sum = reduce([bits], 0, dist.ReduceOp.SUM)[:, 0]
+    emask_sum = seg(bits, "sum", 0)
     hmask = torch.zeros(F, dtype=torch.int64, device=dev)
     emask = torch.zeros(F, dtype=torch.int64, device=dev)
     for b in range(13):
         hmask |= (((sums[:, 7] >> (4 * b)) & 15) > 0).to(torch.int64) << b
         if b < 8:
             emask |= (((emask_sum >> (4 * b)) & 15) > 0).to(torch.int64) << b
-
-    # the merged records assembled as fb_flow_rec words on the device, one download
+    # the merged records as fb_flow_rec words
     has_end = gend != big
-    w = torch.zeros((F, 16), dtype=torch.int64, device=dev)
-    kw = [uniq[:, 2], uniq[:, 3], uniq[:, 4], uniq[:, 5], uniq[:, 7], uniq[:, 8], uniq[:, 9], uniq[:, 10],
-          uniq[:, 6] | (uniq[:, 11] << 16), uniq[:, 0] | (uniq[:, 1] << 8)]
-    for j in range(5):
-        w[:, j] = kw[2 * j] | _hi32(kw[2 * j + 1])
+    w = torch.empty((F, 16), dtype=torch.int64, device=dev)
+    w[:, 0:5] = recv[first, 0:5] if dup else recv[:, 0:5]
     w[:, 5:11] = sums[:, 0:6]
     w[:, 11] = mins[:, 0]
     w[:, 12] = last[:, 0]
@@ -184,4 +259,18 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0):
     cs = torch.where(has_end, _conn_state(emask), 0)
     w[:, 14] = sums[:, 6] | _hi32(hmask | (cs << 16) | (em << 24))
     w[:, 15] = _hi32(last[:, 1])  # slot 0, session_flags
-    return w.cpu().numpy().view(FLOW_REC_DTYPE).reshape(F)
+    # 5. owners' ranges in rank order = Ord order
+    if world > 1:
+        n = torch.tensor([F], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(x.item()) for x in sizes]
+        pad = torch.zeros((max(sizes + [1]), 16), dtype=torch.int64, device=dev)
+        pad[:F] = w
+        got = [torch.zeros_like(pad) for _ in range(world)]
+        dist.all_gather(got, pad, group=group)
+        w = torch.cat([g[:sz] for g, sz in zip(got, sizes)])
+    out = w.view(torch.uint8).reshape(-1, FLOW_REC_DTYPE.itemsize)
+    if as_tensor:
+        return out
+    return w.cpu().numpy().view(FLOW_REC_DTYPE).reshape(-1)

@@ -36,11 +36,13 @@ def _rank_flows(rank, world):
     return fl.export_sorted(), first
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, empty_rank=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         flows, first = _rank_flows(rank, world)
+        if rank == empty_rank:
+            flows = flows[:0]
         if rank == 1:  # the device-tensor input form (fb_flow_export_dev records), on the CPU here
             import torch
             flows = torch.from_numpy(flows.view(np.uint8).reshape(len(flows), N.FLOW_REC_DTYPE.itemsize).copy())
@@ -66,10 +68,26 @@ def test_sort_keys_is_derived_ord():
 
 
 @pytest.mark.timeout(300)
-def test_gloo_world2_global_flow_table(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_global_flow_table(tmp_path, world):
+    """world 2 and 3 (uneven shards, three Ord ranges): every rank ends with the single-process
+    table of the whole batch, byte for byte."""
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
     ref = _rank_flows(0, 1)[0]  # whole batch, one process: counters and ordered state
     for r in range(world):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
         assert got.tobytes() == ref.tobytes(), r
+
+
+@pytest.mark.timeout(300)
+def test_gloo_merge_with_an_empty_rank(tmp_path):
+    """A rank with no flows still takes part in every collective; the result is the other rank's
+    table with global positions."""
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), 1), nprocs=world, start_method="spawn")
+    only, _ = _rank_flows(0, world)
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
+        exp = only.copy()
+        exp["slot"] = 0
+        assert got.tobytes() == exp.tobytes(), r

@@ -1,6 +1,8 @@
 """Time the C5 merge (flodbadd_amd.distributed.global_flow_table) over RCCL at world size 1 on the
 device: the C4 10M-frame table (1.45M flows) exported into a device tensor (fb_flow_export_dev),
-then merged (union, Ord sort, dense ids, all-reduces, records assembled on the device)."""
+then merged (Ord sort of the owned records, equal keys merged, records assembled on the device;
+at W = 1 the owner split and the two collectives are skipped).  Timed with the merged table left
+on the device (as_tensor=True) and, separately, with the download to host records."""
 import os
 import sys
 import time
@@ -32,11 +34,16 @@ for n in (1 << 20, 10 << 20):
     N.check(N.gpu_lib().fb_flow_export_dev(cap.ctx, C.c_void_p(flows.data_ptr()), cnt.value,
                                            C.c_void_p(d_n.data_ptr()), None))
     torch.cuda.synchronize()
-    for rep in range(3):
+    for rep in range(4):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        merged = global_flow_table(dist, flows, device=dev)
+        merged = global_flow_table(dist, flows, device=dev, as_tensor=True)
         torch.cuda.synchronize()
-        print("frames %d flows %d: merge %.1f ms" % (n, len(merged), (time.perf_counter() - t0) * 1e3))
+        t1 = time.perf_counter()
+        host = global_flow_table(dist, flows, device=dev)
+        t2 = time.perf_counter()
+        assert host.view(np.uint8).tobytes() == merged.cpu().numpy().tobytes()
+        print("frames %d flows %d: merge %.2f ms on the device, %.2f ms with the download"
+              % (n, int(merged.shape[0]), (t1 - t0) * 1e3, (t2 - t1) * 1e3))
     cap.close()
 dist.destroy_process_group()

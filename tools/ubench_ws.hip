@@ -1,9 +1,9 @@
-// ubench_ws.hip -- timing + per-wave stamps of the segmented parse kernel (tooling, not
-// product).  Includes the product kernel source and times, interleaved in one process:
+// ubench_ws.hip -- timing of the segmented parse kernel (tooling, not product).  Includes the
+// product kernel source and times, interleaved in one process:
 //   read / copy   plain streaming read of the frame buffer / read frames + write 56 B per frame
 //   seg           the product kernel (k_parse_seg<false>)
-//   seg_no_store, seg_no_classify, seg_no_classify_no_store   ablations (timing only)
-// then one stamped run: per-wave prologue / exit quantiles, by XCD and by dispatch third.
+// (The round-2 ablations -- no stores, no classification, per-wave stamps -- were template flags
+// of the product kernel; they are no longer in the product source.  DESIGN.md keeps their numbers.)
 //   build: tools/build_ubench_ws.sh ; run: tools/ubench_ws [config_id] [n] [rotate] [iters]
 #include "../flodbadd_amd/csrc/fb_parse.hip"
 
@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
         p.cfg = dcfg;
         p.tick = tick;
         ++launch;
-        p.error = err + (launch & 1u); p.error_next = err + ((launch & 1u) ^ 1u); p.dbg = nullptr;
+        p.error = err + (launch & 1u); p.error_next = err + ((launch & 1u) ^ 1u);
         return p;
     };
     auto sb1 = [&](int r, uint32_t* seg) {  // one-batch launch descriptor of k_parse_seg
@@ -125,8 +125,8 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; ++i) caps += std::min<uint32_t>(offs[i + 1] - offs[i], 128u);
     const double algo = (double)caps + 4.0 * (n + 1) + 56.0 * n;
     printf("{\"cus\": %d}\n", prop.multiProcessorCount);
-    const char* names[] = {"read", "copy", "seg", "seg_no_store", "seg_no_classify", "seg_no_classify_no_store"};
-    const int NV = 6;
+    const char* names[] = {"read", "copy", "seg"};
+    const int NV = 3;
     int sbpc = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&sbpc, (fbk::k_parse_seg<false>), fbk::kSegThreads, 0));
     const uint32_t nseg = (n + 63) / 64;
@@ -149,9 +149,6 @@ int main(int argc, char** argv) {
                 case 0: hipLaunchKernelGGL(k_read, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, bytes / 16, sink); break;
                 case 1: hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, s, (const uint4*)bufs[r].fr, (uint4*)bufs[r].out, bytes / 16, n * 56ull / 16); break;
                 case 2: hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
-                case 3: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
-                case 4: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoClassify>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
-                case 5: hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kNoClassify | fbk::kNoStore>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(r, dseg)); break;
                 }
             }
             CK(hipEventRecord(e1, s));
@@ -167,61 +164,6 @@ int main(int argc, char** argv) {
         const double gbs = v == 0 ? bytes / (best[v] * 1e3) : (v == 1 ? (bytes + n * 56.0) / (best[v] * 1e3) : algo / (best[v] * 1e3));
         printf("{\"variant\": \"%s\", \"us_mean\": %.2f, \"us_best\": %.2f, \"Gpps\": %.2f, \"GBs\": %.1f}\n", names[v],
                sum[v] / rounds, best[v], n / (best[v] * 1e3), gbs);
-    }
-    {   // stamped seg run
-        unsigned long long* sd;
-        const size_t sw = (size_t)sgrid * fbk::kSegWaves * 16;
-        CK(hipMalloc(&sd, sw * 8));
-        CK(hipMemset(sd, 0, sw * 8));
-        for (int w = 0; w < 3; ++w) {
-            fbk::ParseParams pp = params(); pp.dbg = sd;
-            hipLaunchKernelGGL((fbk::k_parse_seg<false, fbk::kStamps>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, pp, sb1(w % R, dseg));
-        }
-        CK(hipStreamSynchronize(s));
-        std::vector<unsigned long long> st2(sw);
-        CK(hipMemcpy(st2.data(), sd, sw * 8, hipMemcpyDeviceToHost));
-        unsigned long long z = ~0ull;
-        for (size_t w = 0; w < sw / 16; ++w) if (st2[w * 16]) z = std::min(z, st2[w * 16]);
-        auto qq = [](std::vector<double> v, double fr) { if (v.empty()) return 0.0; std::sort(v.begin(), v.end()); return v[(size_t)(fr * (v.size() - 1))]; };
-        for (int slot = 0; slot < 16; ++slot) {
-            std::vector<double> v;
-            for (size_t w = 0; w < sw / 16; ++w) if (st2[w * 16 + slot]) v.push_back((st2[w * 16 + slot] - z) * 0.01);
-            if (v.empty()) continue;
-            printf("{\"seg_slot\": %d, \"n\": %zu, \"us\": [%.2f, %.2f, %.2f, %.2f]}\n", slot, v.size(), qq(v, 0), qq(v, .5), qq(v, .9), qq(v, 1));
-        }
-        // slot-1 (prologue done) by XCD (b % 8) and by dispatch third (b * 3 / grid)
-        for (int key = 0; key < 2; ++key) {
-            const int nk = key == 0 ? 8 : 3;
-            for (int k = 0; k < nk; ++k) {
-                std::vector<double> v, e;
-                for (size_t w = 0; w < sw / 16; ++w) {
-                    const size_t b = w / fbk::kSegWaves;
-                    const int kk = key == 0 ? (int)(b % 8) : (int)(b * 3 / sgrid);
-                    if (kk != k || !st2[w * 16 + 1]) continue;
-                    v.push_back((st2[w * 16 + 1] - z) * 0.01);
-                    e.push_back((st2[w * 16 + 15] - z) * 0.01);
-                }
-                printf("{\"by\": \"%s\", \"k\": %d, \"prologue_us\": [%.2f, %.2f, %.2f], \"exit_us\": [%.2f, %.2f, %.2f]}\n",
-                       key == 0 ? "xcd" : "third", k, qq(v, 0), qq(v, .5), qq(v, 1), qq(e, 0), qq(e, .5), qq(e, 1));
-            }
-        }
-        {   // per block: exit of its first and last wave (intra- vs inter-CU imbalance)
-            std::vector<double> bmin, bmax, spread;
-            for (size_t b = 0; b < sgrid; ++b) {
-                double lo = 1e30, hi = 0;
-                for (int w = 0; w < fbk::kSegWaves; ++w) {
-                    const unsigned long long t = st2[(b * fbk::kSegWaves + w) * 16 + 15];
-                    if (!t) continue;
-                    lo = std::min(lo, (t - z) * 0.01);
-                    hi = std::max(hi, (t - z) * 0.01);
-                }
-                if (hi > 0) { bmin.push_back(lo); bmax.push_back(hi); spread.push_back(hi - lo); }
-            }
-            printf("{\"block_first_exit_us\": [%.2f, %.2f, %.2f], \"block_last_exit_us\": [%.2f, %.2f, %.2f], "
-                   "\"block_spread_us\": [%.2f, %.2f, %.2f]}\n", qq(bmin, 0), qq(bmin, .5), qq(bmin, 1), qq(bmax, 0),
-                   qq(bmax, .5), qq(bmax, 1), qq(spread, 0), qq(spread, .5), qq(spread, 1));
-        }
-        CK(hipFree(sd));
     }
     hipLaunchKernelGGL((fbk::k_parse_seg<false, 0>), dim3(sgrid), dim3(fbk::kSegThreads), 0, s, params(), sb1(0, dseg));
     CK(hipStreamSynchronize(s));
