@@ -77,37 +77,184 @@ __device__ __forceinline__ void sort_net(uint32_t (&a)[kRunSort]) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* partials, uint32_t parts,
-                                                    uint32_t* part_base, uint32_t* n_hist, uint32_t* slow) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) {
-        carry = 0u;
-        slow[0] = 0u;  // k_hist_part<true> lists the partitions it leaves to k_hist_part<false>
+__device__ __forceinline__ uint32_t block_scan2(uint32_t v, uint32_t v2, uint32_t& tot, uint32_t& ex2, uint32_t& tot2,
+                                                uint32_t* wsum, uint32_t* wsum2) {
+    // block-wide exclusive sums of two values per thread (blockDim.x / 64 <= 16 waves)
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v, x2 = v2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64), y2 = __shfl_up(x2, o, 64);
+        if (lane >= (uint32_t)o) {
+            x += y;
+            x2 += y2;
+        }
+    }
+    if (lane == 63u) {
+        wsum[wave] = x;
+        wsum2[wave] = x2;
     }
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < parts; b0 += 1024u) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t v = i < parts ? (uint32_t)partials[4 * (size_t)i + 3] : 0u;
-        uint32_t x = v;
-        const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
+    uint32_t before = 0u, before2 = 0u;
+    tot = tot2 = 0u;
+    for (uint32_t k = 0; k < nw; ++k) {
+        const uint32_t s = wsum[k], s2 = wsum2[k];
+        if (k < wave) {
+            before += s;
+            before2 += s2;
         }
-        if (lane == 63u) wsum[w] = x;
-        __syncthreads();
-        uint32_t before = carry;
-        for (uint32_t k = 0; k < w; ++k) before += wsum[k];
-        if (i < parts) part_base[i] = before + x - v;
-        __syncthreads();
-        if (threadIdx.x == 1023u) carry = before + x;
-        __syncthreads();
+        tot += s;
+        tot2 += s2;
+    }
+    __syncthreads();
+    ex2 = before2 + x2 - v2;
+    return before + x - v;
+}
+
+// Exclusive scan of the partitions' character counts (partials[4 p + 3] low word) -> part_base;
+// one pass: thread t sums a contiguous group of partitions, one block scan, the group written.
+__global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* partials, uint32_t parts,
+                                                    uint32_t* part_base, uint32_t* n_hist, uint32_t* slow) {
+    __shared__ uint32_t wsum[16], wsum2[16];
+    const uint32_t per = (parts + 1023u) / 1024u, p0 = min(threadIdx.x * per, parts), p1 = min(p0 + per, parts);
+    uint32_t sum = 0u;
+    for (uint32_t i = p0; i < p1; ++i) sum += (uint32_t)partials[4 * (size_t)i + 3];
+    uint32_t tot, ex2, tot2;
+    uint32_t run = block_scan2(sum, 0u, tot, ex2, tot2, wsum, wsum2);
+    for (uint32_t i = p0; i < p1; ++i) {
+        part_base[i] = run;
+        run += (uint32_t)partials[4 * (size_t)i + 3];
     }
     if (threadIdx.x == 0) {
-        part_base[parts] = carry;
-        *n_hist = carry;
+        part_base[parts] = tot;
+        *n_hist = tot;
+        slow[0] = 0u;  // k_hist_uniform lists the partitions it leaves to k_hist_general
+    }
+}
+
+// ---- the uniform case: one chunk round, <= kHistCap entries, every run <= kRunSort plain entries,
+// every wave's share (its 64 runs) <= kHistPer steps of 64
+struct UniLds {
+    uint32_t skeys[kHistCap];                // run-sorted keys, then the output stage
+    uint32_t hist[kHistWaves * kFlowSlots];  // [wave][slot]: count, then next output position
+    uint32_t rn[kHistRuns];                  // run lengths (bit 31: combined) } the walk's slot tags
+    uint32_t rq[kHistRuns];                  // first history word of a run      } (u8 [wave][slot])
+    uint32_t rp[kHistRuns + 1];              // exclusive prefix of rn
+    uint32_t wsum[kHistWaves], wsum2[kHistWaves];
+};
+static_assert(sizeof(UniLds) <= 40u * 1024u, "four workgroups per CU");
+
+__global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
+                                                               uint8_t* out_char, uint32_t* slow) {
+    __shared__ UniLds L;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // every load issued together: the partition's character count and history-word base, its
+    // output offset, its slots' counts, its chunk runs
+    const unsigned long long pw = P.partials[4 * (size_t)q + 3];
+    const uint32_t out_beg = P.part_base[q];
+    const uint32_t hc = P.hcount[(size_t)q * kFlowSlots + tid];
+    const uint32_t vp = tid < chunks ? P.cols[(size_t)q * P.chunk_stride + tid] : 0u;
+    const uint32_t vh = tid < chunks ? P.cols_h[(size_t)q * P.chunk_stride + tid] : 0u;
+    const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
+    if (n_chars == 0u) return;  // uniform: no history characters in this partition
+    for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) L.hist[j] = 0u;
+    const bool comb = (vh & 0x8000u) != 0u;
+    const uint32_t lp = vp >> 16, len = comb ? (vh >> 16) | 0x80000000u : lp;
+    uint32_t tp, ep, tc;
+    // run offsets (entries) and the slots' first output positions, one pair of barriers
+    const uint32_t cur = block_scan2(hc, lp, tc, ep, tp, L.wsum, L.wsum2);  // slot tid's first position
+    L.rp[tid] = ep;
+    if (tid == 0) L.rp[kHistRuns] = tp;
+    __syncthreads();
+    const uint32_t wlen = L.rp[min(64u * wave + 64u, kHistRuns)] - L.rp[64u * wave];
+    if (__syncthreads_or(len > kRunSort || wlen > kHistPer * 64u) || chunks > kHistRuns || tp > kHistCap) {
+        if (tid == 0) slow[1u + atomicAdd(slow, 1u)] = q;  // uniform: the general kernel takes it
+        return;
+    }
+    {   // run tid in record order (K1's scatter leaves a run unordered): key = record in chunk << 13
+        // | slot << 4 | code; the wave's slot counts by LDS atomics (order-free)
+        uint32_t a[kRunSort];
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc((void*)P.hword, (short)0, (int)(P.max_recs * 4u), 0x00020000);
+        const uint32_t vo = (hbase + ep) * 4u;
+#pragma unroll
+        for (uint32_t k = 0; k < kRunSort; ++k)  // unpredicated: all in flight, past-run words masked
+            a[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, vo + 4u * k, 0, 0);
+        uint32_t* hw = L.hist + wave * kFlowSlots;
+#pragma unroll
+        for (uint32_t k = 0; k < kRunSort; ++k) {
+            const uint32_t w = a[k];
+            a[k] = k < len ? (w >> 13) << 13 | (w & 0x1FFu) << 4 | ((w >> 9) & 15u) : ~0u;
+            if (k < len && ((w >> 9) & 15u)) atomicAdd(hw + (w & 0x1FFu), 1u);
+        }
+        uint32_t wl = len;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+        if (wl > 8u) sort_net<16>(a);
+        else if (wl > 4u) sort_net<8>(a);
+        else if (wl > 1u) sort_net<4>(a);
+#pragma unroll
+        for (uint32_t k = 0; k < kRunSort; ++k)
+            if (k < len) L.skeys[ep + k] = a[k];
+    }
+    __syncthreads();
+    {   // per slot: each wave's first output position = the slot's + the earlier waves' counts
+        uint32_t run = cur;
+#pragma unroll
+        for (uint32_t w = 0; w < kHistWaves; ++w) {
+            const uint32_t x = L.hist[w * kFlowSlots + tid];
+            L.hist[w * kFlowSlots + tid] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    // the wave's entries (its 64 runs) in order, 64 a step: a key's position = its wave's next one
+    // for the slot + the step's lanes below it holding the slot; the lowest such lane moves it on.
+    // Lanes sharing a slot find each other through a tag per slot: each TCP lane writes its lane
+    // number and reads it back; a lane finding another number shares its slot, and only those
+    // slots (a few per step) take a ballot each.
+    const uint32_t lo_w = L.rp[64u * wave], hi_w = L.rp[min(64u * wave + 64u, kHistRuns)];
+    uint32_t* hw = L.hist + wave * kFlowSlots;
+    uint8_t* tag = reinterpret_cast<uint8_t*>(L.rn) + wave * kFlowSlots;
+    static_assert(sizeof(L.rn) + sizeof(L.rq) == kHistWaves * kFlowSlots, "tags fill rn and rq");
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t dst[kHistPer], val[kHistPer];
+#pragma unroll
+    for (uint32_t s = 0; s < kHistPer; ++s) {
+        const uint32_t e = lo_w + s * 64u + lane;
+        dst[s] = ~0u;
+        val[s] = 0u;
+        if (lo_w + s * 64u >= hi_w) continue;  // wave-uniform
+        const uint32_t key = e < hi_w ? L.skeys[e] : 0u, sl = (key >> 4) & 511u;
+        const bool tcp = e < hi_w && (key & 15u) != 0u;
+        if (tcp) tag[sl] = (uint8_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long pending = __ballot(tcp && tag[sl] != lane), m = 1ull << lane;
+        while (pending) {  // wave-uniform
+            const uint32_t l = (uint32_t)__builtin_ctzll(pending);
+            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)l);
+            const unsigned long long pm = __ballot(tcp && sl == o);
+            if (tcp && sl == o) m = pm;
+            pending &= ~pm;
+        }
+        if (tcp) {
+            dst[s] = hw[sl] + (uint32_t)__popcll(m & below);
+            val[s] = sl | (uint32_t)hist_char_of(key & 15u) << 16;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();  // every key read: stage the output in its order, one coalesced write
+#pragma unroll
+    for (uint32_t s = 0; s < kHistPer; ++s)
+        if (dst[s] < n_chars) L.skeys[dst[s]] = val[s];
+    __syncthreads();
+    for (uint32_t i = tid; i < n_chars; i += kHistThreads) {
+        const uint32_t v = L.skeys[i];
+        out_slot[out_beg + i] = q * kFlowSlots + (v & 0xFFFFu);
+        out_char[out_beg + i] = (uint8_t)(v >> 16);
     }
 }
 
@@ -122,9 +269,8 @@ struct HistLds {
     uint32_t s_n;
 };
 
-template <bool kUniform>
-__global__ __launch_bounds__(kHistThreads) void k_hist_part(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
-                                                            uint8_t* out_char, uint32_t* slow) {
+__global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
+                                                               uint8_t* out_char, const uint32_t* slow) {
     __shared__ HistLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     // block-wide exclusive sums of one or two values per thread (tot: the sum)
@@ -198,110 +344,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_part(const FlowParams P, 
         };
         const uint32_t nr0 = min(kHistRuns, chunks);
         const uint32_t tv0 = round(0u, nr0);
-        if constexpr (kUniform) {
-            const uint32_t len = L.rn[tid];  // bit 31 (combined) makes it > kRunSort
-            if (__syncthreads_or(len > kRunSort) || chunks > kHistRuns || tv0 > kHistCap) {  // uniform
-                if (tid == 0) slow[1u + atomicAdd(slow, 1u)] = q;
-                return;
-            }
-            uint32_t* skeys = reinterpret_cast<uint32_t*>(L.keys);  // run-sorted keys, then the output
-            uint32_t* hist = skeys + kHistCap;                        // [wave][slot] counts / positions
-            for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) hist[j] = 0u;
-            {   // 1. run tid in record order: key = record in chunk << 13 | slot << 4 | code
-                uint32_t a[kRunSort];
-                // unpredicated buffer loads (a predicated load waits alone): all in flight at once,
-                // words past the array read 0, words past the run are masked
-                const __amdgpu_buffer_rsrc_t rh =
-                    __builtin_amdgcn_make_buffer_rsrc((void*)P.hword, (short)0, (int)(P.max_recs * 4u), 0x00020000);
-                const uint32_t vo = L.rq[tid] * 4u;
-#pragma unroll
-                for (uint32_t k = 0; k < kRunSort; ++k) a[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, vo + 4u * k, 0, 0);
-#pragma unroll
-                for (uint32_t k = 0; k < kRunSort; ++k)
-                    a[k] = k < len ? (a[k] >> 13) << 13 | (a[k] & 0x1FFu) << 4 | ((a[k] >> 9) & 15u) : ~0u;
-                uint32_t wl = len;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
-                if (wl > 8u) sort_net<16>(a);
-                else if (wl > 4u) sort_net<8>(a);
-                else if (wl > 1u) sort_net<4>(a);
-                const uint32_t d = L.rp[tid];
-#pragma unroll
-                for (uint32_t k = 0; k < kRunSort; ++k)
-                    if (k < len) skeys[d + k] = a[k];
-            }
-            __syncthreads();
-            // 2-4: the waves' walks
-            const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-            const uint32_t n = tv0, per = (((n + kHistWaves - 1u) / kHistWaves) + 63u) & ~63u;
-            const uint32_t lo_w = min(wv * per, n), hi_w = min(lo_w + per, n);
-            uint32_t* hw = hist + wv * kFlowSlots;
-            uint8_t* tag = reinterpret_cast<uint8_t*>(L.bcnt) + wv * kFlowSlots;  // (bcnt, boff: unused here)
-            const unsigned long long below = (1ull << lane) - 1ull;
-            // the step's lanes holding this lane's slot: each TCP lane writes its lane number at its
-            // slot's tag and reads it back; a lane that finds another number shares its slot, and
-            // only such slots (a few per step) are resolved, one ballot each
-            auto peers = [&](uint32_t sl, bool tcp) {
-                if (tcp) tag[sl] = (uint8_t)lane;
-                __builtin_amdgcn_wave_barrier();
-                const bool lost = tcp && tag[sl] != lane;
-                unsigned long long pending = __ballot(lost), m = 1ull << lane;
-                while (pending) {  // wave-uniform
-                    const uint32_t l = (uint32_t)__builtin_ctzll(pending);
-                    const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)l);
-                    const unsigned long long pm = __ballot(tcp && sl == s);
-                    if (tcp && sl == s) m = pm;
-                    pending &= ~pm;
-                }
-                __builtin_amdgcn_wave_barrier();  // tag reads before the next step's writes
-                return m;
-            };
-            for (uint32_t e0 = lo_w; e0 < hi_w; e0 += 64u) {  // wave-uniform
-                const uint32_t e = e0 + lane, key = e < hi_w ? skeys[e] : 0u, sl = (key >> 4) & 511u;
-                const bool tcp = e < hi_w && (key & 15u) != 0u;
-                const unsigned long long m = peers(sl, tcp);
-                if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
-            }
-            __syncthreads();
-            {
-                uint32_t run = L.cursor[tid];
-#pragma unroll
-                for (uint32_t w = 0; w < kHistWaves; ++w) {
-                    const uint32_t x = hist[w * kFlowSlots + tid];
-                    hist[w * kFlowSlots + tid] = run;
-                    run += x;
-                }
-            }
-            __syncthreads();
-            uint32_t dst[kHistPer], val[kHistPer];
-#pragma unroll
-            for (uint32_t s = 0; s < kHistPer; ++s) {
-                const uint32_t e = lo_w + s * 64u + lane;
-                dst[s] = ~0u;
-                val[s] = 0u;
-                if (lo_w + s * 64u >= hi_w) continue;  // wave-uniform
-                const uint32_t key = e < hi_w ? skeys[e] : 0u, sl = (key >> 4) & 511u;
-                const bool tcp = e < hi_w && (key & 15u) != 0u;
-                const unsigned long long m = peers(sl, tcp);
-                if (tcp) {
-                    dst[s] = hw[sl] + (uint32_t)__popcll(m & below);
-                    val[s] = sl | (uint32_t)hist_char_of(key & 15u) << 16;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
-            }
-            __syncthreads();  // every key read: stage the output in its order, one coalesced write
-#pragma unroll
-            for (uint32_t s = 0; s < kHistPer; ++s)
-                if (dst[s] < n_chars) skeys[dst[s]] = val[s];
-            __syncthreads();
-            for (uint32_t i = tid; i < n_chars; i += kHistThreads) {
-                const uint32_t v = skeys[i];
-                out_slot[out_beg + i] = q * kFlowSlots + (v & 0xFFFFu);
-                out_char[out_beg + i] = (uint8_t)(v >> 16);
-            }
-            return;
-        } else {
+        {
             // entry e of the round (runs laid end to end): key slot << 36 | record << 4 | code, or
             // ~0 for none (no character, outside the record window)
             auto entry_key = [&](uint32_t e, uint32_t r0, uint32_t r1, uint32_t c0, uint32_t win_lo,
@@ -458,14 +501,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_part(const FlowParams P, 
             }
         }
     };
-    if constexpr (kUniform) {
-        partition(blockIdx.x);
-    } else {
-        const uint32_t n = slow[0];
-        for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-            partition(slow[1u + i]);
-            __syncthreads();  // the LDS is re-initialised for the next partition
-        }
+    const uint32_t n = slow[0];
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        partition(slow[1u + i]);
+        __syncthreads();  // the LDS is re-initialised for the next partition
     }
 }
 
@@ -475,11 +514,12 @@ hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* h
     hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(1024), 0, s, p.partials, p.parts, p.part_base, n_hist, slow);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hist_part<true>, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow);
+    hipLaunchKernelGGL(k_hist_uniform, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hist_part<false>, dim3(min(p.parts, 1024u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
-                       hist, slow);
+    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop
+    hipLaunchKernelGGL(k_hist_general, dim3(min(p.parts, 512u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist,
+                       slow);
     return hipGetLastError();
 }
 
