@@ -395,17 +395,13 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     Set SS[D];
     uint4 pin[4];
     auto load_q = [&](uint32_t g, uint2& q) {
-        // off[i] per lane; off[i + 1] is the next lane's, moved over by DPP (wave_shl:1), and the
-        // last lane's comes from one wave-uniform load: 64 offsets + 1 word instead of 2 x 64
+        // (off[i + 1] taken from the next lane by a DPP wave shift, the last lane's by one scalar
+        // load, measured slower: C2 45.2 -> 42.8 Gpps, C3 -1 % -- the scalar load's lgkmcnt wait
+        // also waits for the LDS staging traffic)
         const uint32_t k = batch_of(k_q, g);
-        const uint32_t i0 = (g - SB.b[k].seg_start) * 64u, n = SB.b[k].n;
+        const uint32_t i = (g - SB.b[k].seg_start) * 64u + lane, n = SB.b[k].n;
         const uint32_t* off = SB.b[k].offsets;
-        const uint32_t x = off[min(i0 + lane, n)];
-        // (a scalar load: the offsets are read-only for the launch, the constant address space
-        // lets the compiler use the scalar cache inside the loop)
-        typedef const __attribute__((address_space(4))) uint32_t cu32;
-        const uint32_t last = ((cu32*)off)[__builtin_amdgcn_readfirstlane(min(i0 + 64u, n))];
-        q = make_uint2(x, (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)x, 0x130, 0xF, 0xF, false));
+        q = make_uint2(off[min(i, n)], off[min(i + 1u, n)]);
     };
     auto load_pre = [&](uint32_t g) {  // kDense (one batch): n_session | n_dns << 32 before segment g
         return P.pre[min(g, nseg - 1u)];
