@@ -64,6 +64,41 @@ def _conn_state(m):
     return torch.where(S & H & F & f, torch.full_like(m, 1), c)  # np.select order: first match wins
 
 
+_LUTS = {}
+
+
+def _luts(device):
+    """Lookup tables for the hist_mask OR-as-SUM: 8 bits -> 4-bit fields, and 4 nibble-flags
+    (bits 0, 4, 8, 12 of a 16-bit chunk) -> 4 bits."""
+    import torch
+    key = str(device)
+    if key not in _LUTS:
+        v = np.arange(256, dtype=np.int64)
+        spread = np.zeros(256, dtype=np.int64)
+        for b in range(8):
+            spread |= ((v >> b) & 1) << (4 * b)
+        c = np.arange(1 << 16, dtype=np.int64)
+        pack = ((c >> 0) & 1) | (((c >> 4) & 1) << 1) | (((c >> 8) & 1) << 2) | (((c >> 12) & 1) << 3)
+        _LUTS[key] = (torch.from_numpy(spread).to(device), torch.from_numpy(pack).to(device))
+    return _LUTS[key]
+
+
+def _spread(mask, device):
+    """Bit b of a 16-bit mask -> bit 4 b (so a SUM over < 16 rows is an OR per bit)."""
+    spread, _ = _luts(device)
+    return spread[mask & 0xFF] | (spread[(mask >> 8) & 0xFF] << 32)
+
+
+def _unspread(x, nbits, device):
+    """Bit b set <=> 4-bit field b of x is non-zero (b < nbits)."""
+    _, pack = _luts(device)
+    t = x | (x >> 1) | (x >> 2) | (x >> 3)
+    t = t & 0x1111111111111111
+    out = pack[t & 0xFFFF] | (pack[(t >> 16) & 0xFFFF] << 4) | (pack[(t >> 32) & 0xFFFF] << 8) | \
+        (pack[(t >> 48) & 0xFFFF] << 12)
+    return out & ((1 << nbits) - 1)
+
+
 def _hi32(x):
     """x (int64 holding a u32) << 32 without leaving int64: sign-extend bit 31 first."""
     return ((x ^ 0x80000000) - 0x80000000) << 32
@@ -84,15 +119,19 @@ def _ord_fields(rows):
             (ports & 0xFFFF, 16), (u32(4), 32), (u32(5), 32), (u32(6), 32), (u32(7), 32), (ports >> 16, 16)]
 
 
-def _pack63(fields, drop_constant):
+_FIELD_WORD = (9, 9, 0, 1, 2, 3, 8, 4, 5, 6, 7, 8)  # the key word each Ord field comes from
+
+
+def _pack63(fields, rows=None):
     """The fields' bits, most significant first, in 63-bit words (non-negative int64): comparing
-    the word lists lexicographically compares the fields.  drop_constant: fields equal on every
-    row are left out (they cannot change an order between those rows)."""
+    the word lists lexicographically compares the fields.  With `rows` ([n, 16] int64 records),
+    fields whose key word is equal on every row are left out (they cannot order those rows):
+    one comparison over the ten key words, one host sync."""
     import torch
-    if drop_constant and fields and fields[0][0].shape[0] > 1:
-        st = torch.stack([v for v, _ in fields], dim=1)
-        keep = (st != st[:1]).any(dim=0).tolist()
-        fields = [f for f, k in zip(fields, keep) if k]
+    if rows is not None and rows.shape[0] > 1:
+        kw = rows.view(torch.int32)[:, :10]
+        varies = (kw != kw[:1]).any(dim=0).tolist()
+        fields = [f for f, j in zip(fields, _FIELD_WORD) if varies[j]]
     words, cur, used = [], None, 0
     for v, bits in fields:
         while bits > 0:
@@ -178,7 +217,7 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0, as_te
             rows[:, j] = g if j != 13 else torch.where(pos != -1, g, pos)  # end_seen NONE stays
     # 2-3. owners by Ord range, records to their owners
     if world > 1:
-        owner = _owners(dist, group, world, _pack63(_ord_fields(rows), False), nl, dev)
+        owner = _owners(dist, group, world, _pack63(_ord_fields(rows)), nl, dev)
         order = torch.sort(owner, stable=True)[1]
         send = rows[order].contiguous()
         send_n = torch.bincount(owner, minlength=world)
@@ -192,7 +231,7 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0, as_te
         recv, src = rows, torch.zeros(nl, dtype=torch.int64, device=dev)
     m = int(recv.shape[0])
     # 4. sort by Ord, merge equal keys
-    words = _pack63(_ord_fields(recv), True)
+    words = _pack63(_ord_fields(recv), recv)
     if m > 1 and words:
         perm = _lsd_order(words, m, dev)
         recv, src = recv[perm], src[perm]
@@ -226,27 +265,24 @@ def global_flow_table(dist, flows, device=None, group=None, shard_first=0, as_te
     mask, end_mask = state & 0xFFFF, (state >> 24) & 0xFF
     end_seen = recv[:, 13]
     end = torch.where(end_seen != -1, end_seen, torch.full_like(end_seen, big))
-    spread = torch.zeros(m, dtype=torch.int64, device=dev)
-    for b in range(13):
-        spread |= ((mask >> b) & 1) << (4 * b)
-    sums = seg(torch.cat([recv[:, 5:11], hist_len[:, None], spread[:, None]], dim=1), "sum", 0)
-    mins = seg(torch.stack([recv[:, 11], end], dim=1), "amin", big)
-    last = seg(torch.stack([recv[:, 12], flags], dim=1), "amax", -1)
-    # conn_state: the ending rank's end_mask | the conn_state characters of the ranks before it
-    gend = mins[:, 1]
-    is_end = (end == at(gend)) & (at(gend) != big)
-    end_rank = seg(torch.where(is_end, src, 0), "sum", 0)
-    before = torch.where(src < at(end_rank), mask & 0xFF, 0) | torch.where(is_end, end_mask, 0)
-    bits = torch.zeros(m, dtype=torch.int64, device=dev)
-    for b in range(8):
-        bits |= ((before >> b) & 1) << (4 * b)
-    emask_sum = seg(bits, "sum", 0)
-    hmask = torch.zeros(F, dtype=torch.int64, device=dev)
-    emask = torch.zeros(F, dtype=torch.int64, device=dev)
-    for b in range(13):
-        hmask |= (((sums[:, 7] >> (4 * b)) & 15) > 0).to(torch.int64) << b
-        if b < 8:
-            emask |= (((emask_sum >> (4 * b)) & 15) > 0).to(torch.int64) << b
+    if dup:
+        sums = seg(torch.cat([recv[:, 5:11], hist_len[:, None], _spread(mask, dev)[:, None]], dim=1), "sum", 0)
+        mins = seg(torch.stack([recv[:, 11], end], dim=1), "amin", big)
+        last = seg(torch.stack([recv[:, 12], flags], dim=1), "amax", -1)
+        # conn_state: the ending rank's end_mask | the conn_state characters of the ranks before it
+        gend = mins[:, 1]
+        is_end = (end == at(gend)) & (at(gend) != big)
+        end_rank = seg(torch.where(is_end, src, 0), "sum", 0)
+        before = torch.where(src < at(end_rank), mask & 0xFF, 0) | torch.where(is_end, end_mask, 0)
+        emask = _unspread(seg(_spread(before, dev), "sum", 0), 8, dev)
+        hmask = _unspread(sums[:, 7], 13, dev)
+    else:  # no key met twice: every reduction is the row itself (the ending row is its own)
+        sums = torch.cat([recv[:, 5:11], hist_len[:, None]], dim=1)
+        mins = torch.stack([recv[:, 11], end], dim=1)
+        last = torch.stack([recv[:, 12], flags], dim=1)
+        gend = end
+        emask = torch.where(end != big, end_mask, 0)
+        hmask = mask
     # the merged records as fb_flow_rec words
     has_end = gend != big
     w = torch.empty((F, 16), dtype=torch.int64, device=dev)

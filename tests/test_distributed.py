@@ -68,10 +68,10 @@ def test_sort_keys_is_derived_ord():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_gloo_global_flow_table(tmp_path, world):
-    """world 2 and 3 (uneven shards, three Ord ranges): every rank ends with the single-process
-    table of the whole batch, byte for byte."""
+    """world 1 (no key met twice), 2 and 3 (uneven shards, three Ord ranges): every rank ends
+    with the single-process table of the whole batch, byte for byte."""
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
     ref = _rank_flows(0, 1)[0]  # whole batch, one process: counters and ordered state
     for r in range(world):

@@ -45,5 +45,11 @@ for n in (1 << 20, 10 << 20):
         assert host.view(np.uint8).tobytes() == merged.cpu().numpy().tobytes()
         print("frames %d flows %d: merge %.2f ms on the device, %.2f ms with the download"
               % (n, int(merged.shape[0]), (t1 - t0) * 1e3, (t2 - t1) * 1e3))
+    if n == (10 << 20) and "--profile" in sys.argv:  # where the merge's time goes, per torch op
+        from torch.profiler import profile, ProfilerActivity
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            global_flow_table(dist, flows, device=dev, as_tensor=True)
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=25))
     cap.close()
 dist.destroy_process_group()
