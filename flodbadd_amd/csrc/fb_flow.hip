@@ -354,19 +354,27 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
 // a FIN or RST packet, and the first of those IS the end packet (the reference's string tests
 // `history.contains(c)` only ask which characters are present).
 constexpr uint32_t kSlotWords = 12;  // u64 words of a slot kept in LDS: tag, key[5], counters[6]
-constexpr uint32_t kScrU32 = 10;     // per-slot batch scratch, u32 words
+constexpr uint32_t kScrU32 = 12;     // per-slot batch scratch, u32 words (8-B aligned: three u64 keys)
 #ifndef FB_K2_TAGS
 #define FB_K2_TAGS 1
 #endif
 constexpr uint32_t kK2Lds = kFlowSlots * (kSlotWords * 8 + kScrU32 * 4 + (FB_K2_TAGS ? 4 : 0));
 constexpr uint32_t kTcpFinRst = 0x01u | 0x04u;
 #ifndef FB_K2_CPT
-#define FB_K2_CPT 2
+#define FB_K2_CPT 1
 #endif
 constexpr uint32_t kK2Cpt = FB_K2_CPT;
 // (kK2Cpt: bucketing chunks per K2 thread and round; C4: 512 chunks, one round)
-// scratch words
-constexpr uint32_t kScFirst = 0, kScLast = 1, kScEnd = 2, kScMask = 3, kScCount = 4, kScChar = 5;  // kScChar..+3: S s H h
+// scratch words: first / last packet as u64 keys rec << 32 | pkt_index (min / max), the end packet
+// as rec << 37 | its FB_HIST_CHARS bit << 32 | pkt_index (min) -- so the fold needs no record
+// read-back --, the mask, the history count, the first rec of S s H h
+constexpr uint32_t kScFirst = 0, kScLast = 2, kScEnd = 4, kScMask = 6, kScCount = 7, kScChar = 8;  // kScChar..+3
+__device__ __forceinline__ unsigned long long* sc64(uint32_t* q, uint32_t w) {
+    return reinterpret_cast<unsigned long long*>(q + w);
+}
+__device__ __forceinline__ unsigned long long end_key(uint32_t rec, uint32_t bit, uint32_t pkt) {
+    return (unsigned long long)rec << 37 | (unsigned long long)bit << 32 | pkt;
+}
 
 __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -608,8 +616,9 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     // ordered state into the batch scratch (see above)
     uint32_t* q = scr + (size_t)i * kScrU32;
     const uint32_t rec = e3.y;
-    atomicMin(q + kScFirst, rec);
-    atomicMax(q + kScLast, rec);
+    const unsigned long long pos = (unsigned long long)rec << 32 | e3.x;  // rec, pkt_index
+    atomicMin(sc64(q, kScFirst), pos);
+    atomicMax(sc64(q, kScLast), pos);
     // inserted by this batch: bit 16, and the session flags the reference stores at insert
     // (is_local_src/dst, is_self_src/dst of the canonical key, src/packets.rs:429-435) in bits 20-23
     if (result == 1) atomicOr(q + kScMask, (1u << 16) | (e3.z & 0x00F00000u));
@@ -618,14 +627,15 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
         const uint32_t b = hist_bit(e3.z & 0xFFu);
         if (b < 16u) atomicOr(q + kScMask, 1u << b);
         if (b < 4u) atomicMin(q + kScChar + b, rec);
-        if ((e3.z >> 8) & kTcpFinRst) atomicMin(q + kScEnd, rec);
+        if ((e3.z >> 8) & kTcpFinRst) atomicMin(sc64(q, kScEnd), end_key(rec, b, e3.x));
     }
     return result;
 }
 
 // A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
 // the group's partial sums / minima / maxima.  Its records' pos_map words point at agg_slot[id].
-__device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr, const uint4 e0, const uint4 e1,
+__device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr,
+                                              const fb_pkt_out* recs, const uint4 e0, const uint4 e1,
                                               const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
                                               const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
                                               uint32_t* err) {
@@ -652,8 +662,14 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     }
     if (agg_slot) agg_slot[e3.x] = slot_base + i;
     uint32_t* q = scr + (size_t)i * kScrU32;
-    atomicMin(q + kScFirst, e2.z);
-    atomicMax(q + kScLast, e2.w);
+    // the group's first / last / end records: their pkt_index (and the end's character) read here
+    // -- combined entries are few
+    auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
+        return ld_u2(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
+    };
+    const uint2 wf = rec_word(e2.z), wl = rec_word(e2.w), we = rec_word(e3.y != ~0u ? e3.y : e2.w);
+    atomicMin(sc64(q, kScFirst), (unsigned long long)e2.z << 32 | wf.y);
+    atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | wl.y);
     const uint32_t hc = e3.z & 0xFFFFu;
     const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) : 0u);
     if (m) atomicOr(q + kScMask, m);
@@ -663,38 +679,36 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
 #pragma unroll
         for (uint32_t b = 0; b < 4u; ++b)
             if (c[b] != ~0u) atomicMin(q + kScChar + b, c[b]);
-        if (e3.y != ~0u) atomicMin(q + kScEnd, e3.y);
+        if (e3.y != ~0u) atomicMin(sc64(q, kScEnd), end_key(e3.y, hist_bit((we.x >> 16) & 0xFFu), we.y));
     }
     return result;
 }
 
 // Fold one slot's batch scratch into its ordered fields (after every entry was applied).  o0, o1 =
 // the slot's ordered fields as loaded with the slice (first_seen, last_seen | end_seen, hist_len,
-// hist_state); the three record words it needs (first / last / end packet) are loaded together.
-__device__ __forceinline__ void finish_slot(FlowSlot* g, const uint32_t* q, const fb_pkt_out* recs, uint32_t batch,
-                                            const uint4 o0, const uint4 o1) {
-    const uint32_t first = q[kScFirst];
-    if (first == ~0u) return;  // not touched by this batch
+// hist_state); the first / last / end packets' pkt_index (and the end's character) are in the
+// scratch keys.
+__device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t batch, const uint4 o0, const uint4 o1) {
+    const unsigned long long first = *sc64(q, kScFirst);
+    if (first == ~0ull) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
-    auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
-        return ld_u2(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
-    };
-    const uint32_t flags = q[kScMask], last = q[kScLast], end = q[kScEnd];
+    const unsigned long long last = *sc64(q, kScLast), end = *sc64(q, kScEnd);
+    const uint32_t flags = q[kScMask];
     const bool fresh = (flags & (1u << 16)) != 0u;  // new flow: start_time = its first packet, end_time None
-    const uint2 wf = rec_word(first), wl = rec_word(last), we = rec_word(end != ~0u ? end : last);
-    const unsigned long long first_seen = fresh ? hi | wf.y : (o0.x | (unsigned long long)o0.y << 32);
+    const unsigned long long first_seen = fresh ? hi | (uint32_t)first : (o0.x | (unsigned long long)o0.y << 32);
     unsigned long long end_seen = fresh ? FB_SEEN_NONE : (o1.x | (unsigned long long)o1.y << 32);
     // hist_state: hist_mask 0-12 | conn_state 16-19 | session flags 20-23 | end_mask 24-31
     const uint32_t state = fresh ? (flags & 0x00F00000u) : o1.w, len = fresh ? 0u : o1.z;
-    const unsigned long long last_seen = hi | wl.y;
+    const unsigned long long last_seen = hi | (uint32_t)last;
     const uint32_t mask = state & 0xFFFFu;
     uint32_t cs = state >> 16;
-    if (end != ~0u && end_seen == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
-        uint32_t m = mask | (1u << hist_bit((we.x >> 16) & 0xFFu));
+    if (end != ~0ull && end_seen == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
+        const uint32_t end_rec = (uint32_t)(end >> 37);
+        uint32_t m = mask | (1u << ((uint32_t)(end >> 32) & 31u));
 #pragma unroll
-        for (uint32_t b = 0; b < 4u; ++b) m |= q[kScChar + b] <= end ? 1u << b : 0u;
+        for (uint32_t b = 0; b < 4u; ++b) m |= q[kScChar + b] <= end_rec ? 1u << b : 0u;
         cs = conn_state_of(m) | (cs & 0xF0u) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
-        end_seen = hi | we.y;
+        end_seen = hi | (uint32_t)end;
     }
     uint4* t = reinterpret_cast<uint4*>(g) + 6;  // bytes 96..127: the ordered fields
     t[0] = make_uint4((uint32_t)first_seen, (uint32_t)(first_seen >> 32), (uint32_t)last_seen, (uint32_t)(last_seen >> 32));
@@ -946,7 +960,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
         if (!dense) load_slice();
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
             const uint32_t w = j % kScrU32;
-            scr[j] = (w == kScLast || w == kScMask || w == kScCount || w == 9u) ? 0u : ~0u;
+            scr[j] = (w == kScLast || w == kScLast + 1u || w == kScMask || w == kScCount) ? 0u : ~0u;
         }
         if (FB_K2_TAGS) tags[threadIdx.x] = tag0;
         if (threadIdx.x == 0) s_hbase = atomicAdd(P.ctl + 2, (uint32_t)total);  // the history words' range
@@ -1027,7 +1041,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 if (v0 & kIdxCombined) {
                     const uint4* t = CE + (size_t)(v0 & ~kIdxCombined) * 8u + 4u;
                     const uint4 t3 = t[3];
-                    const int r = apply_combined(slice, tags, scr, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
+                    const int r = apply_combined(slice, tags, scr, P.recs, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
                                                  part * kFlowSlots, P.agg_slot, P.error);
                     if (r >= 0) {
                         n_new += r == 1;
@@ -1061,13 +1075,14 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             rbase += tot;
             __syncthreads();
         }
-        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.recs, P.batch, ord0, ord1);
+        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1);
         // only the slots this batch touched (inserted or updated) changed; the others' heads are
         // not written back (a 96-B head alone is a partial line)
         uint4* gw = reinterpret_cast<uint4*>(T);
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
             const uint32_t sl = j / kHead16, w = j - sl * kHead16;
-            if (scr[(size_t)sl * kScrU32 + kScFirst] != ~0u) gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
+            if (scr[(size_t)sl * kScrU32 + kScFirst + 1u] != ~0u)  // the first key's rec word: touched
+                gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
         }
     }
     n_new = block_sum(n_new, sh);
