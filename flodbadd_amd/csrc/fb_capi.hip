@@ -42,8 +42,7 @@ struct UpdScratch {
     FlowEntry* comb = nullptr;     // k_flow_combine entries (2 units each), comb_cap of them
     uint32_t* rows = nullptr;      // [flow_chunks][flow_parts]
     uint32_t* cols = nullptr;      // [flow_parts][flow_chunks]
-    uint32_t* rows_h = nullptr;    // [flow_chunks][flow_parts] rows before k_flow_combine (history)
-    uint32_t* cols_h = nullptr;    // [flow_parts][flow_chunks]
+    uint32_t* rows_h = nullptr;    // [flow_chunks][flow_parts] combined groups' rows before k_flow_combine
     uint32_t* e_orig = nullptr;    // [flow_recs] combined groups' original entry words (history)
     uint32_t* pos_map = nullptr;   // [flow_recs] combined groups' position map (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
@@ -221,7 +220,6 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.rows);
     hipFree(u.cols);
     hipFree(u.rows_h);
-    hipFree(u.cols_h);
     hipFree(u.e_orig);
     hipFree(u.pos_map);
     hipFree(u.hot);
@@ -235,7 +233,6 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
     if (hipMalloc(&u.entries, recs * 4ull) != hipSuccess ||
         hipMalloc(&u.comb, (uint64_t)c->comb_cap * 2ull * sizeof(FlowEntry)) != hipSuccess ||
         hipMalloc(&u.rows_h, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.cols_h, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.pos_map, recs * 4ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
@@ -1035,7 +1032,6 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.chunk_stride = (uint32_t)(c->flow_recs / kFlowChunk);
     p.batch = c->flow_batch;
     p.rows_h = u.rows_h;
-    p.cols_h = u.cols_h;
     p.e_orig = u.e_orig;
     p.pos_map = u.pos_map;
     p.hcount = c->d_hcount;

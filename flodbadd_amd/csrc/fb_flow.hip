@@ -264,15 +264,13 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     uint32_t total;
     uint32_t run = block_excl_scan(local, wsum, total);
     uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
-    uint32_t* row_h = P.rows_h + (size_t)blockIdx.x * P.parts;
     const uint32_t hot_min = max(kCombMin, 4u * ((cnt + P.parts - 1u) / P.parts));
     static_assert(kFlowMaxParts / kFlowK1Threads <= 64u, "a thread's partitions fit the hot mask");
     unsigned long long hot = 0ull;  // this thread's hot groups (bit j - j0), handed to k_flow_combine
     uint32_t n_hot = 0u;
     for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
         const uint32_t c = hist.get(j);
-        row[j] = run | (c << 16);
-        row_h[j] = run | (c << 16);
+        row[j] = run | (c << 16);  // run < kFlowChunk <= 2^15: bit 15 is k_flow_combine's mark
         if (c >= hot_min) {
             hot |= 1ull << (j - j0);
             ++n_hot;
@@ -317,19 +315,14 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
         P.ctl[1] = 0u;
         P.ctl[2] = 0u;
     }
-    for (int h = 0; h < 2; ++h) {  // rows -> cols (K2), rows_h -> cols_h (the history)
-        const uint32_t* rows = h ? P.rows_h : P.rows;
-        uint32_t* cols = h ? P.cols_h : P.cols;
-        for (uint32_t y = ty; y < 64u; y += 4u) {
-            const uint32_t c = c0 + y, p = p0 + tx;
-            tile[y][tx] = (c < chunks && p < P.parts) ? rows[(size_t)c * P.parts + p] : 0u;
-        }
-        __syncthreads();
-        for (uint32_t y = ty; y < 64u; y += 4u) {
-            const uint32_t p = p0 + y, c = c0 + tx;
-            if (p < P.parts && c < chunks) cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
-        }
-        __syncthreads();
+    for (uint32_t y = ty; y < 64u; y += 4u) {
+        const uint32_t c = c0 + y, p = p0 + tx;
+        tile[y][tx] = (c < chunks && p < P.parts) ? P.rows[(size_t)c * P.parts + p] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t y = ty; y < 64u; y += 4u) {
+        const uint32_t p = p0 + y, c = c0 + tx;
+        if (p < P.parts && c < chunks) P.cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
     }
 }
 
@@ -776,7 +769,6 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
         const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
-        uint32_t* rowp_h = P.rows_h + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
         for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
@@ -897,9 +889,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta]);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
-        if (threadIdx.x == 0) {
-            *rowp = (row & 0xFFFFu) | ((cursor + n_comb) << 16);
-            *rowp_h |= 0x8000u;  // a combined group: the history reads e_orig / pos_map here
+        if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_orig / pos_map, and
+                                 // the group's original row from rows_h)
+            *rowp = (row & 0x7FFFu) | 0x8000u | ((cursor + n_comb) << 16);
+            P.rows_h[(size_t)chunk * P.parts + part] = row;
         }
         __syncthreads();  // the table is re-initialised for the next group
     }
@@ -985,7 +978,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             for (uint32_t c = 0; c < kK2Cpt; ++c) {
                 const uint32_t j = threadIdx.x * kK2Cpt + c;
                 sp[j] = pre;
-                ss[j] = (g0 + j) * kFlowChunk + (v[c] & 0xFFFFu);
+                ss[j] = (g0 + j) * kFlowChunk + (v[c] & 0x7FFFu);  // (bit 15: combined group)
                 pre += v[c] >> 16;
             }
             __syncthreads();

@@ -155,12 +155,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams 
     const uint32_t out_beg = P.part_base[q];
     const uint32_t hc = P.hcount[(size_t)q * kFlowSlots + tid];
     const uint32_t vp = tid < chunks ? P.cols[(size_t)q * P.chunk_stride + tid] : 0u;
-    const uint32_t vh = tid < chunks ? P.cols_h[(size_t)q * P.chunk_stride + tid] : 0u;
     const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
     if (n_chars == 0u) return;  // uniform: no history characters in this partition
     for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) L.hist[j] = 0u;
-    const bool comb = (vh & 0x8000u) != 0u;
-    const uint32_t lp = vp >> 16, len = comb ? (vh >> 16) | 0x80000000u : lp;
+    const bool comb = (vp & 0x8000u) != 0u;
+    const uint32_t lp = vp >> 16, len = comb ? 0x80000000u : lp;  // (combined: the general kernel's)
     uint32_t tp, ep, tc;
     // run offsets (entries) and the slots' first output positions, one pair of barriers
     const uint32_t cur = block_scan2(hc, lp, tc, ep, tp, L.wsum, L.wsum2);  // slot tid's first position
@@ -316,8 +315,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
         const uint32_t out_beg = P.part_base[q], out_end = P.part_base[q + 1];
         const uint32_t hc = P.hcount[(size_t)q * kFlowSlots + tid];
         const uint32_t* col = P.cols + (size_t)q * P.chunk_stride;
-        const uint32_t* col_h = P.cols_h + (size_t)q * P.chunk_stride;
-        uint32_t vp = tid < chunks ? col[tid] : 0u, vh = tid < chunks ? col_h[tid] : 0u;
+        uint32_t vp = tid < chunks ? col[tid] : 0u;
         const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
         if (n_chars == 0u) return;  // uniform: no history characters in this partition
         {
@@ -329,9 +327,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
         // round setup: the runs of chunks c0 .. c0 + 511 (tid: run tid); returns the entries read
         auto round = [&](uint32_t c0, uint32_t nr) {
             const uint32_t c = c0 + tid;
-            const bool comb = tid < nr && (vh & 0x8000u) != 0u;
+            const bool comb = tid < nr && (vp & 0x8000u) != 0u;
+            // a combined group's original row (its records in e_orig): rows_h, read only for those
+            const uint32_t vh = comb ? P.rows_h[(size_t)c * P.parts + q] : 0u;
             const uint32_t lp = tid < nr ? vp >> 16 : 0u, lv = comb ? vh >> 16 : lp;  // applied / read entries
-            L.rs[tid] = c * kFlowChunk + (vp & 0xFFFFu);  // (k_flow_combine packs a group in place)
+            L.rs[tid] = c * kFlowChunk + (vp & 0x7FFFu);  // (k_flow_combine packs a group in place)
             L.rn[tid] = lv | (comb ? 1u << 31 : 0u);
             uint32_t tv, tp, ep;
             const uint32_t ev = block_scan2(lv, lp, tv, ep, tp);
@@ -476,7 +476,6 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                 const uint32_t nr = min(kHistRuns, chunks - c0);
                 if (c0 != 0u) {
                     vp = tid < nr ? col[c0 + tid] : 0u;
-                    vh = tid < nr ? col_h[c0 + tid] : 0u;
                     round(c0, nr);
                 }
                 // batches of whole runs up to kHistCap entries; a longer run alone, in record windows

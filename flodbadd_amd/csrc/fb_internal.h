@@ -237,9 +237,9 @@ struct FlowParams {
     uint32_t part_shift;        // 64 - log2(P) (64 when P == 1)
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
     uint32_t batch;             // update call number since create / clear (positions' high word)
-    uint32_t* rows_h;           // [chunks][parts] rows before k_flow_combine (the history reads every
-                                // record): start | count << 16, bit 15 set for a combined (hot) group
-    uint32_t* cols_h;           // [parts][chunk_stride] rows_h transposed (K1t)
+    uint32_t* rows_h;           // [chunks][parts] a combined group's row before k_flow_combine (K1c;
+                                // the history reads its records from e_orig); a combined group's
+                                // row in rows / cols has bit 15 set
     uint32_t* e_orig;           // [max_recs] a combined group's original entry words (K1c)
     uint32_t* pos_map;          // [max_recs] a combined group's original position -> the entry's new
                                 // position, or kRecFlowCombined | combined id
