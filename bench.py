@@ -52,7 +52,7 @@ def plan_launches(k, bpl):
 
 
 def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1,
-               synth_kw=None, pipelined=False, stage_extras=True):
+               synth_kw=None, pipelined=False, stage_extras=True, records=True):
     """Time `steps` steps (one step = one batch through the hot path).  mode "seg":
     fb_parse_classify_seg_dev (records compacted per 64-frame wavefront segment, no
     cross-workgroup dependency); mode "dense": fb_parse_classify_dev (the same kernel + the
@@ -64,7 +64,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     plan_launches.  Batch i uses buffer set i % rotate, so rotate >= bpl keeps the batches of a
     launch distinct.  pipelined (flow, mode "seg"): fb_process_seg_async_dev -- each batch's table
     update on the context's own stream while the next batch is parsed (rotate >= 2 buffer sets),
-    joined (fb_flow_join) inside the timed region."""
+    joined (fb_flow_join) inside the timed region.  records=False (flow, mode "seg"): the fused calls
+    keep only the session table (fb_set_session_records 0), as the reference's capture loop does."""
     from flodbadd_amd import synth
     frames, offs = synth.generate(config_id, n, first=rank * n, **(synth_kw or {}))
     nbytes = frames.nbytes
@@ -138,6 +139,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
 
     if flow:
         N.check(lib.fb_flow_clear(ctx, stream.ptr))
+    N.check(lib.fb_set_session_records(ctx, 1 if records else 0))
     run_steps(warmup, plan(warmup))
     if pipelined:
         N.check(lib.fb_flow_join(ctx, stream.ptr))
@@ -231,6 +233,9 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
         stage.update(dns_timing(N, lib, ctx, stream))
     if not flow:
         assert st2.tobytes() == st.tobytes()
+    N.check(lib.fb_set_session_records(ctx, 1))
+    if not records:  # no session record is written: the parse's bytes are the headers, offsets, DNS records
+        algo -= 56 * int(st[0]["n_session"])
     for b in bufs:
         for x in b:
             x.free()
@@ -578,7 +583,7 @@ def load_traffic(config_id, bpl=1):
         return None
 
 
-def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pipe, synth_kw=None):
+def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pipe, synth_kw=None, records=True):
     """The C4 step's parse / update split: for the pipelined line a one-stream fb_process_seg_dev run
     (fewer steps) whose stage event splits each step; plus the side timings the C4 main run took
     (history, enrichment, DNS parse)."""
@@ -588,7 +593,7 @@ def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pip
     if pipe:  # the stage split and the one-stream rate from fb_process_seg_dev, fewer steps
         st_s = max(steps // 2, 10)
         rs = run_config(N, lib, ctx, 4, n, st_s, max(warmup // 2, 2), 1, rank, world, dist, flow=True,
-                        mode=mode, synth_kw=synth_kw, stage_extras=False)
+                        mode=mode, synth_kw=synth_kw, stage_extras=False, records=records)
         split = rs["stage"]
         extra["c4_sync"] = dict(value=round(world * n * st_s / rs["elapsed"] / 1e6, 2), unit="Mpackets/s",
                                 ms_per_step=round(rs["elapsed"] * 1e3 / st_s, 4),
@@ -609,11 +614,12 @@ def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pip
     return extra
 
 
-def c4_algo_bytes(r):
+def c4_algo_bytes(r, records=True):
     """Algorithmic bytes of one C4 step: the parse's (header windows, offsets,
-    records written) + the update's: every SESSION record read once (56 B) and every flow's 128-B
-    table slot read and written once."""
-    return r["algo_bytes"] + 56 * r["stats"]["n_session"] + 2 * 128 * r["stage"]["flows"]
+    records written -- none when the table is the only output) + the update's: every SESSION record
+    read once (56 B; table-only: nothing, the table is built from the headers) and every flow's
+    128-B table slot read and written once."""
+    return r["algo_bytes"] + (56 * r["stats"]["n_session"] if records else 0) + 2 * 128 * r["stage"]["flows"]
 
 
 def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
@@ -622,15 +628,25 @@ def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
     buffer sets, joined inside the timed region), its parse / update split, the step's algorithmic
     bytes against HBM peak, and the CPU parse + upsert baseline beside it."""
     n = 10 * (1 << 20)
-    r = run_config(N, lib, ctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg", pipelined=True)
+    # the reference's capture loop keeps only the session table (each ParsedPacket is dropped after
+    # process_parsed_packet, src/capture.rs:1036-1061): the line's fused calls do the same
+    # (fb_set_session_records 0); c4_records times them storing every SESSION record too
+    r = run_config(N, lib, ctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg", pipelined=True,
+                   records=False)
     out = dict(value=round(world * n * steps / r["elapsed"] / 1e6, 2), unit="Mpackets/s",
                ms_per_step=round(r["elapsed"] * 1e3 / steps, 4), steps=steps, warmup=warmup,
-               workload=WORKLOADS[4], output="fb_process_seg_async_dev (pipelined parse + session upsert)")
-    ach = c4_algo_bytes(r) * steps / (r["ev_ms"] / 1e3) / 1e9
+               workload=WORKLOADS[4], output="fb_process_seg_async_dev (pipelined parse + session upsert; the "
+                                             "session table and the DNS side records are the output)")
+    ach = c4_algo_bytes(r, records=False) * steps / (r["ev_ms"] / 1e3) / 1e9
     out["roofline"] = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                           frac=round(ach / HBM_PEAK_GBS, 4), algo_bytes_per_step=int(c4_algo_bytes(r)),
+                           frac=round(ach / HBM_PEAK_GBS, 4), algo_bytes_per_step=int(c4_algo_bytes(r, records=False)),
                            note="whole step (parse + update, overlapped) over its algorithmic bytes")
-    out.update(c4_split(N, lib, ctx, r, n, steps, warmup, rank, world, dist, "seg", True))
+    rr = run_config(N, lib, ctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg", pipelined=True,
+                    stage_extras=False)
+    out["c4_records"] = dict(value=round(world * n * steps / rr["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                             ms_per_step=round(rr["elapsed"] * 1e3 / steps, 4),
+                             note="the same pipelined calls also storing every SESSION record (fb_pkt_out) in d_out")
+    out.update(c4_split(N, lib, ctx, r, n, steps, warmup, rank, world, dist, "seg", True, records=False))
     if rank == 0 and world == 1 and cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline_c4(r["frames"], r["offs"], cpu_seconds)
     return out
@@ -661,6 +677,8 @@ def main():
                          "default = the rotated batches (C2 / C3 32), 1 for C4")
     ap.add_argument("--c4-sync", action="store_true",
                     help="C4: time fb_process_seg_dev (one stream) instead of the pipelined fb_process_seg_async_dev")
+    ap.add_argument("--table-only", action="store_true",
+                    help="C4 (seg): the fused calls keep only the session table (fb_set_session_records 0)")
     ap.add_argument("--zipf", type=float, default=None,
                     help="profiling: the main run with Zipf(s) flow popularity instead of uniform")
     args = ap.parse_args()
@@ -704,7 +722,7 @@ def main():
     main_kw = dict(zipf=1, zipf_s=args.zipf) if args.zipf else None
     main_r = run_config(N, lib, ctx, args.config, n, args.steps, args.warmup, rotate, rank, world, dist,
                         flow=args.config == 4, mode=args.mode, bpl=bpl,
-                        synth_kw=main_kw, pipelined=pipe)
+                        synth_kw=main_kw, pipelined=pipe, records=not args.table_only)
     # the dominant kernel's launches: algorithmic bytes per launch / average launch duration
     per_launch_s = main_r["ev_ms"] / 1e3 / main_r["launches"]
     algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
@@ -714,7 +732,7 @@ def main():
     extra = {}
     if main_r["stage"]:
         extra.update(c4_split(N, lib, ctx, main_r, n, args.steps, args.warmup, rank, world, dist, args.mode, pipe,
-                              main_kw))
+                              main_kw, records=not args.table_only))
     if args.config == 4 and not args.no_other_mode:  # C4 also with Zipf(1.1) flow popularity
         rz = run_config(N, lib, ctx, 4, n, max(args.steps // 2, 5), max(args.warmup // 2, 2), rotate, rank, world,
                         dist, flow=True, mode=args.mode, synth_kw=dict(zipf=1, zipf_s=1.1))

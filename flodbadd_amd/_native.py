@@ -159,6 +159,7 @@ GPU_SYMBOLS = [
     ("fb_set_lan_v6", _I, [_P, _P, _U32]),
     ("fb_set_own_ips", _I, [_P, _P, _U32]),
     ("fb_set_stage_event", _I, [_P, _P]),
+    ("fb_set_session_records", _I, [_P, C.c_int]),
     ("fb_parse_classify_dev", _I, [_P, _P, _U64, _P, _U32, _P, _P, _P, _P, _P]),
     ("fb_parse_classify", _I, [_P, _P, _U64, _P, _U32, _P, _PU32, _P, _PU32, _P, _P, _P]),
     ("fb_process_parsed_dev", _I, [_P, _P, _U32, _P, _P, _P, _P]),

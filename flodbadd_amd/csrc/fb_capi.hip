@@ -107,6 +107,11 @@ struct fb_ctx {
     const fb_pkt_out* part_recs = nullptr;  // the records part_buf was written for (one update)
     uint32_t* part_buf = nullptr;           // the partition buffer the last fused parse wrote
     uint32_t* part_target = nullptr;        // the buffer the next fused parse writes (null: d_rec_part)
+    uint4* d_rec_ent = nullptr;             // [flow_recs] update entry (UpdEnt, 64 B) per record slot
+    uint4* d_rec_ent2 = nullptr;            // ... of the odd async batches
+    uint4* ent_buf = nullptr;               // the entries the last fused parse wrote (with part_buf)
+    uint4* ent_target = nullptr;            // the entries the next fused parse writes (null: d_rec_ent)
+    bool emit_records = true;               // fb_set_session_records: fused calls store SESSION records
     // fb_process_seg_async_dev: updates on the context's own stream, one batch behind the parses
     hipStream_t upd = nullptr;
     hipEvent_t ev_parsed = nullptr;
@@ -258,10 +263,14 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_hword);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
+    hipFree(c->d_rec_ent);
+    hipFree(c->d_rec_ent2);
     hipFree(c->d_agg_slot);
     c->d_rec_part = c->d_rec_part2 = nullptr;
+    c->d_rec_ent = c->d_rec_ent2 = nullptr;
     c->part_recs = nullptr;
     c->part_buf = nullptr;
+    c->ent_buf = nullptr;
     c->d_hword = nullptr;
     c->comb_cap = 0;
     c->d_agg_slot = nullptr;
@@ -269,6 +278,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     c->last_part = nullptr;
     c->flow_recs = 0;
     if (hipMalloc(&c->d_hword, recs * 4ull) != hipSuccess || hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_rec_ent, recs * 16ull * kUpdEntU4) != hipSuccess ||
         hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     c->flow_recs = recs;
@@ -486,6 +496,8 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_hword);
     hipFree(c->d_rec_part);
     hipFree(c->d_rec_part2);
+    hipFree(c->d_rec_ent);
+    hipFree(c->d_rec_ent2);
     hipFree(c->d_agg_slot);
     if (c->upd) hipStreamDestroy(c->upd);
     if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
@@ -537,6 +549,12 @@ int fb_set_stage_event(fb_ctx* c, void* event) {
     return FB_OK;
 }
 
+int fb_set_session_records(fb_ctx* c, int emit) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    c->emit_records = emit != 0;
+    return FB_OK;
+}
+
 int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
     if (!c || n > FB_MAX_OWN_IPS || (n && !ips)) return set_err(FB_ERR_INVAL, "bad own-ip table");
     c->h_cfg->n_own = n;
@@ -569,9 +587,12 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
     p.n = parsed ? sb.b[0].n : 0u;
     p.rec_part = (want_parts && sb.count == 1u && c->d_table) ? (c->part_target ? c->part_target : c->d_rec_part)
                                                               : nullptr;
+    p.rec_ent = p.rec_part ? (c->ent_target ? c->ent_target : c->d_rec_ent) : nullptr;
+    p.no_records = p.rec_part && !c->emit_records ? 1u : 0u;
     p.part_shift = c->flow_shift;
     c->part_recs = p.rec_part ? sb.b[0].out : nullptr;
     c->part_buf = p.rec_part;
+    c->ent_buf = p.rec_ent;
     p.cfg = c->d_cfg;
     p.tick = c->d_tick;
     if (pass != SegPass::kDenseOut) {
@@ -1042,6 +1063,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.agg_slot = c->d_agg_slot;
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
+    p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
     c->part_recs = nullptr;
     HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
     if (split) {
@@ -1120,6 +1142,8 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     if (rc) return rc;
     if (!c->d_rec_part2 && hipMalloc(&c->d_rec_part2, c->flow_recs * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "second partition buffer");
+    if (!c->d_rec_ent2 && hipMalloc(&c->d_rec_ent2, c->flow_recs * 16ull * kUpdEntU4) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "second update-entry buffer");
     // the same slot's previous batch (k-2): its update must be done before this parse rewrites the
     // slot's partition buffer; before any async batch, the last synchronous update is on `s` already
     if (c->async_k >= 2) HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[slot], 0));
@@ -1128,11 +1152,13 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     if (c->async_k >= 1 && (d_out == c->async_prev[0] || d_seg == c->async_prev[1] || d_stats == c->async_prev[2]))
         HIP_TRY(hipStreamWaitEvent(s, c->ev_upd[slot ^ 1u], 0));
     c->part_target = slot ? c->d_rec_part2 : c->d_rec_part;
+    c->ent_target = slot ? c->d_rec_ent2 : c->d_rec_ent;
     const uint32_t grid_full = c->seg_grid;
     c->seg_grid = c->seg_grid_async;
     rc = parse_seg(c, d_frames, frames_bytes, d_offsets, n, d_out, d_seg, d_class, d_stats, stream, true);
     c->seg_grid = grid_full;
     c->part_target = nullptr;
+    c->ent_target = nullptr;
     if (rc == FB_OK && c->stage_event) rc = hipEventRecord(c->stage_event, s) == hipSuccess
                                                 ? FB_OK : set_err(FB_ERR_HIP, "stage event record failed");
     if (rc) return rc;

@@ -94,23 +94,65 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
 #endif
 constexpr uint32_t kCombMin = FB_COMB_MIN;
 
-// Record slot `rec` of the batch as the four uint4 of a plain FlowEntry (fb_internal.h): key words,
-// key word 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char |
-// tcp_flags << 8 | has_flags << 16 | session flags << 20, the low word of the key's hash.  Records are 56 B, so only 8-B
-// aligned at odd slots: loaded through ld_u4 / ld_u2.
-__device__ __forceinline__ void rec_entry(const fb_pkt_out* recs, uint32_t rec, uint4 (&e)[4]) {
-    const uint32_t* r = reinterpret_cast<const uint32_t*>(recs + rec);
-    const uint4 a = ld_u4(r), b = ld_u4(r + 4), c = ld_u4(r + 8);
-    const uint2 m = ld_u2(r + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
-    const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-    const uint32_t meta = (m.x >> 8) & 0xFFu;
-    const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-    const uint32_t hinfo = ((m.x >> 16) & 0xFFu) | ((m.x & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
-                           ((meta >> 3) & 0xFu) << 20;  // FB_META_LOCAL_SRC .. SELF_DST -> fb_session_flags
-    e[0] = a;
-    e[1] = b;
-    e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
-    e[3] = make_uint4(m.y, rec, hinfo, (uint32_t)flow_hash_words(key));
+// An entry word's record as the four uint4 of a plain FlowEntry (fb_internal.h): key words, key word
+// 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char | tcp_flags
+// << 8 | has_flags << 16 | session flags << 20, the low word of the key's hash.  `rec` orders a
+// flow's packets: the record slot (entry word & kEntRecMask), or -- update entries from the fused
+// parse (P.ent; the word is unit index | IPv6 << 28) -- the pkt_index.  Records are 56 B, so only
+// 8-B aligned at odd slots: loaded through ld_u4 / ld_u2; an entry is one aligned 32-B unit (two
+// for an IPv6 key).  The raw words are loaded first (raw_entry) and decoded when applied
+// (entry_of), so K2 can keep loads in flight.
+__device__ __forceinline__ void raw_entry(const FlowParams& P, uint32_t w, uint4 (&r)[4]) {
+    if (P.ent) {
+        const uint4* u = P.ent + (size_t)(w & kEntUnitMask) * 2u;
+        r[0] = u[0];
+        r[1] = u[1];
+        if (w & kEntV6) {
+            r[2] = u[2];
+            r[3] = u[3];
+        } else {
+            r[2] = r[3] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    } else {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (w & kEntRecMask));
+        r[0] = ld_u4(q);
+        r[1] = ld_u4(q + 4);
+        r[2] = ld_u4(q + 8);
+        const uint2 m = ld_u2(q + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
+        r[3] = make_uint4(m.x, m.y, 0u, 0u);
+    }
+}
+__device__ __forceinline__ void entry_of(bool ent, const uint4 (&r)[4], uint32_t w, uint4 (&e)[4]) {
+    if (ent) {  // UpdEnt units: A = r[0], B = r[1]; IPv6: r[2], r[3] (zero words for IPv4)
+        const uint4 A = r[0], Bw = r[1], C = r[2], D = r[3];
+        const uint32_t key[10] = {A.x, C.x, C.y, C.z, A.y, C.w, D.x, D.y, A.z, A.w & 0xFFFFu};
+        e[0] = make_uint4(key[0], key[1], key[2], key[3]);
+        e[1] = make_uint4(key[4], key[5], key[6], key[7]);
+        e[2] = make_uint4(A.z, A.w & 0x1FFFFu, Bw.x, Bw.y);
+        e[3] = make_uint4(Bw.z, Bw.z, Bw.w & 0x03FFFFFFu, (uint32_t)flow_hash_words(key));
+    } else {
+        const uint4 a = r[0], b = r[1], c = r[2];
+        const uint32_t mx = r[3].x, my = r[3].y;
+        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+        const uint32_t meta = (mx >> 8) & 0xFFu;
+        const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
+        const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
+                               ((meta >> 3) & 0xFu) << 20;  // FB_META_LOCAL_SRC .. SELF_DST -> fb_session_flags
+        e[0] = a;
+        e[1] = b;
+        e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
+        e[3] = make_uint4(my, w & kEntRecMask, hinfo, (uint32_t)flow_hash_words(key));
+    }
+}
+__device__ __forceinline__ void rec_entry(const FlowParams& P, uint32_t w, uint4 (&e)[4]) {
+    uint4 r[4];
+    raw_entry(P, w, r);
+    entry_of(P.ent != nullptr, r, w, e);
+}
+// pkt_index of a combined group's first / last record `rec` (with entries rec IS the pkt_index)
+__device__ __forceinline__ uint32_t rec_pkt(const FlowParams& P, uint32_t rec) {
+    if (P.ent) return rec;
+    return reinterpret_cast<const uint32_t*>(P.recs + rec)[13];
 }
 
 // FB_HIST_CHARS bit of a map_tcp_flags character (16 = not a history character), branch-free (a
@@ -219,9 +261,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t k = threadIdx.x + j * kFlowK1Threads;
-            // partition | history code << 16 (the parse's word: partition | char << 16 | has_flags << 24)
-            const uint32_t w = pv[j];
-            pv[j] = (w & kRecPartMask) | hist_code((w >> 24) & 1u, (w >> 16) & 0xFFu) << 16;
+            // the parse's word: partition | unit offset << 16 | IPv6 << 23 (kRec*, fb_internal.h)
             if (!(k < cnt && ((base + k) & 63u) < (sw[j] & 0xFFFFu))) pv[j] = ~0u;
         }
     } else {            // hashed here, four records' key loads in flight at a time
@@ -292,15 +332,17 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
         }
     }
     __syncthreads();
-    // scatter: entry position -> the record's slot index | its history code (4 B); K2 gathers the
-    // record itself
+    // scatter: entry position -> the record's slot index | its history code, or (entries from the
+    // fused parse) its update entry's unit index | IPv6 << 28 (4 B); K2 gathers the record / entry
     uint32_t* out = P.entries + base;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (pv[j] == ~0u) continue;
         const uint32_t k = threadIdx.x + j * kFlowK1Threads;
         const uint32_t d = hist.add(pv[j] & kRecPartMask);
-        out[d] = (base + k) | (pv[j] >> 16) << kEntCodeShift;
+        out[d] = P.rec_part ? ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j] >> kRecUnitShift) & 127u) |
+                                  ((pv[j] & kRecV6) ? kEntV6 : 0u)
+                            : (base + k) | (pv[j] >> 16) << kEntCodeShift;
     }
 }
 
@@ -628,7 +670,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
 // A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
 // the group's partial sums / minima / maxima.  Its records' pos_map words point at agg_slot[id].
 __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr,
-                                              const fb_pkt_out* recs, const uint4 e0, const uint4 e1,
+                                              const FlowParams& P, const uint4 e0, const uint4 e1,
                                               const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
                                               const uint4 t2, const uint4 t3, uint32_t slot_base, uint32_t* agg_slot,
                                               uint32_t* err) {
@@ -657,12 +699,8 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     uint32_t* q = scr + (size_t)i * kScrU32;
     // the group's first / last / end records: their pkt_index (and the end's character) read here
     // -- combined entries are few
-    auto rec_word = [&](uint32_t rec) {  // (flags | meta << 8 | hist_char << 16, pkt_index)
-        return ld_u2(reinterpret_cast<const uint32_t*>(recs + rec) + 12);
-    };
-    const uint2 wf = rec_word(e2.z), wl = rec_word(e2.w), we = rec_word(e3.y != ~0u ? e3.y : e2.w);
-    atomicMin(sc64(q, kScFirst), (unsigned long long)e2.z << 32 | wf.y);
-    atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | wl.y);
+    atomicMin(sc64(q, kScFirst), (unsigned long long)e2.z << 32 | rec_pkt(P, e2.z));
+    atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | rec_pkt(P, e2.w));
     const uint32_t hc = e3.z & 0xFFFFu;
     const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) : 0u);
     if (m) atomicOr(q + kScMask, m);
@@ -672,7 +710,7 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
 #pragma unroll
         for (uint32_t b = 0; b < 4u; ++b)
             if (c[b] != ~0u) atomicMin(q + kScChar + b, c[b]);
-        if (e3.y != ~0u) atomicMin(sc64(q, kScEnd), end_key(e3.y, hist_bit((we.x >> 16) & 0xFFu), we.y));
+        if (e3.y != ~0u) atomicMin(sc64(q, kScEnd), end_key(e3.y, (t3.w >> 8) & 31u, rec_pkt(P, e3.y)));
     }
     return result;
 }
@@ -784,8 +822,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         for (uint32_t k = threadIdx.x; k < cnt; k += kCombThreads) {
             uint4 e[4];
             const uint32_t w = E[s0 + k];
-            P.e_orig[s0 + k] = w;  // the group's original words stay readable for the history
-            rec_entry(P.recs, w & kEntRecMask, e);
+            rec_entry(P, w, e);
+            // the group's original words stay readable for the history (record order key | code:
+            // with update entries rebuilt from the entry -- its pkt_index and character)
+            P.e_orig[s0 + k] = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
             const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                       e[2].y & 0xFFFFu};
             uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
@@ -807,7 +847,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 const uint32_t b = hist_bit(e[3].z & 0xFFu);
                 if (b < 16u) atomicOr(f + kCfMask, 1u << b);
                 if (b < 4u) atomicMin(f + kCfChar + b, rec);
-                if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec);
+                if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec << 5 | b);  // (rec < 2^27)
             }
         }
         __syncthreads();
@@ -850,7 +890,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
                 if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
                     uint4 e[4];
-                    rec_entry(P.recs, rec & kEntRecMask, e);
+                    rec_entry(P, rec, e);
                     const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                               e[2].y & 0xFFFFu};
                     j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
@@ -882,11 +922,11 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
             o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
             o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
-            o[3] = make_uint4(id, f[kCfEnd], f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
+            o[3] = make_uint4(id, f[kCfEnd] == ~0u ? ~0u : f[kCfEnd] >> 5, f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
             o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
             o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
             o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
-            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta]);
+            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta] | (f[kCfEnd] & 31u) << 8);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
         if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_orig / pos_map, and
@@ -1004,13 +1044,8 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                     r[1] = c[1];
                     r[2] = c[2];
                     r[3] = c[3];
-                } else {  // a record slot of the batch (56 B, 8-B aligned at odd slots)
-                    const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (v & kEntRecMask));
-                    r[0] = ld_u4(q);
-                    r[1] = ld_u4(q + 4);
-                    r[2] = ld_u4(q + 8);
-                    const uint2 m = ld_u2(q + 12);
-                    r[3] = make_uint4(m.x, m.y, 0u, 0u);
+                } else {  // a record slot of the batch: its update entry or its record
+                    raw_entry(P, v, r);
                 }
             };
             uint32_t e = threadIdx.x, ix0 = 0u, v0 = 0u, ix1 = 0u, v1 = 0u;
@@ -1034,29 +1069,26 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                 if (v0 & kIdxCombined) {
                     const uint4* t = CE + (size_t)(v0 & ~kIdxCombined) * 8u + 4u;
                     const uint4 t3 = t[3];
-                    const int r = apply_combined(slice, tags, scr, P.recs, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
+                    const int r = apply_combined(slice, tags, scr, P, r0[0], r0[1], r0[2], r0[3], t[0], t[1], t[2], t3,
                                                  part * kFlowSlots, P.agg_slot, P.error);
                     if (r >= 0) {
                         n_new += r == 1;
                         n_upd += t3.z - (r == 1 ? 1u : 0u);
                     }
                 } else {
-                    // the record as a plain FlowEntry (layout: fb_internal.h; rec_entry above)
-                    const uint4 a = r0[0], b2 = r0[1], c = r0[2];
-                    const uint32_t mx = r0[3].x, my = r0[3].y;
-                    const uint32_t key[10] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w, c.x, c.y & 0xFFFFu};
-                    const uint32_t meta = (mx >> 8) & 0xFFu;
-                    const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-                    const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) |
-                                           ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0xFu) << 20;
+                    // the entry as a plain FlowEntry (layout: fb_internal.h; entry_of above)
+                    uint4 fe[4];
+                    entry_of(P.ent != nullptr, r0, v0, fe);
                     uint32_t sl = ~0u;
-                    const int r = apply_entry(slice, tags, scr, a, b2, make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w),
-                                              make_uint4(my, v0 & kEntRecMask, hinfo, (uint32_t)flow_hash_words(key)), sl,
-                                              P.error);
+                    const int r = apply_entry(slice, tags, scr, fe[0], fe[1], fe[2], fe[3], sl, P.error);
                     n_new += r == 1;
                     n_upd += r == 0;
                     // the history word (layout: fb_internal.h), in this partition's entry order
-                    P.hword[hbase + rbase + e] = r < 0 ? 0u : hist_word(sl, v0);
+                    // (with update entries the code comes from the entry and rec is its pkt_index)
+                    P.hword[hbase + rbase + e] =
+                        r < 0 ? 0u
+                              : P.ent ? hist_word(sl, hist_code((fe[3].z >> 16) & 1u, fe[3].z & 0xFFu), fe[3].y)
+                                      : hist_word(sl, v0);
                 }
 #pragma unroll
                 for (uint32_t w = 0; w < 4u; ++w) r0[w] = r1[w];

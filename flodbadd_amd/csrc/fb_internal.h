@@ -40,6 +40,10 @@ struct ParseParams {
     uint32_t* error;              // this launch's error word (launch parity); set by the flow kernels
     uint32_t* error_next;         // the other parity's word, zeroed by this launch for the next one
     uint32_t* rec_part;           // one batch: partition of each SESSION record slot, or nullptr
+    uint4* rec_ent;               // with rec_part: the update entry of each SESSION record slot
+                                  // (UpdEnt, 64-B units) -- what the table update reads
+    uint32_t no_records;          // with rec_part: SESSION records not stored (the table is the
+                                  // output; DNS records, counts, classes and stats still are)
     const unsigned long long* pre;  // dense pass 2: per segment n_session | n_dns << 32 before it
     fb_pkt_out* dense_out;        // dense pass 2: batch-wide SESSION records (or nullptr)
     fb_dns_out* dense_dns;        // dense pass 2: batch-wide DNS records (or nullptr)
@@ -192,8 +196,11 @@ constexpr uint32_t kEntCodeShift = 27;
 // (4 bits, 0: none) << 9, record slot within its bucketing chunk (15 bits) << 13; 0 for an entry
 // the table could not take.
 static_assert(FB_FLOW_SLOTS == 512 && FB_FLOW_CHUNK <= 32768, "hist_word field widths");
+__device__ __forceinline__ uint32_t hist_word(uint32_t slot_local, uint32_t code, uint32_t rec) {
+    return slot_local | (code & 15u) << 9 | (rec % kFlowChunk) << 13;
+}
 __device__ __forceinline__ uint32_t hist_word(uint32_t slot_local, uint32_t entry_word) {
-    return slot_local | ((entry_word >> kEntCodeShift) & 15u) << 9 | ((entry_word & kEntRecMask) % kFlowChunk) << 13;
+    return hist_word(slot_local, entry_word >> kEntCodeShift, entry_word & kEntRecMask);
 }
 
 // fb_flow_hash of a 40-B session_key (10 words, word 9 = protocol | family << 8) and the
@@ -254,12 +261,37 @@ struct FlowParams {
     const uint32_t* rec_part;   // non-null: partition of each SESSION record slot, written by the
                                 // segmented parse of the same batch (fb_process_seg_dev); K1's
                                 // histogram pass then reads 4 B per record instead of the record
+    const uint4* ent;           // non-null (with rec_part): the slots' update entries (UpdEnt), which
+                                // K1c / K2 read instead of the records
 };
 // The fused parse's per-record word: the table partition (< kFlowMaxParts) in the low 16 bits,
 // the record's history character in bits 16-23 and FB_META_HAS_FLAGS in bit 24 -- so the history
 // keys kernel reads 4 B per record slot instead of the record.
 constexpr uint32_t kRecPartMask = 0xFFFFu;
 static_assert(kFlowMaxParts <= kRecPartMask + 1u, "partition ids fit the low half");
+
+// Update entries (UpdEnt): what the fused parse (fb_process_seg[_async]_dev) hands the table update
+// per SESSION record, packed in 32-B units -- one for an IPv4 key, two for an IPv6 key -- back to
+// back in packet order inside a 4-KB region per 64-frame segment (128 units), so every line the
+// parse writes is whole (per-slot 64-B units with the IPv4 half unwritten cost the C4 parse 1.5x:
+// partial-line writes) and the update's random gathers read one aligned 32-B unit for an IPv4 key
+// instead of a 56-B record that straddles a 128-B line 43 % of the time:
+//   unit 0: key[0], key[4], key[8], key[9] | originator << 16     (addresses' first words, ports,
+//                                                                   protocol | family << 8)
+//           packet_length, ip_packet_length, pkt_index,
+//           hinfo | rank << 26   (hinfo: hist_char | tcp_flags << 8 | has_flags << 16 | session
+//                                 flags << 20; rank: the record's slot in its segment)
+//   unit 1: key[1], key[2], key[3], key[5], key[6], key[7], 0, 0  (IPv6 only)
+// The fused parse's per-slot word (rec_part) then holds partition | unit offset << 16 | IPv6 << 23,
+// and the bucketing pass's index word is unit index | IPv6 << 28.  With entries the update orders a
+// flow's packets by pkt_index (the frame index: monotone in packet order, within the record slots'
+// bucketing chunk) instead of the record slot.
+constexpr uint32_t kUpdUnitsPerSeg = 128;
+constexpr uint32_t kUpdEntU4 = 4;                   // uint4 per record slot of the entry buffer (its size)
+constexpr uint32_t kEntUnitMask = 0x0FFFFFFFu;      // index word: unit index
+constexpr uint32_t kEntV6 = 1u << 28;               // index word: an IPv6 key (two units)
+constexpr uint32_t kRecUnitShift = 16, kRecV6 = 1u << 23;  // rec_part fields
+__host__ __device__ inline bool upd_ent_v6(uint32_t a_w) { return ((a_w >> 8) & 0xFFu) == 10u; }
 
 // Launchers (fb_parse.hip / fb_compact.hip / fb_flow.hip).
 // Which k_parse_seg instance: the segmented output; dense pass 1 (segment counts, classes, stats);

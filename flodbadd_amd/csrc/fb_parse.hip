@@ -329,7 +329,10 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     const uint32_t nb = MULTI ? SB.count : 1u;
     constexpr uint32_t kAcc = kMaxSegBatches * 10u;
     __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
-    __shared__ unsigned long long s_stage[kSegWaves][64 * 7];
+    // a wave's staging area: its segment's compacted records (64 x 56 B), then -- partition-writing
+    // instance -- its update entries (64 x 64 B)
+    constexpr uint32_t kStageU64 = (FLAGS & kPartOut) ? 64u * 8u : 64u * 7u;
+    __shared__ __attribute__((aligned(16))) unsigned long long s_stage[kSegWaves][kStageU64];
     __shared__ uint32_t s_acc[kAcc + 1];  // per batch: block counters (see the stats section); wave arrivals
     const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
     const unsigned long long lmask = (1ull << lane) - 1ull;
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         load_q(next_q, X.q);
     };
     // stores per step: segmented 8 (+1 partition), count-only 2, dense 6
-    constexpr int kStores = (FLAGS & kCountOnly) ? 2 : (FLAGS & kDense) ? 6 : ((FLAGS & kPartOut) ? 9 : 8);
+    constexpr int kStores = (FLAGS & kCountOnly) ? 2 : (FLAGS & kDense) ? 6 : ((FLAGS & kPartOut) ? 13 : 8);
     auto dropped_stores = [&]() {
 #pragma unroll
         for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, r_drop, kOob + 64u * j, 0, 0);
@@ -573,6 +576,10 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             // stores: 4 x 16 B of session records, the 8-B tail, one DNS record, the count, the class
                 const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
                     reinterpret_cast<uint8_t*>(B.out) + (size_t)ls * kSegBytes, (short)0, (int)kSegBytes, 0x00020000);
+                // the SESSION records (not stored when the fused call's table is the only output)
+                const __amdgpu_buffer_rsrc_t r_rec = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<uint8_t*>(B.out) + (size_t)ls * kSegBytes, (short)0,
+                    ((FLAGS & kPartOut) != 0u && P.no_records) ? 0 : (int)kSegBytes, 0x00020000);
                 const __amdgpu_buffer_rsrc_t r_seg =
                     __builtin_amdgcn_make_buffer_rsrc(B.seg, (short)0, (int)(((B.n + 63u) / 64u) * 4u), 0x00020000);
                 const __amdgpu_buffer_rsrc_t r_cls =
@@ -584,13 +591,13 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                     const uint32_t src = min(cc, 223u);
                     const unsigned long long x = stage[2u * src], y = stage[2u * src + 1u];
                     const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? cc * 16u : kOob, 0, FB_ST_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, r_rec, cc < body ? cc * 16u : kOob, 0, FB_ST_AUX);
                 }
                 {
                     const bool tail = (words & 1u) && lane == 0u;
                     const unsigned long long x = stage[words ? words - 1u : 0u];
                     const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b64(v, r_out, tail ? (words - 1u) * 8u : kOob, 0, FB_ST_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b64(v, r_rec, tail ? (words - 1u) * 8u : kOob, 0, FB_ST_AUX);
                 }
                 {
                     const u32x4 v = {kk.w[0], kk.w[1], kk.w[2], kk.w[3]};
@@ -604,11 +611,40 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                         P.rec_part + (size_t)ls * 64u, (short)0, 256, 0x00020000);
                     const uint32_t key[10] = {kk.w[0], kk.w[1], kk.w[2], kk.w[3], kk.w[4],
                                               kk.w[5], kk.w[6], kk.w[7], kk.w[8], kk.w[9] & 0xFFFFu};
-                    // partition | history char << 16 | has_flags << 24 (kRecPart*, fb_internal.h)
-                    const uint32_t pw = part_of(flow_hash_words(key), P.part_shift) | (kk.w[12] & 0x00FF0000u) |
-                                        ((kk.w[12] & 0x100u) << 16);
-                    __builtin_amdgcn_raw_buffer_store_b32(pw, r_part,
-                                                          is_s ? (uint32_t)__popcll(m_sess & lmask) * 4u : kOob, 0, 0);
+                    // update entries (UpdEnt, fb_internal.h): 32-B units packed in packet order, two
+                    // for an IPv6 key, staged in LDS (the records' reads of the stage come first in
+                    // this wave's program order) and stored as whole lines
+                    const uint32_t rank = (uint32_t)__popcll(m_sess & lmask);
+                    const bool v6 = upd_ent_v6(kk.w[9]);
+                    const unsigned long long m_v6 = __ballot(is_s && v6);
+                    const uint32_t uoff = rank + (uint32_t)__popcll(m_v6 & lmask);
+                    const uint32_t units = cs + (uint32_t)__popcll(m_v6);
+                    // partition | unit offset << 16 | IPv6 << 23 (kRec*, fb_internal.h)
+                    const uint32_t pw = part_of(flow_hash_words(key), P.part_shift) | uoff << kRecUnitShift |
+                                        (v6 ? kRecV6 : 0u);
+                    __builtin_amdgcn_raw_buffer_store_b32(pw, r_part, is_s ? rank * 4u : kOob, 0, 0);
+                    if (is_s) {
+                        const uint32_t meta = (kk.w[12] >> 8) & 0xFFu;
+                        const uint32_t hinfo = ((kk.w[12] >> 16) & 0xFFu) | ((kk.w[12] & 0xFFu) << 8) |
+                                               ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0xFu) << 20;
+                        const uint32_t aw = kk.w[9] | ((meta & FB_META_ORIGINATOR) ? 1u << 16 : 0u);
+                        u32x4* e = reinterpret_cast<u32x4*>(stage + (size_t)uoff * 4u);
+                        e[0] = u32x4{kk.w[0], kk.w[4], kk.w[8], aw};
+                        e[1] = u32x4{kk.w[10], kk.w[11], kk.w[13], hinfo | rank << 26};
+                        if (v6) {
+                            e[2] = u32x4{kk.w[1], kk.w[2], kk.w[3], kk.w[5]};
+                            e[3] = u32x4{kk.w[6], kk.w[7], 0u, 0u};
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    const __amdgpu_buffer_rsrc_t r_ent = __builtin_amdgcn_make_buffer_rsrc(
+                        P.rec_ent + (size_t)ls * 64u * kUpdEntU4, (short)0, (int)(units * 32u), 0x00020000);
+#pragma unroll
+                    for (uint32_t k = 0; k < kUpdEntU4; ++k) {  // 4 x 1 KB: up to 128 units
+                        const uint32_t q = k * 64u + lane;
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + (size_t)min(q, 255u) * 2u);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, r_ent, q * 16u, 0, 0);
+                    }
                 }
             }
             __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
@@ -685,44 +721,55 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 // ============================================================================================
 // k_parse_dense -- single-pass batch-wide (dense) output of one frame batch.
 //
-// The batch is cut into tiles of kDnTileSegs 64-frame segments; block b runs tiles b, b + G,
-// b + 2G ... (G = grid).  Per tile it parses and classifies the frames with the records kept in
-// registers (kDnSegs segments per wave), publishes the tile's (n_session, n_dns) in an
-// epoch-tagged status word, looks back over its predecessors' words for the tile's batch-wide
-// offset (decoupled look-back by wave 0, a 64-tile window per step), and stores the records and
-// DNS records at their final positions.  Classes and batch stats as in k_parse_seg.  Replaces
-// pass 1 + scan + pass 2 of the two-pass dense path (fb_compact.hip): the same outputs from one
-// read of the headers.
+// Tiles of kDnTileSegs 64-frame segments; block b owns tiles b, b + G, b + 2G ... (G = grid).
+// A block is kDnWaves PARSE waves and one STORE wave:
+//   parse waves  stream over the block's segments the way k_parse_seg does (one segment per step,
+//                the next segment's headers in flight, segments handed out inside the block from
+//                an LDS counter), put each segment's compacted SESSION records (from the front)
+//                and DNS records (from the back) into the segment's 3,584-B slot of its tile's LDS
+//                buffer, store the classes, and count the segment done.  Two tile buffers: a wave
+//                runs up to one tile ahead of the stores.
+//   store wave   per tile, in order: waits until the tile's segments are done, publishes the
+//                tile's (n_session, n_dns) in an epoch-tagged status word, looks back over its
+//                predecessors' words for the tile's batch-wide offset (decoupled look-back, a
+//                64-tile window per step), publishes the inclusive prefix, copies the records and
+//                DNS records from LDS to their final positions (16-B stores) and frees the buffer.
+// No parse wave waits on a look-back: the status-word round trips (~3 us each under streaming
+// load, MI355X_MICROARCH.md handoff rows) overlap the parse of the next tile.  Round 2's kernel
+// kept the records in registers and ran the look-back and the stores between two block barriers
+// (38.5 us per 1M-frame C2 batch, ~8.5 us of it look-back round trips, ~8 us barriers).
 //
 // Forward progress without assuming every workgroup is resident (a GPU shared with other work
 // may not run all of them at once -- the failure round 1's look-back kernel had): a
-// look-back that has waited kDnSteal polls for a predecessor's word computes that tile's sums
-// itself (count-only classification of its frames, the same deterministic result the owner
+// look-back that has waited P.steal_polls polls for a predecessor's word computes that tile's
+// sums itself (count-only classification of its frames, the same deterministic result the owner
 // will publish), CASes them in as the tile's aggregate if the word is still unpublished, and
 // walks on.  So a look-back never depends on a workgroup that is not running; in the normal case
-// nothing is recomputed.  A ticket counter ordering the tiles instead was measured first: its
-// same-address atomics (~1,500 per 1M frames) cost 16 us per batch.
+// nothing is recomputed.  Inside a block the parse and store waves depend only on each other
+// (all resident): a parse wave waits for a buffer only until the store wave has copied the tile
+// two rounds back, and the store wave waits for segments that parse waves grabbed earlier.
 // ============================================================================================
-#ifndef FB_DN_SEGS
-#define FB_DN_SEGS 2
+#ifndef FB_DN_WAVES
+#define FB_DN_WAVES 15
+#endif
+#ifndef FB_DN_TILE
+#define FB_DN_TILE 16
 #endif
 #ifndef FB_DN_BPC
-#define FB_DN_BPC 2
+#define FB_DN_BPC 1
 #endif
-#ifndef FB_DN_WAVES
-#define FB_DN_WAVES 8
+#ifndef FB_DN_LB
+#define FB_DN_LB 1
 #endif
 #ifndef FB_DN_SLEEP
 #define FB_DN_SLEEP 1
 #endif
-constexpr int kDnWaves = FB_DN_WAVES;
-constexpr int kDnSegs = FB_DN_SEGS;  // segments per wave per tile (records held in registers)
-constexpr uint32_t kDnTileSegs = kDnWaves * kDnSegs;
-constexpr int kDnThreads = 64 * kDnWaves;
-#ifndef FB_DN_LB
-#define FB_DN_LB 1
-#endif
+constexpr int kDnWaves = FB_DN_WAVES;         // parse waves per block (+ the store wave)
+constexpr uint32_t kDnTileSegs = FB_DN_TILE;  // segments per tile
+constexpr int kDnThreads = 64 * (kDnWaves + 1);
 constexpr int kDnLb = FB_DN_LB;  // look-back: status words per lane per step
+constexpr uint32_t kDnSlotU64 = kSegBytes / 8u;  // one segment's slot in a tile buffer (448 u64)
+static_assert(kDnTileSegs <= 64u, "the store wave holds one segment count per lane");
 // tile status word [epoch:8 | P:1 | A:1 | n_dns:27 | n_session:27]: A = the tile's own sums are
 // published, P = its inclusive prefix is (k_seg_scan's format)
 constexpr unsigned long long kDnA = 1ull << 54, kDnP = 1ull << 55, kDn27 = (1ull << 27) - 1ull;
@@ -732,40 +779,70 @@ __device__ __forceinline__ unsigned long long dn_word(uint32_t ep, unsigned long
 __device__ __forceinline__ unsigned long long dn_pair(unsigned long long w) {
     return (w & kDn27) | (((w >> 27) & kDn27) << 32);
 }
+struct DnLds {
+    unsigned long long buf[2][kDnTileSegs][kDnSlotU64];  // tile buffers, one slot per segment
+    unsigned long long base[2];                           // the buffer's tile: batch-wide offset (pair)
+    uint32_t cnt[2][kDnTileSegs];                         // per slot n_session | n_dns << 16
+    uint32_t pre[2][kDnTileSegs];                         // per slot: records | DNS records before it in the tile
+    uint32_t done[2];                                     // slots of the buffer's tile written
+    uint32_t copied[2];                                   // slots of the buffer's tile copied out
+    uint32_t ready_round[2];                              // the round whose offset base / pre hold
+    uint32_t free_round[2];                               // the block round the buffer is free for
+    uint32_t next;                                        // the next segment number to hand out
+    uint32_t acc[11];                                     // the block's stats counters; wave arrivals
+};
 
-__global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_dense(const ParseParams P,
-                                                                                      const SegBatch B) {
+// Blocks per CU: 8-wave blocks (7 parse + 1 store) two per CU.  With 9-wave blocks (8 + 1) at 95
+// VGPRs the occupancy query said two per CU but the hardware admitted one (each block puts three
+// waves on one SIMD; two blocks there need six, the VGPRs allow five), and the grid's second half
+// ran only after the first: the look-backs of the resident half waited for it (5.8 ms per C2 batch).
+__global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) void k_parse_dense(const ParseParams P,
+                                                                                        const SegBatch B) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint32_t nt = P.ntiles, ep = P.dep, n = B.n;
+    const uint32_t nseg = (n + 63u) / 64u;
     __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
-    __shared__ unsigned long long s_stage[kDnWaves][64 * 7];
-    __shared__ unsigned long long s_wsum[2][kDnWaves];  // per wave n_session | n_dns << 32, by tile parity
-    __shared__ unsigned long long s_excl;                // the tile's batch-wide offset (same packing)
-    __shared__ uint32_t s_acc[11];                       // the block's stats counters; wave arrivals
+    __shared__ DnLds L;
     const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
     const unsigned long long lmask = (1ull << lane) - 1ull;
-    unsigned long long* stage = s_stage[wave];
     constexpr uint32_t kOob = 0x80000000u;
-    uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
-    if (tid <= 10u) s_acc[tid] = 0u;
     const __amdgpu_buffer_rsrc_t r_fr =
         __builtin_amdgcn_make_buffer_rsrc((void*)B.frames, (short)0, (int)B.frames_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)n : 0, 0x00020000);
-    uint32_t par = 0u;
-    // the offsets of the wave's segments of tile t (the next tile's are loaded while this one runs,
-    // so a tile waits for one round trip before its headers arrive, not two)
-    uint2 q[kDnSegs];
-    auto load_offsets = [&](uint32_t t, uint2 (&qq)[kDnSegs]) {
-        const uint32_t sg0 = min(t, nt - 1u) * kDnTileSegs + wave * (uint32_t)kDnSegs;
-#pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) {
-            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
-            qq[j] = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
-        }
+    const bool parser = wave < (uint32_t)kDnWaves;
+    if (tid < 2u) {
+        L.done[tid] = 0u;
+        L.copied[tid] = 0u;
+        L.ready_round[tid] = ~0u;
+        L.free_round[tid] = tid;
+    }
+    if (tid <= 10u) L.acc[tid] = 0u;
+    if (tid == 0u) L.next = 2u * kDnWaves;  // the first two segments of each wave are static
+
+    // block-local segment number Ls -> global segment: round Ls / T of the block (tile b + round G),
+    // slot Ls % T of the tile
+    auto seg_of = [&](uint32_t Ls) { return (b + (Ls / kDnTileSegs) * G) * kDnTileSegs + Ls % kDnTileSegs; };
+    auto grab = [&]() {
+        uint32_t v = 0u;
+        if (lane == 0u) v = __hip_atomic_fetch_add(&L.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readfirstlane(v);
     };
-    if (b < nt) load_offsets(b, q);  // in flight with the configuration copy
+    auto load_q = [&](uint32_t g, uint2& q) {  // frame offsets of segment g (past the end: clamped)
+        const uint32_t i = min(g, nseg) * 64u + lane;
+        q = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
+    };
+    auto vmov = [](uint32_t x) {
+        uint32_t y;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+        return y;
+    };
+    // parse waves: the current segment's headers (h) and offsets (c), the next segment's offsets (q)
+    Hdr h;
+    uint2 c = make_uint2(0u, 0u), q = make_uint2(0u, 0u);
+    uint32_t Lc = wave, Ln = wave + kDnWaves;
+    if (parser) load_q(seg_of(Lc), q);  // in flight with the configuration copy
     {
         constexpr uint32_t kCfg16 = kCfgLdsBytes / 16;
         const uint4* src = reinterpret_cast<const uint4*>(P.cfg);
@@ -776,92 +853,76 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
         for (uint32_t k = tid; k < no; k += kDnThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
         if (b == 0u && tid == 0u) *P.error_next = 0u;
     }
-    lds_barrier();  // configuration in LDS (the offsets loads stay in flight)
-    // (n_session, n_dns) of tile j, computed by the calling wave (the look-back's fallback)
-    auto tile_pair = [&](uint32_t j) {
-        unsigned long long acc = 0ull;
-        for (uint32_t sgi = 0; sgi < kDnTileSegs; ++sgi) {
-            const uint32_t i = (j * kDnTileSegs + sgi) * 64u + lane;
-            const bool valid = i < n;
-            const uint2 q = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
-            Hdr h;
-            load_headers1(r_fr, q.x, h);
-            Pkt k;
-            process_frame(r_fr, cfg, cfg, h, valid ? q.x : 1u, valid ? q.y : 0u, B.frames_bytes, i, k);
-            acc += (unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_SESSION)) |
-                   ((unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_DNS)) << 32);
-        }
-        return acc;
+    auto fetch = [&](uint32_t g_after) {  // q holds the next segment's offsets
+        load_headers1(r_fr, q.x, h);
+        c = make_uint2(vmov(q.x), vmov(q.y));
+        load_q(g_after, q);
     };
-    // the current tile's headers: loaded here for the first tile, then during the previous tile's
-    // look-back and stores (issued right after its first barrier), so a tile starts on headers
-    // that are already in registers
-    Hdr h[kDnSegs];
-    if (b < nt) {
-#pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, q[j].x, h[j]);
+    if (parser) {
+        fetch(seg_of(Ln));
+        __builtin_amdgcn_raw_buffer_store_b8(0u, r_cls, kOob, 0, 0);  // the step's VMEM sequence (dropped store)
     }
-    for (uint32_t t = b; t < nt; t += G) {
-        const uint32_t sg0 = t * kDnTileSegs + wave * (uint32_t)kDnSegs;
-        uint2 qn[kDnSegs];
-        load_offsets(t + G, qn);
-        Pkt kk[kDnSegs];
-        uint32_t cs[kDnSegs], cd[kDnSegs], rs[kDnSegs], rd[kDnSegs];
-        bool ss[kDnSegs], sd[kDnSegs];
-        unsigned long long ws = 0ull;
+    lds_barrier();  // configuration and block state in LDS (loads stay in flight); the last block barrier
+
+    if (!parser) {
+        // ---------------- store wave: the tiles' offsets ----------------
+        // (n_session, n_dns) of tile j, computed by this wave (the look-back's fallback)
+        auto tile_pair = [&](uint32_t j) {
+            unsigned long long acc = 0ull;
+            for (uint32_t sgi = 0; sgi < kDnTileSegs; ++sgi) {
+                const uint32_t i = (j * kDnTileSegs + sgi) * 64u + lane;
+                const bool valid = i < n;
+                const uint2 qq = make_uint2(B.offsets[min(i, n)], B.offsets[min(i + 1u, n)]);
+                Hdr hh;
+                load_headers1(r_fr, qq.x, hh);
+                Pkt k;
+                process_frame(r_fr, cfg, cfg, hh, valid ? qq.x : 1u, valid ? qq.y : 0u, B.frames_bytes, i, k);
+                acc += (unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_SESSION)) |
+                       ((unsigned long long)__popcll(__ballot(valid && k.cls == FB_CLASS_DNS)) << 32);
+            }
+            return acc;
+        };
+        for (uint32_t r = 0;; ++r) {
+            const uint32_t t = b + r * G;
+            if (t >= nt) break;
+            const uint32_t p = r & 1u;
+            const uint32_t segs = min(kDnTileSegs, nseg - t * kDnTileSegs);
+            // the buffer serves this round (its previous tile is copied out: done was reset before
+            // free_round moved on) and every slot of the tile is written
+            while (__hip_atomic_load(&L.free_round[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != r ||
+                   __hip_atomic_load(&L.done[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != segs)
+                __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
+            // per slot exclusive prefixes inside the tile (lane j: slot j), and the tile's sums
+            const uint32_t cw = lane < segs ? L.cnt[p][lane] : 0u;
+            uint32_t incl = cw;  // n_session | n_dns << 16 never carries (<= 64 per slot, 16 slots)
 #pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) {
-            const uint32_t i = (sg0 + (uint32_t)j) * 64u + lane;
-            const bool valid = i < n;
-            process_frame(r_fr, cfg, cfg, h[j], valid ? q[j].x : 1u, valid ? q[j].y : 0u, B.frames_bytes, i, kk[j]);
-            const bool is_s = valid && kk[j].cls == FB_CLASS_SESSION;
-            const bool is_d = valid && kk[j].cls == FB_CLASS_DNS;
-            const bool is_f = valid && kk[j].cls == FB_CLASS_FILTERED;
-            const bool counted = is_s || is_f;
-            const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
-            cs[j] = (uint32_t)__popcll(m_sess);
-            cd[j] = (uint32_t)__popcll(m_dns);
-            rs[j] = (uint32_t)__popcll(m_sess & lmask);
-            rd[j] = (uint32_t)__popcll(m_dns & lmask);
-            ss[j] = is_s;
-            sd[j] = is_d;
-            ws += (unsigned long long)cs[j] | ((unsigned long long)cd[j] << 32);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk[j].cls, r_cls, valid ? i : kOob, 0, 0);
-            a_s += cs[j];
-            a_d += cd[j];
-            a_f += __popcll(__ballot(is_f));
-            a_t += __popcll(__ballot(counted && kk[j].tcp));
-            a_4 += __popcll(__ballot(counted && kk[j].v4));
-            a_b += __popcll(__ballot(valid && kk[j].bad));
-            a_n += __popcll(__ballot(valid));
-        }
-        if (lane == 0u) s_wsum[par][wave] = ws;
-        lds_barrier();
-        if (t + G < nt) {  // the next tile's headers, in flight through the look-back and the stores
-#pragma unroll
-            for (int j = 0; j < kDnSegs; ++j) load_headers1(r_fr, qn[j].x, h[j]);
-        }
-        if (wave == 0u) {
-            unsigned long long agg = 0ull;
-#pragma unroll
-            for (int k = 0; k < kDnWaves; ++k) agg += s_wsum[par][k];
+            for (int o = 1; o < (int)kDnTileSegs; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            if (lane < kDnTileSegs) L.pre[p][lane] = incl - cw;
+            const uint32_t tot = __shfl(incl, (int)kDnTileSegs - 1, 64);
+            const unsigned long long agg = (unsigned long long)(tot & 0xFFFFu) | ((unsigned long long)(tot >> 16) << 32);
             unsigned long long excl = 0ull;
             if (t == 0u) {
                 if (lane == 0u) __hip_atomic_store(P.dstatus, dn_word(ep, kDnP, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (lane == 0u)
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnA, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // window of 64 x kDnLb tiles per step: lane l holds tiles jt-1-(l*kDnLb+k), k < kDnLb.
-                // A step waits only for the words in front of the nearest published inclusive prefix
-                // (P) it can see -- words behind it are not needed -- and walks on when there is none.
+                // window of 64 x kDnLb tiles per step (lane l holds tiles jt-1-(l*kDnLb+k), k < kDnLb:
+                // a round's G tiles finish together, so the walk from the last tiles of a round back
+                // to the previous round's inclusive prefixes is G tiles long -- one step when
+                // 64 kDnLb >= G).  A step waits only for the words in front of the nearest published
+                // inclusive prefix (P) it can see, re-polling only those, and walks on when there is
+                // none.
                 int64_t jt = (int64_t)t;
                 auto ready = [&](unsigned long long x) { return (uint32_t)(x >> 56) == ep && (x & (kDnA | kDnP)); };
+                auto probe = [&](int k) {
+                    const int64_t idx = jt - 1 - (int64_t)(lane * (uint32_t)kDnLb + (uint32_t)k);
+                    return idx >= 0 ? __hip_atomic_load(P.dstatus + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : dn_word(ep, kDnP, 0ull);
+                };
                 for (;;) {
-                    auto probe = [&](int k) {
-                        const int64_t idx = jt - 1 - (int64_t)(lane * (uint32_t)kDnLb + (uint32_t)k);
-                        return idx >= 0 ? __hip_atomic_load(P.dstatus + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                        : dn_word(ep, kDnP, 0ull);
-                    };
                     unsigned long long v[kDnLb];
 #pragma unroll
                     for (int k = 0; k < kDnLb; ++k) v[k] = probe(k);
@@ -920,58 +981,151 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
                     __hip_atomic_store(P.dstatus + t, dn_word(ep, kDnP, excl + agg), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (lane == 0u) s_excl = excl;
+            // the offset for the parse waves, which copy their slots out (release: pre and base
+            // are visible before the round is marked ready -- with relaxed orders the compiler
+            // may put the base store after the flag, and a parse wave copied to a stale offset)
+            if (lane == 0u) {
+                L.base[p] = excl;
+                __hip_atomic_store(&L.ready_round[p], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
-        lds_barrier();
-        unsigned long long base = s_excl;
-#pragma unroll
-        for (int k = 0; k < kDnWaves; ++k) base += (uint32_t)k < wave ? s_wsum[par][k] : 0ull;
-#pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) {
-            // the segment's records at record bs of the batch (56 bs is 16-B aligned when bs is even;
-            // otherwise its first 8-B word goes alone and the 16-B body stays aligned), DNS at bd
-            if (ss[j]) {
-                unsigned long long* dd = stage + (size_t)rs[j] * 7;
-#pragma unroll
-                for (int w = 0; w < 7; ++w)
-                    dd[w] = (unsigned long long)kk[j].w[2 * w] | ((unsigned long long)kk[j].w[2 * w + 1] << 32);
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t bs = (uint32_t)base, bd = (uint32_t)(base >> 32);
-            const uint32_t words = cs[j] * 7u, head = cs[j] ? (bs & 1u) : 0u, body = (words - head) >> 1;
-            const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<uint8_t*>(P.dense_out) + (size_t)bs * 56u, (short)0, P.dense_out ? (int)(words * 8u) : 0,
-                0x00020000);
-            const __amdgpu_buffer_rsrc_t r_dns = __builtin_amdgcn_make_buffer_rsrc(
-                P.dense_dns + bd, (short)0, P.dense_dns ? (int)(cd[j] * 16u) : 0, 0x00020000);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t cc = lane + 64u * k;
-                const uint32_t src = head + 2u * min(cc, 223u - head);
-                const unsigned long long x = stage[src], y = stage[src + 1u];
-                const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? head * 8u + cc * 16u : kOob, 0, FB_ST_AUX);
-            }
-            {   // lane 0: the head word (odd base), lane 1: the tail word (odd body remainder)
-                const bool h1 = head && lane == 0u, t1 = ((words - head) & 1u) && lane == 1u;
-                const uint32_t w = lane == 0u ? 0u : (words ? words - 1u : 0u);
-                const unsigned long long x = stage[w];
-                const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b64(v, r_out, (h1 || t1) ? w * 8u : kOob, 0, FB_ST_AUX);
-            }
-            {
-                const u32x4 v = {kk[j].w[0], kk[j].w[1], kk[j].w[2], kk[j].w[3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, r_dns, sd[j] ? 16u * rd[j] : kOob, 0, 0);
-            }
-            __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
-            base += (unsigned long long)cs[j] | ((unsigned long long)cd[j] << 32);
-        }
-        par ^= 1u;
-#pragma unroll
-        for (int j = 0; j < kDnSegs; ++j) q[j] = qn[j];
+        return;
     }
-    // batch stats: as k_parse_seg (one batch): wave counters into LDS, the block's last wave adds
-    // the block's into the five packed device words; the block completing a word writes its fields
+
+    // ---------------- parse waves ----------------
+    // A written slot stays pending in its wave until the store wave has published its tile's
+    // offset; the wave copies it out at a later step.  Two rules keep every wait finite: a wave
+    // only blocks on a copy when each slot it holds is written (its tile can then complete without
+    // it), and while it waits for a free buffer it copies whatever of its own has become ready (a
+    // buffer is free once every slot of its tile two rounds back is copied).  At most two pending
+    // slots per wave.
+    uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
+    uint32_t pend0 = ~0u, pend1 = ~0u;  // pending slots' segment numbers Ls, oldest first (~0u: none)
+    auto ready_of = [&](uint32_t Ls) {
+        const uint32_t rnd = Ls / kDnTileSegs;
+        return __hip_atomic_load(&L.ready_round[rnd & 1u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == rnd;
+    };
+    auto copy_out = [&](uint32_t Ls) {  // (the tile's offset is published)
+        const uint32_t rnd = Ls / kDnTileSegs, p = rnd & 1u, j = Ls % kDnTileSegs;
+        const unsigned long long* stage = L.buf[p][j];
+        const uint32_t cw = L.cnt[p][j], pw = L.pre[p][j];
+        const unsigned long long bp = L.base[p];
+        const uint32_t cs = cw & 0xFFFFu, cd = cw >> 16;
+        // records at batch-wide record bs (56 bs is 16-B aligned when bs is even; otherwise the
+        // first 8-B word goes alone and the 16-B body stays aligned), DNS records at bd
+        const uint32_t bs = (uint32_t)bp + (pw & 0xFFFFu), bd = (uint32_t)(bp >> 32) + (pw >> 16);
+        const uint32_t words = cs * 7u, head = cs ? (bs & 1u) : 0u, body = (words - head) >> 1;
+        const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<uint8_t*>(P.dense_out) + (size_t)bs * 56u, (short)0, P.dense_out ? (int)(words * 8u) : 0,
+            0x00020000);
+        const __amdgpu_buffer_rsrc_t r_dns = __builtin_amdgcn_make_buffer_rsrc(
+            P.dense_dns + bd, (short)0, P.dense_dns ? (int)(cd * 16u) : 0, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t cc = lane + 64u * k;
+            const uint32_t src = head + 2u * min(cc, 223u - head);
+            const unsigned long long x = stage[src], y = stage[src + 1u];
+            const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? head * 8u + cc * 16u : kOob, 0, FB_ST_AUX);
+        }
+        {   // lane 0: the head word (odd base), lane 1: the tail word (odd body remainder)
+            const bool h1 = head && lane == 0u, t1 = ((words - head) & 1u) && lane == 1u;
+            const uint32_t w = lane == 0u ? 0u : (words ? words - 1u : 0u);
+            const unsigned long long x = stage[w];
+            const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(v, r_out, (h1 || t1) ? w * 8u : kOob, 0, FB_ST_AUX);
+        }
+        {   // DNS record k of the slot sits at its back, 16 B each
+            const unsigned long long* e = stage + kDnSlotU64 - 2u * (min(lane, 63u) + 1u);
+            const unsigned long long x = e[0], y = e[1];
+            const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b128(v, r_dns, lane < cd ? 16u * lane : kOob, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's LDS reads have returned
+        if (lane == 0u) {
+            const uint32_t t = b + rnd * G, segs = min(kDnTileSegs, nseg - t * kDnTileSegs);
+            const uint32_t old = __hip_atomic_fetch_add(&L.copied[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old + 1u == segs) {  // the tile's last copy: the buffer serves round rnd + 2
+                L.done[p] = 0u;
+                L.copied[p] = 0u;
+                __hip_atomic_store(&L.free_round[p], rnd + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    };
+    uint32_t sg = seg_of(Lc);
+    while (sg < nseg) {
+        const uint32_t La = grab();
+        const uint32_t g_next = seg_of(Ln);
+        const uint32_t i = sg * 64u + lane;
+        const bool valid = i < n;
+        Pkt kk;
+        process_frame(r_fr, cfg, cfg, h, valid ? c.x : 1u, valid ? c.y : 0u, B.frames_bytes, i, kk);
+        const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
+        const bool is_d = valid && kk.cls == FB_CLASS_DNS;
+        const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
+        const bool counted = is_s || is_f;
+        const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+        const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
+        fetch(seg_of(La));  // the next segment's headers, the offsets of the one after
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
+        // the segment's slot in its tile's buffer (free once the tile two rounds back is copied out);
+        // meanwhile this wave's own ready slots go out
+        const uint32_t rnd = Lc / kDnTileSegs, p = rnd & 1u, j = Lc % kDnTileSegs;
+        for (;;) {
+            if (pend0 != ~0u && ready_of(pend0)) {
+                copy_out(pend0);
+                pend0 = pend1;
+                pend1 = ~0u;
+            }
+            if (__hip_atomic_load(&L.free_round[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == rnd) break;
+            __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
+        }
+        unsigned long long* slot = L.buf[p][j];
+        if (is_s) {
+            unsigned long long* dd = slot + (size_t)__popcll(m_sess & lmask) * 7;
+#pragma unroll
+            for (int w = 0; w < 7; ++w)
+                dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
+        }
+        if (is_d) {
+            unsigned long long* dd = slot + kDnSlotU64 - 2u * (1u + (uint32_t)__popcll(m_dns & lmask));
+            dd[0] = (unsigned long long)kk.w[0] | ((unsigned long long)kk.w[1] << 32);
+            dd[1] = (unsigned long long)kk.w[2] | ((unsigned long long)kk.w[3] << 32);
+        }
+        if (lane == 0u) L.cnt[p][j] = cs | (cd << 16);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is written before it is counted
+        if (lane == 0u) __hip_atomic_fetch_add(&L.done[p], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // pend this slot; with two already pending, the oldest goes out first (every slot this wave
+        // holds is written now, so waiting for its tile cannot wait for this wave)
+        if (pend1 != ~0u) {
+            while (!ready_of(pend0)) __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
+            copy_out(pend0);
+            pend0 = pend1;
+            pend1 = ~0u;
+        }
+        if (pend0 == ~0u) pend0 = Lc;
+        else pend1 = Lc;
+        a_s += cs;
+        a_d += cd;
+        a_f += __popcll(__ballot(is_f));
+        a_t += __popcll(__ballot(counted && kk.tcp));
+        a_4 += __popcll(__ballot(counted && kk.v4));
+        a_b += __popcll(__ballot(valid && kk.bad));
+        a_n += __popcll(__ballot(valid));
+        Lc = Ln;
+        Ln = La;
+        sg = g_next;
+    }
+    for (uint32_t k = 0; k < 2u; ++k) {  // the last pending slots
+        if (pend0 == ~0u) break;
+        while (!ready_of(pend0)) __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
+        copy_out(pend0);
+        pend0 = pend1;
+        pend1 = ~0u;
+    }
+    // batch stats: as k_parse_seg (one batch): wave counters into LDS, the block's last parse wave
+    // adds the block's into the five packed device words; the block completing a word writes its
+    // fields
     {
         const uint32_t a_tot = a_s + a_f;
         const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
@@ -979,16 +1133,16 @@ __global__ __launch_bounds__(kDnThreads, kDnWaves * FB_DN_BPC / 4) void k_parse_
             uint32_t v = 0u;
 #pragma unroll
             for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
-            __hip_atomic_fetch_add(&s_acc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&L.acc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         uint32_t arrived = 0u;
-        if (lane == 0u) arrived = __hip_atomic_fetch_add(&s_acc[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0u) arrived = __hip_atomic_fetch_add(&L.acc[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         arrived = __shfl(arrived, 0, 64);
         if (arrived == (uint32_t)kDnWaves - 1u && lane < 5u) {
             asm volatile("" ::: "memory");
             const uint32_t j = lane;
-            const unsigned long long lo = s_acc[2u * j], hi = s_acc[2u * j + 1u];
+            const unsigned long long lo = L.acc[2u * j], hi = L.acc[2u * j + 1u];
             unsigned long long* word = P.tick + j;
             const unsigned long long add = (1ull << 54) | (hi << 27) | lo;
             const unsigned long long old = __hip_atomic_fetch_add(word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1029,7 +1183,9 @@ hipError_t launch_parse_dense(const ParseParams& p, const SegBatch& b, uint32_t 
     return hipGetLastError();
 }
 hipError_t occupancy_parse_dense(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_parse_dense, kDnThreads, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_parse_dense, kDnThreads, 0);
+    if (e == hipSuccess && *blocks_per_cu > FB_DN_BPC) *blocks_per_cu = FB_DN_BPC;  // (the query can overstate it)
+    return e;
 }
 uint32_t parse_dense_tile_segs() { return kDnTileSegs; }
 

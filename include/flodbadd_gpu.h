@@ -276,6 +276,13 @@ int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
  * (from fb_event_create, caller-owned; NULL clears) is set, fb_process_dev / fb_process_seg_dev
  * record it on their stream between the parse and the session-table update. */
 int fb_set_stage_event(fb_ctx* ctx, void* event);
+/* Whether the fused parse + upsert calls (fb_process_seg_dev, fb_process_seg_async_dev) store the
+ * SESSION records in d_out (default 1).  With 0 the session table is their only per-packet output,
+ * as in the reference's capture loop, which drops each ParsedPacket once process_parsed_packet has
+ * updated the DashMap (src/capture.rs:1036-1061): d_out then receives only the DNS side records at
+ * the segment tails, d_seg / d_class / d_stats are unchanged, and the history, export and
+ * enrichment calls work as before (the update reads the parse's own update entries either way). */
+int fb_set_session_records(fb_ctx* ctx, int emit);
 
 /*
  * Device-resident parse + classify (parse_packet_pcap + the per-packet part of
@@ -285,7 +292,7 @@ int fb_set_stage_event(fb_ctx* ctx, void* event);
  *   d_dns   : >= n fb_dns_out, class-DNS records, packet order
  *   d_class : n bytes, fb_class of every frame
  *   d_stats : one fb_batch_stats (overwritten, not accumulated)
- * One pass (k_parse_dense): 1,024-frame tiles whose batch-wide offsets come from a decoupled
+ * One pass (k_parse_dense): 512-frame tiles whose batch-wide offsets come from a decoupled
  * look-back; a look-back that finds a predecessor tile unpublished for long computes that tile's
  * counts itself instead of waiting on it, so the call never depends on every workgroup being
  * resident and is safe on a GPU shared with other work.

@@ -149,3 +149,53 @@ def test_async_empty_batch_and_table_full():
         for b in keep:
             b.free()
         cap.close()
+
+
+def test_table_only_equals_records(reference):
+    """fb_set_session_records(ctx, 0) (the reference's capture loop keeps only the table): the same
+    table, per-batch stats and history through the pipelined call; no SESSION record is stored in
+    d_out, while the segment counts and the DNS side records at the segment tails are."""
+    from oracle import coracle
+    batches, (ref_rows, ref_stats, ref_hist, ref_cnt) = reference
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 18)
+    stream = N.Stream()
+    keep = []
+    try:
+        N.check(lib.fb_set_session_records(cap.ctx, 0))
+        outs = []
+        for frames, offs in batches:
+            n = len(offs) - 1
+            nseg = (n + 63) // 64
+            b = [N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+                 N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize)]
+            b[2].memset(0x5A)
+            keep += b
+            N.check(lib.fb_process_seg_async_dev(cap.ctx, b[0].ptr, frames.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr,
+                                                 None, b[4].ptr, stream.ptr))
+            outs.append((frames, offs, nseg, b[2], b[3], b[4]))
+        N.check(lib.fb_flow_join(cap.ctx, stream.ptr))
+        stream.sync()
+        st = [o[5].download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr).tobytes() for o in outs]
+        assert st == ref_stats
+        flows = cap.export_flows()
+        assert cap.flow_count() == ref_cnt and rows_sorted(flows) == ref_rows
+        n_last = (len(batches[-1][1]) - 1 + 63) // 64 * 64
+        assert _keyed_history(cap, n_last, flows) == ref_hist
+        for frames, offs, nseg, d_out, d_seg, _ in outs:
+            seg = d_seg.download(np.zeros(nseg, dtype=np.uint32))
+            raw = d_out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8)).reshape(nseg, N.SEG_BYTES)
+            r_out, r_dns, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
+            assert int((seg & 0xFFFF).sum()) == len(r_out) and int((seg >> 16).sum()) == len(r_dns)
+            dns = []
+            for s in range(nseg):
+                cs, cd = int(seg[s] & 0xFFFF), int(seg[s] >> 16)
+                assert (raw[s, :cs * 56] == 0x5A).all(), "a SESSION record was stored"
+                for j in range(cd):
+                    dns.append(raw[s, N.SEG_BYTES - 16 * (j + 1):N.SEG_BYTES - 16 * j].tobytes())
+            assert b"".join(dns) == r_dns.tobytes()
+    finally:
+        N.check(lib.fb_set_session_records(cap.ctx, 1))
+        for b in keep:
+            b.free()
+        cap.close()
