@@ -58,9 +58,8 @@ struct fb_ctx {
     bool need_reset = true;       // zero the tick + error words before the next launch
     uint32_t epoch = 0;           // parse launches so far: its parity picks the launch's error word
     uint32_t seg_grid = 0;        // streaming segmented kernel: co-resident blocks
-    uint32_t seg_grid_async = 0;  // ... in the pipelined call: one block per CU, so the previous
-                                  // batch's table update keeps the rest of each CU (C4: 9,700 ->
-                                  // 10,200-10,300 Mpackets/s against 9,840-9,990 at the full grid)
+    uint32_t seg_grid_async = 0;  // ... in the pipelined call: FB_ASYNC_BPC blocks per CU (not the full
+                                  // grid), so the previous batch's table update keeps part of each CU
     uint32_t* d_error = nullptr;  // [4] error words, indexed by launch & 3 (a launch clears the next one's;
                                   // a pipelined update still writes the one two launches back)
     // dense output (fb_parse_classify_dev & co., fb_seg_compact_dev): segment counts + their scan
@@ -417,7 +416,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
 #ifndef FB_ASYNC_BPC
-#define FB_ASYNC_BPC 1
+#define FB_ASYNC_BPC 2  // round 3 (update entries, K1 staged): 2 blocks per CU 12.87-12.89 vs 12.54-12.55 Gpps at 1
 #endif
         c->seg_grid_async = std::min<uint32_t>((uint32_t)(FB_ASYNC_BPC * prop.multiProcessorCount), c->seg_grid);
         int db = 0;

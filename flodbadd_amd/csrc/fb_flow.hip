@@ -213,6 +213,11 @@ struct PartHist {
 __host__ __device__ inline uint32_t part_hist_bytes(uint32_t parts) {
     return parts > kFlowPackedParts ? parts * 2u : parts * 4u;
 }
+// K1 stages its scatter in LDS (the chunk's 4-B words) when the histogram leaves room for it
+__host__ __device__ inline bool k1_staged(uint32_t parts) { return parts <= kFlowPackedParts; }
+__host__ __device__ inline uint32_t k1_lds_bytes(uint32_t parts) {
+    return part_hist_bytes(parts) + (k1_staged(parts) ? kFlowChunk * 4u : 0u);
+}
 static_assert(kFlowChunk < 65536u, "packed K1 counters hold a chunk's records");
 
 // ---------------------------------------------------------------------------------------------
@@ -334,15 +339,29 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     __syncthreads();
     // scatter: entry position -> the record's slot index | its history code, or (entries from the
     // fused parse) its update entry's unit index | IPv6 << 28 (4 B); K2 gathers the record / entry
+    // Up to kFlowPackedParts partitions the words are scattered into an LDS copy of the chunk's
+    // region and stored coalesced: scattered 4-B global stores left L2 partial lines that were
+    // written back piecemeal (C4: 267 MB written per batch for 42 MB of words).
     uint32_t* out = P.entries + base;
+    const bool staged = k1_staged(P.parts);
+    uint32_t* stg = hist_w + part_hist_bytes(P.parts) / 4u;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (pv[j] == ~0u) continue;
         const uint32_t k = threadIdx.x + j * kFlowK1Threads;
         const uint32_t d = hist.add(pv[j] & kRecPartMask);
-        out[d] = P.rec_part ? ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j] >> kRecUnitShift) & 127u) |
-                                  ((pv[j] & kRecV6) ? kEntV6 : 0u)
-                            : (base + k) | (pv[j] >> 16) << kEntCodeShift;
+        const uint32_t w = P.rec_part ? ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j] >> kRecUnitShift) & 127u) |
+                                            ((pv[j] & kRecV6) ? kEntV6 : 0u)
+                                      : (base + k) | (pv[j] >> 16) << kEntCodeShift;
+        if (staged) stg[d] = w;
+        else out[d] = w;
+    }
+    if (staged) {
+        __syncthreads();
+        uint4* o4 = reinterpret_cast<uint4*>(out);  // (base is a multiple of kFlowChunk: 16-B aligned)
+        const uint4* s4 = reinterpret_cast<const uint4*>(stg);
+        for (uint32_t q = threadIdx.x; q < total / 4u; q += kFlowK1Threads) o4[q] = s4[q];
+        if (threadIdx.x < (total & 3u)) out[(total & ~3u) + threadIdx.x] = stg[(total & ~3u) + threadIdx.x];
     }
 }
 
@@ -1257,11 +1276,11 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
 
 hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_flow_bucket,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)part_hist_bytes(kFlowMaxParts));
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)k_flow_bucket, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)std::max(k1_lds_bytes(kFlowMaxParts), k1_lds_bytes(kFlowPackedParts)));
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), part_hist_bytes(p.parts), s, p);
+    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), k1_lds_bytes(p.parts), s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (p.hot) {
