@@ -727,7 +727,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 //                the next segment's headers in flight, segments handed out inside the block from
 //                an LDS counter), put each segment's compacted SESSION records (from the front)
 //                and DNS records (from the back) into the segment's 3,584-B slot of its tile's LDS
-//                buffer, store the classes, and count the segment done.  Two tile buffers: a wave
+//                buffer, store the classes, and count the segment done.  kDnBufs tile buffers: a wave
 //                runs up to one tile ahead of the stores.
 //   store wave   per tile, in order: waits until the tile's segments are done, publishes the
 //                tile's (n_session, n_dns) in an epoch-tagged status word, looks back over its
@@ -747,7 +747,11 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 // walks on.  So a look-back never depends on a workgroup that is not running; in the normal case
 // nothing is recomputed.  Inside a block the parse and store waves depend only on each other
 // (all resident): a parse wave waits for a buffer only until the store wave has copied the tile
-// two rounds back, and the store wave waits for segments that parse waves grabbed earlier.
+// kDnBufs rounds back, and the store wave waits for segments that parse waves grabbed earlier.
+// Geometry measured (C2 / C3 per 1M frames): 16-segment tiles, two buffers, one 15 + 1-wave block
+// per CU 37.3-38.4 / 47.9-49.1 us; 20-segment tiles 38.2-38.5 / 50.9; 12 x 3 buffers 41.1-41.5;
+// 8 x 3 or 4 buffers 47.9-49.8; poll sleeps of 4 / 16 within noise -- the tile count, not the
+// buffering depth, sets the pace.
 // ============================================================================================
 #ifndef FB_DN_WAVES
 #define FB_DN_WAVES 15
@@ -761,6 +765,9 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
 #ifndef FB_DN_LB
 #define FB_DN_LB 1
 #endif
+#ifndef FB_DN_BUFS
+#define FB_DN_BUFS 2
+#endif
 #ifndef FB_DN_SLEEP
 #define FB_DN_SLEEP 1
 #endif
@@ -768,6 +775,7 @@ constexpr int kDnWaves = FB_DN_WAVES;         // parse waves per block (+ the st
 constexpr uint32_t kDnTileSegs = FB_DN_TILE;  // segments per tile
 constexpr int kDnThreads = 64 * (kDnWaves + 1);
 constexpr int kDnLb = FB_DN_LB;  // look-back: status words per lane per step
+constexpr uint32_t kDnBufs = FB_DN_BUFS;  // tile buffers: a wave runs up to kDnBufs - 1 tiles ahead of the copies
 constexpr uint32_t kDnSlotU64 = kSegBytes / 8u;  // one segment's slot in a tile buffer (448 u64)
 static_assert(kDnTileSegs <= 64u, "the store wave holds one segment count per lane");
 // tile status word [epoch:8 | P:1 | A:1 | n_dns:27 | n_session:27]: A = the tile's own sums are
@@ -780,14 +788,14 @@ __device__ __forceinline__ unsigned long long dn_pair(unsigned long long w) {
     return (w & kDn27) | (((w >> 27) & kDn27) << 32);
 }
 struct DnLds {
-    unsigned long long buf[2][kDnTileSegs][kDnSlotU64];  // tile buffers, one slot per segment
-    unsigned long long base[2];                           // the buffer's tile: batch-wide offset (pair)
-    uint32_t cnt[2][kDnTileSegs];                         // per slot n_session | n_dns << 16
-    uint32_t pre[2][kDnTileSegs];                         // per slot: records | DNS records before it in the tile
-    uint32_t done[2];                                     // slots of the buffer's tile written
-    uint32_t copied[2];                                   // slots of the buffer's tile copied out
-    uint32_t ready_round[2];                              // the round whose offset base / pre hold
-    uint32_t free_round[2];                               // the block round the buffer is free for
+    unsigned long long buf[kDnBufs][kDnTileSegs][kDnSlotU64];  // tile buffers, one slot per segment
+    unsigned long long base[kDnBufs];                     // the buffer's tile: batch-wide offset (pair)
+    uint32_t cnt[kDnBufs][kDnTileSegs];                   // per slot n_session | n_dns << 16
+    uint32_t pre[kDnBufs][kDnTileSegs];                   // per slot: records | DNS records before it in the tile
+    uint32_t done[kDnBufs];                               // slots of the buffer's tile written
+    uint32_t copied[kDnBufs];                             // slots of the buffer's tile copied out
+    uint32_t ready_round[kDnBufs];                        // the round whose offset base / pre hold
+    uint32_t free_round[kDnBufs];                         // the block round the buffer is free for
     uint32_t next;                                        // the next segment number to hand out
     uint32_t acc[11];                                     // the block's stats counters; wave arrivals
 };
@@ -812,7 +820,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         __builtin_amdgcn_make_buffer_rsrc((void*)B.frames, (short)0, (int)B.frames_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(B.cls, (short)0, B.cls ? (int)n : 0, 0x00020000);
     const bool parser = wave < (uint32_t)kDnWaves;
-    if (tid < 2u) {
+    if (tid < kDnBufs) {
         L.done[tid] = 0u;
         L.copied[tid] = 0u;
         L.ready_round[tid] = ~0u;
@@ -885,7 +893,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         for (uint32_t r = 0;; ++r) {
             const uint32_t t = b + r * G;
             if (t >= nt) break;
-            const uint32_t p = r & 1u;
+            const uint32_t p = r % kDnBufs;
             const uint32_t segs = min(kDnTileSegs, nseg - t * kDnTileSegs);
             // the buffer serves this round (its previous tile is copied out: done was reset before
             // free_round moved on) and every slot of the tile is written
@@ -997,16 +1005,16 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
     // offset; the wave copies it out at a later step.  Two rules keep every wait finite: a wave
     // only blocks on a copy when each slot it holds is written (its tile can then complete without
     // it), and while it waits for a free buffer it copies whatever of its own has become ready (a
-    // buffer is free once every slot of its tile two rounds back is copied).  At most two pending
+    // buffer is free once every slot of its tile kDnBufs rounds back is copied).  At most two pending
     // slots per wave.
     uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
     uint32_t pend0 = ~0u, pend1 = ~0u;  // pending slots' segment numbers Ls, oldest first (~0u: none)
     auto ready_of = [&](uint32_t Ls) {
         const uint32_t rnd = Ls / kDnTileSegs;
-        return __hip_atomic_load(&L.ready_round[rnd & 1u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == rnd;
+        return __hip_atomic_load(&L.ready_round[rnd % kDnBufs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == rnd;
     };
     auto copy_out = [&](uint32_t Ls) {  // (the tile's offset is published)
-        const uint32_t rnd = Ls / kDnTileSegs, p = rnd & 1u, j = Ls % kDnTileSegs;
+        const uint32_t rnd = Ls / kDnTileSegs, p = rnd % kDnBufs, j = Ls % kDnTileSegs;
         const unsigned long long* stage = L.buf[p][j];
         const uint32_t cw = L.cnt[p][j], pw = L.pre[p][j];
         const unsigned long long bp = L.base[p];
@@ -1045,10 +1053,10 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         if (lane == 0u) {
             const uint32_t t = b + rnd * G, segs = min(kDnTileSegs, nseg - t * kDnTileSegs);
             const uint32_t old = __hip_atomic_fetch_add(&L.copied[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old + 1u == segs) {  // the tile's last copy: the buffer serves round rnd + 2
+            if (old + 1u == segs) {  // the tile's last copy: the buffer serves round rnd + kDnBufs
                 L.done[p] = 0u;
                 L.copied[p] = 0u;
-                __hip_atomic_store(&L.free_round[p], rnd + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&L.free_round[p], rnd + kDnBufs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
     };
@@ -1068,9 +1076,9 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
         fetch(seg_of(La));  // the next segment's headers, the offsets of the one after
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, 0);
-        // the segment's slot in its tile's buffer (free once the tile two rounds back is copied out);
+        // the segment's slot in its tile's buffer (free once the tile kDnBufs rounds back is copied out);
         // meanwhile this wave's own ready slots go out
-        const uint32_t rnd = Lc / kDnTileSegs, p = rnd & 1u, j = Lc % kDnTileSegs;
+        const uint32_t rnd = Lc / kDnTileSegs, p = rnd % kDnBufs, j = Lc % kDnTileSegs;
         for (;;) {
             if (pend0 != ~0u && ready_of(pend0)) {
                 copy_out(pend0);
