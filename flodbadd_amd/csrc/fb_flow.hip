@@ -1289,12 +1289,17 @@ hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t 
     }
     return e;
 }
-hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s) {
+hipError_t launch_flow_transpose(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
     hipLaunchKernelGGL(k_flow_transpose, dim3((p.parts + 63u) / 64u, (chunks + 63u) / 64u), dim3(256), 0, s, p,
                        chunks);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s, bool transpose) {
+    if (transpose) {
+        const hipError_t e = launch_flow_transpose(p, chunks, s);
+        if (e != hipSuccess) return e;
+    }
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k_flow_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2Lds);
     if (attr != hipSuccess) return attr;
