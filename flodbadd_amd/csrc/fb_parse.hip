@@ -611,17 +611,41 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                         P.rec_part + (size_t)ls * 64u, (short)0, 256, 0x00020000);
                     const uint32_t key[10] = {kk.w[0], kk.w[1], kk.w[2], kk.w[3], kk.w[4],
                                               kk.w[5], kk.w[6], kk.w[7], kk.w[8], kk.w[9] & 0xFFFFu};
-                    // update entries (UpdEnt, fb_internal.h): 32-B units packed in packet order, two
-                    // for an IPv6 key, staged in LDS (the records' reads of the stage come first in
-                    // this wave's program order) and stored as whole lines
+                    // update entries (UpdEnt, fb_internal.h): 32-B units, two for an IPv6 key, in
+                    // the order of their table partition inside the segment -- so the 3-4 entries of
+                    // a 128-B line belong to partitions a few hundred apart, which K2 workgroups
+                    // running at the same time read (the line is fetched once; in packet order each
+                    // entry's line was a line of its own for K2) -- staged in LDS (the records' reads
+                    // of the stage come first in this wave's program order) and stored as whole lines
                     const uint32_t rank = (uint32_t)__popcll(m_sess & lmask);
                     const bool v6 = upd_ent_v6(kk.w[9]);
                     const unsigned long long m_v6 = __ballot(is_s && v6);
-                    const uint32_t uoff = rank + (uint32_t)__popcll(m_v6 & lmask);
                     const uint32_t units = cs + (uint32_t)__popcll(m_v6);
+                    const uint32_t part = part_of(flow_hash_words(key), P.part_shift);
+                    // bitonic sort of (partition | lane) over the wave, non-session lanes last
+                    uint32_t sv = (is_s ? part : 0x10000u) << 6 | lane;  // (partitions < 2^16)
+#pragma unroll
+                    for (uint32_t k = 2; k <= 64u; k <<= 1) {
+#pragma unroll
+                        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                            const uint32_t o = (uint32_t)__shfl_xor((int)sv, (int)j, 64);
+                            const bool up = (lane & k) == 0u, lower = (lane & j) == 0u;
+                            sv = (lower == up) ? min(sv, o) : max(sv, o);
+                        }
+                    }
+                    // sorted position i holds lane src: its units start at the sum of the sizes before it
+                    const uint32_t src = sv & 63u;
+                    const uint32_t sz = lane < cs ? ((m_v6 >> src) & 1ull ? 2u : 1u) : 0u;
+                    uint32_t pre = sz;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+                        if (lane >= (uint32_t)o) pre += y;
+                    }
+                    // back to the entry's own lane (forward permute: lane i sends to lane src)
+                    const uint32_t uoff = (uint32_t)__builtin_amdgcn_ds_permute((int)(src * 4u), (int)(pre - sz));
                     // partition | unit offset << 16 | IPv6 << 23 (kRec*, fb_internal.h)
-                    const uint32_t pw = part_of(flow_hash_words(key), P.part_shift) | uoff << kRecUnitShift |
-                                        (v6 ? kRecV6 : 0u);
+                    const uint32_t pw = part | uoff << kRecUnitShift | (v6 ? kRecV6 : 0u);
                     __builtin_amdgcn_raw_buffer_store_b32(pw, r_part, is_s ? rank * 4u : kOob, 0, 0);
                     if (is_s) {
                         const uint32_t meta = (kk.w[12] >> 8) & 0xFFu;

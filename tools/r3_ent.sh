@@ -3,7 +3,7 @@
 # line with and without SESSION records, and the dense C2 / C3 rates of the product and variants.
 set -u
 cd "${GRAFT_REPO_ROOT}"; R=$(pwd); export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_async.py tests/test_gpu_dense.py tests/test_gpu_history.py tests/test_gpu_segmented.py tests/test_gpu_fullsize.py tests/test_gpu_grow.py tests/test_sessions_filter.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/ent_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_async.py tests/test_gpu_dense.py tests/test_gpu_history.py tests/test_gpu_segmented.py tests/test_gpu_fullsize.py tests/test_gpu_grow.py tests/test_sessions_filter.py -m gpu -x -q --timeout 100 --timeout-method thread -p no:cacheprovider > gpurun_out/ent_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/ent_tests.log; [ $rc -eq 0 ] || exit $rc
 X="--no-cpu-baseline --no-host --no-imix --no-other-mode --no-single-launch"
 for r in 1 2; do
