@@ -132,6 +132,8 @@ struct fb_ctx {
     uint32_t* d_hcount = nullptr;         // [table_cap] history characters per slot of the last update
     uint32_t* d_part_base = nullptr;      // [flow_parts + 1] history output offset per partition
     uint32_t* d_hist_slow = nullptr;      // [flow_parts + 1] count + partitions for the general history kernel
+    uint32_t* d_hist_cnt = nullptr;       // per-block slot counts of hot history partitions (lazy)
+    uint64_t hist_cnt_bytes = 0;
     // enrichment tables (fb_set_asn_tables / fb_set_blacklists)
     fb_asn_range* d_asn4 = nullptr;
     fb_asn_range* d_asn6 = nullptr;
@@ -511,6 +513,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_hcount);
     hipFree(c->d_part_base);
     hipFree(c->d_hist_slow);
+    hipFree(c->d_hist_cnt);
     hipFree(c->s_frames);
     hipFree(c->s_offsets);
     hipFree(c->s_out);
@@ -1211,7 +1214,18 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
         return FB_OK;
     }
     if (!d_hist || !d_hist_slot) return set_err(FB_ERR_INVAL, "d_hist and d_hist_slot are required");
-    HIP_TRY(launch_flow_history(c->last_p, c->last_chunks, d_hist_slot, d_hist, d_n_hist, c->d_hist_slow, s));
+    const uint64_t cnt_bytes = flow_history_cnt_bytes(c->last_chunks);
+    if (cnt_bytes > c->hist_cnt_bytes) {
+        HIP_TRY(hipStreamSynchronize(s));
+        hipFree(c->d_hist_cnt);
+        c->d_hist_cnt = nullptr;
+        c->hist_cnt_bytes = 0;
+        if (hipMalloc(&c->d_hist_cnt, cnt_bytes) != hipSuccess)
+            return set_err(FB_ERR_NOMEM, "history block counts (%llu bytes)", (unsigned long long)cnt_bytes);
+        c->hist_cnt_bytes = cnt_bytes;
+    }
+    HIP_TRY(launch_flow_history(c->last_p, c->last_chunks, d_hist_slot, d_hist, d_n_hist, c->d_hist_slow,
+                                cnt_bytes ? c->d_hist_cnt : nullptr, s));
     return FB_OK;
 }
 

@@ -268,10 +268,22 @@ struct HistLds {
     uint32_t s_n;
 };
 
+// A listed partition with more than kHistSplit characters (a skewed batch: Zipf(1.1) puts ~12 % of
+// the records in one flow) is split by chunk blocks over gridDim.y workgroups: k_hist_general<true>
+// counts every block's characters per slot into cnt[list index][block][slot], and each
+// k_hist_general<false> workgroup starts its slots' cursors after the earlier blocks' counts.  One
+// workgroup for such a partition took 25 ms per C4 Zipf batch.
+constexpr uint32_t kHistSplit = 16384;
+constexpr uint32_t kHistListCap = 256;    // listed partitions that can be split (cnt rows)
+constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
+constexpr uint32_t kHistBlockChunks = 4;
+
+template <bool COUNT>
 __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
-                                                               uint8_t* out_char, const uint32_t* slow) {
+                                                               uint8_t* out_char, const uint32_t* slow, uint32_t* cnt) {
     __shared__ HistLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nblk = gridDim.y, blk = blockIdx.y;
     // block-wide exclusive sums of one or two values per thread (tot: the sum)
     auto block_scan2 = [&](uint32_t v, uint32_t v2, uint32_t& tot, uint32_t& ex2, uint32_t& tot2) {
         uint32_t x = v, x2 = v2;
@@ -308,22 +320,37 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
         return block_scan2(v, 0u, tot, ex2, tot2);
     };
 
-    auto partition = [&](uint32_t q) {
+    auto partition = [&](uint32_t q, uint32_t li) {
         // every load the first round needs, issued together: the partition's character count and
-        // history-word base, its output range, its slots' counts, the first round's group rows
+        // history-word base, its output range, its slots' counts
         const unsigned long long pw = P.partials[4 * (size_t)q + 3];
         const uint32_t out_beg = P.part_base[q], out_end = P.part_base[q + 1];
         const uint32_t hc = P.hcount[(size_t)q * kFlowSlots + tid];
         const uint32_t* col = P.cols + (size_t)q * P.chunk_stride;
-        uint32_t vp = tid < chunks ? col[tid] : 0u;
         const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
         if (n_chars == 0u) return;  // uniform: no history characters in this partition
+        // this workgroup's chunk block (a partition that is not split: block 0 takes every chunk)
+        const bool split = nblk > 1u && li < kHistListCap && n_chars > kHistSplit;
+        if (!split && (COUNT || blk != 0u)) return;
+        const uint32_t cbs = split ? (chunks + nblk - 1u) / nblk : chunks;
+        const uint32_t cb0 = blk * cbs, cb1 = min(chunks, cb0 + cbs);
+        if (cb0 >= cb1) return;  // uniform
+        uint32_t vp = tid < cb1 - cb0 ? col[cb0 + tid] : 0u;
+        uint32_t before = 0u;  // applied entries (history words) of the chunks before the block
+        for (uint32_t c = tid; c < cb0; c += kHistThreads) before += col[c] >> 16;
+        uint32_t* bc = cnt + ((size_t)li * nblk) * kFlowSlots;  // (split) [block][slot] counts
         {
             uint32_t t;
-            L.cursor[tid] = block_scan(hc, t);  // relative to out_beg
+            uint32_t prior = 0u;  // the slot's characters in the earlier blocks
+            if (!COUNT && split)
+                for (uint32_t b = 0; b < blk; ++b) prior += bc[(size_t)b * kFlowSlots + tid];
+            L.cursor[tid] = block_scan(hc, t) + prior;  // relative to out_beg
             L.bcnt[tid] = 0u;
+            uint32_t tb;
+            block_scan(before, tb);
+            before = tb;
         }
-        uint32_t carry = hbase;  // history word of the round's first applied entry
+        uint32_t carry = hbase + before;  // history word of the round's first applied entry
         // round setup: the runs of chunks c0 .. c0 + 511 (tid: run tid); returns the entries read
         auto round = [&](uint32_t c0, uint32_t nr) {
             const uint32_t c = c0 + tid;
@@ -342,9 +369,45 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
             __syncthreads();
             return tv;
         };
-        const uint32_t nr0 = min(kHistRuns, chunks);
-        const uint32_t tv0 = round(0u, nr0);
-        {
+        const uint32_t nr0 = min(kHistRuns, cb1 - cb0);
+        const uint32_t tv0 = round(cb0, nr0);
+        if constexpr (COUNT) {  // this block's characters per slot
+            for (uint32_t c0 = cb0; c0 < cb1; c0 += kHistRuns) {
+                const uint32_t nr = min(kHistRuns, cb1 - c0);
+                if (c0 != cb0) {
+                    vp = tid < nr ? col[c0 + tid] : 0u;
+                    round(c0, nr);
+                }
+                const uint32_t tv = L.rp[nr];
+                for (uint32_t e = tid; e < tv; e += kHistThreads) {
+                    uint32_t lo = 0u, hi = nr - 1u;  // the run holding e
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1u) >> 1;
+                        if (L.rp[mid] <= e) lo = mid; else hi = mid - 1u;
+                    }
+                    const uint32_t k = e - L.rp[lo];
+                    uint32_t slot = 0u, code;
+                    if (!(L.rn[lo] >> 31)) {
+                        const uint32_t w = P.hword[L.rq[lo] + k];
+                        slot = w & (kFlowSlots - 1u);
+                        code = (w >> 9) & 15u;
+                    } else {
+                        const uint32_t w = P.e_orig[L.rs[lo] + k];
+                        code = (w >> kEntCodeShift) & 15u;
+                        if (code != 0u) {
+                            const uint32_t m = P.pos_map[L.rs[lo] + k];
+                            slot = ((m & kRecFlowCombined) ? P.agg_slot[m & ~kRecFlowCombined]
+                                                           : P.hword[L.rq[lo] + (m - L.rs[lo])]) &
+                                   (kFlowSlots - 1u);
+                        }
+                    }
+                    if (code != 0u) atomicAdd(&L.bcnt[slot], 1u);
+                }
+                __syncthreads();
+            }
+            bc[(size_t)blk * kFlowSlots + tid] = L.bcnt[tid];
+            return;
+        } else {
             // entry e of the round (runs laid end to end): key slot << 36 | record << 4 | code, or
             // ~0 for none (no character, outside the record window)
             auto entry_key = [&](uint32_t e, uint32_t r0, uint32_t r1, uint32_t c0, uint32_t win_lo,
@@ -472,9 +535,9 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                     batch_end();
                 }
             };
-            for (uint32_t c0 = 0; c0 < chunks; c0 += kHistRuns) {
-                const uint32_t nr = min(kHistRuns, chunks - c0);
-                if (c0 != 0u) {
+            for (uint32_t c0 = cb0; c0 < cb1; c0 += kHistRuns) {
+                const uint32_t nr = min(kHistRuns, cb1 - c0);
+                if (c0 != cb0) {
                     vp = tid < nr ? col[c0 + tid] : 0u;
                     round(c0, nr);
                 }
@@ -502,13 +565,17 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
     };
     const uint32_t n = slow[0];
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        partition(slow[1u + i]);
+        partition(slow[1u + i], i);
         __syncthreads();  // the LDS is re-initialised for the next partition
     }
 }
 
+uint64_t flow_history_cnt_bytes(uint32_t chunks) {
+    const uint32_t nblk = std::min<uint32_t>(kHistMaxBlocks, (chunks + kHistBlockChunks - 1u) / kHistBlockChunks);
+    return nblk > 1u ? (uint64_t)kHistListCap * nblk * kFlowSlots * 4u : 0u;
+}
 hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* hist_slot, uint8_t* hist,
-                               uint32_t* n_hist, uint32_t* slow, hipStream_t s) {
+                               uint32_t* n_hist, uint32_t* slow, uint32_t* cnt, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
     hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(1024), 0, s, p.partials, p.parts, p.part_base, n_hist, slow);
     hipError_t e = hipGetLastError();
@@ -516,9 +583,17 @@ hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* h
     hipLaunchKernelGGL(k_hist_uniform, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop
-    hipLaunchKernelGGL(k_hist_general, dim3(min(p.parts, 512u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist,
-                       slow);
+    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop; one with many
+    // characters split over chunk blocks (at most kHistMaxBlocks), counted first
+    const uint32_t nblk =
+        cnt ? std::min<uint32_t>(kHistMaxBlocks, (chunks + kHistBlockChunks - 1u) / kHistBlockChunks) : 1u;
+    const dim3 g(min(p.parts, 512u), nblk);
+    if (nblk > 1u) {
+        hipLaunchKernelGGL(k_hist_general<true>, g, dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, cnt);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_hist_general<false>, g, dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, cnt);
     return hipGetLastError();
 }
 

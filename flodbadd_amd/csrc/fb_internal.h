@@ -354,8 +354,10 @@ hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
 
 // Per-flow history characters of the last update (fb_hist.hip): the update's FlowParams (its
 // entries, transposed original rows, combined-group maps, per-slot counts) and the outputs.
+// cnt: flow_history_cnt_bytes(chunks) of scratch (hot partitions split over chunk blocks), or null
+uint64_t flow_history_cnt_bytes(uint32_t chunks);
 hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* hist_slot, uint8_t* hist,
-                               uint32_t* n_hist, uint32_t* slow, hipStream_t s);
+                               uint32_t* n_hist, uint32_t* slow, uint32_t* cnt, hipStream_t s);
 
 // Enrichment tables (fb_set_asn_tables / fb_set_blacklists, fb_enrich.hip).  Blacklists are
 // flattened per family into disjoint elementary intervals: bl*_pos[i] = first address of

@@ -55,6 +55,16 @@ def test_history_synthetic_zipf(seg):
     assert (gf["hist_len"] > 100).any() and (gf["conn_state"] > 0).any()
 
 
+def test_history_zipf_split_partitions():
+    """Batches of more than 16 bucketing chunks with Zipf(1.1) popularity: the hottest flows' partitions
+    carry tens of thousands of characters, so the history splits them over chunk blocks (per-block
+    slot counts first, k_hist_general<true>); every flow's history string equals the oracle's."""
+    batches = [synth.generate(4, 700000, first=0, zipf=1, zipf_s=1.1),
+               synth.generate(4, 400000, first=700000, zipf=1, zipf_s=1.1)]
+    gf = _run(batches, seg=True)
+    assert (gf["hist_len"] > 40000).any()
+
+
 def _flow(src, sport, dst, dport):
     out = lambda fl, n=0: fg.tcp_frame(src, sport, dst, dport, fl, n)
     back = lambda fl, n=0: fg.tcp_frame(dst, dport, src, sport, fl, n)
