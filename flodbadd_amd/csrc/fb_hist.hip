@@ -114,7 +114,8 @@ __device__ __forceinline__ uint32_t block_scan2(uint32_t v, uint32_t v2, uint32_
 // Exclusive scan of the partitions' character counts (partials[4 p + 3] low word) -> part_base;
 // one pass: thread t sums a contiguous group of partitions, one block scan, the group written.
 __global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* partials, uint32_t parts,
-                                                    uint32_t* part_base, uint32_t* n_hist, uint32_t* slow) {
+                                                    uint32_t* part_base, uint32_t* n_hist, uint32_t* slow,
+                                                    uint32_t* hot) {
     __shared__ uint32_t wsum[16], wsum2[16];
     const uint32_t per = (parts + 1023u) / 1024u, p0 = min(threadIdx.x * per, parts), p1 = min(p0 + per, parts);
     uint32_t sum = 0u;
@@ -129,8 +130,20 @@ __global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* pa
         part_base[parts] = tot;
         *n_hist = tot;
         slow[0] = 0u;  // k_hist_uniform lists the partitions it leaves to k_hist_general
+        if (hot) hot[0] = 0u;
     }
 }
+
+// A listed partition with more than kHistSplitMin characters (a skewed batch: Zipf(1.1) puts ~12 % of
+// the records in one flow) goes to a second list (up to kHistListCap) and is split by chunk blocks:
+// k_hist_general<true> counts each block's characters per slot into cnt[list index][block][slot],
+// and each block's k_hist_general<false> workgroup starts its slots' cursors after the earlier
+// blocks' counts.  One workgroup for such a partition took 25 ms per C4 Zipf batch.
+constexpr uint32_t kHistSplitMin = 16384;
+constexpr uint32_t kHistListCap = 256;    // split partitions (cnt rows)
+constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
+constexpr uint32_t kHistBlockChunks = 4;
+constexpr uint32_t kHistSplitGrid = 2048;  // workgroups over the split partitions' (partition, block) pairs
 
 // ---- the uniform case: one chunk round, <= kHistCap entries, every run <= kRunSort plain entries,
 // every wave's share (its 64 runs) <= kHistPer steps of 64
@@ -145,7 +158,7 @@ struct UniLds {
 static_assert(sizeof(UniLds) <= 40u * 1024u, "four workgroups per CU");
 
 __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
-                                                               uint8_t* out_char, uint32_t* slow) {
+                                                               uint8_t* out_char, uint32_t* slow, uint32_t* hot) {
     __shared__ UniLds L;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -168,7 +181,12 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams 
     __syncthreads();
     const uint32_t wlen = L.rp[min(64u * wave + 64u, kHistRuns)] - L.rp[64u * wave];
     if (__syncthreads_or(len > kRunSort || wlen > kHistPer * 64u) || chunks > kHistRuns || tp > kHistCap) {
-        if (tid == 0) slow[1u + atomicAdd(slow, 1u)] = q;  // uniform: the general kernel takes it
+        if (tid == 0) {  // uniform: the general kernels take it (a partition with many characters split)
+            uint32_t h = ~0u;
+            if (hot && n_chars > kHistSplitMin) h = atomicAdd(hot, 1u);
+            if (h < kHistListCap) hot[1u + h] = q;
+            else slow[1u + atomicAdd(slow, 1u)] = q;
+        }
         return;
     }
     {   // run tid in record order (K1's scatter leaves a run unordered): key = record in chunk << 13
@@ -268,22 +286,14 @@ struct HistLds {
     uint32_t s_n;
 };
 
-// A listed partition with more than kHistSplit characters (a skewed batch: Zipf(1.1) puts ~12 % of
-// the records in one flow) is split by chunk blocks over gridDim.y workgroups: k_hist_general<true>
-// counts every block's characters per slot into cnt[list index][block][slot], and each
-// k_hist_general<false> workgroup starts its slots' cursors after the earlier blocks' counts.  One
-// workgroup for such a partition took 25 ms per C4 Zipf batch.
-constexpr uint32_t kHistSplit = 16384;
-constexpr uint32_t kHistListCap = 256;    // listed partitions that can be split (cnt rows)
-constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
-constexpr uint32_t kHistBlockChunks = 4;
-
+// Listed partitions: `list` = slow (one workgroup each, every chunk) or, with nblk > 1, the split
+// partitions -- a grid-stride loop over (list index, chunk block) pairs; cnt = that list's counts.
 template <bool COUNT>
 __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
-                                                               uint8_t* out_char, const uint32_t* slow, uint32_t* cnt) {
+                                                               uint8_t* out_char, const uint32_t* list, uint32_t* cnt,
+                                                               uint32_t nblk) {
     __shared__ HistLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t nblk = gridDim.y, blk = blockIdx.y;
     // block-wide exclusive sums of one or two values per thread (tot: the sum)
     auto block_scan2 = [&](uint32_t v, uint32_t v2, uint32_t& tot, uint32_t& ex2, uint32_t& tot2) {
         uint32_t x = v, x2 = v2;
@@ -320,7 +330,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
         return block_scan2(v, 0u, tot, ex2, tot2);
     };
 
-    auto partition = [&](uint32_t q, uint32_t li) {
+    auto partition = [&](uint32_t q, uint32_t li, uint32_t blk) {
         // every load the first round needs, issued together: the partition's character count and
         // history-word base, its output range, its slots' counts
         const unsigned long long pw = P.partials[4 * (size_t)q + 3];
@@ -329,9 +339,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
         const uint32_t* col = P.cols + (size_t)q * P.chunk_stride;
         const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
         if (n_chars == 0u) return;  // uniform: no history characters in this partition
-        // this workgroup's chunk block (a partition that is not split: block 0 takes every chunk)
-        const bool split = nblk > 1u && li < kHistListCap && n_chars > kHistSplit;
-        if (!split && (COUNT || blk != 0u)) return;
+        // this workgroup's chunk block (a partition that is not split: every chunk)
+        const bool split = nblk > 1u;
         const uint32_t cbs = split ? (chunks + nblk - 1u) / nblk : chunks;
         const uint32_t cb0 = blk * cbs, cb1 = min(chunks, cb0 + cbs);
         if (cb0 >= cb1) return;  // uniform
@@ -563,37 +572,42 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
             }
         }
     };
-    const uint32_t n = slow[0];
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        partition(slow[1u + i], i);
+    const uint32_t n = min(list[0], nblk > 1u ? kHistListCap : 0xFFFFFFFFu);
+    for (uint32_t i = blockIdx.x; i < n * nblk; i += gridDim.x) {  // (blocks of one partition adjacent)
+        partition(list[1u + i / nblk], i / nblk, i % nblk);
         __syncthreads();  // the LDS is re-initialised for the next partition
     }
 }
 
-uint64_t flow_history_cnt_bytes(uint32_t chunks) {
+uint64_t flow_history_cnt_bytes(uint32_t chunks) {  // the split list (count + entries), then the counts
     const uint32_t nblk = std::min<uint32_t>(kHistMaxBlocks, (chunks + kHistBlockChunks - 1u) / kHistBlockChunks);
-    return nblk > 1u ? (uint64_t)kHistListCap * nblk * kFlowSlots * 4u : 0u;
+    return nblk > 1u ? (kHistListCap + 1u) * 4ull + (uint64_t)kHistListCap * nblk * kFlowSlots * 4u : 0u;
 }
 hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* hist_slot, uint8_t* hist,
                                uint32_t* n_hist, uint32_t* slow, uint32_t* cnt, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
-    hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(1024), 0, s, p.partials, p.parts, p.part_base, n_hist, slow);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hist_uniform, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop; one with many
-    // characters split over chunk blocks (at most kHistMaxBlocks), counted first
     const uint32_t nblk =
         cnt ? std::min<uint32_t>(kHistMaxBlocks, (chunks + kHistBlockChunks - 1u) / kHistBlockChunks) : 1u;
-    const dim3 g(min(p.parts, 512u), nblk);
-    if (nblk > 1u) {
-        hipLaunchKernelGGL(k_hist_general<true>, g, dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, cnt);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_hist_general<false>, g, dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, cnt);
+    uint32_t* hot = nblk > 1u ? cnt : nullptr;  // the split list; its counts after it
+    uint32_t* hcnt = hot ? hot + kHistListCap + 1u : nullptr;
+    hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(1024), 0, s, p.partials, p.parts, p.part_base, n_hist, slow, hot);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hist_uniform, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, hot);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop
+    hipLaunchKernelGGL(k_hist_general<false>, dim3(min(p.parts, 512u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
+                       hist, slow, nullptr, 1u);
+    e = hipGetLastError();
+    if (e != hipSuccess || !hot) return e;
+    // the split ones: per-block slot counts, then the blocks
+    hipLaunchKernelGGL(k_hist_general<true>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist,
+                       hot, hcnt, nblk);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hist_general<false>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
+                       hist, hot, hcnt, nblk);
     return hipGetLastError();
 }
 
