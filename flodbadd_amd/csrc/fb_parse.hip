@@ -824,10 +824,11 @@ struct DnLds {
     uint32_t acc[11];                                     // the block's stats counters; wave arrivals
 };
 
-// Blocks per CU: 8-wave blocks (7 parse + 1 store) two per CU.  With 9-wave blocks (8 + 1) at 95
-// VGPRs the occupancy query said two per CU but the hardware admitted one (each block puts three
-// waves on one SIMD; two blocks there need six, the VGPRs allow five), and the grid's second half
-// ran only after the first: the look-backs of the resident half waited for it (5.8 ms per C2 batch).
+// Blocks per CU: FB_DN_BPC (default one 16-wave block: 15 parse + 1 store, two 57-KiB tile
+// buffers).  The host caps the occupancy query at FB_DN_BPC: with 9-wave blocks (8 + 1) at 95 VGPRs
+// the query said two per CU but the hardware admitted one (each block puts three waves on one SIMD;
+// two blocks there need six, the VGPRs allow five), and the grid's second half ran only after the
+// first: the look-backs of the resident half waited for it (5.8 ms per C2 batch).
 __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) void k_parse_dense(const ParseParams P,
                                                                                         const SegBatch B) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
