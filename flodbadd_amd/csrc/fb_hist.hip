@@ -139,7 +139,7 @@ __global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* pa
 // k_hist_general<true> counts each block's characters per slot into cnt[list index][block][slot],
 // and each block's k_hist_general<false> workgroup starts its slots' cursors after the earlier
 // blocks' counts.  One workgroup for such a partition took 25 ms per C4 Zipf batch.
-constexpr uint32_t kHistSplitMin = 16384;
+constexpr uint32_t kHistSplitMin = 32768;  // (16,384: Zipf history 1.02 ms, 32,768: 0.90, 8,192: 1.23)
 constexpr uint32_t kHistListCap = 256;    // split partitions (cnt rows)
 constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
 constexpr uint32_t kHistBlockChunks = 4;
