@@ -418,7 +418,9 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         if (occupancy_parse_seg(&sb) != hipSuccess || sb < 1) sb = 1;
         c->seg_grid = std::min<uint32_t>((uint32_t)(sb * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
 #ifndef FB_ASYNC_BPC
-#define FB_ASYNC_BPC 2  // round 3 (update entries, K1 staged): 2 blocks per CU 12.87-12.89 vs 12.54-12.55 Gpps at 1
+#define FB_ASYNC_BPC 1  // round 3: with unsorted update entries 2 blocks per CU led (12.88 vs 12.55 Gpps);
+                        // with the entries sorted by partition 1 block leaves K2 more of each CU
+                        // (14.19-14.22 vs 13.74-13.75; 3 blocks 13.49-13.80)
 #endif
         c->seg_grid_async = std::min<uint32_t>((uint32_t)(FB_ASYNC_BPC * prop.multiProcessorCount), c->seg_grid);
         int db = 0;
