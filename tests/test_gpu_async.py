@@ -199,3 +199,46 @@ def test_table_only_equals_records(reference):
         for b in keep:
             b.free()
         cap.close()
+
+
+@pytest.mark.parametrize("v6_permille", [1000, 500], ids=["v6-only", "v6-half"])
+def test_table_only_ipv6_segments(v6_permille):
+    """IPv6-heavy batches through the pipelined table-only call: an IPv6 key takes two 32-B update
+    units, so an all-IPv6 segment fills its 128-unit region exactly.  The table equals the C
+    oracle's row for row, and each batch's new / updated counts equal the oracle's."""
+    from oracle import coracle
+    from test_gpu_grow import _same_table
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 18)
+    stream = N.Stream()
+    ref = coracle.Flows()
+    cfg = coracle.make_cfg(2)
+    keep, want, got = [], [], []
+    try:
+        N.check(lib.fb_set_session_records(cap.ctx, 0))
+        for k in range(4):
+            frames, offs = synth.generate(4, 70000 + 64 * k + 17, first=k * 80000, v6_permille=v6_permille,
+                                          dns_permille=0, n_flows=1 << 15)
+            r_out, _, _, _ = coracle.parse_classify(cfg, frames, offs)
+            st = np.zeros(1, dtype=N.STATS_DTYPE)
+            ref.update(r_out, st)
+            want.append((int(st[0]["new_sessions"]), int(st[0]["updated_sessions"])))
+            n = len(offs) - 1
+            nseg = (n + 63) // 64
+            b = [N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+                 N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize)]
+            keep += b
+            N.check(lib.fb_process_seg_async_dev(cap.ctx, b[0].ptr, frames.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr,
+                                                 None, b[4].ptr, stream.ptr))
+            got.append(b[4])
+        N.check(lib.fb_flow_join(cap.ctx, stream.ptr))
+        stream.sync()
+        st = [g.download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)[0] for g in got]
+        assert [int(s["error"]) for s in st] == [0] * len(st)
+        assert [(int(s["new_sessions"]), int(s["updated_sessions"])) for s in st] == want
+        _same_table(cap.export_flows(), ref.export_sorted())
+    finally:
+        N.check(lib.fb_set_session_records(cap.ctx, 1))
+        for b in keep:
+            b.free()
+        cap.close()
