@@ -8,15 +8,19 @@ frames per GPU.  Batches rotate over R distinct device buffer sets (C2: 32, 4 GB
 set exceeds the 256 MB Infinity Cache and the timing is HBM-bound, not MALL-bound; consecutive
 steps share launches of up to 32 batches (fb_parse_classify_seg_batches_dev), split evenly.
 
-Multi-GPU: one process per GPU (torchrun); packets are sharded by index (each rank owns the
-contiguous range [rank*n, (rank+1)*n) of the virtual batch) with no data-path collective
-("scaling": "weak"); torch.distributed (gloo, CPU) only provides the barrier and the max over
-ranks of the timed region.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every process is one rank;
+`python3 bench.py --gpus N` with no WORLD_SIZE spawns the N rank processes itself (spawn_ranks,
+before anything touches the GPU) and exits with their status.  Packets are sharded by index (each
+rank owns the contiguous range [rank*n, (rank+1)*n) of the virtual batch) with no data-path
+collective ("scaling": "weak"); torch.distributed (gloo, CPU) only provides the barrier and the
+max over ranks of the timed region; the C5 extra exchanges the per-flow table over RCCL.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -186,7 +190,7 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     stream.sync()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
+    elapsed = local_elapsed = t1 - t0
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -239,7 +243,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     for b in bufs:
         for x in b:
             x.free()
-    return dict(frames=frames, offs=offs, elapsed=elapsed, ev_ms=ev_ms, algo_bytes=algo, stage=stage,
+    return dict(frames=frames, offs=offs, elapsed=elapsed, local_elapsed=local_elapsed, ev_ms=ev_ms,
+                algo_bytes=algo, stage=stage,
                 host_us=round((t1 - t0) * 1e6 - ev_ms * 1e3, 1),
                 launches=n_launch, stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
@@ -464,7 +469,8 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
         tt = torch.tensor(t, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
         t = tt.cpu().numpy()
-    return dict(frames_per_rank=n, total_frames=n * world, local_flows=local, global_flows=int(len(merged)),
+    return dict(ranks_in_group=dist.get_world_size(group), frames_per_rank=n, total_frames=n * world,
+                local_flows=local, global_flows=int(len(merged)),
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),
                 note="per-rank fused parse+flow upsert of the rank's shard, then the table exported (to a device "
@@ -652,6 +658,60 @@ def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
     return out
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N child processes of this script, rank r with
+    RANK = LOCAL_RANK = r, WORLD_SIZE = N and a loopback rendezvous (torchrun's environment), and
+    wait for all of them.  The parent never touches the GPU and never execs (it runs the children
+    as subprocesses); rank 0 prints the JSON line.  Returns the exit status: 0 only if every rank
+    exited 0 (a failing rank ends the others)."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                for q in live:  # a rank died: the others would wait for it at the next collective
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return status
+
+
+def world_check(args, world, rank):
+    """--world-check: the launch plumbing only (no GPU): every rank joins the gloo group, the ranks
+    all-reduce their rank numbers, rank 0 prints what the group saw."""
+    import torch
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+    t = torch.tensor([rank, 1], dtype=torch.int64)
+    if world > 1:
+        tdist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "requested_gpus": args.gpus, "group_size": int(t[1]),
+                          "rank_sum": int(t[0]), "master": "%s:%s" % (os.environ.get("MASTER_ADDR"),
+                                                                       os.environ.get("MASTER_PORT"))}))
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -681,11 +741,20 @@ def main():
                     help="C4 (seg): the fused calls keep only the session table (fb_set_session_records 0)")
     ap.add_argument("--zipf", type=float, default=None,
                     help="profiling: the main run with Zipf(s) flow popularity instead of uniform")
+    ap.add_argument("--world-check", action="store_true",
+                    help="launch plumbing only: the ranks join the group and rank 0 reports it (no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process only starts the N ranks (before any HIP call) and waits
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d but the launcher started %d ranks" % (args.gpus, world))
+    if args.world_check:
+        return world_check(args, world, rank)
     dist = None
     if world > 1:
         import torch.distributed as tdist
@@ -728,6 +797,14 @@ def main():
     algo_per_launch = main_r["algo_bytes"] * args.steps / main_r["launches"]
     achieved = algo_per_launch / per_launch_s / 1e9
     value = world * n * args.steps / main_r["elapsed"] / 1e6
+    per_rank = None
+    if dist:  # every rank's own kernel rate (its GPU's roofline fraction) beside the aggregate
+        import torch
+        mine = torch.tensor([achieved, n * args.steps / main_r["local_elapsed"] / 1e6], dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [dict(rank=r, Mpackets_s=round(float(t[1]), 2), roofline_frac=round(float(t[0]) / HBM_PEAK_GBS, 4))
+                    for r, t in enumerate(allr)]
 
     extra = {}
     if main_r["stage"]:
@@ -844,6 +921,9 @@ def main():
             "cpu_baseline": cpu,
             "batch_stats": main_r["stats"],
         }
+        if per_rank:
+            line["per_rank"] = per_rank
+            line["roofline"]["note"] = "rank 0's GPU; every rank's own fraction in per_rank"
         if extra:
             line["extra"] = extra
         print(json.dumps(line))

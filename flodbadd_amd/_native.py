@@ -46,8 +46,9 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
     ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8"),
     ("first_seen", "<u8"), ("last_seen", "<u8"), ("end_seen", "<u8"), ("hist_len", "<u4"),
     ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("session_flags", "<u4")])
-# fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst at insert)
-SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST = 1, 2, 4, 8
+# fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst and
+# dst_service is Some, at insert)
+SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST, SESSION_DST_SERVICE = 1, 2, 4, 8, 16
 # fb_flow_rec positions: (update call << 32) | pkt_index; FB_SEEN_NONE = None
 FB_SEEN_NONE = (1 << 64) - 1
 FB_HIST_CHARS = "SsHhFfRr><Aa-"

@@ -228,7 +228,9 @@ class FlodbaddGpuCapture:
         gen = self.table_info()["generation"]
         if gen == self._generation:
             return
-        assert gen == self._generation + 1, "more than one growth between two batches"
+        if gen != self._generation + 1:  # fb_flow_slot_remap keeps only the last growth's map
+            raise N.FbError(N.FB_ERR_INTERNAL, "the table grew %d times since the histories were keyed"
+                            % (gen - self._generation))
         self._generation = gen
         if not self.histories:
             return

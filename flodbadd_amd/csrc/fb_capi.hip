@@ -11,7 +11,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "fb_host.h"
@@ -114,6 +116,11 @@ struct fb_ctx {
     // fb_process_seg_async_dev: updates on the context's own stream, one batch behind the parses
     hipStream_t upd = nullptr;
     hipEvent_t ev_parsed = nullptr;
+    // after the last fb_flow_history_dev: it reads the last update's shared scratch (history words,
+    // partials, slot counts, combined-entry slots), which the next update rewrites -- that update
+    // waits for it on every stream it uses, whichever stream the history ran on
+    hipEvent_t ev_hist = nullptr;
+    bool hist_pending = false;
     hipEvent_t ev_upd[2] = {nullptr, nullptr};  // after the update of async batch k (k & 1)
     uint64_t async_k = 0;                       // async batches issued
     uint32_t* d_rec_part2 = nullptr;            // partitions of the odd async batches
@@ -185,6 +192,7 @@ static int guard_next_error_word(fb_ctx* c, hipStream_t s) {
 }
 static int drain_updates(fb_ctx* c) {
     if (c->async_k && c->upd) HIP_TRY(hipStreamSynchronize(c->upd));
+    if (c->hist_pending) HIP_TRY(hipEventSynchronize(c->ev_hist));  // (before scratch is freed)
     return FB_OK;
 }
 
@@ -504,6 +512,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_agg_slot);
     if (c->upd) hipStreamDestroy(c->upd);
     if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
+    if (c->ev_hist) hipEventDestroy(c->ev_hist);
     for (hipEvent_t e : c->ev_upd)
         if (e) hipEventDestroy(e);
     hipFree(c->d_asn4);
@@ -993,14 +1002,31 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
 // Before an update call: grow while the occupancy the last completed update reported, plus the new
 // flows of the updates still in flight (each estimated at the last reported update's count) and of
 // this one (twice that: arrival rates rise), spread over the partitions, plus slack for the spread
-// between partitions, would pass 7/8 of a partition, or the flows 3/4 of the table.  No device
-// wait: the report sits in host-mapped memory.  A burst beyond that estimate inside one batch can
-// still fill a partition: the update then reports error bit 4 (FB_ERR_TABLE_FULL).
+// between partitions, would pass 7/8 of a partition, or the flows 3/4 of the table.  The report sits
+// in host-mapped memory; the decision needs the report of the update two calls back (the second call
+// after a create / clear: the first update's), so a host that enqueues asynchronous batches faster
+// than the device runs them waits here for that report (the device keeps the previous batch's work)
+// instead of projecting from an older one -- or from none, which let the table fill.  A burst
+// beyond the estimate inside one batch can still fill a partition: the update then reports error
+// bit 4 (FB_ERR_TABLE_FULL).
 static constexpr uint64_t kGrowPart = kFlowSlots * 7u / 8u;
+static constexpr double kMailboxWaitS = 120.0;
 static int maybe_grow(fb_ctx* c, hipStream_t s) {
     if (!c->d_table || !c->grow || c->part_recs) return FB_OK;  // (a fused parse already bucketed for this geometry)
     const volatile FlowMailbox* m = c->h_mbox;
-    const uint64_t seq = __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE);
+    const uint64_t issued = c->upd_seq - c->clear_seq;              // updates since create / clear
+    const uint64_t need = c->clear_seq + (issued >= 2u ? issued - 1u : issued);
+    uint64_t seq = __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE);
+    if (seq < need) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0; (seq = __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE)) < need; ++spin) {
+            if (spin > 64u) std::this_thread::yield();
+            if ((spin & 1023u) == 0u &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kMailboxWaitS)
+                return set_err(FB_ERR_HIP, "no table-occupancy report from update %llu after %.0f s",
+                               (unsigned long long)need, kMailboxWaitS);
+        }
+    }
     if (seq == 0 || seq <= c->clear_seq) return FB_OK;
     const uint64_t flows = m->flows, newf = m->new_flows;
     const uint64_t ahead = c->upd_seq - seq + 2u;  // in flight, plus this call counted twice
@@ -1035,6 +1061,11 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     if (!rc) rc = ensure_flow_scratch(c, n_slots, s_bucket);
     if (!rc && set == 1u && !c->us[1].entries) rc = alloc_upd_scratch(c, c->us[1], s_bucket);
     if (rc) return rc;
+    if (c->hist_pending) {  // the last history's reads of the shared update scratch come first
+        HIP_TRY(hipStreamWaitEvent(s_bucket, c->ev_hist, 0));
+        if (s != s_bucket) HIP_TRY(hipStreamWaitEvent(s, c->ev_hist, 0));
+        c->hist_pending = false;
+    }
     const UpdScratch& u = c->us[set];
     // record slots of the batch: at most last_n records (dense) / n_slots slots (segmented)
     const uint32_t chunks = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_slots + kFlowChunk - 1) / kFlowChunk);
@@ -1226,8 +1257,12 @@ int fb_flow_history_dev(fb_ctx* c, uint8_t* d_hist, uint32_t* d_hist_slot, uint3
             return set_err(FB_ERR_NOMEM, "history block counts (%llu bytes)", (unsigned long long)cnt_bytes);
         c->hist_cnt_bytes = cnt_bytes;
     }
+    if (!c->ev_hist && hipEventCreateWithFlags(&c->ev_hist, hipEventDisableTiming) != hipSuccess)
+        return set_err(FB_ERR_HIP, "history event");
     HIP_TRY(launch_flow_history(c->last_p, c->last_chunks, d_hist_slot, d_hist, d_n_hist, c->d_hist_slow,
                                 cnt_bytes ? c->d_hist_cnt : nullptr, s));
+    HIP_TRY(hipEventRecord(c->ev_hist, s));
+    c->hist_pending = true;
     return FB_OK;
 }
 

@@ -137,7 +137,7 @@ __device__ __forceinline__ void entry_of(bool ent, const uint4 (&r)[4], uint32_t
         const uint32_t meta = (mx >> 8) & 0xFFu;
         const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
         const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
-                               ((meta >> 3) & 0xFu) << 20;  // FB_META_LOCAL_SRC .. SELF_DST -> fb_session_flags
+                               ((meta >> 3) & 0x1Fu) << 20;  // FB_META_LOCAL_SRC .. DST_SERVICE -> fb_session_flags
         e[0] = a;
         e[1] = b;
         e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
@@ -675,7 +675,8 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     atomicMax(sc64(q, kScLast), pos);
     // inserted by this batch: bit 16, and the session flags the reference stores at insert
     // (is_local_src/dst, is_self_src/dst of the canonical key, src/packets.rs:429-435) in bits 20-23
-    if (result == 1) atomicOr(q + kScMask, (1u << 16) | (e3.z & 0x00F00000u));
+    // dst_service (src/packets.rs:441-466) in bit 15
+    if (result == 1) atomicOr(q + kScMask, (1u << 16) | (e3.z & 0x00F00000u) | ((e3.z >> 24) & 1u) << 15);
     if (e3.z & 0x10000u) {                              // Some(flags): history.push(map_tcp_flags(..))
         atomicAdd(q + kScCount, 1u);
         const uint32_t b = hist_bit(e3.z & 0xFFu);
@@ -698,6 +699,7 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     const int result = k2_find_insert(slice, tags, key, e3.w, i);
     if (result < 0) {
         atomicOr(err, result == -2 ? 16u : 4u);
+        if (agg_slot) agg_slot[e3.x] = ~0u;  // the history drops the group's characters (combined_slot)
         return -1;
     }
     unsigned long long* s = slice + (size_t)i * kSlotWords;
@@ -721,7 +723,7 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     atomicMin(sc64(q, kScFirst), (unsigned long long)e2.z << 32 | rec_pkt(P, e2.z));
     atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | rec_pkt(P, e2.w));
     const uint32_t hc = e3.z & 0xFFFFu;
-    const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) : 0u);
+    const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) | ((t3.w >> 4) & 1u) << 15 : 0u);
     if (m) atomicOr(q + kScMask, m);
     if (hc) {
         atomicAdd(q + kScCount, hc);
@@ -747,7 +749,7 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t b
     const bool fresh = (flags & (1u << 16)) != 0u;  // new flow: start_time = its first packet, end_time None
     const unsigned long long first_seen = fresh ? hi | (uint32_t)first : (o0.x | (unsigned long long)o0.y << 32);
     unsigned long long end_seen = fresh ? FB_SEEN_NONE : (o1.x | (unsigned long long)o1.y << 32);
-    // hist_state: hist_mask 0-12 | conn_state 16-19 | session flags 20-23 | end_mask 24-31
+    // hist_state: hist_mask 0-12 | dst_service 15 | conn_state 16-19 | session flags 20-23 | end_mask 24-31
     const uint32_t state = fresh ? (flags & 0x00F00000u) : o1.w, len = fresh ? 0u : o1.z;
     const unsigned long long last_seen = hi | (uint32_t)last;
     const uint32_t mask = state & 0xFFFFu;
@@ -858,7 +860,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
             atomicAdd(f + kCfRecs, 1u);
             f[kCfHash] = e[3].w;  // every lane of the key stores the same word
-            f[kCfMeta] = (e[3].z >> 20) & 0xFu;  // session flags: a function of the key and the configuration
+            f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
             atomicMin(f + kCfFirst, rec);
             atomicMax(f + kCfLast, rec);
             if (e[3].z & 0x10000u) {
@@ -1252,11 +1254,11 @@ __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned
             r.last_seen = T[i].last_seen;
             r.end_seen = T[i].end_seen;
             r.hist_len = T[i].hist_len;
-            r.hist_mask = (uint16_t)(T[i].hist_state & 0xFFFFu);
+            r.hist_mask = (uint16_t)(T[i].hist_state & 0x1FFFu);
             r.conn_state = (uint8_t)((T[i].hist_state >> 16) & 0xFu);
             r.end_mask = (uint8_t)(T[i].hist_state >> 24);
             r.slot = (uint32_t)i;
-            r.session_flags = (T[i].hist_state >> 20) & 0xFu;
+            r.session_flags = ((T[i].hist_state >> 20) & 0xFu) | ((T[i].hist_state >> 15) & 1u) << 4;
             out[pos] = r;
         }
         __syncthreads();

@@ -288,6 +288,18 @@ struct HistLds {
 
 // Listed partitions: `list` = slow (one workgroup each, every chunk) or, with nblk > 1, the split
 // partitions -- a grid-stride loop over (list index, chunk block) pairs; cnt = that list's counts.
+// Slot (within the partition) of a record of a combined group: its combined entry's agg_slot, or the
+// history word of its moved plain entry.  An entry the table could not take (partition full / spin
+// expired: error bit 4 / 16) left agg_slot ~0 or history word 0 -- its character is dropped (code 0)
+// instead of being filed under a slot some other flow holds.
+__device__ __forceinline__ uint32_t combined_slot(const FlowParams& P, uint32_t m, uint32_t rq, uint32_t rs,
+                                                  uint32_t& code) {
+    const bool comb = (m & kRecFlowCombined) != 0u;
+    const uint32_t v = comb ? P.agg_slot[m & ~kRecFlowCombined] : P.hword[rq + (m - rs)];
+    if (comb ? v == ~0u : v == 0u) code = 0u;
+    return v & (kFlowSlots - 1u);
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
                                                                uint8_t* out_char, const uint32_t* list, uint32_t* cnt,
@@ -405,9 +417,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                         code = (w >> kEntCodeShift) & 15u;
                         if (code != 0u) {
                             const uint32_t m = P.pos_map[L.rs[lo] + k];
-                            slot = ((m & kRecFlowCombined) ? P.agg_slot[m & ~kRecFlowCombined]
-                                                           : P.hword[L.rq[lo] + (m - L.rs[lo])]) &
-                                   (kFlowSlots - 1u);
+                            slot = combined_slot(P, m, L.rq[lo], L.rs[lo], code);
                         }
                     }
                     if (code != 0u) atomicAdd(&L.bcnt[slot], 1u);
@@ -439,9 +449,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                     rec = w & kEntRecMask;
                     if (code != 0u) {
                         const uint32_t m = P.pos_map[L.rs[lo] + k];
-                        slot = ((m & kRecFlowCombined) ? P.agg_slot[m & ~kRecFlowCombined]
-                                                       : P.hword[L.rq[lo] + (m - L.rs[lo])]) &
-                               (kFlowSlots - 1u);
+                        slot = combined_slot(P, m, L.rq[lo], L.rs[lo], code);
                     }
                 }
                 if (code == 0u || rec < win_lo || rec >= win_hi) return ~0ull;

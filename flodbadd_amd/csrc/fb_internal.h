@@ -161,8 +161,9 @@ struct FlowSlot {
                                 // orig_ip_bytes, resp_ip_bytes
     unsigned long long first_seen, last_seen, end_seen;
     uint32_t hist_len;
-    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | conn_state << 16 (4 bits) |
-                                // session flags << 20 (fb_session_flags, set at insert) | end_mask << 24
+    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | dst_service << 15 | conn_state << 16
+                                // (4 bits) | session flags << 20 (fb_session_flags 0-3, set at insert) |
+                                // end_mask << 24
 };
 static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
@@ -280,7 +281,8 @@ static_assert(kFlowMaxParts <= kRecPartMask + 1u, "partition ids fit the low hal
 //                                                                   protocol | family << 8)
 //           packet_length, ip_packet_length, pkt_index,
 //           hinfo | rank << 26   (hinfo: hist_char | tcp_flags << 8 | has_flags << 16 | session
-//                                 flags << 20; rank: the record's slot in its segment)
+//                                 flags << 20 | dst_service << 24; rank: the record's slot in its
+//                                 segment)
 //   unit 1: key[1], key[2], key[3], key[5], key[6], key[7], 0, 0  (IPv6 only)
 // The fused parse's per-slot word (rec_part) then holds partition | unit offset << 16 | IPv6 << 23,
 // and the bucketing pass's index word is unit index | IPv6 << 28.  With entries the update orders a

@@ -650,7 +650,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
                     if (is_s) {
                         const uint32_t meta = (kk.w[12] >> 8) & 0xFFu;
                         const uint32_t hinfo = ((kk.w[12] >> 16) & 0xFFu) | ((kk.w[12] & 0xFFu) << 8) |
-                                               ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0xFu) << 20;
+                                               ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) | ((meta >> 3) & 0x1Fu) << 20;
                         const uint32_t aw = kk.w[9] | ((meta & FB_META_ORIGINATOR) ? 1u << 16 : 0u);
                         u32x4* e = reinterpret_cast<u32x4*>(stage + (size_t)uoff * 4u);
                         e[0] = u32x4{kk.w[0], kk.w[4], kk.w[8], aw};

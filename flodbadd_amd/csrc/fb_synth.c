@@ -22,6 +22,9 @@ typedef struct fb_synth_cfg {
     uint32_t dns_permille; /* flows on port 53 (5) */
     uint32_t zipf;         /* 0 uniform flow choice, 1 Zipf(s) */
     double zipf_s;         /* 1.1 */
+    uint32_t lan_dst_permille; /* flows whose dst is a LAN address too (0: SURVEY.md §8d's mix, every
+                                  dst public); with a LAN src (50 %) such a flow is local, so the
+                                  Local/Global filters drop a large share (filter parity tests) */
 } fb_synth_cfg;
 
 static uint64_t splitmix64(uint64_t* s) {
@@ -77,6 +80,16 @@ static void make_flow(const fb_synth_cfg* c, uint32_t f, flow* o) {
         }
         o->src[0] = lan_src ? (0xFD000000u | (o->src[0] & 0x00FFFFFFu)) : (0x20000000u | (o->src[0] & 0x1FFFFFFFu));
         o->dst[0] = 0x20000000u | (o->dst[0] & 0x1FFFFFFFu);
+    }
+    if (c->lan_dst_permille) { /* its own stream: the mix above is unchanged */
+        uint64_t t = mix(c->seed ^ 0x1A4D57ull, f);
+        if (below(&t, 1000) < c->lan_dst_permille) {
+            uint32_t r = (uint32_t)(splitmix64(&t) >> 32);
+            if (!o->v6) /* 192.168/16 or 10/8 */
+                o->dst[0] = (r & 1) ? (0xC0A80000u | (r >> 16)) : (0x0A000000u | (r >> 8));
+            else        /* fe80::/10 or fd00::/8 */
+                o->dst[0] = (r & 1) ? (0xFE800000u | ((r >> 8) & 0x003FFFFFu)) : (0xFD000000u | (r >> 8));
+        }
     }
     o->sport = (uint16_t)(32768 + below(&s, 61000 - 32768));
     if (below(&s, 1000) < c->dns_permille) {

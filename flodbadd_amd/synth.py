@@ -5,6 +5,8 @@ Configs (BASELINE.json `configs`):
   C3: 1M IMIX 64/576/1500 (7:4:1), v4/v6, TCP/UDP     -> config_id 3, mode 1
   C4: 10M IMIX + flow table, pool 2^20 (uniform/Zipf) -> config_id 4, mode 1
   C5: 80M = 8 x 10M shards by packet index            -> config_id 5, mode 1
+Override lan_dst_permille (e.g. 800) for a LAN-heavy variant in which the Local/Global filters
+drop a large share of the batch.
 """
 import ctypes as C
 import os
@@ -17,7 +19,7 @@ from ._native import SYNTH_LIB_PATH, NativeLibraryMissing
 class SynthCfg(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n_flows", C.c_uint32), ("mode", C.c_uint32),
                 ("v6_permille", C.c_uint32), ("udp_permille", C.c_uint32), ("dns_permille", C.c_uint32),
-                ("zipf", C.c_uint32), ("zipf_s", C.c_double)]
+                ("zipf", C.c_uint32), ("zipf_s", C.c_double), ("lan_dst_permille", C.c_uint32)]
 
 
 CONFIGS = {

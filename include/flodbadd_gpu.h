@@ -246,17 +246,20 @@ typedef struct fb_flow_rec {
     uint32_t slot;           /* 120: table slot (the flow id of fb_flow_history_dev)           */
     uint32_t session_flags;  /* 124: fb_session_flags as stored when the session was inserted
                                 (src/packets.rs:429-435: is_local_src/dst, is_self_src/dst of the
-                                canonical key under the configuration of that update call)      */
+                                canonical key under the configuration of that update call; and
+                                dst_service is Some, src/packets.rs:441-466)                      */
 } fb_flow_rec;               /* 128 bytes */
 
 /* fb_flow_rec.session_flags (SessionInfo.is_local_src / is_local_dst / is_self_src / is_self_dst,
- * src/sessions.rs:40-61, set once at insert, src/packets.rs:429-435).  Same bit values as
- * fb_enrich_bits. */
+ * src/sessions.rs:40-61, set once at insert, src/packets.rs:429-435; bits 0-3 have the same values
+ * as fb_enrich_bits) and FB_SESSION_DST_SERVICE: SessionInfo.dst_service is Some, i.e. the
+ * service-port table names the canonical key's dst port at insert (src/packets.rs:441-466). */
 enum fb_session_flags {
     FB_SESSION_LOCAL_SRC = 1u,
     FB_SESSION_LOCAL_DST = 2u,
     FB_SESSION_SELF_SRC = 4u,
-    FB_SESSION_SELF_DST = 8u
+    FB_SESSION_SELF_DST = 8u,
+    FB_SESSION_DST_SERVICE = 16u
 };
 
 typedef struct fb_ctx fb_ctx;

@@ -460,8 +460,9 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
             s->rec.key = r->key;
             s->rec.first_seen = pos; /* start_time, src/packets.rs:352 */
             s->rec.end_seen = FB_SEEN_NONE;
-            /* is_local_src/dst, is_self_src/dst of the key, stored once at insert (src/packets.rs:429-435) */
-            s->rec.session_flags = ((uint32_t)r->meta >> 3) & 0xFu;
+            /* is_local_src/dst, is_self_src/dst of the key (src/packets.rs:429-435) and dst_service
+               (src/packets.rs:441-466), stored once at insert */
+            s->rec.session_flags = ((uint32_t)r->meta >> 3) & 0x1Fu;
             f->count++;
             if (st) st->new_sessions++;
         } else if (st) {

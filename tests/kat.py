@@ -73,6 +73,8 @@ def check_case(case, records, flows, histories=None):
             # dst_service is set at session creation from the first packet (src/packets.rs:441-464)
             first = next(r for r in records if Session.from_key(r) == k)
             assert bool(int(first["meta"]) & META_DST_SERVICE) == e["dst_service"], (name, k.dst_port)
+            # ... and stored in the session (SessionInfo.dst_service.is_some(), src/packets.rs:866-870)
+            assert (sess[k].dst_service is not None) == e["dst_service"], (name, sess[k].dst_service)
 
 
 def filter_of(case):

@@ -1,0 +1,46 @@
+"""bench.py's multi-GPU launch plumbing on the CPU (no GPU is touched): `python3 bench.py --gpus N`
+without a launcher spawns N rank processes with torchrun's environment, the ranks form one gloo
+group, and rank 0 reports N; a launcher whose world disagrees with --gpus is an error."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env=None, timeout=180):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH] + args, env=e, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_spawns_n_ranks(n):
+    p = _run(["--gpus", str(n), "--world-check"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["requested_gpus"] == n and d["group_size"] == n
+    assert d["rank_sum"] == n * (n - 1) // 2  # every rank joined exactly once
+    assert d["master"].startswith("127.0.0.1:")
+
+
+@pytest.mark.timeout(120)
+def test_single_gpu_runs_in_process():
+    p = _run(["--gpus", "1", "--world-check"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["group_size"] == 1
+
+
+@pytest.mark.timeout(120)
+def test_world_mismatch_is_an_error():
+    p = _run(["--gpus", "4", "--world-check"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "launcher started 2 ranks" in (p.stderr + p.stdout)

@@ -45,6 +45,27 @@ def test_full_size_headline_launch(gpu_capture, cid):
         _conserved(r[3], FULL)
 
 
+@pytest.mark.parametrize("cid", [2, 3])
+@pytest.mark.parametrize("flt", [SessionFilter.LocalOnly, SessionFilter.GlobalOnly])
+def test_full_size_filter_drops(gpu_capture, cid, flt):
+    """The headline launch at full size on a LAN-heavy variant of the mix (80 % of the flows with a
+    LAN dst as well, synth lan_dst_permille): ~40 % of the SESSION frames are local, so LocalOnly
+    drops ~60 % and GlobalOnly ~40 % of them (src/packets.rs:321-327, src/sessions.rs:660-672),
+    bit-exact against the oracle batch for batch."""
+    batches = [synth.generate(cid, FULL, first=k * FULL, lan_dst_permille=800) for k in range(2)]
+    gpu_capture.set_filter(flt)
+    try:
+        res = _run_batches(gpu_capture, batches)
+    finally:
+        gpu_capture.set_filter(SessionFilter.All)
+    for (frames, offs), r in zip(batches, res):
+        _check(gpu_capture, frames, offs, flt=int(flt), res=r)
+        _conserved(r[3], FULL)
+        s = r[3][0]
+        kept = int(s["n_session"]) / (int(s["n_session"]) + int(s["n_filtered"]))
+        assert (0.3 < kept < 0.5) if flt == SessionFilter.LocalOnly else (0.5 < kept < 0.7), kept
+
+
 def _void_sorted(arr):
     """Order-independent view of flow rows (table slot zeroed: placement, not content)."""
     arr = arr.copy()

@@ -132,3 +132,54 @@ def test_stream_more_than_4m_flows_async():
         for x in keep:
             x.free()
         cap.close()
+
+
+def test_stream_async_without_joins_grows_in_time():
+    """The C4 bench's calling pattern with growth on: fb_process_seg_async_dev batches enqueued back
+    to back with two rotating buffer sets and NO join or host read between them (the host runs
+    ahead of the device), past the initial capacity and across several growths.  Each growth
+    decision reads the report of the update two calls back (maybe_grow waits for it), so no batch
+    may report error bit 4 (FB_ERR_TABLE_FULL: dropped packets, where the reference's map is
+    unbounded), and the table equals the oracle's."""
+    n, batches = 1 << 19, 8
+    lib = N.gpu_lib()
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 20, max_batch_packets=n)
+    stream = N.Stream()
+    ref = coracle.Flows()
+    cfg = coracle.make_cfg(2)
+    bufs, st_bufs = [], []
+    try:
+        nseg = (n + 63) // 64
+        sets = [(N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4)) for _ in range(2)]
+        for b in range(batches):  # every batch resident first: the timed loop below only enqueues
+            frames, offs = synth.generate(2, n, first=b * n, n_flows=1 << 23)
+            r_out, _, _, _ = coracle.parse_classify(cfg, frames, offs)
+            ref.update(r_out)
+            bufs.append((N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+                         frames.nbytes))
+            st_bufs.append(N.DeviceBuffer(N.STATS_DTYPE.itemsize))
+        gen0 = cap.table_info()["generation"]
+        for b, (d_fr, d_off, nbytes) in enumerate(bufs):
+            d_out, d_seg = sets[b & 1]
+            N.check(lib.fb_process_seg_async_dev(cap.ctx, d_fr.ptr, nbytes, d_off.ptr, n, d_out.ptr, d_seg.ptr, None,
+                                                 st_bufs[b].ptr, stream.ptr))
+        N.check(lib.fb_flow_join(cap.ctx, stream.ptr))
+        stream.sync()
+        stats = [x.download(np.zeros(1, dtype=N.STATS_DTYPE), stream=stream.ptr)[0].copy() for x in st_bufs]
+        assert all(int(s["error"]) == 0 for s in stats), [int(s["error"]) for s in stats]
+        assert sum(int(s["new_sessions"]) for s in stats) == ref.count()
+        assert sum(int(s["new_sessions"]) + int(s["updated_sessions"]) for s in stats) == n * batches - \
+            sum(int(s["n_dns"]) for s in stats)
+        info = cap.table_info()
+        assert info["generation"] >= gen0 + 2 and ref.count() > (1 << 21), (info, ref.count())
+        _same_table(cap.export_flows(), ref.export_sorted())
+    finally:
+        for d_out, d_seg in sets:
+            d_out.free()
+            d_seg.free()
+        for d_fr, d_off, _ in bufs:
+            d_fr.free()
+            d_off.free()
+        for x in st_bufs:
+            x.free()
+        cap.close()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Run one GPU validation/measurement pass on the gpurun box.  Each GPU step has its own time
 # limit; a crash/abort/timeout (rc >= 2 from pytest, or any signal) stops the script.
-# usage: tools/gpu_step.sh [pytest|smoke|bench|prof|all] ...
+# usage: tools/experiments/gpu_step.sh [pytest|smoke|bench|prof|all] ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

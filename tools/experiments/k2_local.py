@@ -2,7 +2,7 @@
 """Experiment (not product): how much of the C4 table update is the random record gather?
 Runs bench.py's C4 one-stream line on the SAME frames reordered so that every table partition's
 records are contiguous (a valid capture, just in partition order): K2's gathers then stream.
-Usage: python3 tools/k2_local.py [--order partition|original] -- <bench args>"""
+Usage: python3 tools/experiments/k2_local.py [--order partition|original] -- <bench args>"""
 import os
 import sys
 

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-2 profiles at HEAD: C2/C3/C4 bench + kernel trace + FETCH/WRITE passes (tools/r2_profile.sh),
+# Round-2 profiles at HEAD: C2/C3/C4 bench + kernel trace + FETCH/WRITE passes (tools/experiments/r2_profile.sh),
 # the driver's C2 command under a kernel trace (tools/prof_driver.sh), and a dense-mode C2 trace.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 R=$(pwd)
-bash tools/r2_profile.sh || exit 1
+bash tools/experiments/r2_profile.sh || exit 1
 bash tools/prof_driver.sh || exit 1
 OUT=$R/gpurun_out/profdense; rm -rf "$OUT"; mkdir -p "$OUT"; export TMPDIR=/tmp
 cd /tmp

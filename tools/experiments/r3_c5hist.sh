@@ -6,4 +6,4 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_c5.py -m gpu -x -q --timeou
 tail -2 gpurun_out/c5_test.log
 timeout -k 10 300 python -u tools/c5_merge_time.py > gpurun_out/c5_merge_time.log 2>&1 || { tail -20 gpurun_out/c5_merge_time.log; exit 1; }
 grep merge gpurun_out/c5_merge_time.log
-VARS="${VARS:-product nobatch norank}" bash tools/r3_histvar.sh
+VARS="${VARS:-product nobatch norank}" bash tools/experiments/r3_histvar.sh

@@ -15,7 +15,7 @@ print('c4_records', e['c4']['c4_records']['value'], 'c4_sync', e['c4']['c4_sync'
 "
 bash tools/prof_driver.sh || exit 1
 cp -r gpurun_out/profdrv $O/profdrv
-NOSQ=1 bash tools/r3_c4prof.sh || exit 1
+NOSQ=1 bash tools/experiments/r3_c4prof.sh || exit 1
 cp -r gpurun_out/c4prof $O/c4prof
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/dense -o run -- python3 $R/bench.py --mode dense --steps 100 --warmup 10 \

@@ -1,5 +1,5 @@
 #!/bin/bash
-# K2 with partition-ordered frames (tools/k2_local.py) vs the original order, kernel traces; then
+# K2 with partition-ordered frames (tools/experiments/k2_local.py) vs the original order, kernel traces; then
 # the default bench line at the driver's settings (with the new C4 extra).
 set -u
 cd "${GRAFT_REPO_ROOT}"; R=$(pwd); export TMPDIR=/tmp
@@ -17,7 +17,7 @@ PY
 for o in partition original; do
   rm -rf $R/gpurun_out/k2l_$o; mkdir -p $R/gpurun_out/k2l_$o
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/k2l_$o -o run -- python3 $R/tools/k2_local.py --order $o -- --config 4 --c4-sync --steps 10 --warmup 2 --no-cpu-baseline --no-host --no-imix --no-other-mode > $R/gpurun_out/k2l_$o/bench.json 2> $R/gpurun_out/k2l_$o/bench.err || { grep -v "^[WIE]20" $R/gpurun_out/k2l_$o/bench.err | tail -5; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/k2l_$o -o run -- python3 $R/tools/experiments/k2_local.py --order $o -- --config 4 --c4-sync --steps 10 --warmup 2 --no-cpu-baseline --no-host --no-imix --no-other-mode > $R/gpurun_out/k2l_$o/bench.json 2> $R/gpurun_out/k2l_$o/bench.err || { grep -v "^[WIE]20" $R/gpurun_out/k2l_$o/bench.err | tail -5; exit 1; }
   cd $R
   echo "== $o"; summ $R/gpurun_out/k2l_$o
   python3 -c "import json;d=json.load(open('$R/gpurun_out/k2l_$o/bench.json'));print(d['value'],d['extra']['c4_stages']['parse_ms'],d['extra']['c4_stages']['flow_update_ms'])"

@@ -17,7 +17,7 @@ PY
 for o in partition original; do
   D=$R/gpurun_out/k2n_$o; rm -rf $D; mkdir -p $D
   cd /tmp
-  FLODBADD_GPU_LIB=$R/flodbadd_amd/build/var_nocomb.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D -o run -- python3 $R/tools/k2_local.py --order $o -- --config 4 --c4-sync --steps 10 --warmup 2 --no-cpu-baseline --no-host --no-imix --no-other-mode > $D/bench.json 2> $D/bench.err || { grep -v "^[WIE]20" $D/bench.err | tail -5; exit 1; }
+  FLODBADD_GPU_LIB=$R/flodbadd_amd/build/var_nocomb.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D -o run -- python3 $R/tools/experiments/k2_local.py --order $o -- --config 4 --c4-sync --steps 10 --warmup 2 --no-cpu-baseline --no-host --no-imix --no-other-mode > $D/bench.json 2> $D/bench.err || { grep -v "^[WIE]20" $D/bench.err | tail -5; exit 1; }
   cd $R
   echo "== nocomb $o"; summ $D
 done

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C2 headline A/B over prebuilt library variants (tools/build_variants.sh), interleaved rounds:
-# SWEEP_VARIANTS="a b" [SWEEP_ROUNDS="1 2 3"] [STEPS=200] bash tools/sweep_c2.sh
+# SWEEP_VARIANTS="a b" [SWEEP_ROUNDS="1 2 3"] [STEPS=200] bash tools/experiments/sweep_c2.sh
 mkdir -p gpurun_out/sweepc2
 set -e
 for r in ${SWEEP_ROUNDS:-1 2 3}; do

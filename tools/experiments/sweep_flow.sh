@@ -1,5 +1,5 @@
 # C4 session-table sweep over prebuilt variants (tools/build_variants.sh), interleaved rounds:
-# SWEEP_VARIANTS="a b" [SWEEP_ROUNDS="1 2"] [ZIPF=1.1] bash tools/sweep_flow.sh
+# SWEEP_VARIANTS="a b" [SWEEP_ROUNDS="1 2"] [ZIPF=1.1] bash tools/experiments/sweep_flow.sh
 mkdir -p gpurun_out/sweepf
 set -e
 Z=""; [ -n "${ZIPF:-}" ] && Z="--zipf $ZIPF"

@@ -1,7 +1,7 @@
 // Microbenchmark: header-window loads of 64-B frames at 2-mod-4 byte offsets (10, 26, 42 + a dword
 // at 66, as k_parse_seg issues them) vs dword-aligned ones (8, 24, 40 + 64), one lane per frame,
 // each lane storing 56 B (as a record) so the read/write mix matches C2.
-// Build: hipcc --offload-arch=gfx950 -O3 -o gpurun_out/ubench_align tools/ubench_align.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o gpurun_out/ubench_align tools/experiments/ubench_align.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

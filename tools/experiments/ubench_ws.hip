@@ -4,7 +4,7 @@
 //   seg           the product kernel (k_parse_seg<false>)
 // (The round-2 ablations -- no stores, no classification, per-wave stamps -- were template flags
 // of the product kernel; they are no longer in the product source.  DESIGN.md keeps their numbers.)
-//   build: tools/build_ubench_ws.sh ; run: tools/ubench_ws [config_id] [n] [rotate] [iters]
+//   build: tools/experiments/build_ubench_ws.sh ; run: tools/ubench_ws [config_id] [n] [rotate] [iters]
 #include "../flodbadd_amd/csrc/fb_parse.hip"
 
 #include <stdio.h>

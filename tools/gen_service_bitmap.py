@@ -26,16 +26,23 @@ import sys
 REF = "/root/reference/src/port_vulns_db.rs"
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "flodbadd_amd", "data", "service_ports.bin")
+# port -> non-empty name (what SessionInfo.dst_service holds, src/packets.rs:441-466)
+NAMES_OUT = os.path.join(HERE, "..", "flodbadd_amd", "data", "service_names.json")
 EXPECTED_SHA256 = "04be3230d59a9c3dbe578f188b1f6113ebc188d8140f88fd6ea17dc595b32dad"
 
 
-def build_bitmap(src_text: str) -> bytes:
+def port_names(src_text: str) -> dict:
     start = src_text.index('r####"') + len('r####"')
     end = src_text.rindex('"####')
     doc = json.loads(src_text[start:end])
     names = {}
     for entry in doc["vulnerabilities"]:
         names[int(entry["port"])] = entry["name"]  # last insert wins
+    return names
+
+
+def build_bitmap(src_text: str) -> bytes:
+    names = port_names(src_text)
     bm = bytearray(8192)
     for port, name in names.items():
         if name != "":
@@ -45,7 +52,8 @@ def build_bitmap(src_text: str) -> bytes:
 
 def main() -> int:
     with open(REF, "r", encoding="utf-8") as f:
-        bm = build_bitmap(f.read())
+        text = f.read()
+    bm = build_bitmap(text)
     digest = hashlib.sha256(bm).hexdigest()
     if digest != EXPECTED_SHA256:
         print(f"sha256 mismatch: {digest}", file=sys.stderr)
@@ -53,6 +61,10 @@ def main() -> int:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     with open(OUT, "wb") as f:
         f.write(bm)
+    named = {str(p): n for p, n in sorted(port_names(text).items()) if n != ""}
+    with open(NAMES_OUT, "w") as f:
+        json.dump(named, f, separators=(",", ":"))
+    print(f"wrote {NAMES_OUT} ({len(named)} names)")
     print(f"wrote {OUT} ({len(bm)} bytes, {sum(bin(b).count('1') for b in bm)} service ports, sha256 {digest})")
     return 0
 

@@ -41,6 +41,13 @@ def kernel_stats(d):
     return out
 
 
+def dispatches(d, sub):
+    """Every dispatch of the kernels whose name contains `sub`, in start order: (name, us)."""
+    c = db_of(d)
+    return [(n, dur / 1e3) for n, dur, _ in
+            c.execute("select name, duration, start from kernels order by start") if sub in n]
+
+
 def counter(d, name):
     c = db_of(d)
     vals = [v for k, cn, v in c.execute("select kernel_name, counter_name, value from counters_collection")
@@ -61,6 +68,9 @@ def main():
     ap.add_argument("--kernel", default=None, help="substring of the dominant kernel's name (default k_parse_seg)")
     ap.add_argument("--algo-bytes", type=float, default=None, help="algorithmic bytes per launch (bench line)")
     ap.add_argument("--bpl", type=int, default=1, help="batches per launch of the profiled bench run")
+    ap.add_argument("--key", default=None, help="pmc_traffic.json key (default: --config)")
+    ap.add_argument("--dispatch-kernel", default=None,
+                    help="with --trace: also write every dispatch of the kernels matching this substring")
     a = ap.parse_args()
     global PARSE_KERNEL
     if a.kernel:
@@ -77,6 +87,13 @@ def main():
         print("wrote", p)
         for r in st[:5]:
             print(r)
+        if a.dispatch_kernel:
+            p = os.path.join(ROOT, "profiles", "%s_dispatches.csv" % a.tag)
+            with open(p, "w") as f:
+                f.write("Index,Name,DurationUs\n")
+                for i, (n, us) in enumerate(dispatches(a.trace, a.dispatch_kernel)):
+                    f.write('%d,"%s",%.3f\n' % (i, n, us))
+            print("wrote", p)
     if a.fetch and a.write:
         fkb, nf = counter(a.fetch, "FETCH_SIZE")
         wkb, nw = counter(a.write, "WRITE_SIZE")
@@ -89,7 +106,7 @@ def main():
             d = json.load(open(p))
         except (OSError, ValueError):
             d = {}
-        d[str(a.config)] = dict(
+        d[a.key or str(a.config)] = dict(
             tag=a.tag, kernel=PARSE_KERNEL, launches_fetch=nf, launches_write=nw,
             fetch_size_kib_median=fkb, write_size_kib_median=wkb,
             fetch_bytes_raw=fetch_raw, fetch_bytes_corrected_x2=fetch_corr, write_bytes=write_raw,
@@ -100,7 +117,7 @@ def main():
                   "overlapping, so the x2 is an upper estimate; Infinity-Cache hits are counted too"))
         with open(p, "w") as f:
             json.dump(d, f, indent=1, sort_keys=True)
-        print("wrote", p, d[str(a.config)])
+        print("wrote", p, d[a.key or str(a.config)])
 
 
 if __name__ == "__main__":
