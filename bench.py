@@ -414,8 +414,8 @@ def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
 def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     """BASELINE config C5 after the timed region: rank r's shard of a world x per_rank frame batch
     (C4 mix, flow pool 2^20; packets [r * per_rank, (r+1) * per_rank)) through the fused parse +
-    classify + session-table kernels, then the global per-flow counter merge
-    (flodbadd_amd.distributed: all-gather of keys, dense ids, all_reduce over RCCL)."""
+    classify + session-table kernels, then the global session table (flodbadd_amd.distributed:
+    owner-grouped export and owner merge in the library, all_to_all + all_gather over RCCL)."""
     from flodbadd_amd import synth
     from flodbadd_amd.distributed import global_flow_table
     shard_first = rank * per_rank
@@ -438,21 +438,13 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
 
     def export_merge():
-        if device.type == "cuda":  # RCCL: the table is exported straight into a device tensor
+        # the library exports the owner groups into a device tensor, the collectives move them
+        # (RCCL with device tensors; gloo via host memory), the library merges each owner's records
+        merged = global_flow_table(dist, ctx, shard_first=shard_first, device=device, group=group, as_tensor=True)
+        if device.type == "cuda":
             import torch
-            flows = torch.empty((max(cnt.value, 1), N.FLOW_REC_DTYPE.itemsize), dtype=torch.uint8, device=device)
-            d_n = torch.zeros(1, dtype=torch.int64, device=device)
-            N.check(lib.fb_flow_export_dev(ctx, C.c_void_p(flows.data_ptr()), cnt.value, C.c_void_p(d_n.data_ptr()),
-                                           None))
             torch.cuda.synchronize(device)
-            local = int(d_n.item())
-            return local, global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first,
-                                            as_tensor=True)
-        flows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
-        got = C.c_uint64()
-        N.check(lib.fb_flow_export(ctx, N.ptr(flows), cnt.value, C.byref(got), None))
-        local = int(got.value)
-        return local, global_flow_table(dist, flows[:local], device=device, group=group, shard_first=shard_first)
+        return int(cnt.value), merged
 
     # the first merge also sets up the group's communicators and loads the sort kernels: timed apart
     t0 = time.perf_counter()
@@ -473,9 +465,9 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                 local_flows=local, global_flows=int(len(merged)),
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),
-                note="per-rank fused parse+flow upsert of the rank's shard, then the table exported (to a device "
-                     "tensor with RCCL) and merged: records all_to_all to their Ord-range owners, owner sort + "
-                     "merge, all-gather of the merged records (left on the device)")
+                note="per-rank fused parse+flow upsert of the rank's shard, then the global session table: "
+                     "fb_flow_export_merge_dev (owner groups, device tensor), all_to_all to the owners, "
+                     "fb_flow_merge_dev on each owner, all_gather of the merged records (left on the device)")
 
 
 def usable_cores():
@@ -869,8 +861,7 @@ def main():
             # CPU tensors when the ranks share one GPU (rehearsal on a one-GPU box)
             backend = os.environ.get("FB_C5_BACKEND", "nccl")
             dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
-            if backend == "nccl":
-                torch.cuda.set_device(dev)
+            torch.cuda.set_device(torch.device("cuda", device))  # the library's exports land on this GPU
             g = tdist.new_group(backend=backend)
             extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, args.c5_frames, rank, world, tdist, g, dev)
             extra["c5_flow_reduce"]["backend"] = "rccl" if backend == "nccl" else backend

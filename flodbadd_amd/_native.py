@@ -46,6 +46,10 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
     ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8"),
     ("first_seen", "<u8"), ("last_seen", "<u8"), ("end_seen", "<u8"), ("hist_len", "<u4"),
     ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("session_flags", "<u4")])
+# fb_flow_mrec: a flow record exported for the multi-GPU merge (positions global, slot = the rank) and
+# the update call of the flow's first S, s, H, h (FB_CALL_NONE: none)
+FLOW_MREC_DTYPE = np.dtype([("rec", FLOW_REC_DTYPE), ("char_call", "<u4", (4,))])
+FB_CALL_NONE = 0xFFFFFFFF
 # fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst and
 # dst_service is Some, at insert)
 SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST, SESSION_DST_SERVICE = 1, 2, 4, 8, 16
@@ -190,6 +194,9 @@ GPU_SYMBOLS = [
     ("fb_flow_table_info_get", _I, [_P, C.POINTER(FlowTableInfo)]),
     ("fb_flow_slot_remap", _I, [_P, _P, _U64, _PU64]),
     ("fb_flow_hash", _U64, [_P]),
+    ("fb_flow_export_merge_dev", _I, [_P, _U32, _U32, _U64, _P, _U64, _P, _P]),
+    ("fb_flow_merge_dev", _I, [_P, _P, _U64, _P, _P, _P]),
+    ("fb_flow_owner", _U32, [_P, _U32]),
     ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),
     ("fb_ring_destroy", _I, [_P]),
     ("fb_ring_push", _I, [_P, _P, _U32]),

@@ -99,6 +99,9 @@ struct fb_ctx {
     uint64_t generation = 0;        // growths so far
     bool grow = true;               // FB_CFG_FIXED_TABLE clears it
     uint32_t* d_remap = nullptr;    // the last growth's old -> new slot map
+    uint4* d_char_call = nullptr;   // [table_cap] first update call of S s H h per slot (the merge's)
+    void* d_mscratch = nullptr;     // multi-GPU merge scratch (export owner counts / merge tables)
+    uint64_t mscratch_bytes = 0;
     uint64_t remap_n = 0;
     unsigned long long* d_n = nullptr;
     // ordered per-flow state: update calls since create/clear, table slot of each record slot
@@ -467,6 +470,7 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         c->flow_shift = 64u - lg;
         ok = hipMalloc(&c->d_table, cap * sizeof(FlowSlot)) == hipSuccess &&
              hipMemset(c->d_table, 0, cap * sizeof(FlowSlot)) == hipSuccess &&
+             hipMalloc(&c->d_char_call, cap * sizeof(uint4)) == hipSuccess &&
              hipMalloc(&c->d_partials, 4ull * c->flow_parts * 8ull) == hipSuccess &&
              hipMalloc(&c->d_hcount, cap * 4ull) == hipSuccess &&
              hipMalloc(&c->d_part_base, (c->flow_parts + 1ull) * 4ull) == hipSuccess &&
@@ -502,6 +506,8 @@ int fb_destroy(fb_ctx* c) {
     for (UpdScratch& u : c->us) free_upd_scratch(u);
     hipFree(c->d_partials);
     hipFree(c->d_remap);
+    hipFree(c->d_char_call);
+    hipFree(c->d_mscratch);
     if (c->h_mbox) hipHostFree(c->h_mbox);
     hipFree(c->d_n);
     hipFree(c->d_hword);
@@ -969,7 +975,14 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
         return set_err(FB_ERR_NOMEM, "slot remap");
     }
     HIP_TRY(hipMemsetAsync(nw, 0, cap * sizeof(FlowSlot), s));
-    HIP_TRY(launch_flow_grow(c->d_table, c->flow_parts, k, c->flow_shift - k, nw, c->d_remap, s));
+    uint4* nw_cc = nullptr;
+    if (hipMalloc(&nw_cc, cap * sizeof(uint4)) != hipSuccess) {
+        hipFree(nw);
+        free_new();
+        return set_err(FB_ERR_NOMEM, "grown character-call array");
+    }
+    HIP_TRY(launch_flow_grow(c->d_table, c->flow_parts, k, c->flow_shift - k, nw, c->d_remap, c->d_char_call, nw_cc,
+                             s));
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_table);
     hipFree(c->d_partials);
@@ -977,6 +990,8 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     hipFree(c->d_part_base);
     hipFree(c->d_hist_slow);
     c->d_table = nw;
+    hipFree(c->d_char_call);
+    c->d_char_call = nw_cc;
     c->d_partials = partials;
     c->d_hcount = hcount;
     c->d_part_base = part_base;
@@ -1099,6 +1114,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
+    p.char_call = c->d_char_call;
     c->part_recs = nullptr;
     HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
     if (split) {
@@ -1385,6 +1401,46 @@ int fb_flow_export_sessions_dev(fb_ctx* c, uint32_t filter, fb_flow_rec* d_out, 
 
 int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_n, void* stream) {
     return fb_flow_export_sessions_dev(c, FB_FILTER_ALL, d_out, cap, d_n, stream);
+}
+
+// ---- multi-GPU merge (fb_merge.hip) ---------------------------------------------------------------
+static int ensure_mscratch(fb_ctx* c, uint64_t bytes, hipStream_t s) {
+    if (bytes <= c->mscratch_bytes) return FB_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(c->d_mscratch);
+    c->d_mscratch = nullptr;
+    c->mscratch_bytes = 0;
+    if (hipMalloc(&c->d_mscratch, bytes) != hipSuccess)
+        return set_err(FB_ERR_NOMEM, "merge scratch (%llu bytes)", (unsigned long long)bytes);
+    c->mscratch_bytes = bytes;
+    return FB_OK;
+}
+
+int fb_flow_export_merge_dev(fb_ctx* c, uint32_t world, uint32_t rank, uint64_t shard_first, fb_flow_mrec* d_out,
+                             uint64_t cap, uint64_t* d_counts, void* stream) {
+    if (!c || !d_counts || (cap && !d_out)) return set_err(FB_ERR_INVAL, "ctx, d_counts and d_out are required");
+    if (world == 0 || world > 64 || rank >= world) return set_err(FB_ERR_INVAL, "1 <= world <= 64, rank < world");
+    if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = join_updates(c, s);
+    if (!rc) rc = ensure_mscratch(c, merge_export_scratch_bytes(c->table_cap, world), s);
+    if (rc) return rc;
+    HIP_TRY(launch_merge_export(c->d_table, c->d_char_call, c->table_cap, world, rank, shard_first, d_out, cap,
+                                (unsigned long long*)d_counts, c->d_mscratch, s));
+    return FB_OK;
+}
+
+int fb_flow_merge_dev(fb_ctx* c, const fb_flow_mrec* d_in, uint64_t n, fb_flow_rec* d_out, uint64_t* d_n,
+                      void* stream) {
+    if (!c || !d_n || (n && (!d_in || !d_out))) return set_err(FB_ERR_INVAL, "ctx, d_in, d_out and d_n are required");
+    if (n >= 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "n %llu >= 2^32", (unsigned long long)n);
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = ensure_mscratch(c, n ? merge_scratch_bytes(n) : 0, s);
+    if (rc) return rc;
+    HIP_TRY(launch_merge(d_in, n, d_out, (unsigned long long*)d_n, c->d_mscratch, s));
+    return FB_OK;
 }
 
 int fb_flow_export_sessions(fb_ctx* c, uint32_t filter, fb_flow_rec* out, uint64_t cap, uint64_t* n, void* stream) {

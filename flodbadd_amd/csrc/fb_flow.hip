@@ -434,15 +434,7 @@ __device__ __forceinline__ unsigned long long lds_ld(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
-__device__ __forceinline__ uint32_t conn_state_of(uint32_t m) {
-    const bool S = m & 1u, H = m & 4u, h = m & 8u, F = m & 16u, f = m & 32u, R = m & 64u, r = m & 128u;
-    if (S && H && F && f) return FB_CONN_SF;
-    if (S && !h && !r) return FB_CONN_S0;
-    if (R || r) return FB_CONN_REJ;
-    if (S && H && !F && !f) return FB_CONN_S1;
-    return FB_CONN_OTHER;
-}
+// determine_conn_state: conn_state_of (fb_internal.h).
 
 // Find or insert `key` in an LDS open-addressing table of kSlots slots of kStride u64 words
 // (tag: 0 empty, 1 being inserted, hash | 2; then the 5 key words), home slot h32 & (kSlots-1).
@@ -740,7 +732,8 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
 // the slot's ordered fields as loaded with the slice (first_seen, last_seen | end_seen, hist_len,
 // hist_state); the first / last / end packets' pkt_index (and the end's character) are in the
 // scratch keys.
-__device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t batch, const uint4 o0, const uint4 o1) {
+__device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t batch, const uint4 o0, const uint4 o1,
+                                            uint4* cc) {
     const unsigned long long first = *sc64(q, kScFirst);
     if (first == ~0ull) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
@@ -753,6 +746,23 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t b
     const uint32_t state = fresh ? (flags & 0x00F00000u) : o1.w, len = fresh ? 0u : o1.z;
     const unsigned long long last_seen = hi | (uint32_t)last;
     const uint32_t mask = state & 0xFFFFu;
+    // the update call of the first S, s, H, h of the flow (FB_CALL_NONE: none yet), kept beside the
+    // table for the multi-GPU merge (it decides which of a rank's characters precede another rank's
+    // end packet): written when a character first appears -- its mask bit was clear -- and whole at
+    // insert, so nothing is read here
+    if (cc) {
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b) w[b] = q[kScChar + b] != ~0u ? batch : FB_CALL_NONE;
+        if (fresh) {
+            *cc = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            uint32_t* c = reinterpret_cast<uint32_t*>(cc);
+#pragma unroll
+            for (uint32_t b = 0; b < 4u; ++b)
+                if (w[b] != FB_CALL_NONE && !(mask & (1u << b))) c[b] = batch;
+        }
+    }
     uint32_t cs = state >> 16;
     if (end != ~0ull && end_seen == FB_SEEN_NONE) {  // the flow's first FIN/RST is in this batch
         const uint32_t end_rec = (uint32_t)(end >> 37);
@@ -1121,7 +1131,8 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             rbase += tot;
             __syncthreads();
         }
-        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1);
+        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1,
+                    P.char_call ? P.char_call + (size_t)part * kFlowSlots + threadIdx.x : nullptr);
         // only the slots this batch touched (inserted or updated) changed; the others' heads are
         // not written back (a 96-B head alone is a partial line)
         uint4* gw = reinterpret_cast<uint4*>(T);
@@ -1186,7 +1197,8 @@ __global__ __launch_bounds__(1024) void k_flow_finish(fb_batch_stats* S, const u
 // its unchanged home slot (low bits of the hash) by linear probing, the claim made on an LDS array
 // per new partition.
 __global__ __launch_bounds__(kFlowSlots) void k_flow_grow(const FlowSlot* old, uint32_t new_shift, uint32_t k,
-                                                          FlowSlot* nw, uint32_t* remap) {
+                                                          FlowSlot* nw, uint32_t* remap, const uint4* old_cc,
+                                                          uint4* new_cc) {
     extern __shared__ uint32_t claim_w[];  // [2^k][kFlowSlots]
     const uint32_t p = blockIdx.x, i = threadIdx.x;
     for (uint32_t j = i; j < (kFlowSlots << k); j += kFlowSlots) claim_w[j] = 0u;
@@ -1207,6 +1219,7 @@ __global__ __launch_bounds__(kFlowSlots) void k_flow_grow(const FlowSlot* old, u
         uint4* d = reinterpret_cast<uint4*>(nw + dst);
 #pragma unroll
         for (int k = 0; k < 8; ++k) d[k] = src[k];
+        if (old_cc) new_cc[dst] = old_cc[(size_t)p * kFlowSlots + i];
     }
     remap[(size_t)p * kFlowSlots + i] = dst;
 }
@@ -1241,26 +1254,7 @@ __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned
         __syncthreads();
         unsigned long long pos = s_base + __popcll(m & ((1ull << lane) - 1ull));
         for (uint32_t w = 0; w < wave; ++w) pos += sh[w];
-        if (occ && pos < out_cap) {
-            fb_flow_rec r;
-            __builtin_memcpy(&r.key, T[i].key, 40);
-            r.outbound_bytes = T[i].cnt[0];
-            r.inbound_bytes = T[i].cnt[1];
-            r.orig_pkts = T[i].cnt[2];
-            r.resp_pkts = T[i].cnt[3];
-            r.orig_ip_bytes = T[i].cnt[4];
-            r.resp_ip_bytes = T[i].cnt[5];
-            r.first_seen = T[i].first_seen;
-            r.last_seen = T[i].last_seen;
-            r.end_seen = T[i].end_seen;
-            r.hist_len = T[i].hist_len;
-            r.hist_mask = (uint16_t)(T[i].hist_state & 0x1FFFu);
-            r.conn_state = (uint8_t)((T[i].hist_state >> 16) & 0xFu);
-            r.end_mask = (uint8_t)(T[i].hist_state >> 24);
-            r.slot = (uint32_t)i;
-            r.session_flags = ((T[i].hist_state >> 20) & 0xFu) | ((T[i].hist_state >> 15) & 1u) << 4;
-            out[pos] = r;
-        }
+        if (occ && pos < out_cap) out[pos] = flow_rec_of(T[i], (uint32_t)i);
         __syncthreads();
     }
 }
@@ -1314,10 +1308,10 @@ hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* p
     return hipGetLastError();
 }
 hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k, uint32_t new_shift, FlowSlot* nw,
-                            uint32_t* remap, hipStream_t s) {
+                            uint32_t* remap, const uint4* old_cc, uint4* new_cc, hipStream_t s) {
     if (k < 1u || k > 5u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_flow_grow, dim3(old_parts), dim3(kFlowSlots), (kFlowSlots << k) * 4u, s, old, new_shift, k, nw,
-                       remap);
+                       remap, old_cc, new_cc);
     return hipGetLastError();
 }
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,

@@ -264,7 +264,47 @@ struct FlowParams {
                                 // histogram pass then reads 4 B per record instead of the record
     const uint4* ent;           // non-null (with rec_part): the slots' update entries (UpdEnt), which
                                 // K1c / K2 read instead of the records
+    uint4* char_call = nullptr; // [capacity] per slot: the update call of the flow's first S, s, H, h
+                                // (FB_CALL_NONE: none), for the multi-GPU merge (fb_flow_merge_dev)
 };
+
+// determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
+__host__ __device__ inline uint32_t conn_state_of(uint32_t m) {
+    const bool S = m & 1u, H = m & 4u, h = m & 8u, F = m & 16u, f = m & 32u, R = m & 64u, r = m & 128u;
+    if (S && H && F && f) return FB_CONN_SF;
+    if (S && !h && !r) return FB_CONN_S0;
+    if (R || r) return FB_CONN_REJ;
+    if (S && H && !F && !f) return FB_CONN_S1;
+    return FB_CONN_OTHER;
+}
+
+// A table slot as its export record (fb_flow_export, fb_flow_export_merge_dev).
+__device__ __forceinline__ fb_flow_rec flow_rec_of(const FlowSlot& t, uint32_t slot) {
+    fb_flow_rec r;
+    __builtin_memcpy(&r.key, t.key, 40);
+    r.outbound_bytes = t.cnt[0];
+    r.inbound_bytes = t.cnt[1];
+    r.orig_pkts = t.cnt[2];
+    r.resp_pkts = t.cnt[3];
+    r.orig_ip_bytes = t.cnt[4];
+    r.resp_ip_bytes = t.cnt[5];
+    r.first_seen = t.first_seen;
+    r.last_seen = t.last_seen;
+    r.end_seen = t.end_seen;
+    r.hist_len = t.hist_len;
+    r.hist_mask = (uint16_t)(t.hist_state & 0x1FFFu);
+    r.conn_state = (uint8_t)((t.hist_state >> 16) & 0xFu);
+    r.end_mask = (uint8_t)(t.hist_state >> 24);
+    r.slot = slot;
+    r.session_flags = ((t.hist_state >> 20) & 0xFu) | ((t.hist_state >> 15) & 1u) << 4;
+    return r;
+}
+
+// Owner rank of a key in the multi-GPU merge (fb_flow_export_merge_dev): the high word of its
+// fb_flow_hash scaled to [0, world).
+__host__ __device__ inline uint32_t flow_owner(unsigned long long h, uint32_t world) {
+    return (uint32_t)(((h >> 32) * (unsigned long long)world) >> 32);
+}
 // The fused parse's per-record word: the table partition (< kFlowMaxParts) in the low 16 bits,
 // the record's history character in bits 16-23 and FB_META_HAS_FLAGS in bit 24 -- so the history
 // keys kernel reads 4 B per record slot instead of the record.
@@ -345,7 +385,7 @@ hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* p
 // (old_parts << k partitions, zeroed): a key's new partition is k more top bits of its hash, its home
 // slot the same low bits; remap[old slot] = new slot (~0u for empty slots).
 hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k, uint32_t new_shift, FlowSlot* nw,
-                            uint32_t* remap, hipStream_t s);
+                            uint32_t* remap, const uint4* old_cc, uint4* new_cc, hipStream_t s);
 // filter: fb_filter evaluated per flow at export time against `cfg` (is_local_session!,
 // src/sessions.rs:660-672); FB_FILTER_ALL (cfg may be null) exports every flow.
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,
@@ -353,6 +393,19 @@ hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_
                               hipStream_t s, uint32_t filter = FB_FILTER_ALL, const DevConfig* cfg = nullptr);
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
                              unsigned long long* d_n, hipStream_t s);
+
+// Multi-GPU merge (fb_merge.hip).  Export: every flow as an fb_flow_mrec grouped by owner rank
+// (flow_owner), slot order inside each group, positions made global (+ shard_first), rec.slot = rank;
+// d_counts[world] (u64) receives the group sizes.  scratch: merge_export_scratch_bytes(cap, world).
+uint64_t merge_export_scratch_bytes(unsigned long long cap, uint32_t world);
+hipError_t launch_merge_export(const FlowSlot* table, const uint4* char_call, unsigned long long cap, uint32_t world,
+                               uint32_t rank, unsigned long long shard_first, fb_flow_mrec* out,
+                               unsigned long long out_cap, unsigned long long* d_counts, void* scratch, hipStream_t s);
+// Merge: n records of one owner (every rank's group, rank order) -> one record per key in d_out (in
+// the order of each key's first record), *d_n (u64) = keys.  scratch: merge_scratch_bytes(n).
+uint64_t merge_scratch_bytes(unsigned long long n);
+hipError_t launch_merge(const fb_flow_mrec* in, unsigned long long n, fb_flow_rec* out, unsigned long long* d_n,
+                        void* scratch, hipStream_t s);
 
 // Per-flow history characters of the last update (fb_hist.hip): the update's FlowParams (its
 // entries, transposed original rows, combined-group maps, per-slot counts) and the outputs.

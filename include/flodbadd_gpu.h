@@ -221,6 +221,7 @@ enum fb_conn_state {
  * fb_flow_clear (from 0).  Stands for the wall-clock `now` the reference samples per packet
  * (src/packets.rs:209) -- a host maps it to capture timestamps.  FB_SEEN_NONE = None. */
 #define FB_SEEN_NONE 0xFFFFFFFFFFFFFFFFull
+#define FB_CALL_NONE 0xFFFFFFFFu /* fb_flow_mrec.char_call: the character has not occurred */
 
 /* Flow-table export record: canonical key + SessionStats integer counters
  * (src/sessions.rs:76-82; update rules src/packets.rs:111-120, 383-391) + the ordered per-flow
@@ -569,6 +570,39 @@ int fb_flow_slot_remap(fb_ctx* ctx, uint32_t* old_to_new, uint64_t cap, uint64_t
 /* The table's deterministic 64-bit key hash (the reference's DashMap uses SipHash with a random
  * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */
 uint64_t fb_flow_hash(const fb_session_key* key);
+
+/* ---- multi-GPU session table (BASELINE configs[4]) ------------------------------
+ * The reference runs one capture task per interface into ONE shared DashMap (src/capture.rs:946-1016,
+ * src/packets.rs:329-535); W ranks that each parse a contiguous packet-index shard into their own
+ * table merge them into that one table:
+ *   1. every rank exports its table with fb_flow_export_merge_dev: records grouped by owner rank
+ *      (the key's fb_flow_hash high word scaled to [0, world)), d_counts[world] = group sizes;
+ *   2. all-to-all of the groups (RCCL), each owner receiving every rank's group in rank order;
+ *   3. the owner merges them with fb_flow_merge_dev: one fb_flow_rec per key;
+ *   4. all-gather of the owners' merged records.
+ * The result equals the table ONE context builds from the same packets in global order (call k of
+ * every rank = its shard of global batch k; global batch k is the ranks' shards in rank order) --
+ * integer sums, MIN first_seen / end_seen, MAX last_seen, hist_len SUM, hist_mask OR, session flags
+ * (a function of key and configuration) -- and conn_state / end_mask re-decided at the global first
+ * FIN/RST: the ending rank's end_mask OR the S s H h of the other ranks that precede it (their
+ * first occurrence in an earlier call, or in the same call on a lower rank).  Exact for any number
+ * of update calls per rank.  Positions become global: (call << 32) | (shard_first + pkt_index). */
+typedef struct fb_flow_mrec {
+    fb_flow_rec rec;        /* positions global; rec.slot = the exporting rank                    */
+    uint32_t char_call[4];  /* update call of the flow's first S, s, H, h (FB_CALL_NONE: none)     */
+} fb_flow_mrec;             /* 144 bytes */
+/* Every flow of the table, grouped by owner rank (slot order inside a group), into d_out (room for
+ * cap records); d_counts: `world` device u64 group sizes.  1 <= world <= 64, rank < world.
+ * DEVICE pointers, asynchronous. */
+int fb_flow_export_merge_dev(fb_ctx* ctx, uint32_t world, uint32_t rank, uint64_t shard_first, fb_flow_mrec* d_out,
+                             uint64_t cap, uint64_t* d_counts, void* stream);
+/* Merge n records received by one owner (each rank's group, in rank order; a key at most once per
+ * rank) into one fb_flow_rec per key (slot 0), in the order of each key's first record; *d_n
+ * (device u64) = keys.  d_out: room for n records.  DEVICE pointers, asynchronous. */
+int fb_flow_merge_dev(fb_ctx* ctx, const fb_flow_mrec* d_in, uint64_t n, fb_flow_rec* d_out, uint64_t* d_n,
+                      void* stream);
+/* The owner rank fb_flow_export_merge_dev assigns a key to. */
+uint32_t fb_flow_owner(const fb_session_key* key, uint32_t world);
 
 /* ---- host ingest ring (replaces the reader thread -> Vec<u8> -> mpsc(1000) -> processor path,
  *      src/capture.rs:1016, 1082-1142, 1183-1249) ---------------------------------------------

@@ -70,6 +70,12 @@ def lib():
         L.orc_pipeline_mt.argtypes = [P, P, C.c_int, P, U64, P, U32, P, P, P]
         L.orc_key_cmp.restype = C.c_int
         L.orc_key_cmp.argtypes = [P, P]
+        L.orc_flow_hash.restype = U64
+        L.orc_flow_hash.argtypes = [P]
+        L.orc_flows_export_merge.restype = U64
+        L.orc_flows_export_merge.argtypes = [P, U32, U32, U64, P, P]
+        L.orc_flow_merge.restype = U64
+        L.orc_flow_merge.argtypes = [P, U64, P]
         _lib = L
     return _lib
 
@@ -208,6 +214,14 @@ class Flows:
             return None, None
         return self._buf.raw[:n].decode(), (self._cs.value.decode() or None)
 
+    def export_merge(self, world, rank, shard_first):
+        """orc_flows_export_merge: FLOW_MREC_DTYPE records grouped by owner rank, and the group sizes."""
+        n = self.count()
+        out = np.zeros(max(n, 1), dtype=N.FLOW_MREC_DTYPE)
+        counts = np.zeros(world, dtype=np.uint64)
+        m = lib().orc_flows_export_merge(self.h, world, rank, shard_first, out.ctypes.data, counts.ctypes.data)
+        return out[:m], counts
+
     def clear(self):
         lib().orc_flows_clear(self.h)
 
@@ -232,3 +246,11 @@ def pipeline_mt(cfg, frames, offsets, threads, tables=None):
     lib().orc_pipeline_mt(C.byref(cfg), hs, threads, frames.ctypes.data, frames.nbytes, offsets.ctypes.data, n,
                           out.ctypes.data, dns.ctypes.data, st.ctypes.data)
     return tables, st
+
+
+def flow_merge(mrecs):
+    """orc_flow_merge: one owner's received FLOW_MREC_DTYPE records -> merged FLOW_REC_DTYPE records."""
+    mrecs = np.ascontiguousarray(mrecs, dtype=N.FLOW_MREC_DTYPE)
+    out = np.zeros(max(len(mrecs), 1), dtype=FLOW_REC_DTYPE)
+    k = lib().orc_flow_merge(mrecs.ctypes.data if len(mrecs) else None, len(mrecs), out.ctypes.data)
+    return out[:k]

@@ -365,6 +365,7 @@ typedef struct orc_flow {
     char conn_state[4];
     int ended; /* end_time.is_some() */
     int used;
+    uint32_t char_call[4]; /* update call of the first S, s, H, h (FB_CALL_NONE: none), for the merge */
 } orc_flow;
 
 struct orc_flows {
@@ -463,6 +464,7 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
             /* is_local_src/dst, is_self_src/dst of the key (src/packets.rs:429-435) and dst_service
                (src/packets.rs:441-466), stored once at insert */
             s->rec.session_flags = ((uint32_t)r->meta >> 3) & 0x1Fu;
+            for (int b = 0; b < 4; ++b) s->char_call[b] = FB_CALL_NONE;
             f->count++;
             if (st) st->new_sessions++;
         } else if (st) {
@@ -486,6 +488,7 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
             s->rec.hist_len = (uint32_t)s->hist_len;
             const uint32_t b = hist_bit((char)r->hist_char);
             if (b < 16u) s->rec.hist_mask |= (uint16_t)(1u << b);
+            if (b < 4u && s->char_call[b] == FB_CALL_NONE) s->char_call[b] = f->batch;
             if ((r->tcp_flags & (TCP_FIN | TCP_RST)) && !s->ended) {
                 s->ended = 1; /* end_time = now, src/packets.rs:192-197, 422-426 */
                 s->rec.end_seen = pos;
@@ -545,6 +548,155 @@ int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* b
         }
     }
     return (int64_t)s->hist_len;
+}
+
+/* ---- multi-GPU session-table merge (restated for the tests; flodbadd_amd/csrc/fb_merge.hip is
+ * the product).  W ranks each hold a table of their contiguous packet-index shards, update call k
+ * of every rank being its shard of global batch k (global order: batch, then rank, then packet).
+ * The merged table must equal ONE table fed the packets in global order (src/packets.rs:329-535):
+ * counters sum, start = earliest, last_activity = latest, history = the ranks' strings interleaved
+ * in global order -- so its length sums and its character set is the union -- and end_time /
+ * conn_state are decided at the globally first FIN/RST packet over the characters present then.
+ * ------------------------------------------------------------------------------------------- */
+
+/* The library's key hash (fb_flow_hash, flodbadd_amd/csrc/fb_internal.h flow_hash_words): the merge
+ * assigns each key to the owner rank ((hash >> 32) * world) >> 32. */
+uint64_t orc_flow_hash(const fb_session_key* key) {
+    uint32_t k[10];
+    memcpy(k, key, 40);
+    k[9] &= 0xFFFFu;
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int j = 0; j < 10; j += 2) {
+        h ^= (uint64_t)k[j] | ((uint64_t)k[j + 1] << 32);
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    return h;
+}
+
+static uint32_t owner_of(const fb_session_key* k, uint32_t world) {
+    return (uint32_t)(((orc_flow_hash(k) >> 32) * (uint64_t)world) >> 32);
+}
+
+static uint64_t globalize(uint64_t pos, uint64_t shard_first) {
+    return (pos & 0xFFFFFFFF00000000ull) | ((pos & 0xFFFFFFFFull) + shard_first);
+}
+
+uint64_t orc_flows_export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
+                                fb_flow_mrec* out, uint64_t* counts) {
+    /* the table in Ord order, then stably grouped by owner */
+    const uint64_t n = f->count;
+    fb_flow_rec* recs = (fb_flow_rec*)malloc((n ? n : 1) * sizeof(fb_flow_rec));
+    uint32_t(*calls)[4] = (uint32_t(*)[4])malloc((n ? n : 1) * sizeof(uint32_t[4]));
+    uint64_t m = orc_flows_export_sorted(f, recs, n);
+    for (uint64_t i = 0; i < m; ++i) {
+        orc_flow* s = find_slot(f->slots, f->cap, &recs[i].key);
+        memcpy(calls[i], s->char_call, sizeof(calls[i]));
+    }
+    uint64_t w = 0;
+    for (uint32_t o = 0; o < world; ++o) {
+        counts[o] = 0;
+        for (uint64_t i = 0; i < m; ++i) {
+            if (owner_of(&recs[i].key, world) != o) continue;
+            fb_flow_mrec* x = &out[w++];
+            x->rec = recs[i];
+            x->rec.first_seen = globalize(x->rec.first_seen, shard_first);
+            x->rec.last_seen = globalize(x->rec.last_seen, shard_first);
+            if (x->rec.end_seen != FB_SEEN_NONE) x->rec.end_seen = globalize(x->rec.end_seen, shard_first);
+            x->rec.slot = rank;
+            memcpy(x->char_call, calls[i], sizeof(x->char_call));
+            counts[o]++;
+        }
+    }
+    free(recs);
+    free(calls);
+    return w;
+}
+
+typedef struct { const fb_flow_mrec* r; uint64_t idx; } mref;
+static int mref_cmp(const void* x, const void* y) {
+    const mref *a = (const mref*)x, *b = (const mref*)y;
+    int c = orc_key_cmp(&a->r->rec.key, &b->r->rec.key);
+    if (c) return c;
+    return a->idx < b->idx ? -1 : (a->idx > b->idx);
+}
+static int idx_cmp(const void* x, const void* y) {
+    const uint64_t a = *(const uint64_t*)x, b = *(const uint64_t*)y;
+    return a < b ? -1 : (a > b);
+}
+
+uint64_t orc_flow_merge(const fb_flow_mrec* in, uint64_t n, fb_flow_rec* out) {
+    mref* v = (mref*)malloc((n ? n : 1) * sizeof(mref));
+    for (uint64_t i = 0; i < n; ++i) { v[i].r = &in[i]; v[i].idx = i; }
+    qsort(v, n, sizeof(mref), mref_cmp);
+    /* one merged record per run of equal keys, kept with the run's first input index */
+    typedef struct { uint64_t first; fb_flow_rec rec; } merged;
+    merged* mg = (merged*)malloc((n ? n : 1) * sizeof(merged));
+    uint64_t nk = 0;
+    for (uint64_t a = 0; a < n;) {
+        uint64_t b = a + 1;
+        while (b < n && orc_key_cmp(&v[a].r->rec.key, &v[b].r->rec.key) == 0) ++b;
+        fb_flow_rec o = v[a].r->rec;
+        uint64_t end = FB_SEEN_NONE;
+        uint32_t r0 = 0;
+        for (uint64_t i = a; i < b; ++i) { /* the globally first FIN/RST and its rank */
+            const fb_flow_rec* x = &v[i].r->rec;
+            if (x->end_seen < end) { end = x->end_seen; r0 = x->slot; }
+        }
+        o.outbound_bytes = o.inbound_bytes = o.orig_pkts = o.resp_pkts = o.orig_ip_bytes = o.resp_ip_bytes = 0;
+        o.first_seen = FB_SEEN_NONE;
+        o.last_seen = 0;
+        o.hist_len = 0;
+        o.hist_mask = 0;
+        uint32_t present = 0; /* FB_HIST_CHARS bits present at the end packet */
+        for (uint64_t i = a; i < b; ++i) {
+            const fb_flow_mrec* x = v[i].r;
+            o.outbound_bytes += x->rec.outbound_bytes;
+            o.inbound_bytes += x->rec.inbound_bytes;
+            o.orig_pkts += x->rec.orig_pkts;
+            o.resp_pkts += x->rec.resp_pkts;
+            o.orig_ip_bytes += x->rec.orig_ip_bytes;
+            o.resp_ip_bytes += x->rec.resp_ip_bytes;
+            if (x->rec.first_seen < o.first_seen) o.first_seen = x->rec.first_seen;
+            if (x->rec.last_seen > o.last_seen) o.last_seen = x->rec.last_seen;
+            o.hist_len += x->rec.hist_len;
+            o.hist_mask |= x->rec.hist_mask;
+            if (end == FB_SEEN_NONE) continue;
+            if (x->rec.end_seen == end) { /* the ending rank: its characters at the end packet */
+                present |= x->rec.end_mask;
+            } else { /* another rank's S s H h that came before the end packet in global order */
+                const uint32_t call_e = (uint32_t)(end >> 32);
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t c = x->char_call[k];
+                    if (c != FB_CALL_NONE && (c < call_e || (c == call_e && x->rec.slot < r0))) present |= 1u << k;
+                }
+            }
+        }
+        o.end_seen = end;
+        o.end_mask = 0;
+        o.conn_state = FB_CONN_NONE;
+        if (end != FB_SEEN_NONE) { /* determine_conn_state over a string holding those characters */
+            char chars[16], cs[4];
+            int nc = 0;
+            for (int k = 0; k < 8; ++k)
+                if (present & (1u << k)) chars[nc++] = FB_HIST_CHARS[k];
+            o.conn_state = conn_state_of(chars, (uint64_t)nc, cs);
+            o.end_mask = (uint8_t)present;
+        }
+        o.slot = 0;
+        mg[nk].first = v[a].idx;
+        mg[nk].rec = o;
+        ++nk;
+        a = b;
+    }
+    qsort(mg, nk, sizeof(merged), idx_cmp); /* (first is the leading u64 of each entry) */
+    for (uint64_t i = 0; i < nk; ++i) out[i] = mg[i].rec;
+    free(mg);
+    free(v);
+    return nk;
 }
 
 uint64_t orc_pipeline(const orc_cfg* c, orc_flows* fl, const uint8_t* frames, uint64_t fb,

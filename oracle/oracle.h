@@ -96,6 +96,17 @@ uint64_t orc_flows_export_sorted(const orc_flows* f, fb_flow_rec* out, uint64_t 
 int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* buf,
                           uint64_t cap, char* conn_state, uint64_t cs_cap);
 
+/* Multi-GPU merge restated (fb_flow_export_merge_dev / fb_flow_merge_dev semantics, include/
+ * flodbadd_gpu.h): the table's flows grouped by owner rank (Ord order inside a group), positions
+ * global, rec.slot = rank; counts[world] = group sizes.  Returns the records written (the table's
+ * flow count; `out` must hold it). */
+uint64_t orc_flow_hash(const fb_session_key* key);
+uint64_t orc_flows_export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
+                                fb_flow_mrec* out, uint64_t* counts);
+/* One owner's received records (rank order) -> one record per key, in the order of each key's first
+ * record.  Returns the keys written (`out` must hold n). */
+uint64_t orc_flow_merge(const fb_flow_mrec* in, uint64_t n, fb_flow_rec* out);
+
 /* Bench helper: parse+classify+upsert with a scratch record buffer; returns packets done. */
 /* ---- new-session enrichment (ASN src/asn_db.rs:82-166, blacklists src/blacklists.rs:205-260) ---- */
 uint32_t orc_asn_prepare(fb_asn_range* recs, uint32_t n, uint32_t family);

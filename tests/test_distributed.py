@@ -1,20 +1,26 @@
-"""N>1 path on the CPU (gloo, world size 2): packet-index sharding and the global per-flow
-counter merge of flodbadd_amd.distributed (the C5 exchange).  The per-rank flow tables come
-from the CPU oracle, standing in for each rank's GPU table (no GPU here); the code under test is
-the shard arithmetic and the all-gather / dense-id / all-reduce merge, checked against the
-single-process table of the whole batch."""
+"""N>1 path on the CPU (gloo, world sizes 1-3): packet-index sharding and the global session table
+of flodbadd_amd.distributed (BASELINE configs[4]): owner-grouped export, all_to_all, owner merge,
+all_gather.  The per-rank tables come from the CPU oracle (standing in for each rank's GPU table:
+no GPU here), and so does the per-owner merge (orc_flows_export_merge / orc_flow_merge restate
+fb_flow_export_merge_dev / fb_flow_merge_dev; tests/test_gpu_c5.py checks the device kernels
+against them).  The code under test is the exchange plumbing and the merge rules, checked against
+ONE table fed the same packets in global order -- over several update calls per rank, so flows
+start, carry history and end in different calls and on different ranks."""
 import os
 import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from flodbadd_amd import _native as N
-from flodbadd_amd.distributed import global_flow_table, shard_range, sort_keys, _key_words
+from flodbadd_amd.distributed import MREC_WORDS, _key_words, exchange_merge, shard_range, sort_by_ord, sort_keys
 
-TOTAL = 30000
+TOTAL = 9000   # frames per global batch
+CALLS = 3      # update calls (global batches) per rank
+POOL = 400     # flows: each is seen in every call, on every rank, with SYN / FIN / RST here and there
 
 
 def _free_port():
@@ -25,31 +31,60 @@ def _free_port():
     return p
 
 
-def _rank_flows(rank, world):
+def _batch(k, first, count):
     from flodbadd_amd import synth
+    return synth.generate(4, count, first=k * TOTAL + first, n_flows=POOL)
+
+
+def _rank_table(rank, world):
+    """Rank `rank`'s table after CALLS update calls on its shard of each global batch."""
     from oracle import coracle
     first, count = shard_range(TOTAL, rank, world)
-    frames, offs = synth.generate(4, count, first=first)
-    out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
     fl = coracle.Flows()
-    fl.update(out)
-    return fl.export_sorted(), first
+    for k in range(CALLS):
+        frames, offs = _batch(k, first, count)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
+        fl.update(out)
+    return fl, first
+
+
+def single_table():
+    """ONE table fed the global batches in order (pkt_index = the packet's index in its batch)."""
+    from oracle import coracle
+    fl = coracle.Flows()
+    for k in range(CALLS):
+        frames, offs = _batch(k, 0, TOTAL)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
+        fl.update(out)
+    return fl.export_sorted()
+
+
+def _oracle_merge(rows):
+    from oracle import coracle
+    m = np.ascontiguousarray(rows.numpy()).view(N.FLOW_MREC_DTYPE).reshape(-1)
+    merged = coracle.flow_merge(m)
+    return torch.from_numpy(np.ascontiguousarray(merged).view(np.int64).reshape(len(merged), 16).copy())
 
 
 def _worker(rank, world, port, outdir, empty_rank=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        flows, first = _rank_flows(rank, world)
+        fl, first = _rank_table(rank, world)
         if rank == empty_rank:
-            flows = flows[:0]
-        if rank == 1:  # the device-tensor input form (fb_flow_export_dev records), on the CPU here
-            import torch
-            flows = torch.from_numpy(flows.view(np.uint8).reshape(len(flows), N.FLOW_REC_DTYPE.itemsize).copy())
-        merged = global_flow_table(dist, flows, shard_first=first)
-        np.save(os.path.join(outdir, "r%d.npy" % rank), merged.view(np.uint8))
+            fl.clear()
+        mrecs, counts = fl.export_merge(world, rank, first)
+        rows = torch.from_numpy(np.ascontiguousarray(mrecs).view(np.int64).reshape(len(mrecs), MREC_WORDS).copy())
+        table = exchange_merge(dist, rows, counts.tolist(), _oracle_merge)
+        np.save(os.path.join(outdir, "r%d.npy" % rank), table.numpy().view(np.uint8))
     finally:
         dist.destroy_process_group()
+
+
+def _rows(a):
+    a = sort_by_ord(a.copy())
+    a["slot"] = 0
+    return a
 
 
 def test_shard_range_covers_batch():
@@ -60,23 +95,37 @@ def test_shard_range_covers_batch():
 
 
 def test_sort_keys_is_derived_ord():
-    from oracle import coracle
-    flows = _rank_flows(0, 1)[0]
+    flows = single_table()
     rng = np.random.default_rng(1)
     shuffled = flows[rng.permutation(len(flows))]
     assert shuffled[sort_keys(_key_words(shuffled))].tobytes() == flows.tobytes()  # oracle sorts by Ord
 
 
+def test_fixture_exercises_the_ordered_merge():
+    """The stream must make the merge's hard cases happen: flows ended in a later call than their
+    first packet, and on a rank other than their first."""
+    ref = single_table()
+    ended = ref[ref["end_seen"] != N.FB_SEEN_NONE]
+    assert len(ended) > POOL // 2
+    assert ((ended["end_seen"] >> 32) > (ended["first_seen"] >> 32)).any()
+    assert len(np.unique(ended["conn_state"])) >= 3
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_gloo_global_flow_table(tmp_path, world):
-    """world 1 (no key met twice), 2 and 3 (uneven shards, three Ord ranges): every rank ends
-    with the single-process table of the whole batch, byte for byte."""
+    """Every rank ends with the single table of the whole stream (3 update calls), byte for byte:
+    counters, positions, history length / set, and end_seen / end_mask / conn_state re-decided at
+    the globally first FIN/RST."""
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
-    ref = _rank_flows(0, 1)[0]  # whole batch, one process: counters and ordered state
+    ref = single_table()
     for r in range(world):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
-        assert got.tobytes() == ref.tobytes(), r
+        assert len(got) == len(ref), (len(got), len(ref))
+        g, e = _rows(got), _rows(ref)
+        bad = np.flatnonzero(g.view(np.uint8).reshape(len(g), 128).any(axis=1) &
+                             (g.view(np.uint8).reshape(len(g), 128) != e.view(np.uint8).reshape(len(e), 128)).any(axis=1))
+        assert g.tobytes() == e.tobytes(), (r, bad[:5], g[bad[:2]], e[bad[:2]])
 
 
 @pytest.mark.timeout(300)
@@ -85,9 +134,20 @@ def test_gloo_merge_with_an_empty_rank(tmp_path):
     table with global positions."""
     world = 2
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), 1), nprocs=world, start_method="spawn")
-    only, _ = _rank_flows(0, world)
+    from oracle import coracle
+    only, first = _rank_table(0, world)
+    m, _ = only.export_merge(1, 0, first)
+    exp = coracle.flow_merge(m)  # world 1: every key once
     for r in range(world):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
-        exp = only.copy()
-        exp["slot"] = 0
-        assert got.tobytes() == exp.tobytes(), r
+        assert _rows(got).tobytes() == _rows(exp).tobytes(), r
+
+
+def test_oracle_merge_of_one_rank_is_its_table():
+    """World 1: the merge returns every flow once, unchanged (positions +0, conn_state as decided)."""
+    from oracle import coracle
+    fl, _ = _rank_table(0, 1)
+    m, counts = fl.export_merge(1, 0, 0)
+    assert int(counts[0]) == len(m) == fl.count()
+    merged = coracle.flow_merge(m)
+    assert _rows(merged).tobytes() == _rows(fl.export_sorted()).tobytes()

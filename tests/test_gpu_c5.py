@@ -1,18 +1,154 @@
-"""C5 exchange on the GPU: global_flow_table with device tensors over RCCL (the "nccl" backend),
-world size 1 on the one-GPU box -- the union, Ord sort and dense ids run as torch ops on the
-device and the all-gather / all-reduce go through RCCL.  The merged table must equal the GPU
-session table of the same batch sorted by Session's derived Ord (the oracle's order).  World
-size 2 runs in tests/test_distributed.py (gloo, CPU)."""
+"""The global session table on the GPU (BASELINE configs[4]).
+
+* The library's export and merge kernels (fb_flow_export_merge_dev, fb_flow_merge_dev,
+  flodbadd_amd/csrc/fb_merge.hip) with W "ranks" as W contexts in one process: each context runs
+  its packet-index shards of several global batches (one update call per batch), exports its table
+  grouped by owner, each owner's groups are concatenated in rank order and merged on the device.
+  The union equals ONE table fed the same packets in global order (the oracle's), byte for byte --
+  including end_seen / end_mask / conn_state decided at the globally first FIN/RST -- and every
+  exported group equals the oracle's restatement (orc_flows_export_merge).
+* global_flow_table over RCCL (the "nccl" backend) at world size 1 on the one-GPU box: the export
+  lands in a device tensor, the merge runs on it, nothing goes through the host.  World sizes 2-3
+  of the exchange itself run in tests/test_distributed.py (gloo, CPU)."""
 import os
 import socket
 
 import numpy as np
 import pytest
 
+from flodbadd_amd import _native as N
 from flodbadd_amd import synth
+from flodbadd_amd.distributed import shard_range, sort_by_ord
 from oracle import coracle
 
 pytestmark = pytest.mark.gpu
+
+TOTAL, CALLS, POOL = 60000, 3, 3000
+
+
+def _batch(k, first, count, pool=POOL):
+    return synth.generate(4, count, first=k * TOTAL + first, n_flows=pool)
+
+
+def _rows(a):
+    a = sort_by_ord(np.ascontiguousarray(a).copy())
+    a["slot"] = 0
+    return a
+
+
+def _single(pool=POOL):
+    fl = coracle.Flows()
+    for k in range(CALLS):
+        fr, of = _batch(k, 0, TOTAL, pool)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+        fl.update(out)
+    return fl.export_sorted()
+
+
+def _export(cap, world, rank, first):
+    import ctypes as C
+    lib = N.gpu_lib()
+    n = cap.flow_count()
+    d_out, d_cnt = N.DeviceBuffer(max(n, 1) * N.FLOW_MREC_DTYPE.itemsize), N.DeviceBuffer(8 * world)
+    N.check(lib.fb_flow_export_merge_dev(cap.ctx, world, rank, first, d_out.ptr, n, d_cnt.ptr, None))
+    counts = d_cnt.download(np.zeros(world, dtype=np.uint64))
+    m = d_out.download(np.zeros(max(n, 1), dtype=N.FLOW_MREC_DTYPE))[: int(counts.sum())]
+    d_out.free()
+    d_cnt.free()
+    assert int(counts.sum()) == n
+    return m, counts
+
+
+def _merge_dev(cap, mrecs):
+    lib = N.gpu_lib()
+    m = len(mrecs)
+    d_in = N.DeviceBuffer(max(m, 1) * N.FLOW_MREC_DTYPE.itemsize)
+    if m:
+        d_in.upload(np.ascontiguousarray(mrecs))
+    d_out, d_n = N.DeviceBuffer(max(m, 1) * N.FLOW_REC_DTYPE.itemsize), N.DeviceBuffer(8)
+    N.check(lib.fb_flow_merge_dev(cap.ctx, d_in.ptr, m, d_out.ptr, d_n.ptr, None))
+    k = int(d_n.download(np.zeros(1, dtype=np.uint64))[0])
+    out = d_out.download(np.zeros(max(m, 1), dtype=N.FLOW_REC_DTYPE))[:k]
+    for b in (d_in, d_out, d_n):
+        b.free()
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_device_export_and_merge_equal_one_table(world):
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.sessions import SessionFilter
+    caps = [FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 16) for _ in range(world)]
+    try:
+        groups = []  # per rank: (mrecs, counts)
+        for r, cap in enumerate(caps):
+            first, count = shard_range(TOTAL, r, world)
+            ref = coracle.Flows()
+            for k in range(CALLS):
+                fr, of = _batch(k, first, count)
+                g = cap.process_frames_seg(fr, of) if k % 2 else cap.process_frames(fr, of)
+                out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+                ref.update(out)
+                assert g.stats["error"] == 0
+            m, counts = _export(cap, world, r, first)
+            em, ecounts = ref.export_merge(world, r, first)
+            assert np.array_equal(counts, ecounts)
+            # the same records per owner group (the library's groups are in slot order, the oracle's in Ord)
+            for o in range(world):
+                a = m[int(counts[:o].sum()): int(counts[: o + 1].sum())]
+                b = em[int(ecounts[:o].sum()): int(ecounts[: o + 1].sum())]
+                assert np.all(a["rec"]["slot"] == r)
+                ka = np.ascontiguousarray(a).view(np.uint8).reshape(len(a), 144)
+                kb = np.ascontiguousarray(b).view(np.uint8).reshape(len(b), 144)
+                ka, kb = ka[np.lexsort(ka[:, :40].T[::-1])], kb[np.lexsort(kb[:, :40].T[::-1])]
+                assert ka.tobytes() == kb.tobytes(), (r, o)
+            groups.append((m, counts))
+        merged = []
+        for o in range(world):  # owner o receives every rank's group o, in rank order
+            recv = np.concatenate([m[int(c[:o].sum()): int(c[: o + 1].sum())] for m, c in groups])
+            got = _merge_dev(caps[o], recv)
+            assert _rows(got).tobytes() == _rows(coracle.flow_merge(recv)).tobytes(), o
+            # order: each key where its first received record is
+            firsts = {}
+            for i, x in enumerate(recv):
+                firsts.setdefault(bytes(x["rec"].tobytes()[:40]), i)
+            assert [firsts[bytes(x.tobytes()[:40])] for x in got] == sorted(firsts.values())
+            merged.append(got)
+        table = np.concatenate(merged)
+        ref = _single()
+        assert len(table) == len(ref)
+        assert _rows(table).tobytes() == _rows(ref).tobytes()
+        ended = ref[ref["end_seen"] != N.FB_SEEN_NONE]
+        assert ((ended["end_seen"] >> 32) > (ended["first_seen"] >> 32)).any()  # ends in later calls
+    finally:
+        for c in caps:
+            c.close()
+
+
+def test_merge_of_many_copies_per_key():
+    """Sixteen ranks' records of the same few keys (every key on every rank): sums, min / max and
+    the ending rank over 16 copies, against the oracle's merge."""
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.sessions import SessionFilter
+    world, pool = 16, 64
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 12)
+    try:
+        recv = []
+        for r in range(world):
+            first, count = shard_range(TOTAL, r, world)
+            ref = coracle.Flows()
+            for k in range(2):
+                fr, of = synth.generate(4, count, first=k * TOTAL + first, n_flows=pool)
+                out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+                ref.update(out)
+            m, _ = ref.export_merge(1, r, first)
+            recv.append(m)
+        recv = np.concatenate(recv)
+        got = _merge_dev(cap, recv)
+        exp = coracle.flow_merge(recv)
+        assert len(got) == len(exp) and got.tobytes() == exp.tobytes()  # same order too
+    finally:
+        cap.close()
 
 
 def _free_port():
@@ -24,20 +160,21 @@ def _free_port():
 
 
 def _child(rank, port, out):
-    """The RCCL merge in a fresh process: its own HIP runtime state and communicator, whatever the
-    test process did on the device before."""
+    """The RCCL exchange in a fresh process: its own HIP runtime state and communicator, whatever
+    the test process did on the device before."""
     import torch
     import torch.distributed as dist
     from flodbadd_amd.capture import FlodbaddGpuCapture
     from flodbadd_amd.distributed import global_flow_table
     from flodbadd_amd.sessions import SessionFilter
-    frames, offs = synth.generate(4, 200000, first=7)
     cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 18)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        cap.process_frames(frames, offs)
-        merged = global_flow_table(dist, cap.export_flows(), device=torch.device("cuda", 0))
+        for k in range(CALLS):
+            fr, of = _batch(k, 0, TOTAL, pool=1 << 20)
+            cap.process_frames(fr, of)
+        merged = global_flow_table(dist, cap.ctx, device=torch.device("cuda", 0))
         np.save(out, merged.view(np.uint8))
     finally:
         dist.destroy_process_group()
@@ -46,16 +183,8 @@ def _child(rank, port, out):
 
 def test_rccl_world1_global_flow_table(tmp_path):
     import torch.multiprocessing as mp
-    from flodbadd_amd import _native as N
     out = str(tmp_path / "merged.npy")
     mp.start_processes(_child, args=(_free_port(), out), nprocs=1, start_method="spawn")
     merged = np.load(out).view(N.FLOW_REC_DTYPE)
-    frames, offs = synth.generate(4, 200000, first=7)
-    r_out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
-    ref = coracle.Flows()
-    ref.update(r_out)
-    exp = ref.export_sorted()
-    a, b = merged.copy(), exp.copy()
-    a["slot"] = 0
-    b["slot"] = 0
-    assert len(a) == len(b) and a.tobytes() == b.tobytes()
+    ref = _single(pool=1 << 20)
+    assert len(merged) == len(ref) and _rows(merged).tobytes() == _rows(ref).tobytes()
