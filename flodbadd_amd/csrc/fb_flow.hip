@@ -423,6 +423,7 @@ constexpr uint32_t kK2Cpt = FB_K2_CPT;
 // as rec << 37 | its FB_HIST_CHARS bit << 32 | pkt_index (min) -- so the fold needs no record
 // read-back --, the mask, the history count, the first rec of S s H h
 constexpr uint32_t kScFirst = 0, kScLast = 2, kScEnd = 4, kScMask = 6, kScCount = 7, kScChar = 8;  // kScChar..+3
+constexpr uint32_t kScOrd = 4;  // after the fold: the slot's new ordered fields (2 uint4, 16-B aligned)
 __device__ __forceinline__ unsigned long long* sc64(uint32_t* q, uint32_t w) {
     return reinterpret_cast<unsigned long long*>(q + w);
 }
@@ -731,9 +732,9 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
 // Fold one slot's batch scratch into its ordered fields (after every entry was applied).  o0, o1 =
 // the slot's ordered fields as loaded with the slice (first_seen, last_seen | end_seen, hist_len,
 // hist_state); the first / last / end packets' pkt_index (and the end's character) are in the
-// scratch keys.
-__device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t batch, const uint4 o0, const uint4 o1,
-                                            uint4* cc) {
+// scratch keys.  The new ordered fields (bytes 96..127 of the slot) go to scratch words 4..11 --
+// read before they are written -- so the write-back stores each touched slot as one whole line.
+__device__ __forceinline__ void finish_slot(uint32_t* q, uint32_t batch, const uint4 o0, const uint4 o1, uint4* cc) {
     const unsigned long long first = *sc64(q, kScFirst);
     if (first == ~0ull) return;  // not touched by this batch
     const unsigned long long hi = (unsigned long long)batch << 32;
@@ -772,9 +773,13 @@ __device__ __forceinline__ void finish_slot(FlowSlot* g, uint32_t* q, uint32_t b
         cs = conn_state_of(m) | (cs & 0xF0u) | (m & 0xFFu) << 8;  // + the conn_state characters present at the end
         end_seen = hi | (uint32_t)end;
     }
-    uint4* t = reinterpret_cast<uint4*>(g) + 6;  // bytes 96..127: the ordered fields
-    t[0] = make_uint4((uint32_t)first_seen, (uint32_t)(first_seen >> 32), (uint32_t)last_seen, (uint32_t)(last_seen >> 32));
-    t[1] = make_uint4((uint32_t)end_seen, (uint32_t)(end_seen >> 32), len + q[kScCount], (mask | (flags & 0xFFFFu)) | (cs << 16));
+    const uint4 t0 = make_uint4((uint32_t)first_seen, (uint32_t)(first_seen >> 32), (uint32_t)last_seen,
+                                (uint32_t)(last_seen >> 32));
+    const uint4 t1 = make_uint4((uint32_t)end_seen, (uint32_t)(end_seen >> 32), len + q[kScCount],
+                                (mask | (flags & 0xFFFFu)) | (cs << 16));
+    uint4* t = reinterpret_cast<uint4*>(q + kScOrd);  // bytes 96..127 of the slot
+    t[0] = t0;
+    t[1] = t1;
 }
 static_assert(offsetof(FlowSlot, first_seen) == 96 && offsetof(FlowSlot, hist_state) == 124, "ordered fields at 96..127");
 
@@ -1019,7 +1024,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     if (dense) load_slice();
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
-    uint32_t hbase_out = 0u;
+    uint32_t hbase_out = 0u, hc = 0u;
     if (total != 0ull) {
         if (!dense) load_slice();
         for (uint32_t j = threadIdx.x; j < kFlowSlots * kScrU32; j += kFlowK2Threads) {
@@ -1131,15 +1136,21 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             rbase += tot;
             __syncthreads();
         }
-        finish_slot(T + threadIdx.x, scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1,
+        hc = scr[(size_t)threadIdx.x * kScrU32 + kScCount];  // (before the fold reuses the word)
+        finish_slot(scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1,
                     P.char_call ? P.char_call + (size_t)part * kFlowSlots + threadIdx.x : nullptr);
-        // only the slots this batch touched (inserted or updated) changed; the others' heads are
-        // not written back (a 96-B head alone is a partial line)
+        __syncthreads();  // every slot's new ordered fields are in its scratch
+        // only the slots this batch touched (inserted or updated) changed; each is written back as
+        // one whole 128-B line (head from the slice, ordered fields from the scratch): eight
+        // consecutive lanes per slot, so a wavefront stores eight full lines
         uint4* gw = reinterpret_cast<uint4*>(T);
-        for (uint32_t j = threadIdx.x; j < kFlowSlots * kHead16; j += kFlowK2Threads) {
-            const uint32_t sl = j / kHead16, w = j - sl * kHead16;
-            if (scr[(size_t)sl * kScrU32 + kScFirst + 1u] != ~0u)  // the first key's rec word: touched
-                gw[(size_t)sl * (sizeof(FlowSlot) / 16u) + w] = slice4[j];
+        constexpr uint32_t kSlot16 = sizeof(FlowSlot) / 16u;  // 8
+        for (uint32_t j = threadIdx.x; j < kFlowSlots * kSlot16; j += kFlowK2Threads) {
+            const uint32_t sl = j / kSlot16, w = j - sl * kSlot16;
+            const uint32_t* q = scr + (size_t)sl * kScrU32;
+            if (q[kScFirst + 1u] != ~0u)  // the first key's rec word: touched
+                gw[j] = w < kHead16 ? slice4[(size_t)sl * kHead16 + w]
+                                    : reinterpret_cast<const uint4*>(q + kScOrd)[w - kHead16];
         }
     }
     n_new = block_sum(n_new, sh);
@@ -1149,7 +1160,6 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                                            : g[(size_t)threadIdx.x * 8u].x >= 2u;
     occ = block_sum(occ, sh);
     // history characters per slot this update (the history's output offsets), and their total
-    const uint32_t hc = total != 0ull ? scr[(size_t)threadIdx.x * kScrU32 + kScCount] : 0u;
     P.hcount[(size_t)part * kFlowSlots + threadIdx.x] = hc;
     const unsigned long long hcs = block_sum((unsigned long long)hc, sh);
     if (threadIdx.x == 0) {
