@@ -275,16 +275,24 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams 
     }
 }
 
+constexpr uint32_t kBmWords = kFlowChunk / 32u;  // a chunk's records as a bitmap (640 words)
 struct HistLds {
-    unsigned long long keys[kHistCap];  // (general) batch keys; (uniform) run-sorted keys + wave counts
-    uint32_t cursor[kFlowSlots], bcnt[kFlowSlots], boff[kFlowSlots];
+    uint32_t skey[kHistCap];                 // the batch's keys in entry order: record in chunk << 13 |
+                                             // slot << 4 | code, ~0 for no character
+    uint32_t skey2[kHistCap];                // the same with every run sorted by record
+    uint32_t wcnt[kHistWaves * kFlowSlots];  // the walk: [wave][slot] counts, then output positions
+    uint8_t tag[kHistWaves * kFlowSlots];    // the walk's slot tags
+    uint32_t bm[kBmWords], bmp[kBmWords];    // a long run's records as a bitmap, prefix popcounts
+    uint32_t cursor[kFlowSlots], bcnt[kFlowSlots];
     uint32_t rs[kHistRuns];      // run r (chunk c0 + r): its first entry position
     uint32_t rn[kHistRuns];      // its entries to read (bit 31: a combined group, e_orig)
     uint32_t rp[kHistRuns + 1];  // exclusive prefix of rn
     uint32_t rq[kHistRuns];      // the history word of its first applied entry
+    uint32_t lst[kHistRuns];     // the batch's runs of more than 64 entries (then of 17..64: from the back)
     uint32_t wsum[kHistThreads / 64], wsum2[kHistThreads / 64];
-    uint32_t s_n;
+    uint32_t s_n, s_m;
 };
+static_assert(sizeof(HistLds) <= 80u * 1024u, "two workgroups per CU");
 
 // Listed partitions: `list` = slow (one workgroup each, every chunk) or, with nblk > 1, the split
 // partitions -- a grid-stride loop over (list index, chunk block) pairs; cnt = that list's counts.
@@ -427,129 +435,202 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
             bc[(size_t)blk * kFlowSlots + tid] = L.bcnt[tid];
             return;
         } else {
-            // entry e of the round (runs laid end to end): key slot << 36 | record << 4 | code, or
-            // ~0 for none (no character, outside the record window)
-            auto entry_key = [&](uint32_t e, uint32_t r0, uint32_t r1, uint32_t c0, uint32_t win_lo,
-                                 uint32_t win_hi) {
-                uint32_t lo = r0, hi = r1 - 1u;  // the run holding e: the largest r with rp[r] <= e
+            // Output order per slot = record order.  A batch of whole runs (<= kHistCap entries, runs
+            // in chunk order) is loaded as 32-bit keys (record in chunk << 13 | slot << 4 | code),
+            // each run sorted by record -- K1's scatter leaves a run unordered: runs of <= 16 entries
+            // by their thread in registers, <= 64 by a wavefront (bitonic over the lanes), longer ones
+            // block-wide by a bitmap of the chunk's records (rank = the set bits below) -- so the
+            // batch is in record order; the walk then hands each character its slot's next output
+            // position (per-wave slot counts, a scan per slot, the k_hist_uniform walk).  No
+            // comparison sort of a whole batch: a skewed batch (one slot with most of its keys)
+            // costs what a uniform one does.
+            auto run_of = [&](uint32_t e, uint32_t r0, uint32_t r1) {  // the largest r with rp[r] <= e
+                uint32_t lo = r0, hi = r1 - 1u;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi + 1u) >> 1;
                     if (L.rp[mid] <= e) lo = mid; else hi = mid - 1u;
                 }
-                const uint32_t k = e - L.rp[lo];
+                return lo;
+            };
+            auto key_of = [&](uint32_t e, uint32_t r, uint32_t c0) {  // round entry e of run r
+                const uint32_t k = e - L.rp[r];
                 uint32_t slot = 0u, code, rec;
-                if (!(L.rn[lo] >> 31)) {
-                    const uint32_t w = P.hword[L.rq[lo] + k];
+                if (!(L.rn[r] >> 31)) {
+                    const uint32_t w = P.hword[L.rq[r] + k];
                     slot = w & (kFlowSlots - 1u);
                     code = (w >> 9) & 15u;
-                    rec = (c0 + lo) * kFlowChunk + (w >> 13);
+                    rec = w >> 13;  // (record % kFlowChunk)
                 } else {
-                    const uint32_t w = P.e_orig[L.rs[lo] + k];
+                    const uint32_t w = P.e_orig[L.rs[r] + k];
                     code = (w >> kEntCodeShift) & 15u;
-                    rec = w & kEntRecMask;
-                    if (code != 0u) {
-                        const uint32_t m = P.pos_map[L.rs[lo] + k];
-                        slot = combined_slot(P, m, L.rq[lo], L.rs[lo], code);
-                    }
+                    rec = (w & kEntRecMask) - (c0 + r) * kFlowChunk;
+                    if (code != 0u) slot = combined_slot(P, P.pos_map[L.rs[r] + k], L.rq[r], L.rs[r], code);
                 }
-                if (code == 0u || rec < win_lo || rec >= win_hi) return ~0ull;
-                return ((unsigned long long)slot << 36) | ((unsigned long long)rec << 4) | code;
+                return code != 0u ? rec << 13 | slot << 4 | code : ~0u;
             };
-            auto emit = [&](uint32_t dst, unsigned long long key) {
+            auto emit = [&](uint32_t dst, uint32_t key) {
                 dst += out_beg;
                 if (dst < out_end) {  // (a table-full batch may hold fewer slot counts than characters)
-                    out_slot[dst] = q * kFlowSlots + (uint32_t)(key >> 36);
+                    out_slot[dst] = q * kFlowSlots + ((key >> 4) & (kFlowSlots - 1u));
                     out_char[dst] = hist_char_of(key & 15u);
                 }
             };
-            // the batch's n keys in keys[0 .. n), slot buckets counted (bcnt) and placed (boff):
-            // bitonic sort by (slot, record); a key's place in its slot's run = its index - the
-            // bucket's offset
-            auto sort_emit = [&](uint32_t n) {
-                uint32_t n2 = 1u;
-                while (n2 < n) n2 <<= 1;
-                for (uint32_t i = n + tid; i < n2; i += kHistThreads) L.keys[i] = ~0ull;
+            // block-wide exclusive scan of the bitmap's popcounts (nw <= kBmWords words)
+            auto bitmap_prefix = [&](uint32_t nw) {
+                const uint32_t w0 = 2u * tid, c0w = w0 < nw ? __popc(L.bm[w0]) : 0u,
+                               c1w = w0 + 1u < nw ? __popc(L.bm[w0 + 1u]) : 0u;
+                uint32_t tot;
+                const uint32_t ex = block_scan(c0w + c1w, tot);
+                if (w0 < nw) L.bmp[w0] = ex;
+                if (w0 + 1u < nw) L.bmp[w0 + 1u] = ex + c0w;
                 __syncthreads();
-                for (uint32_t k = 2; k <= n2; k <<= 1) {
-                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                        for (uint32_t i = tid; i < n2 / 2u; i += kHistThreads) {
-                            const uint32_t a = 2u * i - (i & (j - 1u)), b = a + j;
-                            const unsigned long long x = L.keys[a], y = L.keys[b];
-                            if ((x > y) == ((a & k) == 0u)) {
-                                L.keys[a] = y;
-                                L.keys[b] = x;
-                            }
-                        }
-                        __syncthreads();
+                return tot;
+            };
+            auto rank_of = [&](uint32_t rec) {
+                const uint32_t w = rec >> 5;
+                return L.bmp[w] + __popc(L.bm[w] & ((1u << (rec & 31u)) - 1u));
+            };
+            static_assert(2u * kHistThreads >= kBmWords, "two bitmap words per thread");
+            // the walk over skey2[0 .. n): stable per slot, output positions from the slots' cursors
+            auto walk = [&](uint32_t n) {
+                const uint32_t span = ((n + kHistThreads - 1u) / kHistThreads) * 64u;
+                const uint32_t lo_w = min(wave * span, n), hi_w = min(lo_w + span, n);
+                uint32_t* hw = L.wcnt + wave * kFlowSlots;
+                for (uint32_t i = lo_w + lane; i < hi_w; i += 64u) {
+                    const uint32_t k = L.skey2[i];
+                    if (k != ~0u) atomicAdd(hw + ((k >> 4) & (kFlowSlots - 1u)), 1u);
+                }
+                __syncthreads();
+                {   // slot tid: each wave's first position = the cursor + the earlier waves' counts
+                    uint32_t run = L.cursor[tid];
+#pragma unroll
+                    for (uint32_t w = 0; w < kHistWaves; ++w) {
+                        const uint32_t x = L.wcnt[w * kFlowSlots + tid];
+                        L.wcnt[w * kFlowSlots + tid] = run;
+                        run += x;
                     }
+                    L.cursor[tid] = run;
+                }
+                __syncthreads();
+                uint8_t* tg = L.tag + wave * kFlowSlots;
+                const unsigned long long below = (1ull << lane) - 1ull;
+                for (uint32_t b0 = lo_w; b0 < hi_w; b0 += 64u) {  // wave-uniform
+                    const uint32_t i = b0 + lane;
+                    const uint32_t k = i < hi_w ? L.skey2[i] : ~0u;
+                    const bool tcp = k != ~0u;
+                    const uint32_t sl = (k >> 4) & (kFlowSlots - 1u);
+                    if (tcp) tg[sl] = (uint8_t)lane;
+                    __builtin_amdgcn_wave_barrier();
+                    unsigned long long pending = __ballot(tcp && tg[sl] != lane), m = 1ull << lane;
+                    while (pending) {  // the few slots several lanes hold: one ballot each
+                        const uint32_t l = (uint32_t)__builtin_ctzll(pending);
+                        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)l);
+                        const unsigned long long pm = __ballot(tcp && sl == o);
+                        if (tcp && sl == o) m = pm;
+                        pending &= ~pm;
+                    }
+                    if (tcp) emit(hw[sl] + (uint32_t)__popcll(m & below), k);
+                    __builtin_amdgcn_wave_barrier();
+                    if (tcp && (m & below) == 0ull) hw[sl] += (uint32_t)__popcll(m);
+                    __builtin_amdgcn_wave_barrier();
+                }
+                __syncthreads();
+                for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) L.wcnt[j] = 0u;
+                // (the next writer of wcnt is past a barrier)
+            };
+            for (uint32_t j = tid; j < kHistWaves * kFlowSlots; j += kHistThreads) L.wcnt[j] = 0u;
+            // entries [e0, e1) (<= kHistCap) of runs r0 .. r1 - 1
+            auto batch = [&](uint32_t r0, uint32_t r1, uint32_t e0, uint32_t e1, uint32_t c0) {
+                const uint32_t n = e1 - e0;
+                if (tid == 0) {
+                    L.s_n = 0u;
+                    L.s_m = 0u;
                 }
                 for (uint32_t i = tid; i < n; i += kHistThreads) {
-                    const unsigned long long key = L.keys[i];
-                    const uint32_t sl = (uint32_t)(key >> 36);
-                    emit(L.cursor[sl] + (i - L.boff[sl]), key);
+                    const uint32_t e = e0 + i;
+                    L.skey[i] = key_of(e, run_of(e, r0, r1), c0);
                 }
-            };
-            auto batch_end = [&]() {
                 __syncthreads();
-                L.cursor[tid] += L.bcnt[tid];
-                L.bcnt[tid] = 0u;
-                __syncthreads();
-            };
-            // entries [e0, e1) (<= kHistCap) of runs r0 .. r1 - 1: keys in registers, bucketed by
-            // slot; a key's place by a scan of its bucket, or a sort of the batch
-            auto batch = [&](uint32_t r0, uint32_t r1, uint32_t e0, uint32_t e1, uint32_t c0) {
-                unsigned long long kk[kHistPer];
-                uint32_t sub[kHistPer];
+                {   // runs of <= kRunSort entries: their thread, in registers; the others listed
+                    const uint32_t r = r0 + tid;
+                    const uint32_t b = r < r1 ? L.rp[r] - e0 : 0u, len = r < r1 ? L.rp[r + 1u] - L.rp[r] : 0u;
+                    if (len > 64u) L.lst[atomicAdd(&L.s_n, 1u)] = r;
+                    else if (len > kRunSort) L.lst[kHistRuns - 1u - atomicAdd(&L.s_m, 1u)] = r;
+                    uint32_t a[kRunSort];
 #pragma unroll
-                for (uint32_t u = 0; u < kHistPer; ++u) {
-                    const uint32_t e = e0 + tid + u * kHistThreads;
-                    kk[u] = e < e1 ? entry_key(e, r0, r1, c0, 0u, ~0u) : ~0ull;
+                    for (uint32_t k = 0; k < kRunSort; ++k) a[k] = (len <= kRunSort && k < len) ? L.skey[b + k] : ~0u;
+                    uint32_t wl = len <= kRunSort ? len : 0u;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+                    if (wl > 8u) sort_net<16>(a);
+                    else if (wl > 4u) sort_net<8>(a);
+                    else if (wl > 1u) sort_net<4>(a);
+#pragma unroll
+                    for (uint32_t k = 0; k < kRunSort; ++k)
+                        if (len <= kRunSort && k < len) L.skey2[b + k] = a[k];
                 }
-#pragma unroll
-                for (uint32_t u = 0; u < kHistPer; ++u)
-                    if (kk[u] != ~0ull) sub[u] = atomicAdd(&L.bcnt[(uint32_t)(kk[u] >> 36)], 1u);
                 __syncthreads();
-                const uint32_t c = L.bcnt[tid];
-                uint32_t n;
-                L.boff[tid] = block_scan(c, n);
-                const bool heavy = __syncthreads_or(c > kHistScan);
-                if (n == 0u) return;  // uniform (bcnt all zero)
+                // runs of 17..64 entries: a wavefront each, bitonic over the lanes
+                for (uint32_t j = wave; j < L.s_m; j += kHistWaves) {
+                    const uint32_t r = L.lst[kHistRuns - 1u - j];
+                    const uint32_t b = L.rp[r] - e0, len = L.rp[r + 1u] - L.rp[r];
+                    uint32_t x = lane < len ? L.skey[b + lane] : ~0u;
 #pragma unroll
-                for (uint32_t u = 0; u < kHistPer; ++u)
-                    if (kk[u] != ~0ull) L.keys[L.boff[(uint32_t)(kk[u] >> 36)] + sub[u]] = kk[u];
-                __syncthreads();
-                if (heavy) {
-                    sort_emit(n);
-                } else {
+                    for (uint32_t k = 2; k <= 64u; k <<= 1) {
 #pragma unroll
-                    for (uint32_t u = 0; u < kHistPer; ++u) {
-                        if (kk[u] == ~0ull) continue;
-                        const uint32_t sl = (uint32_t)(kk[u] >> 36), b0 = L.boff[sl], bc = L.bcnt[sl];
-                        uint32_t rank = 0u;
-                        for (uint32_t j = 0; j < bc; ++j) rank += L.keys[b0 + j] < kk[u];
-                        emit(L.cursor[sl] + rank, kk[u]);
+                        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                            const uint32_t o = (uint32_t)__shfl_xor((int)x, (int)jj, 64);
+                            const bool up = (lane & k) == 0u, lower = (lane & jj) == 0u;
+                            x = (lower == up) ? min(x, o) : max(x, o);
+                        }
                     }
+                    if (lane < len) L.skey2[b + lane] = x;
                 }
-                batch_end();
+                // longer runs: block-wide, one at a time, ranked by the bitmap of the chunk's records
+                const uint32_t nl = L.s_n;
+                for (uint32_t j = 0; j < nl; ++j) {  // uniform
+                    const uint32_t r = L.lst[j];
+                    const uint32_t b = L.rp[r] - e0, len = L.rp[r + 1u] - L.rp[r];
+                    for (uint32_t w = tid; w < kBmWords; w += kHistThreads) L.bm[w] = 0u;
+                    for (uint32_t i = tid; i < len; i += kHistThreads) L.skey2[b + i] = ~0u;
+                    __syncthreads();
+                    for (uint32_t i = tid; i < len; i += kHistThreads) {
+                        const uint32_t k = L.skey[b + i];
+                        if (k != ~0u) atomicOr(&L.bm[k >> 18], 1u << ((k >> 13) & 31u));
+                    }
+                    __syncthreads();
+                    bitmap_prefix(kBmWords);
+                    for (uint32_t i = tid; i < len; i += kHistThreads) {
+                        const uint32_t k = L.skey[b + i];
+                        if (k != ~0u) L.skey2[b + rank_of(k >> 13)] = k;
+                    }
+                    __syncthreads();
+                }
+                __syncthreads();
+                walk(n);
             };
-            // one run longer than kHistCap, in record windows of kHistCap (each holds at most
-            // kHistCap of its entries): keys appended in LDS, then sorted
+            // one run longer than kHistCap: record windows of kHistCap (each holds at most kHistCap of
+            // its entries), each gathered in record order through the window's bitmap, then walked
             auto long_run = [&](uint32_t r, uint32_t c0) {
-                const uint32_t cb = (c0 + r) * kFlowChunk;
+                const uint32_t e_lo = L.rp[r], len = L.rp[r + 1u] - e_lo;
+                constexpr uint32_t kWinWords = kHistCap / 32u;
                 for (uint32_t w0 = 0; w0 < kFlowChunk; w0 += kHistCap) {
-                    if (tid == 0) L.s_n = 0u;
+                    for (uint32_t w = tid; w < kWinWords; w += kHistThreads) L.bm[w] = 0u;
                     __syncthreads();
-                    for (uint32_t e = L.rp[r] + tid; e < L.rp[r + 1u]; e += kHistThreads) {
-                        const unsigned long long key = entry_key(e, r, r + 1u, c0, cb + w0, cb + w0 + kHistCap);
-                        if (key == ~0ull) continue;
-                        L.keys[atomicAdd(&L.s_n, 1u)] = key;
-                        atomicAdd(&L.bcnt[(uint32_t)(key >> 36)], 1u);
+                    for (uint32_t i = tid; i < len; i += kHistThreads) {
+                        const uint32_t k = key_of(e_lo + i, r, c0), rec = k >> 13;
+                        if (k != ~0u && rec >= w0 && rec < w0 + kHistCap)
+                            atomicOr(&L.bm[(rec - w0) >> 5], 1u << ((rec - w0) & 31u));
                     }
                     __syncthreads();
-                    uint32_t n;
-                    L.boff[tid] = block_scan(L.bcnt[tid], n);
-                    if (n != 0u) sort_emit(n);  // uniform
-                    batch_end();
+                    const uint32_t n = bitmap_prefix(kWinWords);
+                    if (n == 0u) continue;  // uniform
+                    for (uint32_t i = tid; i < len; i += kHistThreads) {
+                        const uint32_t k = key_of(e_lo + i, r, c0), rec = k >> 13;
+                        if (k != ~0u && rec >= w0 && rec < w0 + kHistCap) L.skey2[rank_of(rec - w0)] = k;
+                    }
+                    __syncthreads();
+                    walk(n);
                 }
             };
             for (uint32_t c0 = cb0; c0 < cb1; c0 += kHistRuns) {
