@@ -570,15 +570,16 @@ def cpu_baseline_c4(frames, offs, seconds):
 
 def load_traffic(config_id, bpl=1):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
-    (tools/prof_summary.py), scaled to `bpl` batches per launch."""
+    (tools/prof_summary.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH x2 for gfx950), scaled to
+    `bpl` batches per launch, and the tag of the profiled run it comes from."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f).get(str(config_id), {})
         b = d.get("hbm_bytes_per_launch")
-        return None if b is None else b / d.get("batches_per_launch", 1) * bpl
+        return (None if b is None else b / d.get("batches_per_launch", 1) * bpl), d.get("tag")
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def c4_split(N, lib, ctx, main_r, n, steps, warmup, rank, world, dist, mode, pipe, synth_kw=None, records=True):
@@ -885,6 +886,7 @@ def main():
     else:
         output_desc = ("batch-wide compaction (fb_process_dev)" if args.config == 4 else
                        "batch-wide compaction (fb_parse_classify_dev)")
+    traffic, traffic_tag = load_traffic(args.config, args.steps / main_r["launches"])
     if rank == 0:
         line = {
             "metric": "Mpackets/s device-resident header parse + 5-tuple classify, 64B & IMIX frames",
@@ -904,7 +906,7 @@ def main():
                        "output": output_desc,
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, args.steps / main_r["launches"]),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_pmc_run": traffic_tag,
                          "algo_bytes_per_launch": int(algo_per_launch),
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 5),
                          "launches": main_r["launches"],
