@@ -308,6 +308,44 @@ __device__ __forceinline__ uint32_t combined_slot(const FlowParams& P, uint32_t 
     return v & (kFlowSlots - 1u);
 }
 
+// One run of 17 .. 64 K keys sorted by a wavefront: key i in register i / 64 of lane i % 64,
+// bitonic network (partners 64 or more apart in the lane's registers, closer ones by shuffles),
+// ~0 padding sorts last; src -> dst (LDS).
+constexpr uint32_t kWaveSortMax = 512;  // longer runs: the block's bitmap rank
+template <uint32_t K>
+__device__ __forceinline__ void wave_sort_run(const uint32_t* src, uint32_t* dst, uint32_t len, uint32_t lane) {
+    uint32_t x[K];
+#pragma unroll
+    for (uint32_t j = 0; j < K; ++j) x[j] = j * 64u + lane < len ? src[j * 64u + lane] : ~0u;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64u * K; k <<= 1) {
+#pragma unroll
+        for (uint32_t d = k >> 1; d > 0; d >>= 1) {
+            if (d >= 64u) {  // partner: register j ^ (d / 64) of this lane
+#pragma unroll
+                for (uint32_t j = 0; j < K; ++j) {
+                    const uint32_t dj = d / 64u;
+                    if (j & dj) continue;
+                    const bool up = ((j * 64u + lane) & k) == 0u;
+                    const uint32_t lo = min(x[j], x[j | dj]), hi = max(x[j], x[j | dj]);
+                    x[j] = up ? lo : hi;
+                    x[j | dj] = up ? hi : lo;
+                }
+            } else {         // partner: lane ^ d, same register
+#pragma unroll
+                for (uint32_t j = 0; j < K; ++j) {
+                    const uint32_t o = (uint32_t)__shfl_xor((int)x[j], (int)d, 64);
+                    const bool up = ((j * 64u + lane) & k) == 0u, lower = (lane & d) == 0u;
+                    x[j] = (lower == up) ? min(x[j], o) : max(x[j], o);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < K; ++j)
+        if (j * 64u + lane < len) dst[j * 64u + lane] = x[j];
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
                                                                uint8_t* out_char, const uint32_t* list, uint32_t* cnt,
@@ -551,11 +589,13 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                     L.skey[i] = key_of(e, run_of(e, r0, r1), c0);
                 }
                 __syncthreads();
-                {   // runs of <= kRunSort entries: their thread, in registers; the others listed
+                {   // runs of <= kRunSort entries: their thread, in registers; the others listed --
+                    // up to kWaveSortMax entries for a wavefront (front of lst), longer ones for the
+                    // whole block (back of lst)
                     const uint32_t r = r0 + tid;
                     const uint32_t b = r < r1 ? L.rp[r] - e0 : 0u, len = r < r1 ? L.rp[r + 1u] - L.rp[r] : 0u;
-                    if (len > 64u) L.lst[atomicAdd(&L.s_n, 1u)] = r;
-                    else if (len > kRunSort) L.lst[kHistRuns - 1u - atomicAdd(&L.s_m, 1u)] = r;
+                    if (len > kWaveSortMax) L.lst[kHistRuns - 1u - atomicAdd(&L.s_n, 1u)] = r;
+                    else if (len > kRunSort) L.lst[atomicAdd(&L.s_m, 1u)] = r;
                     uint32_t a[kRunSort];
 #pragma unroll
                     for (uint32_t k = 0; k < kRunSort; ++k) a[k] = (len <= kRunSort && k < len) ? L.skey[b + k] : ~0u;
@@ -570,26 +610,18 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                         if (len <= kRunSort && k < len) L.skey2[b + k] = a[k];
                 }
                 __syncthreads();
-                // runs of 17..64 entries: a wavefront each, bitonic over the lanes
+                // runs of 17 .. kWaveSortMax entries: a wavefront each, bitonic over 64 / 256 / 512 keys
                 for (uint32_t j = wave; j < L.s_m; j += kHistWaves) {
-                    const uint32_t r = L.lst[kHistRuns - 1u - j];
+                    const uint32_t r = L.lst[j];
                     const uint32_t b = L.rp[r] - e0, len = L.rp[r + 1u] - L.rp[r];
-                    uint32_t x = lane < len ? L.skey[b + lane] : ~0u;
-#pragma unroll
-                    for (uint32_t k = 2; k <= 64u; k <<= 1) {
-#pragma unroll
-                        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-                            const uint32_t o = (uint32_t)__shfl_xor((int)x, (int)jj, 64);
-                            const bool up = (lane & k) == 0u, lower = (lane & jj) == 0u;
-                            x = (lower == up) ? min(x, o) : max(x, o);
-                        }
-                    }
-                    if (lane < len) L.skey2[b + lane] = x;
+                    if (len <= 64u) wave_sort_run<1>(L.skey + b, L.skey2 + b, len, lane);
+                    else if (len <= 256u) wave_sort_run<4>(L.skey + b, L.skey2 + b, len, lane);
+                    else wave_sort_run<8>(L.skey + b, L.skey2 + b, len, lane);
                 }
                 // longer runs: block-wide, one at a time, ranked by the bitmap of the chunk's records
                 const uint32_t nl = L.s_n;
                 for (uint32_t j = 0; j < nl; ++j) {  // uniform
-                    const uint32_t r = L.lst[j];
+                    const uint32_t r = L.lst[kHistRuns - 1u - j];
                     const uint32_t b = L.rp[r] - e0, len = L.rp[r + 1u] - L.rp[r];
                     for (uint32_t w = tid; w < kBmWords; w += kHistThreads) L.bm[w] = 0u;
                     for (uint32_t i = tid; i < len; i += kHistThreads) L.skey2[b + i] = ~0u;
