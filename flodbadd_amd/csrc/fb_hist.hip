@@ -140,6 +140,9 @@ __global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* pa
 // and each block's k_hist_general<false> workgroup starts its slots' cursors after the earlier
 // blocks' counts.  One workgroup for such a partition took 25 ms per C4 Zipf batch.
 constexpr uint32_t kHistSplitMin = 32768;  // (16,384: Zipf history 1.02 ms, 32,768: 0.90, 8,192: 1.23)
+// ... or more than this many entries (a hot UDP flow: few characters, but every entry is read and
+// sorted -- under Zipf(1.1) one such partition of 143K entries took 0.9 ms on one workgroup)
+constexpr uint32_t kHistSplitEntries = 16384;
 constexpr uint32_t kHistListCap = 256;    // split partitions (cnt rows)
 constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
 constexpr uint32_t kHistBlockChunks = 4;
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams 
     if (__syncthreads_or(len > kRunSort || wlen > kHistPer * 64u) || chunks > kHistRuns || tp > kHistCap) {
         if (tid == 0) {  // uniform: the general kernels take it (a partition with many characters split)
             uint32_t h = ~0u;
-            if (hot && n_chars > kHistSplitMin) h = atomicAdd(hot, 1u);
+            if (hot && (n_chars > kHistSplitMin || tp > kHistSplitEntries)) h = atomicAdd(hot, 1u);
             if (h < kHistListCap) hot[1u + h] = q;
             else slow[1u + atomicAdd(slow, 1u)] = q;
         }
