@@ -311,46 +311,49 @@ __device__ __forceinline__ uint32_t combined_slot(const FlowParams& P, uint32_t 
     return v & (kFlowSlots - 1u);
 }
 
-// One run of 17 .. 64 K keys sorted by a wavefront: key i in register i / 64 of lane i % 64,
-// bitonic network (partners 64 or more apart in the lane's registers, closer ones by shuffles),
-// ~0 padding sorts last; src -> dst (LDS).
+// One run of 17 .. 64 K keys placed in record order by a wavefront: lane l holds keys l, l + 64 ..
+// (K per lane); a key's place = the run's keys below it (keys are distinct records, read from LDS
+// four at a time, the same address in every lane: broadcasts); ~0 (no character) keys go after the
+// others, in lane order.  src -> dst (LDS).  (A bitonic network over the lanes spent a dependent
+// cross-lane permute per step: ~20 per 64 keys.)
 constexpr uint32_t kWaveSortMax = 512;  // longer runs: the block's bitmap rank
 template <uint32_t K>
 __device__ __forceinline__ void wave_sort_run(const uint32_t* src, uint32_t* dst, uint32_t len, uint32_t lane) {
-    uint32_t x[K];
+    uint32_t x[K], rank[K];
 #pragma unroll
-    for (uint32_t j = 0; j < K; ++j) x[j] = j * 64u + lane < len ? src[j * 64u + lane] : ~0u;
+    for (uint32_t j = 0; j < K; ++j) {
+        x[j] = j * 64u + lane < len ? src[j * 64u + lane] : ~0u;
+        rank[j] = 0u;
+    }
+    const uint32_t len4 = len & ~3u;
+    for (uint32_t i = 0; i < len4; i += 4u) {  // (src is 4-B aligned only: four scalar-address reads)
+        const uint32_t y0 = src[i], y1 = src[i + 1u], y2 = src[i + 2u], y3 = src[i + 3u];
 #pragma unroll
-    for (uint32_t k = 2; k <= 64u * K; k <<= 1) {
+        for (uint32_t j = 0; j < K; ++j)
+            rank[j] += (uint32_t)(y0 < x[j]) + (uint32_t)(y1 < x[j]) + (uint32_t)(y2 < x[j]) + (uint32_t)(y3 < x[j]);
+    }
+    for (uint32_t i = len4; i < len; ++i) {
+        const uint32_t y = src[i];
 #pragma unroll
-        for (uint32_t d = k >> 1; d > 0; d >>= 1) {
-            if (d >= 64u) {  // partner: register j ^ (d / 64) of this lane
+        for (uint32_t j = 0; j < K; ++j) rank[j] += (uint32_t)(y < x[j]);
+    }
+    // the ~0 keys: after the n_tcp others, in (register, lane) order
+    uint32_t none_before = 0u;
 #pragma unroll
-                for (uint32_t j = 0; j < K; ++j) {
-                    const uint32_t dj = d / 64u;
-                    if (j & dj) continue;
-                    const bool up = ((j * 64u + lane) & k) == 0u;
-                    const uint32_t lo = min(x[j], x[j | dj]), hi = max(x[j], x[j | dj]);
-                    x[j] = up ? lo : hi;
-                    x[j | dj] = up ? hi : lo;
-                }
-            } else {         // partner: lane ^ d, same register
-#pragma unroll
-                for (uint32_t j = 0; j < K; ++j) {
-                    const uint32_t o = (uint32_t)__shfl_xor((int)x[j], (int)d, 64);
-                    const bool up = ((j * 64u + lane) & k) == 0u, lower = (lane & d) == 0u;
-                    x[j] = (lower == up) ? min(x[j], o) : max(x[j], o);
-                }
-            }
-        }
+    for (uint32_t j = 0; j < K; ++j) {
+        const bool in = j * 64u + lane < len, none = in && x[j] == ~0u;
+        const unsigned long long m = __ballot(none);
+        if (none) rank[j] += none_before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        none_before += (uint32_t)__popcll(m);
+        // (a ~0 key counted the run's other keys below ~0, i.e. every TCP key: its base is n_tcp)
     }
 #pragma unroll
     for (uint32_t j = 0; j < K; ++j)
-        if (j * 64u + lane < len) dst[j * 64u + lane] = x[j];
+        if (j * 64u + lane < len) dst[rank[j]] = x[j];
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
+__global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
                                                                uint8_t* out_char, const uint32_t* list, uint32_t* cnt,
                                                                uint32_t nblk) {
     __shared__ HistLds L;
@@ -587,9 +590,52 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_general(const FlowParams 
                     L.s_n = 0u;
                     L.s_m = 0u;
                 }
-                for (uint32_t i = tid; i < n; i += kHistThreads) {
-                    const uint32_t e = e0 + i;
-                    L.skey[i] = key_of(e, run_of(e, r0, r1), c0);
+                // the keys, kLoadGroup per thread with their loads in flight together: each entry's
+                // run (binary search in LDS), its history word / original entry word and, for a
+                // combined group, pos_map; then the combined records' slots (agg_slot / the moved
+                // entry's history word)
+                constexpr uint32_t kLoadGroup = 4;
+                for (uint32_t g0 = 0; g0 < kHistPer; g0 += kLoadGroup) {
+                    uint32_t rr[kLoadGroup], w1[kLoadGroup], m1[kLoadGroup], w2[kLoadGroup];
+#pragma unroll
+                    for (uint32_t u = 0; u < kLoadGroup; ++u) {
+                        const uint32_t i = tid + (g0 + u) * kHistThreads;
+                        rr[u] = i < n ? run_of(e0 + i, r0, r1) : r0;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kLoadGroup; ++u) {
+                        const uint32_t i = tid + (g0 + u) * kHistThreads, r = rr[u];
+                        const uint32_t k = e0 + i - L.rp[r];
+                        const bool comb = (L.rn[r] >> 31) != 0u;
+                        w1[u] = i < n ? (comb ? P.e_orig[L.rs[r] + k] : P.hword[L.rq[r] + k]) : 0u;
+                        m1[u] = (i < n && comb) ? P.pos_map[L.rs[r] + k] : 0u;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kLoadGroup; ++u) {
+                        const uint32_t i = tid + (g0 + u) * kHistThreads, r = rr[u];
+                        const bool need = i < n && (L.rn[r] >> 31) != 0u && ((w1[u] >> kEntCodeShift) & 15u) != 0u;
+                        const uint32_t m = m1[u];
+                        w2[u] = !need ? 0u : (m & kRecFlowCombined) ? P.agg_slot[m & ~kRecFlowCombined]
+                                                                      : P.hword[L.rq[r] + (m - L.rs[r])];
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kLoadGroup; ++u) {
+                        const uint32_t i = tid + (g0 + u) * kHistThreads, r = rr[u];
+                        if (i >= n) continue;
+                        uint32_t slot, code, rec;
+                        if (!(L.rn[r] >> 31)) {
+                            slot = w1[u] & (kFlowSlots - 1u);
+                            code = (w1[u] >> 9) & 15u;
+                            rec = w1[u] >> 13;
+                        } else {
+                            code = (w1[u] >> kEntCodeShift) & 15u;
+                            rec = (w1[u] & kEntRecMask) - (c0 + r) * kFlowChunk;
+                            // an entry the table could not take: agg_slot ~0 / history word 0 (combined_slot)
+                            if ((m1[u] & kRecFlowCombined) ? w2[u] == ~0u : w2[u] == 0u) code = 0u;
+                            slot = w2[u] & (kFlowSlots - 1u);
+                        }
+                        L.skey[i] = code != 0u ? rec << 13 | slot << 4 | code : ~0u;
+                    }
                 }
                 __syncthreads();
                 {   // runs of <= kRunSort entries: their thread, in registers; the others listed --
