@@ -46,7 +46,7 @@ struct UpdScratch {
     uint32_t* cols = nullptr;      // [flow_parts][flow_chunks]
     uint32_t* rows_h = nullptr;    // [flow_chunks][flow_parts] combined groups' rows before k_flow_combine
     uint32_t* e_orig = nullptr;    // [flow_recs] combined groups' original entry words (history)
-    uint32_t* pos_map = nullptr;   // [flow_recs] combined groups' position map (history)
+    uint2* e_sort = nullptr;       // [flow_recs] combined groups' records in record order (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* ctl = nullptr;       // [3] its counters (FlowParams::ctl)
 };
@@ -238,7 +238,7 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.cols);
     hipFree(u.rows_h);
     hipFree(u.e_orig);
-    hipFree(u.pos_map);
+    hipFree(u.e_sort);
     hipFree(u.hot);
     hipFree(u.ctl);
     u = UpdScratch();
@@ -250,7 +250,7 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
     if (hipMalloc(&u.entries, recs * 4ull) != hipSuccess ||
         hipMalloc(&u.comb, (uint64_t)c->comb_cap * 2ull * sizeof(FlowEntry)) != hipSuccess ||
         hipMalloc(&u.rows_h, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.pos_map, recs * 4ull) != hipSuccess ||
+        hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.e_sort, recs * 8ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess) {
@@ -1104,7 +1104,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.batch = c->flow_batch;
     p.rows_h = u.rows_h;
     p.e_orig = u.e_orig;
-    p.pos_map = u.pos_map;
+    p.e_sort = u.e_sort;
     p.hcount = c->d_hcount;
     p.part_base = c->d_part_base;
     p.hword = c->d_hword;

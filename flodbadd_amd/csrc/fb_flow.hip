@@ -681,7 +681,7 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
 }
 
 // A combined entry (head e0..e3, tail t0..t3; layout in fb_internal.h): the same reductions with
-// the group's partial sums / minima / maxima.  Its records' pos_map words point at agg_slot[id].
+// the group's partial sums / minima / maxima.  Its records' e_sort words point at agg_slot[id].
 __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_t* tags, uint32_t* scr,
                                               const FlowParams& P, const uint4 e0, const uint4 e1,
                                               const uint4 e2, const uint4 e3, const uint4 t0, const uint4 t1,
@@ -815,20 +815,28 @@ constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4
 // kCombJc records, so the pack pass finds them without gathering the 56-B records again: K1c is
 // bound by those random record reads (under Zipf(1.1) ~4.6M records per C4 batch sit in hot
 // groups), not by its same-key LDS atomics (folding a hot key's lanes with wave reductions first
-// measured slower: 318 -> 348-358 us).  C4 Zipf(1.1): K1c 371 -> 317 us.
+// measured slower: 318 -> 348-358 us).  C4 Zipf(1.1): K1c 371 -> 317 us.  (2560: the order bitmap
+// below keeps the workgroup within 40 KiB; a Zipf(1.1) group holds up to ~2,460 records.)
 #ifndef FB_COMB_JC
-#define FB_COMB_JC 4096
+#define FB_COMB_JC 2560
 #endif
 constexpr uint32_t kCombJc = FB_COMB_JC;
+// The group's records in record order for the history (e_sort): a bitmap of the records' places in
+// the chunk (kFlowChunk bits) and its prefix popcounts; a record's rank = the set bits below it.
+constexpr uint32_t kCombBm = kFlowChunk / 64u;
 struct CombLds {
     unsigned long long tab[kCombSlots * 6];    // tag + key words (lds_upsert layout)
     unsigned long long bytes[kCombSlots * 4];  // outbound, inbound, orig ip, resp ip
     uint32_t f[kCombSlots * kCombF];
+    unsigned long long bm[kCombBm];            // the group's records in the chunk
+    uint16_t bmp[kCombBm];                     // exclusive prefix popcounts of bm
     uint8_t jc[kCombJc > 0 ? kCombJc : 1];     // the reduce pass's key slot per record
     uint32_t wsum[kCombThreads / 64];
     uint32_t base;
     uint32_t pool_next, pool_end;  // this workgroup's reserved combined-entry ids
 };
+static_assert(sizeof(CombLds) <= 40u * 1024u, "four K1c workgroups per CU");
+static_assert(kFlowChunk % 64u == 0u && 2u * kCombThreads >= kCombBm, "two bitmap words per thread");
 
 __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
@@ -845,6 +853,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
+        for (uint32_t j = threadIdx.x; j < kCombBm; j += kCombThreads) L.bm[j] = 0ull;
         for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
             L.tab[j * 6] = 0ull;
 #pragma unroll
@@ -859,9 +868,15 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint4 e[4];
             const uint32_t w = E[s0 + k];
             rec_entry(P, w, e);
-            // the group's original words stay readable for the history (record order key | code:
-            // with update entries rebuilt from the entry -- its pkt_index and character)
-            P.e_orig[s0 + k] = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
+            // the record's original word for the history (record order key | code: with update
+            // entries rebuilt from the entry -- its pkt_index and character), read back by this
+            // thread in the pack pass; its place in the chunk marked in the order bitmap
+            const uint32_t eo = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
+            P.e_orig[s0 + k] = eo;
+            {
+                const uint32_t rc = (eo & kEntRecMask) - chunk * kFlowChunk;  // (< kFlowChunk, distinct)
+                if (rc < kFlowChunk) atomicOr(&L.bm[rc >> 6], 1ull << (rc & 63u));
+            }
             const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                       e[2].y & 0xFFFFu};
             uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
@@ -914,15 +929,26 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint32_t* f = L.f + (threadIdx.x * kPer + u) * kCombF;
             if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
         }
+        {   // the order bitmap's prefix popcounts (thread t: words 2t, 2t + 1)
+            const uint32_t w0 = 2u * threadIdx.x;
+            const uint32_t c0 = w0 < kCombBm ? (uint32_t)__popcll(L.bm[w0]) : 0u;
+            const uint32_t c1 = w0 + 1u < kCombBm ? (uint32_t)__popcll(L.bm[w0 + 1u]) : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan(c0 + c1, L.wsum, tot);
+            if (w0 < kCombBm) L.bmp[w0] = (uint16_t)ex;
+            if (w0 + 1u < kCombBm) L.bmp[w0 + 1u] = (uint16_t)(ex + c0);
+        }
         __syncthreads();
         // pack the remaining plain entries (record indices) to the front, tile by tile (a tile is
-        // loaded before any of its stores, and stores land below the next tile)
+        // loaded before any of its stores, and stores land below the next tile); every record's
+        // original word and new position (combined id or moved entry) go to e_sort at its rank
         uint32_t cursor = 0u;
         for (uint32_t t = 0; t < cnt; t += kCombThreads) {
             const uint32_t k = t + threadIdx.x;
-            uint32_t keep = 0u, rec = 0u;
+            uint32_t keep = 0u, rec = 0u, eo = 0u, v = 0u;
             if (k < cnt) {
                 rec = E[s0 + k];
+                eo = P.e_orig[s0 + k];  // (this thread's own store of the reduce pass)
                 uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
                 if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
                     uint4 e[4];
@@ -931,17 +957,19 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                                               e[2].y & 0xFFFFu};
                     j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
                 }
-                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) {
-                    P.pos_map[s0 + k] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
-                } else {
-                    keep = 1u;
-                }
+                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) v = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                else keep = 1u;
             }
             uint32_t kept;
             const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
             if (keep) {
-                P.pos_map[s0 + k] = (uint32_t)(s0 + cursor + pos);  // the entry moved
+                v = (uint32_t)(s0 + cursor + pos);  // the entry moved
                 E[s0 + cursor + pos] = rec;
+            }
+            if (k < cnt) {
+                const uint32_t rc = min((eo & kEntRecMask) - chunk * kFlowChunk, kFlowChunk - 1u);
+                const uint32_t rank = L.bmp[rc >> 6] + (uint32_t)__popcll(L.bm[rc >> 6] & ((1ull << (rc & 63u)) - 1ull));
+                P.e_sort[s0 + min(rank, cnt - 1u)] = make_uint2(eo, v);
             }
             cursor += kept;
         }
@@ -965,7 +993,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta] | (f[kCfEnd] & 31u) << 8);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
-        if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_orig / pos_map, and
+        if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_sort, and
                                  // the group's original row from rows_h)
             *rowp = (row & 0x7FFFu) | 0x8000u | ((cursor + n_comb) << 16);
             P.rows_h[(size_t)chunk * P.parts + part] = row;

@@ -9,29 +9,29 @@
 // bucketing chunk), each partition's words contiguous and in chunk (= record) order:
 //   k_hist_scan : exclusive scan of the per-partition character counts k_flow_apply reported
 //                 (partials[4 p + 3]) -> each partition's output offset; the total -> *n_hist.
-//   k_hist_part<true> : one workgroup per partition, for a partition of one chunk round, at most
+//   k_hist_uniform : one workgroup per partition, for a partition of one chunk round, at most
 //                 kHistCap entries, no combined group and no chunk run over kRunSort entries (the
-//                 uniform case; others are listed for the general kernel):
+//                 uniform case; the others are listed for k_hist_general):
 //                 1. thread t sorts chunk run t by record in registers (K1's scatter leaves a run
 //                    unordered) into LDS at the run's place: the partition is then in record order;
-//                 2. wave w takes a contiguous eighth, 64 entries a step: the lanes holding one
-//                    slot find each other (a ballot per slot bit) and the lowest adds their count
-//                    to the wave's count of the slot;
-//                 3. per slot, a scan over the waves from the slot's offset (hcount scanned);
-//                 4. the walk again: a key's output position = its wave's position for the slot +
-//                    the slot's lanes below it in the step; the lowest lane moves it on.  Stable by
-//                    record without a comparison sort; the output is staged in LDS and written
-//                    coalesced.
-//   k_hist_part<false> : the listed partitions, a grid-stride loop: chunk rounds of 512 runs,
-//                 batches of at most kHistCap entries; a run k_flow_combine folded (a hot group)
-//                 is read from its original entry words (e_orig), each record's slot from the
-//                 combined entry's agg_slot or, for a record left plain, the word of its moved
-//                 entry (pos_map).  A batch is counting-sorted by slot in LDS; a record's place in
-//                 its slot's run is the number of the slot's records of the batch before it (a
-//                 scan of the slot's bucket), or -- a slot with more than kHistScan records in the
-//                 batch, or a run longer than kHistCap taken in record windows -- its index after
-//                 a bitonic sort of the batch by (slot, record).
-// Bytes per entry: its 4-B history word read; per character 5 B written (+ the count arrays).
+//                 2. per wave and slot, the characters counted (LDS atomics); per slot, a scan over
+//                    the waves from the slot's offset (hcount scanned);
+//                 3. the walk: wave w takes its 64 runs, 64 entries a step: a key's output position
+//                    = its wave's position for the slot + the slot's lanes below it in the step;
+//                    the lowest lane moves it on.  Stable by record without a comparison sort; the
+//                    output is staged in LDS and written coalesced.
+//   k_hist_general : the listed partitions, a grid-stride loop: chunk rounds of 512 runs, batches
+//                 of at most kHistCap entries, each put in record order and walked as above.  A
+//                 run k_flow_combine folded (a hot group) is read from e_sort, which K1c wrote in
+//                 record order (the original entry word, and the record's slot through its
+//                 combined entry's agg_slot or its moved entry's history word); a plain run of
+//                 more than kRunSort entries is sorted by a wavefront or, past kWaveSortMax, by a
+//                 bitmap of the chunk's records.  A partition with many entries or characters (a
+//                 skewed batch) is split over chunk blocks: k_hist_general<true> counts each
+//                 block's characters per slot, k_hist_blocks scans them over the blocks, and each
+//                 block starts its slots after the earlier blocks'.
+// Bytes per entry: its 4-B history word (8-B e_sort word) read; per character 5 B written (+ the
+// count arrays).
 #include "fb_internal.h"
 
 namespace fbk {
@@ -42,7 +42,6 @@ constexpr uint32_t kHistThreads = 512;
 #endif
 constexpr uint32_t kHistCap = FB_HIST_CAP;  // entries per batch (8 B of LDS each)
 constexpr uint32_t kHistRuns = 512;         // chunk runs per round: one per thread
-constexpr uint32_t kHistScan = 64;          // (general) a slot with more records in a batch takes the sort
 constexpr uint32_t kRunSort = 16;           // (uniform) the longest chunk run sorted in registers
 constexpr uint32_t kHistWaves = kHistThreads / 64;
 constexpr uint32_t kHistPer = kHistCap / kHistThreads;
@@ -134,15 +133,21 @@ __global__ __launch_bounds__(1024) void k_hist_scan(const unsigned long long* pa
     }
 }
 
-// A listed partition with more than kHistSplitMin characters (a skewed batch: Zipf(1.1) puts ~12 % of
-// the records in one flow) goes to a second list (up to kHistListCap) and is split by chunk blocks:
-// k_hist_general<true> counts each block's characters per slot into cnt[list index][block][slot],
-// and each block's k_hist_general<false> workgroup starts its slots' cursors after the earlier
-// blocks' counts.  One workgroup for such a partition took 25 ms per C4 Zipf batch.
-constexpr uint32_t kHistSplitMin = 32768;  // (16,384: Zipf history 1.02 ms, 32,768: 0.90, 8,192: 1.23)
-// ... or more than this many entries (a hot UDP flow: few characters, but every entry is read and
-// sorted -- under Zipf(1.1) one such partition of 143K entries took 0.9 ms on one workgroup)
-constexpr uint32_t kHistSplitEntries = 16384;
+// A listed partition with more than kHistSplitEntries entries to read (a combined group's: its
+// records) goes to a second list (up to kHistListCap) and is split by chunk blocks of about
+// kHistBlockEntries entries: k_hist_general<true> counts each block's characters per slot into
+// cnt[list index][block][slot], k_hist_blocks scans them over the blocks, and each block's
+// k_hist_general<false> workgroup starts its slots' cursors there.  Skewed batches need it: under
+// Zipf(1.1) one workgroup spent 25 ms on the hottest flow's partition (~12 % of the records) and
+// ~1.5 ms on one of 42K entries (a flow with ~0.4 %).  A C4 partition holds ~2,560 entries.
+#ifndef FB_HIST_SPLIT_ENTRIES
+#define FB_HIST_SPLIT_ENTRIES 8192
+#endif
+constexpr uint32_t kHistSplitEntries = FB_HIST_SPLIT_ENTRIES;
+#ifndef FB_HIST_BLOCK_ENTRIES
+#define FB_HIST_BLOCK_ENTRIES 4096
+#endif
+constexpr uint32_t kHistBlockEntries = FB_HIST_BLOCK_ENTRIES;
 constexpr uint32_t kHistListCap = 256;    // split partitions (cnt rows)
 constexpr uint32_t kHistMaxBlocks = 128;  // chunk blocks of at least kHistBlockChunks chunks
 constexpr uint32_t kHistBlockChunks = 4;
@@ -184,10 +189,19 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_uniform(const FlowParams 
     __syncthreads();
     const uint32_t wlen = L.rp[min(64u * wave + 64u, kHistRuns)] - L.rp[64u * wave];
     if (__syncthreads_or(len > kRunSort || wlen > kHistPer * 64u) || chunks > kHistRuns || tp > kHistCap) {
-        if (tid == 0) {  // uniform: the general kernels take it (a partition with many characters split)
+        // uniform: the general kernels take it; a partition with many characters or entries to read
+        // (a combined group's: its original row) is split
+        uint32_t rd = 0u, tr, ex2, tot2;
+        for (uint32_t c = tid; hot && c < chunks; c += kHistThreads) {
+            const uint32_t v = P.cols[(size_t)q * P.chunk_stride + c];
+            rd += (v & 0x8000u) ? P.rows_h[(size_t)c * P.parts + q] >> 16 : v >> 16;
+        }
+        block_scan2(rd, 0u, tr, ex2, tot2, L.wsum, L.wsum2);
+        if (tid == 0) {
             uint32_t h = ~0u;
-            if (hot && (n_chars > kHistSplitMin || tp > kHistSplitEntries)) h = atomicAdd(hot, 1u);
-            if (h < kHistListCap) hot[1u + h] = q;
+            if (hot && tr > kHistSplitEntries) h = atomicAdd(hot, 1u);
+            // the split list entry: partition | blocks wanted << 16 (k_hist_general caps them)
+            if (h < kHistListCap) hot[1u + h] = q | min((tr + kHistBlockEntries - 1u) / kHistBlockEntries, 0xFFFFu) << 16;
             else slow[1u + atomicAdd(slow, 1u)] = q;
         }
         return;
@@ -311,7 +325,7 @@ __device__ __forceinline__ uint32_t combined_slot(const FlowParams& P, uint32_t 
     return v & (kFlowSlots - 1u);
 }
 
-// One run of 17 .. 64 K keys placed in record order by a wavefront: lane l holds keys l, l + 64 ..
+// One plain run of 17 .. 64 K keys placed in record order by a wavefront: lane l holds keys l, l + 64 ..
 // (K per lane); a key's place = the run's keys below it (keys are distinct records, read from LDS
 // four at a time, the same address in every lane: broadcasts); ~0 (no character) keys go after the
 // others, in lane order.  src -> dst (LDS).  (A bitonic network over the lanes spent a dependent
@@ -394,7 +408,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
         return block_scan2(v, 0u, tot, ex2, tot2);
     };
 
-    auto partition = [&](uint32_t q, uint32_t li, uint32_t blk) {
+    auto partition = [&](uint32_t q, uint32_t li, uint32_t blk, uint32_t nb) {
         // every load the first round needs, issued together: the partition's character count and
         // history-word base, its output range, its slots' counts
         const unsigned long long pw = P.partials[4 * (size_t)q + 3];
@@ -404,8 +418,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
         const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
         if (n_chars == 0u) return;  // uniform: no history characters in this partition
         // this workgroup's chunk block (a partition that is not split: every chunk)
-        const bool split = nblk > 1u;
-        const uint32_t cbs = split ? (chunks + nblk - 1u) / nblk : chunks;
+        const bool split = nblk > 1u;  // (nb blocks of this partition, <= nblk)
+        const uint32_t cbs = split ? (chunks + nb - 1u) / nb : chunks;
         const uint32_t cb0 = blk * cbs, cb1 = min(chunks, cb0 + cbs);
         if (cb0 >= cb1) return;  // uniform
         uint32_t vp = tid < cb1 - cb0 ? col[cb0 + tid] : 0u;
@@ -414,9 +428,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
         uint32_t* bc = cnt + ((size_t)li * nblk) * kFlowSlots;  // (split) [block][slot] counts
         {
             uint32_t t;
-            uint32_t prior = 0u;  // the slot's characters in the earlier blocks
-            if (!COUNT && split)
-                for (uint32_t b = 0; b < blk; ++b) prior += bc[(size_t)b * kFlowSlots + tid];
+            // the slot's characters in the earlier blocks (k_hist_blocks' prefix)
+            const uint32_t prior = (!COUNT && split) ? bc[(size_t)blk * kFlowSlots + tid] : 0u;
             L.cursor[tid] = block_scan(hc, t) + prior;  // relative to out_beg
             L.bcnt[tid] = 0u;
             uint32_t tb;
@@ -465,12 +478,9 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                         slot = w & (kFlowSlots - 1u);
                         code = (w >> 9) & 15u;
                     } else {
-                        const uint32_t w = P.e_orig[L.rs[lo] + k];
-                        code = (w >> kEntCodeShift) & 15u;
-                        if (code != 0u) {
-                            const uint32_t m = P.pos_map[L.rs[lo] + k];
-                            slot = combined_slot(P, m, L.rq[lo], L.rs[lo], code);
-                        }
+                        const uint2 es = P.e_sort[L.rs[lo] + k];
+                        code = (es.x >> kEntCodeShift) & 15u;
+                        if (code != 0u) slot = combined_slot(P, es.y, L.rq[lo], L.rs[lo], code);
                     }
                     if (code != 0u) atomicAdd(&L.bcnt[slot], 1u);
                 }
@@ -505,10 +515,10 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                     code = (w >> 9) & 15u;
                     rec = w >> 13;  // (record % kFlowChunk)
                 } else {
-                    const uint32_t w = P.e_orig[L.rs[r] + k];
-                    code = (w >> kEntCodeShift) & 15u;
-                    rec = (w & kEntRecMask) - (c0 + r) * kFlowChunk;
-                    if (code != 0u) slot = combined_slot(P, P.pos_map[L.rs[r] + k], L.rq[r], L.rs[r], code);
+                    const uint2 es = P.e_sort[L.rs[r] + k];
+                    code = (es.x >> kEntCodeShift) & 15u;
+                    rec = (es.x & kEntRecMask) - (c0 + r) * kFlowChunk;
+                    if (code != 0u) slot = combined_slot(P, es.y, L.rq[r], L.rs[r], code);
                 }
                 return code != 0u ? rec << 13 | slot << 4 | code : ~0u;
             };
@@ -591,9 +601,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                     L.s_m = 0u;
                 }
                 // the keys, kLoadGroup per thread with their loads in flight together: each entry's
-                // run (binary search in LDS), its history word / original entry word and, for a
-                // combined group, pos_map; then the combined records' slots (agg_slot / the moved
-                // entry's history word)
+                // run (binary search in LDS), its history word or (a combined group) its e_sort
+                // word; then the combined records' slots (agg_slot / the moved entry's history word)
                 constexpr uint32_t kLoadGroup = 4;
                 for (uint32_t g0 = 0; g0 < kHistPer; g0 += kLoadGroup) {
                     uint32_t rr[kLoadGroup], w1[kLoadGroup], m1[kLoadGroup], w2[kLoadGroup];
@@ -607,8 +616,14 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                         const uint32_t i = tid + (g0 + u) * kHistThreads, r = rr[u];
                         const uint32_t k = e0 + i - L.rp[r];
                         const bool comb = (L.rn[r] >> 31) != 0u;
-                        w1[u] = i < n ? (comb ? P.e_orig[L.rs[r] + k] : P.hword[L.rq[r] + k]) : 0u;
-                        m1[u] = (i < n && comb) ? P.pos_map[L.rs[r] + k] : 0u;
+                        if (i < n && comb) {
+                            const uint2 es = P.e_sort[L.rs[r] + k];
+                            w1[u] = es.x;
+                            m1[u] = es.y;
+                        } else {
+                            w1[u] = i < n ? P.hword[L.rq[r] + k] : 0u;
+                            m1[u] = 0u;
+                        }
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < kLoadGroup; ++u) {
@@ -634,15 +649,17 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                             if ((m1[u] & kRecFlowCombined) ? w2[u] == ~0u : w2[u] == 0u) code = 0u;
                             slot = w2[u] & (kFlowSlots - 1u);
                         }
-                        L.skey[i] = code != 0u ? rec << 13 | slot << 4 | code : ~0u;
+                        // a combined run (e_sort) is in record order already: straight to skey2
+                        (L.rn[r] >> 31 ? L.skey2 : L.skey)[i] = code != 0u ? rec << 13 | slot << 4 | code : ~0u;
                     }
                 }
                 __syncthreads();
-                {   // runs of <= kRunSort entries: their thread, in registers; the others listed --
-                    // up to kWaveSortMax entries for a wavefront (front of lst), longer ones for the
-                    // whole block (back of lst)
+                {   // plain runs of <= kRunSort entries: their thread, in registers; the others listed
+                    // -- up to kWaveSortMax entries for a wavefront (front of lst), longer ones for
+                    // the whole block (back of lst)
                     const uint32_t r = r0 + tid;
-                    const uint32_t b = r < r1 ? L.rp[r] - e0 : 0u, len = r < r1 ? L.rp[r + 1u] - L.rp[r] : 0u;
+                    const bool plain = r < r1 && !(L.rn[r] >> 31);
+                    const uint32_t b = plain ? L.rp[r] - e0 : 0u, len = plain ? L.rp[r + 1u] - L.rp[r] : 0u;
                     if (len > kWaveSortMax) L.lst[kHistRuns - 1u - atomicAdd(&L.s_n, 1u)] = r;
                     else if (len > kRunSort) L.lst[atomicAdd(&L.s_m, 1u)] = r;
                     uint32_t a[kRunSort];
@@ -659,11 +676,12 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
                         if (len <= kRunSort && k < len) L.skey2[b + k] = a[k];
                 }
                 __syncthreads();
-                // runs of 17 .. kWaveSortMax entries: a wavefront each, bitonic over 64 / 256 / 512 keys
+                // plain runs of 17 .. kWaveSortMax entries: a wavefront each, 1 / 2 / 4 / 8 keys a lane
                 for (uint32_t j = wave; j < L.s_m; j += kHistWaves) {
                     const uint32_t r = L.lst[j];
                     const uint32_t b = L.rp[r] - e0, len = L.rp[r + 1u] - L.rp[r];
                     if (len <= 64u) wave_sort_run<1>(L.skey + b, L.skey2 + b, len, lane);
+                    else if (len <= 128u) wave_sort_run<2>(L.skey + b, L.skey2 + b, len, lane);
                     else if (len <= 256u) wave_sort_run<4>(L.skey + b, L.skey2 + b, len, lane);
                     else wave_sort_run<8>(L.skey + b, L.skey2 + b, len, lane);
                 }
@@ -694,6 +712,15 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
             // its entries), each gathered in record order through the window's bitmap, then walked
             auto long_run = [&](uint32_t r, uint32_t c0) {
                 const uint32_t e_lo = L.rp[r], len = L.rp[r + 1u] - e_lo;
+                if (L.rn[r] >> 31) {  // a combined run is in record order: windows of kHistCap entries
+                    for (uint32_t e = 0; e < len; e += kHistCap) {
+                        const uint32_t m = min(kHistCap, len - e);
+                        for (uint32_t i = tid; i < m; i += kHistThreads) L.skey2[i] = key_of(e_lo + e + i, r, c0);
+                        __syncthreads();
+                        walk(m);
+                    }
+                    return;
+                }
                 constexpr uint32_t kWinWords = kHistCap / 32u;
                 for (uint32_t w0 = 0; w0 < kFlowChunk; w0 += kHistCap) {
                     for (uint32_t w = tid; w < kWinWords; w += kHistThreads) L.bm[w] = 0u;
@@ -744,8 +771,29 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
     };
     const uint32_t n = min(list[0], nblk > 1u ? kHistListCap : 0xFFFFFFFFu);
     for (uint32_t i = blockIdx.x; i < n * nblk; i += gridDim.x) {  // (blocks of one partition adjacent)
-        partition(list[1u + i / nblk], i / nblk, i % nblk);
+        const uint32_t v = list[1u + i / nblk];
+        const uint32_t nb = nblk > 1u ? min(max(v >> 16, 2u), nblk) : 1u;
+        if (i % nblk < nb) partition(v & 0xFFFFu, i / nblk, i % nblk, nb);
         __syncthreads();  // the LDS is re-initialised for the next partition
+    }
+}
+
+// The split partitions' per-block slot counts -> their exclusive prefix over the blocks, in place
+// (block b of a split partition starts slot s after blocks 0 .. b - 1).
+__global__ __launch_bounds__(kFlowSlots) void k_hist_blocks(const uint32_t* list, uint32_t* cnt, uint32_t nblk) {
+    if (blockIdx.x >= min(list[0], kHistListCap)) return;
+    uint32_t* c = cnt + (size_t)blockIdx.x * nblk * kFlowSlots + threadIdx.x;
+    uint32_t run = 0u;
+    constexpr uint32_t kG = 8;  // loads of kG blocks in flight, then their stores
+    for (uint32_t b0 = 0; b0 < nblk; b0 += kG) {
+        uint32_t x[kG];
+#pragma unroll
+        for (uint32_t u = 0; u < kG; ++u) x[u] = b0 + u < nblk ? c[(size_t)(b0 + u) * kFlowSlots] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kG; ++u) {
+            if (b0 + u < nblk) c[(size_t)(b0 + u) * kFlowSlots] = run;
+            run += x[u];
+        }
     }
 }
 
@@ -774,6 +822,9 @@ hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* h
     // the split ones: per-block slot counts, then the blocks
     hipLaunchKernelGGL(k_hist_general<true>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist,
                        hot, hcnt, nblk);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hist_blocks, dim3(kHistListCap), dim3(kFlowSlots), 0, s, hot, hcnt, nblk);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hist_general<false>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot,

@@ -187,7 +187,7 @@ static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 // of S s H h (~0 none), records, 0.
 constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the originator)
 constexpr uint32_t kEntTail = 1u << 18;
-constexpr uint32_t kRecFlowCombined = 0x80000000u;  // pos_map value: combined id, slot in agg_slot
+constexpr uint32_t kRecFlowCombined = 0x80000000u;  // e_sort position word: combined id, slot in agg_slot
 // entries[] word: the record slot (< 2^27) | its history code << 27 (0: no history character --
 // not TCP --, else 1 + the character's FB_HIST_CHARS index), or kIdxCombined | a combined id
 constexpr uint32_t kIdxCombined = 0x80000000u;
@@ -248,9 +248,10 @@ struct FlowParams {
     uint32_t* rows_h;           // [chunks][parts] a combined group's row before k_flow_combine (K1c;
                                 // the history reads its records from e_orig); a combined group's
                                 // row in rows / cols has bit 15 set
-    uint32_t* e_orig;           // [max_recs] a combined group's original entry words (K1c)
-    uint32_t* pos_map;          // [max_recs] a combined group's original position -> the entry's new
-                                // position, or kRecFlowCombined | combined id
+    uint32_t* e_orig;           // [max_recs] K1c scratch: a combined group's original entry words
+    uint2* e_sort;              // [max_recs] a combined group's records in record order (K1c): the
+                                // original entry word, and the entry's new position or
+                                // kRecFlowCombined | combined id
     uint32_t* hword;            // [max_recs] K2: a hist_word per entry it applied, each partition's in
                                 // its entry order from partials[4 p + 3] >> 32 (coalesced writes)
     uint32_t* hcount;           // [capacity] history characters each slot got this update (K2)
