@@ -307,12 +307,13 @@ struct HistLds {
     uint32_t rq[kHistRuns];      // the history word of its first applied entry
     uint32_t lst[kHistRuns];     // the batch's runs of more than 64 entries (then of 17..64: from the back)
     uint32_t wsum[kHistThreads / 64], wsum2[kHistThreads / 64];
+    uint32_t pairs[kHistListCap + 1];  // (split) exclusive prefix of the listed partitions' blocks
     uint32_t s_n, s_m;
 };
 static_assert(sizeof(HistLds) <= 80u * 1024u, "two workgroups per CU");
 
-// Listed partitions: `list` = slow (one workgroup each, every chunk) or, with nblk > 1, the split
-// partitions -- a grid-stride loop over (list index, chunk block) pairs; cnt = that list's counts.
+// Listed partitions: `slow` (one workgroup each, every chunk) and `hot`, the split partitions (with
+// nblk > 1; cnt = their [list index][block][slot] counts) -- a grid-stride loop over the pairs.
 // Slot (within the partition) of a record of a combined group: its combined entry's agg_slot, or the
 // history word of its moved plain entry.  An entry the table could not take (partition full / spin
 // expired: error bit 4 / 16) left agg_slot ~0 or history word 0 -- its character is dropped (code 0)
@@ -368,8 +369,8 @@ __device__ __forceinline__ void wave_sort_run(const uint32_t* src, uint32_t* dst
 
 template <bool COUNT>
 __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowParams P, uint32_t chunks, uint32_t* out_slot,
-                                                               uint8_t* out_char, const uint32_t* list, uint32_t* cnt,
-                                                               uint32_t nblk) {
+                                                               uint8_t* out_char, const uint32_t* slow,
+                                                               const uint32_t* hot, uint32_t* cnt, uint32_t nblk) {
     __shared__ HistLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     // block-wide exclusive sums of one or two values per thread (tot: the sum)
@@ -418,7 +419,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
         const uint32_t n_chars = (uint32_t)pw, hbase = (uint32_t)(pw >> 32);
         if (n_chars == 0u) return;  // uniform: no history characters in this partition
         // this workgroup's chunk block (a partition that is not split: every chunk)
-        const bool split = nblk > 1u;  // (nb blocks of this partition, <= nblk)
+        const bool split = nb > 1u;  // (nb blocks of this partition, <= nblk)
         const uint32_t cbs = split ? (chunks + nb - 1u) / nb : chunks;
         const uint32_t cb0 = blk * cbs, cb1 = min(chunks, cb0 + cbs);
         if (cb0 >= cb1) return;  // uniform
@@ -769,31 +770,64 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
             }
         }
     };
-    const uint32_t n = min(list[0], nblk > 1u ? kHistListCap : 0xFFFFFFFFu);
-    for (uint32_t i = blockIdx.x; i < n * nblk; i += gridDim.x) {  // (blocks of one partition adjacent)
-        const uint32_t v = list[1u + i / nblk];
-        const uint32_t nb = nblk > 1u ? min(max(v >> 16, 2u), nblk) : 1u;
-        if (i % nblk < nb) partition(v & 0xFFFFu, i / nblk, i % nblk, nb);
+    // pairs i: first the slow list's partitions (a workgroup each, every chunk; not in the counting
+    // pass), then the split list's (partition, block) pairs numbered densely -- each split
+    // partition takes the blocks it asked for (capped at nblk), so every workgroup gets some
+    const uint32_t n_slow = (!COUNT && slow) ? slow[0] : 0u;
+    uint32_t n = 0u, total = 0u;
+    if (hot) {  // (uniform)
+        n = min(hot[0], kHistListCap);
+        static_assert(kHistListCap <= kHistThreads, "one listed partition per thread");
+        const uint32_t nbt = tid < n ? min(max(hot[1u + tid] >> 16, 2u), nblk) : 0u;
+        const uint32_t ex = block_scan(nbt, total);
+        if (tid <= n) L.pairs[tid] = ex;  // (pairs[n] = total)
+        __syncthreads();
+    }
+    for (uint32_t i = blockIdx.x; i < n_slow + total; i += gridDim.x) {  // (blocks of one partition adjacent)
+        if (i < n_slow) {
+            partition(slow[1u + i], 0u, 0u, 1u);
+        } else {
+            const uint32_t j = i - n_slow;
+            uint32_t lo = 0u, hi = n - 1u;  // the split partition holding pair j
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1u) >> 1;
+                if (L.pairs[mid] <= j) lo = mid; else hi = mid - 1u;
+            }
+            partition(hot[1u + lo] & 0xFFFFu, lo, j - L.pairs[lo], L.pairs[lo + 1u] - L.pairs[lo]);
+        }
         __syncthreads();  // the LDS is re-initialised for the next partition
     }
 }
 
 // The split partitions' per-block slot counts -> their exclusive prefix over the blocks, in place
-// (block b of a split partition starts slot s after blocks 0 .. b - 1).
-__global__ __launch_bounds__(kFlowSlots) void k_hist_blocks(const uint32_t* list, uint32_t* cnt, uint32_t nblk) {
-    if (blockIdx.x >= min(list[0], kHistListCap)) return;
-    uint32_t* c = cnt + (size_t)blockIdx.x * nblk * kFlowSlots + threadIdx.x;
-    uint32_t run = 0u;
-    constexpr uint32_t kG = 8;  // loads of kG blocks in flight, then their stores
-    for (uint32_t b0 = 0; b0 < nblk; b0 += kG) {
-        uint32_t x[kG];
+// (block b of a split partition starts slot s after blocks 0 .. b - 1).  Workgroup (partition, 32
+// slots): thread (g, s) takes blocks 8 g .. 8 g + 7 of its slot, all loads in flight, then adds the
+// earlier groups' sums.
+constexpr uint32_t kHbSlots = 32, kHbPer = 8;
+static_assert(kHbPer * (kHistThreads / kHbSlots) >= kHistMaxBlocks, "every block in a group");
+__global__ __launch_bounds__(kHistThreads) void k_hist_blocks(const uint32_t* list, uint32_t* cnt, uint32_t nblk) {
+    __shared__ uint32_t gsum[kHistThreads / kHbSlots][kHbSlots];
+    const uint32_t li = blockIdx.x / (kFlowSlots / kHbSlots);
+    if (li >= min(list[0], kHistListCap)) return;
+    const uint32_t nb = min(max(list[1u + li] >> 16, 2u), nblk);  // (k_hist_general's blocks)
+    const uint32_t g = threadIdx.x / kHbSlots, sl = (blockIdx.x % (kFlowSlots / kHbSlots)) * kHbSlots + threadIdx.x % kHbSlots;
+    uint32_t* c = cnt + (size_t)li * nblk * kFlowSlots + sl;
+    uint32_t x[kHbPer], run = 0u;
 #pragma unroll
-        for (uint32_t u = 0; u < kG; ++u) x[u] = b0 + u < nblk ? c[(size_t)(b0 + u) * kFlowSlots] : 0u;
+    for (uint32_t u = 0; u < kHbPer; ++u) {
+        const uint32_t b = g * kHbPer + u;
+        x[u] = b < nb ? c[(size_t)b * kFlowSlots] : 0u;
+        run += x[u];
+    }
+    gsum[g][threadIdx.x % kHbSlots] = run;
+    __syncthreads();
+    run = 0u;
+    for (uint32_t k = 0; k < g; ++k) run += gsum[k][threadIdx.x % kHbSlots];
 #pragma unroll
-        for (uint32_t u = 0; u < kG; ++u) {
-            if (b0 + u < nblk) c[(size_t)(b0 + u) * kFlowSlots] = run;
-            run += x[u];
-        }
+    for (uint32_t u = 0; u < kHbPer; ++u) {
+        const uint32_t b = g * kHbPer + u;
+        if (b < nb) c[(size_t)b * kFlowSlots] = run;
+        run += x[u];
     }
 }
 
@@ -814,21 +848,23 @@ hipError_t launch_flow_history(const FlowParams& p, uint32_t chunks, uint32_t* h
     hipLaunchKernelGGL(k_hist_uniform, dim3(p.parts), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist, slow, hot);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // the listed partitions (a handful unless the batch is skewed): a grid-stride loop
-    hipLaunchKernelGGL(k_hist_general<false>, dim3(min(p.parts, 512u)), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
-                       hist, slow, nullptr, 1u);
-    e = hipGetLastError();
-    if (e != hipSuccess || !hot) return e;
-    // the split ones: per-block slot counts, then the blocks
+    if (!hot) {  // the listed partitions (a handful unless the batch is skewed): a grid-stride loop
+        hipLaunchKernelGGL(k_hist_general<false>, dim3(min(p.parts, 512u)), dim3(kHistThreads), 0, s, p, chunks,
+                           hist_slot, hist, slow, nullptr, nullptr, 1u);
+        return hipGetLastError();
+    }
+    // the split ones' per-block slot counts, their prefix over the blocks, then the slow list's
+    // partitions and the split ones' blocks in one launch
     hipLaunchKernelGGL(k_hist_general<true>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot, hist,
-                       hot, hcnt, nblk);
+                       nullptr, hot, hcnt, nblk);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hist_blocks, dim3(kHistListCap), dim3(kFlowSlots), 0, s, hot, hcnt, nblk);
+    hipLaunchKernelGGL(k_hist_blocks, dim3(kHistListCap * (kFlowSlots / kHbSlots)), dim3(kHistThreads), 0, s, hot, hcnt,
+                       nblk);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hist_general<false>, dim3(kHistSplitGrid), dim3(kHistThreads), 0, s, p, chunks, hist_slot,
-                       hist, hot, hcnt, nblk);
+                       hist, slow, hot, hcnt, nblk);
     return hipGetLastError();
 }
 
