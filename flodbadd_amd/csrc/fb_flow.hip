@@ -821,6 +821,10 @@ constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4
 #define FB_COMB_JC 2560
 #endif
 constexpr uint32_t kCombJc = FB_COMB_JC;
+#ifndef FB_COMB_U
+#define FB_COMB_U 1  // (4: C4 Zipf K1c 328 -> 415 us)
+#endif
+constexpr uint32_t kCombU = FB_COMB_U;  // records per thread with their loads in flight together
 // The group's records in record order for the history (e_sort): a bitmap of the records' places in
 // the chunk (kFlowChunk bits) and its prefix popcounts; a record's rank = the set bits below it.
 constexpr uint32_t kCombBm = kFlowChunk / 64u;
@@ -863,44 +867,98 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 L.f[j * kCombF + w] = (w == kCfFirst || w == kCfEnd || (w >= kCfChar && w < kCfChar + 4)) ? ~0u : 0u;
         }
         __syncthreads();
-        // reduce per key (a key the table cannot take stays a plain entry)
-        for (uint32_t k = threadIdx.x; k < cnt; k += kCombThreads) {
-            uint4 e[4];
-            const uint32_t w = E[s0 + k];
-            rec_entry(P, w, e);
-            // the record's original word for the history (record order key | code: with update
-            // entries rebuilt from the entry -- its pkt_index and character), read back by this
-            // thread in the pack pass; its place in the chunk marked in the order bitmap
-            const uint32_t eo = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
-            P.e_orig[s0 + k] = eo;
-            {
-                const uint32_t rc = (eo & kEntRecMask) - chunk * kFlowChunk;  // (< kFlowChunk, distinct)
-                if (rc < kFlowChunk) atomicOr(&L.bm[rc >> 6], 1ull << (rc & 63u));
+        // reduce per key (a key the table cannot take stays a plain entry), kCombU records per
+        // thread at a time with their loads in flight together.  A thread sums its consecutive
+        // records of one key in registers and adds them to the key's fields when the key changes:
+        // in a hot group most of a wavefront's lanes hold the same key, and one LDS atomic per
+        // record and field serialised 64 lanes on one address (C4 Zipf(1.1) K1c 328 -> DESIGN us).
+        uint32_t aj = ~0u, a_pk = 0u, a_hash = 0u, a_meta = 0u, a_first = ~0u, a_last = 0u, a_hcnt = 0u, a_mask = 0u,
+                 a_end = ~0u, a_ch[4] = {~0u, ~0u, ~0u, ~0u};
+        unsigned long long a_by[4] = {0ull, 0ull, 0ull, 0ull};
+        auto flush = [&]() {
+            if (aj == ~0u) return;
+            uint32_t* f = L.f + aj * kCombF;
+#pragma unroll
+            for (uint32_t q = 0; q < 4u; ++q)
+                if (a_by[q]) atomicAdd(&L.bytes[aj * 4 + q], a_by[q]);
+            atomicAdd(f + kCfPk, a_pk);
+            atomicAdd(f + kCfRecs, (a_pk & 0xFFFFu) + (a_pk >> 16));
+            f[kCfHash] = a_hash;  // every lane of the key stores the same word
+            f[kCfMeta] = a_meta;
+            atomicMin(f + kCfFirst, a_first);
+            atomicMax(f + kCfLast, a_last);
+            if (a_hcnt) {
+                atomicAdd(f + kCfHcnt, a_hcnt);
+                if (a_mask) atomicOr(f + kCfMask, a_mask);
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; ++q)
+                    if (a_ch[q] != ~0u) atomicMin(f + kCfChar + q, a_ch[q]);
+                if (a_end != ~0u) atomicMin(f + kCfEnd, a_end);
             }
-            const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
-                                      e[2].y & 0xFFFFu};
-            uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
-            const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
-            if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
-            if (no_slot) continue;
-            const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
-            uint32_t* f = L.f + j * kCombF;
-            atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
-            atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e[2].w);
-            atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
-            atomicAdd(f + kCfRecs, 1u);
-            f[kCfHash] = e[3].w;  // every lane of the key stores the same word
-            f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
-            atomicMin(f + kCfFirst, rec);
-            atomicMax(f + kCfLast, rec);
-            if (e[3].z & 0x10000u) {
-                atomicAdd(f + kCfHcnt, 1u);
-                const uint32_t b = hist_bit(e[3].z & 0xFFu);
-                if (b < 16u) atomicOr(f + kCfMask, 1u << b);
-                if (b < 4u) atomicMin(f + kCfChar + b, rec);
-                if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec << 5 | b);  // (rec < 2^27)
+            a_pk = a_hcnt = a_mask = a_last = 0u;
+            a_first = a_end = ~0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 4u; ++q) {
+                a_ch[q] = ~0u;
+                a_by[q] = 0ull;
+            }
+        };
+        for (uint32_t k0 = 0; k0 < cnt; k0 += kCombU * kCombThreads) {
+            uint32_t wv[kCombU];
+            uint4 rv[kCombU][4];
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = k0 + u * kCombThreads + threadIdx.x;
+                wv[u] = k < cnt ? E[s0 + k] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u)
+                if (k0 + u * kCombThreads + threadIdx.x < cnt) raw_entry(P, wv[u], rv[u]);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = k0 + u * kCombThreads + threadIdx.x, w = wv[u];
+                if (k >= cnt) continue;
+                uint4 e[4];
+                entry_of(P.ent != nullptr, rv[u], w, e);
+                // the record's original word for the history (record order key | code: with update
+                // entries rebuilt from the entry -- its pkt_index and character), read back by this
+                // thread in the pack pass; its place in the chunk marked in the order bitmap
+                const uint32_t eo = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
+                P.e_orig[s0 + k] = eo;
+                {
+                    const uint32_t rc = (eo & kEntRecMask) - chunk * kFlowChunk;  // (< kFlowChunk, distinct)
+                    if (rc < kFlowChunk) atomicOr(&L.bm[rc >> 6], 1ull << (rc & 63u));
+                }
+                const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                          e[2].y & 0xFFFFu};
+                uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
+                const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
+                if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
+                if (no_slot) continue;
+                if (j != aj) {  // another key: the accumulated one goes to the table
+                    flush();
+                    aj = j;
+                }
+                const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
+                a_by[orig ? 0 : 1] += e[2].z;
+                a_by[orig ? 2 : 3] += e[2].w;
+                a_pk += orig ? 1u : 0x10000u;
+                a_hash = e[3].w;
+                a_meta = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
+                a_first = min(a_first, rec);
+                a_last = max(a_last, rec);
+                if (e[3].z & 0x10000u) {
+                    ++a_hcnt;
+                    const uint32_t b = hist_bit(e[3].z & 0xFFu);
+                    if (b < 16u) a_mask |= 1u << b;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; ++q)
+                        if (b == q) a_ch[q] = min(a_ch[q], rec);
+                    if ((e[3].z >> 8) & kTcpFinRst) a_end = min(a_end, rec << 5 | b);  // (rec < 2^27)
+                }
             }
         }
+        flush();
         __syncthreads();
         // number the keys met more than once; one global atomic per group for their ids
         constexpr uint32_t kPer = kCombSlots / kCombThreads;
@@ -939,37 +997,49 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             if (w0 + 1u < kCombBm) L.bmp[w0 + 1u] = (uint16_t)(ex + c0);
         }
         __syncthreads();
-        // pack the remaining plain entries (record indices) to the front, tile by tile (a tile is
-        // loaded before any of its stores, and stores land below the next tile); every record's
-        // original word and new position (combined id or moved entry) go to e_sort at its rank
+        // pack the remaining plain entries (record indices) to the front, tile by tile of kCombU
+        // records per thread (a tile is loaded before any of its stores, and stores land below the
+        // next tile); every record's original word and new position (combined id or moved entry)
+        // go to e_sort at its rank
         uint32_t cursor = 0u;
-        for (uint32_t t = 0; t < cnt; t += kCombThreads) {
-            const uint32_t k = t + threadIdx.x;
-            uint32_t keep = 0u, rec = 0u, eo = 0u, v = 0u;
-            if (k < cnt) {
-                rec = E[s0 + k];
-                eo = P.e_orig[s0 + k];  // (this thread's own store of the reduce pass)
+        for (uint32_t t = 0; t < cnt; t += kCombU * kCombThreads) {
+            uint32_t rec[kCombU], eo[kCombU], v[kCombU], nk = 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                rec[u] = k < cnt ? E[s0 + k] : 0u;
+                eo[u] = k < cnt ? P.e_orig[s0 + k] : 0u;  // (this thread's own store of the reduce pass)
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                v[u] = ~0u;  // ~0: kept (its new position follows the scan)
+                if (k >= cnt) continue;
                 uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
                 if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
                     uint4 e[4];
-                    rec_entry(P, rec, e);
+                    rec_entry(P, rec[u], e);
                     const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
                                               e[2].y & 0xFFFFu};
                     j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
                 }
-                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) v = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
-                else keep = 1u;
+                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) v[u] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                else ++nk;
             }
             uint32_t kept;
-            const uint32_t pos = block_excl_scan(keep, L.wsum, kept);
-            if (keep) {
-                v = (uint32_t)(s0 + cursor + pos);  // the entry moved
-                E[s0 + cursor + pos] = rec;
-            }
-            if (k < cnt) {
-                const uint32_t rc = min((eo & kEntRecMask) - chunk * kFlowChunk, kFlowChunk - 1u);
+            uint32_t pos = cursor + block_excl_scan(nk, L.wsum, kept);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                if (k >= cnt) continue;
+                if (v[u] == ~0u) {
+                    v[u] = (uint32_t)(s0 + pos);  // the entry moved
+                    E[s0 + pos] = rec[u];
+                    ++pos;
+                }
+                const uint32_t rc = min((eo[u] & kEntRecMask) - chunk * kFlowChunk, kFlowChunk - 1u);
                 const uint32_t rank = L.bmp[rc >> 6] + (uint32_t)__popcll(L.bm[rc >> 6] & ((1ull << (rc & 63u)) - 1ull));
-                P.e_sort[s0 + min(rank, cnt - 1u)] = make_uint2(eo, v);
+                P.e_sort[s0 + min(rank, cnt - 1u)] = make_uint2(eo[u], v[u]);
             }
             cursor += kept;
         }
