@@ -932,41 +932,9 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         }
         __syncthreads();
         // reduce per key (a key the table cannot take stays a plain entry), kCombU records per
-        // thread at a time with their loads in flight together.  A thread sums its consecutive
-        // records of one key in registers and adds them to the key's fields when the key changes:
-        // in a hot group most of a wavefront's lanes hold the same key, and one LDS atomic per
-        // record and field serialised 64 lanes on one address (C4 Zipf(1.1) K1c 328 -> DESIGN us).
-        uint32_t aj = ~0u, a_pk = 0u, a_hash = 0u, a_meta = 0u, a_first = ~0u, a_last = 0u, a_hcnt = 0u, a_mask = 0u,
-                 a_end = ~0u, a_ch[4] = {~0u, ~0u, ~0u, ~0u};
-        unsigned long long a_by[4] = {0ull, 0ull, 0ull, 0ull};
-        auto flush = [&]() {
-            if (aj == ~0u) return;
-            uint32_t* f = L.f + aj * kCombF;
-#pragma unroll
-            for (uint32_t q = 0; q < 4u; ++q)
-                if (a_by[q]) atomicAdd(&L.bytes[aj * 4 + q], a_by[q]);
-            atomicAdd(f + kCfPk, a_pk);
-            atomicAdd(f + kCfRecs, (a_pk & 0xFFFFu) + (a_pk >> 16));
-            f[kCfHash] = a_hash;  // every lane of the key stores the same word
-            f[kCfMeta] = a_meta;
-            atomicMin(f + kCfFirst, a_first);
-            atomicMax(f + kCfLast, a_last);
-            if (a_hcnt) {
-                atomicAdd(f + kCfHcnt, a_hcnt);
-                if (a_mask) atomicOr(f + kCfMask, a_mask);
-#pragma unroll
-                for (uint32_t q = 0; q < 4u; ++q)
-                    if (a_ch[q] != ~0u) atomicMin(f + kCfChar + q, a_ch[q]);
-                if (a_end != ~0u) atomicMin(f + kCfEnd, a_end);
-            }
-            a_pk = a_hcnt = a_mask = a_last = 0u;
-            a_first = a_end = ~0u;
-#pragma unroll
-            for (uint32_t q = 0; q < 4u; ++q) {
-                a_ch[q] = ~0u;
-                a_by[q] = 0ull;
-            }
-        };
+        // thread at a time with their loads in flight together.  (Measured and not kept: four
+        // records per thread, C4 Zipf(1.1) K1c 328 -> 415 us; a thread's consecutive records of
+        // one key summed in registers before the LDS atomics, 328 -> 342 us.)
         for (uint32_t k0 = 0; k0 < cnt; k0 += kCombU * kCombThreads) {
             uint32_t wv[kCombU];
             uint4 rv[kCombU][4];
@@ -999,30 +967,25 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
                 if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
                 if (no_slot) continue;
-                if (j != aj) {  // another key: the accumulated one goes to the table
-                    flush();
-                    aj = j;
-                }
                 const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
-                a_by[orig ? 0 : 1] += e[2].z;
-                a_by[orig ? 2 : 3] += e[2].w;
-                a_pk += orig ? 1u : 0x10000u;
-                a_hash = e[3].w;
-                a_meta = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
-                a_first = min(a_first, rec);
-                a_last = max(a_last, rec);
+                uint32_t* f = L.f + j * kCombF;
+                atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
+                atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e[2].w);
+                atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
+                atomicAdd(f + kCfRecs, 1u);
+                f[kCfHash] = e[3].w;  // every lane of the key stores the same word
+                f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
+                atomicMin(f + kCfFirst, rec);
+                atomicMax(f + kCfLast, rec);
                 if (e[3].z & 0x10000u) {
-                    ++a_hcnt;
+                    atomicAdd(f + kCfHcnt, 1u);
                     const uint32_t b = hist_bit(e[3].z & 0xFFu);
-                    if (b < 16u) a_mask |= 1u << b;
-#pragma unroll
-                    for (uint32_t q = 0; q < 4u; ++q)
-                        if (b == q) a_ch[q] = min(a_ch[q], rec);
-                    if ((e[3].z >> 8) & kTcpFinRst) a_end = min(a_end, rec << 5 | b);  // (rec < 2^27)
+                    if (b < 16u) atomicOr(f + kCfMask, 1u << b);
+                    if (b < 4u) atomicMin(f + kCfChar + b, rec);
+                    if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec << 5 | b);  // (rec < 2^27)
                 }
             }
         }
-        flush();
         __syncthreads();
         // number the keys met more than once; one global atomic per group for their ids
         constexpr uint32_t kPer = kCombSlots / kCombThreads;
