@@ -49,6 +49,8 @@ struct UpdScratch {
     uint2* e_sort = nullptr;       // [flow_recs] combined groups' records in record order (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* ctl = nullptr;       // [3] its counters (FlowParams::ctl)
+    uint4* ent_sorted = nullptr;   // [flow_recs] update entries moved into partition order by K1
+                                   // (FB_K1_UNITS=1, experimental), 64 B per record slot
 };
 
 struct fb_ctx {
@@ -113,8 +115,6 @@ struct fb_ctx {
     uint32_t* part_target = nullptr;        // the buffer the next fused parse writes (null: d_rec_part)
     uint4* d_rec_ent = nullptr;             // [flow_recs] update entry (UpdEnt, 64 B) per record slot
     uint4* d_rec_ent2 = nullptr;            // ... of the odd async batches
-    uint4* d_ent_sorted = nullptr;          // [flow_recs] update entries moved into partition order
-                                            // by K1 (FB_K1_UNITS=1, experimental), 64 B per slot
     uint4* ent_buf = nullptr;               // the entries the last fused parse wrote (with part_buf)
     uint4* ent_target = nullptr;            // the entries the next fused parse writes (null: d_rec_ent)
     bool emit_records = true;               // fb_set_session_records: fused calls store SESSION records
@@ -243,6 +243,7 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.e_sort);
     hipFree(u.hot);
     hipFree(u.ctl);
+    hipFree(u.ent_sorted);
     u = UpdScratch();
 }
 
@@ -255,7 +256,9 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
         hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.e_sort, recs * 8ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess) {
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess ||
+        (getenv("FB_K1_UNITS") && atoi(getenv("FB_K1_UNITS")) &&
+         hipMalloc(&u.ent_sorted, recs * 16ull * kUpdEntU4) != hipSuccess)) {
         free_upd_scratch(u);
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     }
@@ -279,10 +282,9 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     hipFree(c->d_rec_part2);
     hipFree(c->d_rec_ent);
     hipFree(c->d_rec_ent2);
-    hipFree(c->d_ent_sorted);
     hipFree(c->d_agg_slot);
     c->d_rec_part = c->d_rec_part2 = nullptr;
-    c->d_rec_ent = c->d_rec_ent2 = c->d_ent_sorted = nullptr;
+    c->d_rec_ent = c->d_rec_ent2 = nullptr;
     c->part_recs = nullptr;
     c->part_buf = nullptr;
     c->ent_buf = nullptr;
@@ -294,9 +296,7 @@ static int ensure_flow_scratch(fb_ctx* c, uint64_t recs, hipStream_t s) {
     c->flow_recs = 0;
     if (hipMalloc(&c->d_hword, recs * 4ull) != hipSuccess || hipMalloc(&c->d_rec_part, recs * 4ull) != hipSuccess ||
         hipMalloc(&c->d_rec_ent, recs * 16ull * kUpdEntU4) != hipSuccess ||
-        hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess ||
-        (getenv("FB_K1_UNITS") && atoi(getenv("FB_K1_UNITS")) &&
-         hipMalloc(&c->d_ent_sorted, recs * 16ull * kUpdEntU4) != hipSuccess))
+        hipMalloc(&c->d_agg_slot, (recs / 2 + 1) * 4ull) != hipSuccess)
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     c->flow_recs = recs;
     // combined entries: at most one per two records of the hot groups; a quarter of the batch's
@@ -520,7 +520,6 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_rec_part2);
     hipFree(c->d_rec_ent);
     hipFree(c->d_rec_ent2);
-    hipFree(c->d_ent_sorted);
     hipFree(c->d_agg_slot);
     if (c->upd) hipStreamDestroy(c->upd);
     if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
@@ -1120,9 +1119,9 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
-    if (p.ent && c->d_ent_sorted && flow_units_ok(p.parts)) {  // K1 moves them into partition order
+    if (p.ent && u.ent_sorted && flow_units_ok(p.parts)) {  // K1 moves them into partition order
         p.ent_src = p.ent;
-        p.ent_dst = c->d_ent_sorted;
+        p.ent_dst = u.ent_sorted;
         p.ent = p.ent_dst;
     }
     p.char_call = c->d_char_call;

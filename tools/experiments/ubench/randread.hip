@@ -32,7 +32,44 @@ __global__ __launch_bounds__(256) void k_rand(const uint4* buf, unsigned long lo
             acc.y += a[k].y ^ b[k].x;
         }
     }
-    if (acc.x == 0x12345678u) out[tid] = acc;
+    if (acc.x == 0x12345678u) out[tid & ((1u << 20) - 1u)] = acc;
+}
+
+
+// Two lanes per unit: lanes 2i and 2i+1 read the two 16-B halves of unit(2i) in one instruction and
+// of unit(2i+1) in the next (one line request per unit instead of two), then swap halves.
+__global__ __launch_bounds__(256) void k_rand_pair(const uint4* buf, unsigned long long units, unsigned long long n,
+                                                   uint4* out) {
+    const unsigned long long tid = blockIdx.x * 256ull + threadIdx.x, nt = gridDim.x * 256ull;
+    const uint32_t lane = threadIdx.x & 63u, odd = lane & 1u;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (unsigned long long i0 = tid; i0 < n; i0 += nt * 4) {
+        uint4 a[4], b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned long long i = i0 + k * nt;
+            const unsigned long long u = mix(i) % units;                  // this lane's unit
+            const unsigned long long up = __shfl_xor((long long)u, 1, 64);  // the partner's
+            const unsigned long long ue = odd ? up : u, uo = odd ? u : up;  // unit of lane 2i, of 2i+1
+            a[k] = buf[2 * ue + odd];  // instruction 1: unit(2i), half = lane parity
+            b[k] = buf[2 * uo + odd];  // instruction 2: unit(2i+1)
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // lane 2i keeps a (half 0 of its unit) and takes the partner's a (half 1);
+            // lane 2i+1 keeps b (half 1 of its unit) and takes the partner's b (half 0)
+            const uint4 mine = odd ? b[k] : a[k];
+            const uint4 give = odd ? a[k] : b[k];
+            uint4 other;
+            other.x = __shfl_xor((int)give.x, 1, 64);
+            other.y = __shfl_xor((int)give.y, 1, 64);
+            other.z = __shfl_xor((int)give.z, 1, 64);
+            other.w = __shfl_xor((int)give.w, 1, 64);
+            acc.x ^= mine.x ^ other.y;
+            acc.y += mine.y ^ other.x;
+        }
+    }
+    if (acc.x == 0x12345678u) out[tid & ((1u << 20) - 1u)] = acc;
 }
 
 int main() {
@@ -62,6 +99,21 @@ int main() {
             printf("cluster %3llu span %5llu MB: %8.1f us  %6.2f Greads/s  %7.1f GB/s\n", cl, span >> 20, best * 1e3,
                    n / (best * 1e-3) / 1e9, n * 32.0 / (best * 1e-3) / 1e9);
         }
+    }
+    for (unsigned long long span : spans) {
+        const unsigned long long units = span / 32;
+        float best = 1e9f;
+        for (int r = 0; r < 5; ++r) {
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k_rand_pair, dim3(8192), dim3(256), 0, 0, buf, units, n, out);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (ms < best) best = ms;
+        }
+        printf("paired      span %5llu MB: %8.1f us  %6.2f Greads/s  %7.1f GB/s\n", span >> 20, best * 1e3,
+               n / (best * 1e-3) / 1e9, n * 32.0 / (best * 1e-3) / 1e9);
     }
     return 0;
 }
