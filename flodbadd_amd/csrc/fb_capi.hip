@@ -49,8 +49,6 @@ struct UpdScratch {
     uint2* e_sort = nullptr;       // [flow_recs] combined groups' records in record order (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* ctl = nullptr;       // [3] its counters (FlowParams::ctl)
-    uint4* ent_sorted = nullptr;   // [flow_recs] update entries moved into partition order by K1
-                                   // (FB_K1_UNITS=1, experimental), 64 B per record slot
 };
 
 struct fb_ctx {
@@ -243,7 +241,6 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.e_sort);
     hipFree(u.hot);
     hipFree(u.ctl);
-    hipFree(u.ent_sorted);
     u = UpdScratch();
 }
 
@@ -256,9 +253,7 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
         hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.e_sort, recs * 8ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess ||
-        (getenv("FB_K1_UNITS") && atoi(getenv("FB_K1_UNITS")) &&
-         hipMalloc(&u.ent_sorted, recs * 16ull * kUpdEntU4) != hipSuccess)) {
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess) {
         free_upd_scratch(u);
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     }
@@ -1119,11 +1114,6 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
-    if (p.ent && u.ent_sorted && flow_units_ok(p.parts)) {  // K1 moves them into partition order
-        p.ent_src = p.ent;
-        p.ent_dst = u.ent_sorted;
-        p.ent = p.ent_dst;
-    }
     p.char_call = c->d_char_call;
     c->part_recs = nullptr;
     HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));

@@ -197,10 +197,10 @@ __device__ __forceinline__ uint32_t hist_code(uint32_t has_flags, uint32_t ch) {
 struct PartHist {
     uint32_t* w;
     bool packed;
-    __device__ __forceinline__ uint32_t add(uint32_t p, uint32_t inc = 1u) const {  // returns the old count / cursor
-        if (!packed) return atomicAdd(&w[p], inc);
+    __device__ __forceinline__ uint32_t add(uint32_t p) const {  // returns the old count / cursor
+        if (!packed) return atomicAdd(&w[p], 1u);
         const uint32_t sh = 16u * (p & 1u);
-        return (atomicAdd(&w[p >> 1], inc << sh) >> sh) & 0xFFFFu;
+        return (atomicAdd(&w[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
     }
     __device__ __forceinline__ uint32_t get(uint32_t p) const {
         return packed ? reinterpret_cast<const uint16_t*>(w)[p] : w[p];
@@ -215,13 +215,10 @@ __host__ __device__ inline uint32_t part_hist_bytes(uint32_t parts) {
 }
 // K1 stages its scatter in LDS (the chunk's 4-B words) when the histogram leaves room for it
 __host__ __device__ inline bool k1_staged(uint32_t parts) { return parts <= kFlowPackedParts; }
-// With `units` (k1_units_ok) K1 also moves the fused parse's update entries into partition order
-// and keeps a second histogram of their 32-B units (an IPv6 key takes two)
-__host__ __device__ inline uint32_t k1_lds_bytes(uint32_t parts, bool units = false) {
-    return part_hist_bytes(parts) * (units ? 2u : 1u) + (k1_staged(parts) ? kFlowChunk * 4u : 0u);
+__host__ __device__ inline uint32_t k1_lds_bytes(uint32_t parts) {
+    return part_hist_bytes(parts) + (k1_staged(parts) ? kFlowChunk * 4u : 0u);
 }
-__host__ __device__ inline bool k1_units_ok(uint32_t parts) { return k1_lds_bytes(parts, true) <= 144u * 1024u; }
-static_assert(2u * kFlowChunk < 65536u, "packed K1 counters hold a chunk's records and units");
+static_assert(kFlowChunk < 65536u, "packed K1 counters hold a chunk's records");
 
 // ---------------------------------------------------------------------------------------------
 // K1: bucket one chunk of records by partition (counting sort in LDS).
@@ -236,12 +233,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     if (base >= n) return;
     const uint32_t cnt = min(kFlowChunk, n - base);
     const fb_pkt_out* R = P.recs + base;
-    // with P.ent_src: the update entries move into partition order too (ent_dst; K1c / K2 read them
-    // there through the index words), counted in 32-B units by a second histogram
-    const bool units = P.ent_src != nullptr && P.rec_part != nullptr;
-    const PartHist uh{hist_w + part_hist_bytes(P.parts) / 4u, P.parts > kFlowPackedParts};
-    for (uint32_t j = threadIdx.x; j < part_hist_bytes(P.parts) / 4u * (units ? 2u : 1u); j += kFlowK1Threads)
-        hist_w[j] = 0u;
+    for (uint32_t j = threadIdx.x; j < part_hist_bytes(P.parts) / 4u; j += kFlowK1Threads) hist_w[j] = 0u;
     // every thread owns the chunk's slots threadIdx.x + j * kFlowK1Threads; their partitions stay in
     // registers from the histogram pass to the scatter pass, and each pass issues all its loads
     // before the first LDS atomic (a loop of load -> atomic iterations waits a full memory round
@@ -307,10 +299,7 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     __syncthreads();  // hist zeroed
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j)
-        if (pv[j] != ~0u) {
-            hist.add(pv[j] & kRecPartMask);
-            if (units) uh.add(pv[j] & kRecPartMask, (pv[j] & kRecV6) ? 2u : 1u);
-        }
+        if (pv[j] != ~0u) hist.add(pv[j] & kRecPartMask);
     __syncthreads();
     // exclusive scan of hist[0..parts): each thread owns E consecutive partitions
     const uint32_t E = (P.parts + kFlowK1Threads - 1u) / kFlowK1Threads;
@@ -319,16 +308,6 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) local += hist.get(j);
     uint32_t total;
     uint32_t run = block_excl_scan(local, wsum, total);
-    if (units) {  // the units' cursors (uniform)
-        uint32_t ul = 0u, ut;
-        for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) ul += uh.get(j);
-        uint32_t urun = block_excl_scan(ul, wsum, ut);
-        for (uint32_t j = j0; j < j0 + E && j < P.parts; ++j) {
-            const uint32_t c = uh.get(j);
-            uh.set(j, urun);
-            urun += c;
-        }
-    }
     uint32_t* row = P.rows + (size_t)blockIdx.x * P.parts;
     const uint32_t hot_min = max(kCombMin, 4u * ((cnt + P.parts - 1u) / P.parts));
     static_assert(kFlowMaxParts / kFlowK1Threads <= 64u, "a thread's partitions fit the hot mask");
@@ -365,60 +344,17 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     // written back piecemeal (C4: 267 MB written per batch for 42 MB of words).
     uint32_t* out = P.entries + base;
     const bool staged = k1_staged(P.parts);
-    uint32_t* stg = hist_w + part_hist_bytes(P.parts) / 4u * (units ? 2u : 1u);
-    if (units) {
-        // the chunk's units in partition order at 2 kFlowChunk units per chunk; kG records per
-        // thread with their unit loads in flight together
-        const uint32_t ubase = blockIdx.x * 2u * kFlowChunk;
-        constexpr uint32_t kG = 4;
+    uint32_t* stg = hist_w + part_hist_bytes(P.parts) / 4u;
 #pragma unroll
-        for (uint32_t j0 = 0; j0 < kPer; j0 += kG) {
-            uint4 a[kG], bq[kG], c6[kG], d6[kG];
-#pragma unroll
-            for (uint32_t u = 0; u < kG; ++u) {
-                const uint32_t k = threadIdx.x + (j0 + u) * kFlowK1Threads;
-                const uint32_t src = ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j0 + u] >> kRecUnitShift) & 127u);
-                if (pv[j0 + u] != ~0u) {
-                    const uint4* q = P.ent_src + (size_t)src * 2u;
-                    a[u] = q[0];
-                    bq[u] = q[1];
-                    if (pv[j0 + u] & kRecV6) {
-                        c6[u] = q[2];
-                        d6[u] = q[3];
-                    }
-                }
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kG; ++u) {
-                const uint32_t v = pv[j0 + u];
-                if (v == ~0u) continue;
-                const bool v6 = (v & kRecV6) != 0u;
-                const uint32_t d = hist.add(v & kRecPartMask);
-                const uint32_t du = ubase + uh.add(v & kRecPartMask, v6 ? 2u : 1u);
-                uint4* o = P.ent_dst + (size_t)du * 2u;
-                o[0] = a[u];
-                o[1] = bq[u];
-                if (v6) {
-                    o[2] = c6[u];
-                    o[3] = d6[u];
-                }
-                const uint32_t w = du | (v6 ? kEntV6 : 0u);
-                if (staged) stg[d] = w;
-                else out[d] = w;
-            }
-        }
-    } else {
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; ++j) {
-            if (pv[j] == ~0u) continue;
-            const uint32_t k = threadIdx.x + j * kFlowK1Threads;
-            const uint32_t d = hist.add(pv[j] & kRecPartMask);
-            const uint32_t w = P.rec_part ? ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j] >> kRecUnitShift) & 127u) |
-                                                ((pv[j] & kRecV6) ? kEntV6 : 0u)
-                                          : (base + k) | (pv[j] >> 16) << kEntCodeShift;
-            if (staged) stg[d] = w;
-            else out[d] = w;
-        }
+    for (uint32_t j = 0; j < kPer; ++j) {
+        if (pv[j] == ~0u) continue;
+        const uint32_t k = threadIdx.x + j * kFlowK1Threads;
+        const uint32_t d = hist.add(pv[j] & kRecPartMask);
+        const uint32_t w = P.rec_part ? ((base + k) >> 6) * kUpdUnitsPerSeg + ((pv[j] >> kRecUnitShift) & 127u) |
+                                            ((pv[j] & kRecV6) ? kEntV6 : 0u)
+                                      : (base + k) | (pv[j] >> 16) << kEntCodeShift;
+        if (staged) stg[d] = w;
+        else out[d] = w;
     }
     if (staged) {
         __syncthreads();
@@ -904,7 +840,8 @@ struct CombLds {
     uint32_t pool_next, pool_end;  // this workgroup's reserved combined-entry ids
 };
 static_assert(sizeof(CombLds) <= 40u * 1024u, "four K1c workgroups per CU");
-static_assert(kFlowChunk % 64u == 0u && 2u * kCombThreads >= kCombBm, "two bitmap words per thread");
+static_assert(kFlowChunk % 64u == 0u, "whole bitmap words");
+constexpr uint32_t kCombBmPer = (kCombBm + kCombThreads - 1u) / kCombThreads;  // bitmap words per thread
 
 __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
@@ -1014,14 +951,21 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint32_t* f = L.f + (threadIdx.x * kPer + u) * kCombF;
             if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
         }
-        {   // the order bitmap's prefix popcounts (thread t: words 2t, 2t + 1)
-            const uint32_t w0 = 2u * threadIdx.x;
-            const uint32_t c0 = w0 < kCombBm ? (uint32_t)__popcll(L.bm[w0]) : 0u;
-            const uint32_t c1 = w0 + 1u < kCombBm ? (uint32_t)__popcll(L.bm[w0 + 1u]) : 0u;
+        {   // the order bitmap's prefix popcounts (thread t: words kCombBmPer t ..)
+            const uint32_t w0 = kCombBmPer * threadIdx.x;
+            uint32_t c[kCombBmPer], sum = 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < kCombBmPer; ++u) {
+                c[u] = w0 + u < kCombBm ? (uint32_t)__popcll(L.bm[w0 + u]) : 0u;
+                sum += c[u];
+            }
             uint32_t tot;
-            const uint32_t ex = block_excl_scan(c0 + c1, L.wsum, tot);
-            if (w0 < kCombBm) L.bmp[w0] = (uint16_t)ex;
-            if (w0 + 1u < kCombBm) L.bmp[w0 + 1u] = (uint16_t)(ex + c0);
+            uint32_t ex = block_excl_scan(sum, L.wsum, tot);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombBmPer; ++u) {
+                if (w0 + u < kCombBm) L.bmp[w0 + u] = (uint16_t)ex;
+                ex += c[u];
+            }
         }
         __syncthreads();
         // pack the remaining plain entries (record indices) to the front, tile by tile of kCombU
@@ -1405,15 +1349,13 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
     if (threadIdx.x == 0 && c) atomicAdd(d_n, c);
 }
 
-bool flow_units_ok(uint32_t parts) { return k1_units_ok(parts); }
 hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
     static const hipError_t attr = hipFuncSetAttribute(
         (const void*)k_flow_bucket, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)std::max(k1_lds_bytes(kFlowMaxParts), k1_lds_bytes(kFlowPackedParts)));
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads),
-                       k1_lds_bytes(p.parts, p.ent_src != nullptr && p.rec_part != nullptr), s, p);
+    hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), k1_lds_bytes(p.parts), s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (p.hot) {

@@ -265,9 +265,6 @@ struct FlowParams {
                                 // histogram pass then reads 4 B per record instead of the record
     const uint4* ent;           // non-null (with rec_part): the slots' update entries (UpdEnt), which
                                 // K1c / K2 read instead of the records
-    const uint4* ent_src = nullptr;  // non-null (with rec_part): K1 moves the parse's update entries
-    uint4* ent_dst = nullptr;        // (ent_src) into partition order in ent_dst (= ent, 2 kFlowChunk
-                                     // units per chunk), and the index words point there
     uint4* char_call = nullptr; // [capacity] per slot: the update call of the flow's first S, s, H, h
                                 // (FB_CALL_NONE: none), for the multi-GPU merge (fb_flow_merge_dev)
 };
@@ -371,7 +368,6 @@ hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, ui
 // One table update = launch_flow_bucket (K1 bucketing, K1c hot-group combine), launch_flow_transpose
 // (K1t) and launch_flow_apply (K2; with transpose = true K1t first) -- separate calls so the
 // pipelined path can put them on different streams.
-bool flow_units_ok(uint32_t parts);  // K1 can move the update entries (LDS for two histograms)
 hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_transpose(const FlowParams& p, uint32_t chunks, hipStream_t s);
 hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s, bool transpose = true);
