@@ -48,7 +48,7 @@ struct UpdScratch {
     uint32_t* e_orig = nullptr;    // [flow_recs] combined groups' original entry words (history)
     uint2* e_sort = nullptr;       // [flow_recs] combined groups' records in record order (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
-    uint32_t* ctl = nullptr;       // [3] its counters (FlowParams::ctl)
+    uint32_t* ctl = nullptr;       // [4] its counters (FlowParams::ctl)
 };
 
 struct fb_ctx {
@@ -253,11 +253,11 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
         hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.e_sort, recs * 8ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 12) != hipSuccess) {
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 16) != hipSuccess) {
         free_upd_scratch(u);
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     }
-    HIP_TRY(hipMemsetAsync(u.ctl, 0, 12, s));
+    HIP_TRY(hipMemsetAsync(u.ctl, 0, 16, s));
     return FB_OK;
 }
 

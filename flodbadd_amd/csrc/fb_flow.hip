@@ -375,6 +375,7 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
         P.ctl[0] = 0u;
         P.ctl[1] = 0u;
         P.ctl[2] = 0u;
+        P.ctl[3] = 0u;
     }
     for (uint32_t y = ty; y < 64u; y += 4u) {
         const uint32_t c = c0 + y, p = p0 + tx;
@@ -838,6 +839,7 @@ struct CombLds {
     uint32_t wsum[kCombThreads / 64];
     uint32_t base;
     uint32_t pool_next, pool_end;  // this workgroup's reserved combined-entry ids
+    uint32_t grp_next;             // the group this workgroup took from the list
 };
 static_assert(sizeof(CombLds) <= 40u * 1024u, "four K1c workgroups per CU");
 static_assert(kFlowChunk % 64u == 0u, "whole bitmap words");
@@ -853,7 +855,15 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     if (threadIdx.x == 0) L.pool_next = L.pool_end = 0u;  // published by the group loop's first barrier
     uint32_t* E = P.entries;
     uint4* CE = reinterpret_cast<uint4*>(P.comb);
-    for (uint32_t h = blockIdx.x; h < n_hot; h += gridDim.x) {
+    // Groups are taken one at a time (ctl[3]), not by a fixed stride: their sizes vary by 50x under
+    // skew (48 .. ~2,500 records), and with the stride the busiest workgroup held 2.2x the mean's
+    // records (C4 Zipf(1.1) K1c 346 -> 288 us).  (Big groups first, from the back of the list:
+    // K1c -5 us, K1 +7 us; not kept.)
+    for (;;) {
+        if (threadIdx.x == 0) L.grp_next = atomicAdd(P.ctl + 3, 1u);
+        __syncthreads();  // (every thread read the previous value before the last group's barriers)
+        const uint32_t h = L.grp_next;
+        if (h >= n_hot) break;  // (uniform)
         const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;

@@ -256,7 +256,8 @@ struct FlowParams {
                                 // its entry order from partials[4 p + 3] >> 32 (coalesced writes)
     uint32_t* hcount;           // [capacity] history characters each slot got this update (K2)
     uint32_t* hot;              // [hot_cap] (chunk << 16 | part) groups K1 hands to k_flow_combine
-    uint32_t* ctl;              // [3] hot groups, combined entries, hword entries (reset by K1t)
+    uint32_t* ctl;              // [4] hot groups, combined entries, hword entries, K1c's next group
+                                // (reset by K1t)
     uint32_t* agg_slot;         // [max_recs / 2 + 1] table slot of each combined entry
     uint32_t hot_cap;
     uint32_t* part_base;        // [parts + 1] the history's output offset per partition (history)
