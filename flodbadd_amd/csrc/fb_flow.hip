@@ -859,10 +859,15 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     // skew (48 .. ~2,500 records), and with the stride the busiest workgroup held 2.2x the mean's
     // records (C4 Zipf(1.1) K1c 346 -> 288 us).  (Big groups first, from the back of the list:
     // K1c -5 us, K1 +7 us; not kept.)
-    for (;;) {
-        if (threadIdx.x == 0) L.grp_next = atomicAdd(P.ctl + 3, 1u);
-        __syncthreads();  // (every thread read the previous value before the last group's barriers)
-        const uint32_t h = L.grp_next;
+    // The first group of a workgroup is its block index (a batch with few hot groups costs no
+    // atomics in the workgroups that have none: 1,024 grabs on an empty list took 9 us).
+    for (uint32_t it = 0;; ++it) {
+        uint32_t h = blockIdx.x;
+        if (it != 0u) {
+            if (threadIdx.x == 0) L.grp_next = gridDim.x + atomicAdd(P.ctl + 3, 1u);
+            __syncthreads();  // (every thread read the previous value before the last group's barriers)
+            h = L.grp_next;
+        }
         if (h >= n_hot) break;  // (uniform)
         const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
