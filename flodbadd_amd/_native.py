@@ -273,7 +273,8 @@ class DeviceBuffer:
 
     def upload(self, arr, stream=None):
         arr = np.ascontiguousarray(arr)
-        assert arr.nbytes <= self.nbytes
+        if arr.nbytes > self.nbytes:
+            raise ValueError("upload of %d bytes into a %d-byte device buffer" % (arr.nbytes, self.nbytes))
         check(gpu_lib().fb_memcpy_h2d(self.ptr, ptr(arr), arr.nbytes, stream))
         if stream is None:
             check(gpu_lib().fb_stream_sync(None))

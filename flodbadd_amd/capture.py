@@ -60,7 +60,8 @@ class FlodbaddGpuCapture:
         cfg.filter = int(session_filter)
         if service_bitmap is not None:
             bm = np.ascontiguousarray(np.frombuffer(bytes(service_bitmap), dtype=np.uint8))
-            assert bm.size == 8192
+            if bm.size != 8192:
+                raise ValueError("service bitmap must be 8192 bytes (one bit per port), got %d" % bm.size)
             self._keep.append(bm)
             cfg.service_bitmap = bm.ctypes.data
         lt = lan_v6_table(list(lan_v6))
@@ -96,7 +97,8 @@ class FlodbaddGpuCapture:
 
     def set_service_bitmap(self, bitmap):
         bm = np.ascontiguousarray(np.frombuffer(bytes(bitmap), dtype=np.uint8))
-        assert bm.size == 8192
+        if bm.size != 8192:
+            raise ValueError("service bitmap must be 8192 bytes (one bit per port), got %d" % bm.size)
         N.check(N.gpu_lib().fb_set_service_bitmap(self.ctx, N.ptr(bm)))
 
     def set_lan_v6(self, prefixes):

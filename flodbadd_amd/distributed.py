@@ -71,7 +71,9 @@ def exchange_merge(dist, mrecs, counts, merge, device=None, group=None):
     dev = torch.device("cpu") if device is None else torch.device(device)
     world = dist.get_world_size(group)
     counts = [int(c) for c in counts]
-    assert len(counts) == world and sum(counts) == int(mrecs.shape[0]), (counts, mrecs.shape)
+    if len(counts) != world or sum(counts) != int(mrecs.shape[0]):
+        raise ValueError("group sizes %s do not cover the %d exported records of %d ranks"
+                         % (counts, int(mrecs.shape[0]), world))
     if world > 1:
         send_n = torch.tensor(counts, dtype=torch.int64, device=dev)
         recv_n = torch.empty_like(send_n)
