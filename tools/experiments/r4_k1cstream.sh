@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT}"
 R=$(pwd); OUT=$R/gpurun_out/r4ks; rm -rf "$OUT"; mkdir -p "$OUT"
 X="--no-cpu-baseline --no-host --no-imix --no-other-mode --no-single-launch --table-only --config 4 --steps 20 --warmup 3"
 for rep in 1 2; do
-  for v in product k1cpar; do
+  for v in product ${VARS:-k1cpar}; do
     L=""; [ "$v" != product ] && L=$R/flodbadd_amd/build/var_$v.so
     for z in "" "--zipf 1.1"; do
       FLODBADD_GPU_LIB=$L timeout -k 10 200 python3 bench.py $z $X > "$OUT/$v$rep${z:+z}.json" 2> "$OUT/$v$rep${z:+z}.err" || { tail -3 "$OUT/$v$rep${z:+z}.err"; exit 1; }
