@@ -687,6 +687,25 @@ def spawn_ranks(n, argv):
     return status
 
 
+_result_out = None  # the process's original stdout: only the result line goes there (_emit)
+
+
+def _quiet_stdout():
+    """Send fd 1 to stderr for the rest of the run, keeping the original stdout for the one result
+    line: libraries write their notices to fd 1 from native code (gloo's "Rank r is connected to
+    ... peer ranks", RCCL banners), which would otherwise land before the JSON line."""
+    global _result_out
+    sys.stdout.flush()
+    _result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def _emit(obj):
+    out = _result_out or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def world_check(args, world, rank):
     """--world-check: the launch plumbing only (no GPU): every rank joins the gloo group, the ranks
     all-reduce their rank numbers, rank 0 prints what the group saw."""
@@ -698,9 +717,8 @@ def world_check(args, world, rank):
     if world > 1:
         tdist.all_reduce(t)
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "requested_gpus": args.gpus, "group_size": int(t[1]),
-                          "rank_sum": int(t[0]), "master": "%s:%s" % (os.environ.get("MASTER_ADDR"),
-                                                                       os.environ.get("MASTER_PORT"))}))
+        _emit({"n_gpus": world, "requested_gpus": args.gpus, "group_size": int(t[1]),
+               "rank_sum": int(t[0]), "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))})
     if world > 1:
         tdist.destroy_process_group()
 
@@ -746,6 +764,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py --gpus %d but the launcher started %d ranks" % (args.gpus, world))
+    _quiet_stdout()
     if args.world_check:
         return world_check(args, world, rank)
     dist = None
@@ -919,7 +938,7 @@ def main():
             line["roofline"]["note"] = "rank 0's GPU; every rank's own fraction in per_rank"
         if extra:
             line["extra"] = extra
-        print(json.dumps(line))
+        _emit(line)
     if dist:
         dist.destroy_process_group()
 
