@@ -67,7 +67,8 @@ def generate(config_id, n, first=0, threads=None, frames_out=None, **overrides):
     if frames_out is None:
         frames = np.empty(max(total, 1), dtype=np.uint8)[:total]
     else:
-        assert frames_out.nbytes >= total
+        if frames_out.nbytes < total:
+            raise ValueError("frames_out holds %d bytes, the batch needs %d" % (frames_out.nbytes, total))
         frames = frames_out[:total]
     if threads is None:
         threads = min(16, os.cpu_count() or 1)

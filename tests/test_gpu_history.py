@@ -194,3 +194,24 @@ def test_history_combine_table_overflow():
     assert max(len(set(v)) for v in groups.values() if len(v) >= 2048) > 256
     gf = _run(batches, capacity=1 << 14)
     assert (gf["hist_len"] > 10000).sum() == 1
+
+
+def test_history_split_list_overflow():
+    """More partitions over kHistSplitEntries (8192 entries to read) than the split list holds
+    (kHistListCap = 256): a 2^18-slot table has 512 partitions and a 5M-record batch over 100K
+    flows puts ~9,800 records into each, so 256 partitions are split by chunk blocks and the rest
+    go whole to k_hist_general's slow list; every flow's history string equals the oracle's."""
+    big = synth.generate(2, 5_000_000, first=0, n_flows=100_000)
+    tail = synth.generate(2, 300_000, first=5_000_000, n_flows=100_000)
+    # precondition (host-side hash): > 256 of the 512 partitions hold > 8192 records
+    lib = N.gpu_lib()
+    recs = coracle.parse_classify(coracle.make_cfg(2), *big)[0]
+    keys = np.ascontiguousarray(np.ascontiguousarray(recs).view(np.uint8).reshape(len(recs), -1)[:, :40])
+    uniq, first, counts = np.unique(keys.view("V40").ravel(), return_index=True, return_counts=True)
+    per_part = np.zeros(512, dtype=np.int64)
+    for i, c in zip(first, counts):
+        per_part[lib.fb_flow_hash(N.ptr(recs[i: i + 1])) >> 55] += c
+    assert (per_part > 8192).sum() > 256, per_part
+    del recs, keys, uniq
+    gf = _run([big, tail], seg=True, capacity=1 << 18)
+    assert len(gf) > 90_000 and (gf["hist_len"] > 20).any()
