@@ -822,6 +822,10 @@ constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4
 #define FB_COMB_JC 2560
 #endif
 constexpr uint32_t kCombJc = FB_COMB_JC;
+#ifndef FB_COMB_U
+#define FB_COMB_U 1  // (4: C4 Zipf K1c 328 -> 415 us)
+#endif
+constexpr uint32_t kCombU = FB_COMB_U;  // records per thread with their loads in flight together
 // The group's records in record order for the history (e_sort): a bitmap of the records' places in
 // the chunk (kFlowChunk bits) and its prefix popcounts; a record's rank = the set bits below it.
 constexpr uint32_t kCombBm = kFlowChunk / 64u;
@@ -844,11 +848,11 @@ constexpr uint32_t kCombBmPer = (kCombBm + kCombThreads - 1u) / kCombThreads;  /
 __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
     const uint32_t n_hot = min(P.ctl[0], P.hot_cap);
-    const uint32_t tid = threadIdx.x;
     // combined-entry ids: a workgroup reserves them `pool` at a time (one returned atomic per group on
     // one address serialised ~19K of them per Zipf C4 batch); the reservations leave most of comb_cap
     // (a quarter of the batch's records) to spare
     const uint32_t pool = max(1u, min(32u, P.comb_cap / (4u * gridDim.x)));
+    if (threadIdx.x == 0) L.pool_next = L.pool_end = 0u;  // published by the group loop's first barrier
     uint32_t* E = P.entries;
     uint4* CE = reinterpret_cast<uint4*>(P.comb);
     // Groups are taken one at a time (ctl[3]), not by a fixed stride: their sizes vary by 50x under
@@ -857,39 +861,20 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     // K1c -5 us, K1 +7 us; not kept.)
     // The first group of a workgroup is its block index (a batch with few hot groups costs no
     // atomics in the workgroups that have none: 1,024 grabs on an empty list took 9 us).
-    // A group is a chain of memory round trips behind workgroup barriers (per-workgroup stamps,
-    // C4 Zipf(1.1): ~5.7 us of a group's ~13 us in the reduce pass -- its index words, then its
-    // records gathered -- and ~3.5 us in the pack pass, which read both back).  So the next group is
-    // fetched while this one is finished: its id two groups ahead, its list word and row one phase
-    // later, then its index words and its first kCombThreads records (registers, one per thread);
-    // and a group's first tile stays in registers from the reduce pass to the pack pass.
-    uint32_t h = blockIdx.x;
-    if (h >= n_hot) return;  // (uniform)
-    if (tid == 0) L.pool_next = L.pool_end = 0u;
-    uint32_t grp = P.hot[h];
-    uint32_t row = P.rows[(size_t)(grp >> 16) * P.parts + (grp & 0xFFFFu)];
-    uint32_t w0 = 0u;  // this group's first tile: index word, record
-    uint4 r0[4];
-    if (tid < (row >> 16)) {
-        w0 = E[(size_t)(grp >> 16) * kFlowChunk + (row & 0xFFFFu) + tid];
-        raw_entry(P, w0, r0);
-    }
-    if (tid == 0) L.grp_next = gridDim.x + atomicAdd(P.ctl + 3, 1u);
-    __syncthreads();  // (also publishes the pool reset)
-    uint32_t hn = L.grp_next, gn = hn < n_hot ? P.hot[hn] : 0u;  // the next group and its list word
-    for (;;) {
-        const uint32_t chunk = grp >> 16, part = grp & 0xFFFFu;
-        uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
-        const uint32_t cnt = row >> 16;
-        const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
-        const bool more = hn < n_hot;  // (uniform)
-        uint32_t nx = 0u, rown = 0u;   // the group after next (thread 0), the next group's row
-        if (more) {
-            if (tid == 0) nx = gridDim.x + atomicAdd(P.ctl + 3, 1u);
-            rown = P.rows[(size_t)(gn >> 16) * P.parts + (gn & 0xFFFFu)];
+    for (uint32_t it = 0;; ++it) {
+        uint32_t h = blockIdx.x;
+        if (it != 0u) {
+            if (threadIdx.x == 0) L.grp_next = gridDim.x + atomicAdd(P.ctl + 3, 1u);
+            __syncthreads();  // (every thread read the previous value before the last group's barriers)
+            h = L.grp_next;
         }
-        for (uint32_t j = tid; j < kCombBm; j += kCombThreads) L.bm[j] = 0ull;
-        for (uint32_t j = tid; j < kCombSlots; j += kCombThreads) {
+        if (h >= n_hot) break;  // (uniform)
+        const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
+        uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
+        const uint32_t row = *rowp, cnt = row >> 16;
+        const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
+        for (uint32_t j = threadIdx.x; j < kCombBm; j += kCombThreads) L.bm[j] = 0ull;
+        for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
             L.tab[j * 6] = 0ull;
 #pragma unroll
             for (uint32_t w = 0; w < 4u; ++w) L.bytes[j * 4 + w] = 0ull;
@@ -898,189 +883,178 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 L.f[j * kCombF + w] = (w == kCfFirst || w == kCfEnd || (w >= kCfChar && w < kCfChar + 4)) ? ~0u : 0u;
         }
         __syncthreads();
-        // reduce per key (a key the table cannot take stays a plain entry), one record per thread
-        // and tile.  (Measured and not kept: four records per thread with their loads in flight, C4
-        // Zipf(1.1) K1c 328 -> 415 us; a thread's consecutive records of one key summed in registers
-        // before the LDS atomics, 328 -> 342 us.)
-        uint32_t eo0 = 0u;  // tile 0's original word, for the pack pass
-        for (uint32_t k0 = 0; k0 < cnt; k0 += kCombThreads) {
-            const uint32_t k = k0 + tid;
-            uint32_t w = w0;
-            uint4 rv[4] = {r0[0], r0[1], r0[2], r0[3]};
-            if (k0 != 0u && k < cnt) {
-                w = E[s0 + k];
-                raw_entry(P, w, rv);
+        // reduce per key (a key the table cannot take stays a plain entry), kCombU records per
+        // thread at a time with their loads in flight together.  (Measured and not kept: four
+        // records per thread, C4 Zipf(1.1) K1c 328 -> 415 us; a thread's consecutive records of
+        // one key summed in registers before the LDS atomics, 328 -> 342 us.)
+        for (uint32_t k0 = 0; k0 < cnt; k0 += kCombU * kCombThreads) {
+            uint32_t wv[kCombU];
+            uint4 rv[kCombU][4];
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = k0 + u * kCombThreads + threadIdx.x;
+                wv[u] = k < cnt ? E[s0 + k] : 0u;
             }
-            if (k >= cnt) continue;
-            uint4 e[4];
-            entry_of(P.ent != nullptr, rv, w, e);
-            // the record's original word for the history (record order key | code: with update
-            // entries rebuilt from the entry -- its pkt_index and character), read back by this
-            // thread in the pack pass (past tile 0: through e_orig); its place in the chunk marked in
-            // the order bitmap
-            const uint32_t eo = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
-            if (k0 == 0u) eo0 = eo;
-            else P.e_orig[s0 + k] = eo;
-            {
-                const uint32_t rc = (eo & kEntRecMask) - chunk * kFlowChunk;  // (< kFlowChunk, distinct)
-                if (rc < kFlowChunk) atomicOr(&L.bm[rc >> 6], 1ull << (rc & 63u));
-            }
-            const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
-                                      e[2].y & 0xFFFFu};
-            uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
-            const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
-            if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
-            if (no_slot) continue;
-            const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
-            uint32_t* f = L.f + j * kCombF;
-            atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
-            atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e[2].w);
-            atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
-            atomicAdd(f + kCfRecs, 1u);
-            f[kCfHash] = e[3].w;  // every lane of the key stores the same word
-            f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
-            atomicMin(f + kCfFirst, rec);
-            atomicMax(f + kCfLast, rec);
-            if (e[3].z & 0x10000u) {
-                atomicAdd(f + kCfHcnt, 1u);
-                const uint32_t b = hist_bit(e[3].z & 0xFFu);
-                if (b < 16u) atomicOr(f + kCfMask, 1u << b);
-                if (b < 4u) atomicMin(f + kCfChar + b, rec);
-                if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec << 5 | b);  // (rec < 2^27)
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u)
+                if (k0 + u * kCombThreads + threadIdx.x < cnt) raw_entry(P, wv[u], rv[u]);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = k0 + u * kCombThreads + threadIdx.x, w = wv[u];
+                if (k >= cnt) continue;
+                uint4 e[4];
+                entry_of(P.ent != nullptr, rv[u], w, e);
+                // the record's original word for the history (record order key | code: with update
+                // entries rebuilt from the entry -- its pkt_index and character), read back by this
+                // thread in the pack pass; its place in the chunk marked in the order bitmap
+                const uint32_t eo = P.ent ? e[3].y | hist_code((e[3].z >> 16) & 1u, e[3].z & 0xFFu) << kEntCodeShift : w;
+                P.e_orig[s0 + k] = eo;
+                {
+                    const uint32_t rc = (eo & kEntRecMask) - chunk * kFlowChunk;  // (< kFlowChunk, distinct)
+                    if (rc < kFlowChunk) atomicOr(&L.bm[rc >> 6], 1ull << (rc & 63u));
+                }
+                const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                          e[2].y & 0xFFFFu};
+                uint32_t j = lds_lookup<6, kCombSlots>(L.tab, key, e[3].w);
+                const bool no_slot = j == ~0u && lds_upsert<6, kCombSlots>(L.tab, key, e[3].w, j) < 0;
+                if (k < kCombJc) L.jc[k] = (no_slot || j >= 255u) ? 0xFFu : (uint8_t)j;
+                if (no_slot) continue;
+                const uint32_t orig = (e[2].y >> 16) & 1u, rec = e[3].y;
+                uint32_t* f = L.f + j * kCombF;
+                atomicAdd(&L.bytes[j * 4 + (orig ? 0u : 1u)], (unsigned long long)e[2].z);
+                atomicAdd(&L.bytes[j * 4 + (orig ? 2u : 3u)], (unsigned long long)e[2].w);
+                atomicAdd(f + kCfPk, orig ? 1u : 0x10000u);
+                atomicAdd(f + kCfRecs, 1u);
+                f[kCfHash] = e[3].w;  // every lane of the key stores the same word
+                f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
+                atomicMin(f + kCfFirst, rec);
+                atomicMax(f + kCfLast, rec);
+                if (e[3].z & 0x10000u) {
+                    atomicAdd(f + kCfHcnt, 1u);
+                    const uint32_t b = hist_bit(e[3].z & 0xFFu);
+                    if (b < 16u) atomicOr(f + kCfMask, 1u << b);
+                    if (b < 4u) atomicMin(f + kCfChar + b, rec);
+                    if ((e[3].z >> 8) & kTcpFinRst) atomicMin(f + kCfEnd, rec << 5 | b);  // (rec < 2^27)
+                }
             }
         }
-        // the next group's index words (its row came in during the reduce pass)
-        const uint32_t cntn = rown >> 16;
-        const size_t sn = (size_t)(gn >> 16) * kFlowChunk + (rown & 0xFFFFu);
-        uint32_t wn = 0u;
-        if (more && tid < cntn) wn = E[sn + tid];
-        if (tid == 0 && more) L.grp_next = nx;
         __syncthreads();
-        const uint32_t hn2 = more ? L.grp_next : ~0u;
-        const uint32_t gn2 = hn2 < n_hot ? P.hot[hn2] : 0u;
         // number the keys met more than once; one global atomic per group for their ids
         constexpr uint32_t kPer = kCombSlots / kCombThreads;
         uint32_t nc = 0u;
 #pragma unroll
-        for (uint32_t u = 0; u < kPer; ++u) nc += L.f[(tid * kPer + u) * kCombF + kCfRecs] >= 2u;
+        for (uint32_t u = 0; u < kPer; ++u) nc += L.f[(threadIdx.x * kPer + u) * kCombF + kCfRecs] >= 2u;
         uint32_t n_comb;
         uint32_t rank = block_excl_scan(nc, L.wsum, n_comb);
-        if (n_comb != 0u) {  // (uniform)
-            if (tid == 0) {
-                uint32_t nx2 = L.pool_next, en = L.pool_end;
-                if (en - nx2 < n_comb) {
-                    const uint32_t g = max(n_comb, pool);
-                    nx2 = atomicAdd(P.ctl + 1, g);
-                    en = nx2 + g;
-                }
-                L.base = nx2;
-                L.pool_next = nx2 + n_comb;
-                L.pool_end = en;
+        if (n_comb == 0u) continue;  // uniform across the block; the table is re-initialised above
+        if (threadIdx.x == 0) {
+            uint32_t nx = L.pool_next, en = L.pool_end;
+            if (en - nx < n_comb) {
+                const uint32_t g = max(n_comb, pool);
+                nx = atomicAdd(P.ctl + 1, g);
+                en = nx + g;
             }
-            __syncthreads();
+            L.base = nx;
+            L.pool_next = nx + n_comb;
+            L.pool_end = en;
         }
+        __syncthreads();
         const uint32_t id0 = L.base;
-        // a group with no key met twice, or no room for its combined entries, stays as it is
-        const bool go = n_comb != 0u && id0 + n_comb <= P.comb_cap;  // (uniform)
-        if (go) {
+        if (id0 + n_comb > P.comb_cap) continue;  // no room for its combined entries: the group stays plain
 #pragma unroll
-            for (uint32_t u = 0; u < kPer; ++u) {
-                uint32_t* f = L.f + (tid * kPer + u) * kCombF;
-                if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
-            }
-            {   // the order bitmap's prefix popcounts (thread t: words kCombBmPer t ..)
-                const uint32_t w0b = kCombBmPer * tid;
-                uint32_t c[kCombBmPer], sum = 0u;
-#pragma unroll
-                for (uint32_t u = 0; u < kCombBmPer; ++u) {
-                    c[u] = w0b + u < kCombBm ? (uint32_t)__popcll(L.bm[w0b + u]) : 0u;
-                    sum += c[u];
-                }
-                uint32_t tot;
-                uint32_t ex = block_excl_scan(sum, L.wsum, tot);
-#pragma unroll
-                for (uint32_t u = 0; u < kCombBmPer; ++u) {
-                    if (w0b + u < kCombBm) L.bmp[w0b + u] = (uint16_t)ex;
-                    ex += c[u];
-                }
-            }
-            __syncthreads();
+        for (uint32_t u = 0; u < kPer; ++u) {
+            uint32_t* f = L.f + (threadIdx.x * kPer + u) * kCombF;
+            if (f[kCfRecs] >= 2u) f[kCfId] = rank++;
         }
-        // the next group's first records, gathered while this one is packed
-        uint4 rn[4];
-        if (more && tid < cntn) raw_entry(P, wn, rn);
-        if (go) {
-            // pack the remaining plain entries (record indices) to the front, tile by tile (a tile is
-            // loaded before any of its stores, and stores land below the next tile); every record's
-            // original word and new position (combined id or moved entry) go to e_sort at its rank
-            uint32_t cursor = 0u;
-            for (uint32_t t = 0; t < cnt; t += kCombThreads) {
-                const uint32_t k = t + tid;
-                uint32_t rec = w0, eo = eo0, v = ~0u, nk = 0u;  // v ~0: kept (its new position follows the scan)
-                if (t != 0u) {
-                    rec = k < cnt ? E[s0 + k] : 0u;
-                    eo = k < cnt ? P.e_orig[s0 + k] : 0u;  // (this thread's own store of the reduce pass)
-                }
-                if (k < cnt) {
-                    uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
-                    if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
-                        uint4 e[4];
-                        rec_entry(P, rec, e);
-                        const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
-                                                  e[2].y & 0xFFFFu};
-                        j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
-                    }
-                    if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) v = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
-                    else nk = 1u;
-                }
-                uint32_t kept;
-                const uint32_t pos = cursor + block_excl_scan(nk, L.wsum, kept);
-                if (k < cnt) {
-                    if (v == ~0u) {
-                        v = (uint32_t)(s0 + pos);  // the entry moved
-                        E[s0 + pos] = rec;
-                    }
-                    const uint32_t rc = min((eo & kEntRecMask) - chunk * kFlowChunk, kFlowChunk - 1u);
-                    const uint32_t rk = L.bmp[rc >> 6] + (uint32_t)__popcll(L.bm[rc >> 6] & ((1ull << (rc & 63u)) - 1ull));
-                    P.e_sort[s0 + min(rk, cnt - 1u)] = make_uint2(eo, v);
-                }
-                cursor += kept;
-            }
-            // the combined entries (two units each in P.comb) and their index words behind the kept ones
+        {   // the order bitmap's prefix popcounts (thread t: words kCombBmPer t ..)
+            const uint32_t w0 = kCombBmPer * threadIdx.x;
+            uint32_t c[kCombBmPer], sum = 0u;
 #pragma unroll
-            for (uint32_t u = 0; u < kPer; ++u) {
-                const uint32_t j = tid * kPer + u;
-                const uint32_t* f = L.f + j * kCombF;
-                if (f[kCfRecs] < 2u) continue;
-                const uint32_t id = id0 + f[kCfId];
-                const unsigned long long* tw = L.tab + j * 6;
-                const unsigned long long* by = L.bytes + j * 4;
-                uint4* o = CE + (size_t)id * 8u;
-                o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
-                o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
-                o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
-                o[3] = make_uint4(id, f[kCfEnd] == ~0u ? ~0u : f[kCfEnd] >> 5, f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
-                o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
-                o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
-                o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
-                o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta] | (f[kCfEnd] & 31u) << 8);
-                E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
+            for (uint32_t u = 0; u < kCombBmPer; ++u) {
+                c[u] = w0 + u < kCombBm ? (uint32_t)__popcll(L.bm[w0 + u]) : 0u;
+                sum += c[u];
             }
-            if (tid == 0) {  // bit 15: a combined group (the history reads e_sort, and the group's
-                             // original row from rows_h)
-                *rowp = (row & 0x7FFFu) | 0x8000u | ((cursor + n_comb) << 16);
-                P.rows_h[(size_t)chunk * P.parts + part] = row;
+            uint32_t tot;
+            uint32_t ex = block_excl_scan(sum, L.wsum, tot);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombBmPer; ++u) {
+                if (w0 + u < kCombBm) L.bmp[w0 + u] = (uint16_t)ex;
+                ex += c[u];
             }
+        }
+        __syncthreads();
+        // pack the remaining plain entries (record indices) to the front, tile by tile of kCombU
+        // records per thread (a tile is loaded before any of its stores, and stores land below the
+        // next tile); every record's original word and new position (combined id or moved entry)
+        // go to e_sort at its rank
+        uint32_t cursor = 0u;
+        for (uint32_t t = 0; t < cnt; t += kCombU * kCombThreads) {
+            uint32_t rec[kCombU], eo[kCombU], v[kCombU], nk = 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                rec[u] = k < cnt ? E[s0 + k] : 0u;
+                eo[u] = k < cnt ? P.e_orig[s0 + k] : 0u;  // (this thread's own store of the reduce pass)
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                v[u] = ~0u;  // ~0: kept (its new position follows the scan)
+                if (k >= cnt) continue;
+                uint32_t j = k < kCombJc ? L.jc[k] : 0xFFu;
+                if (j == 0xFFu) {  // past the cache, no slot, or slot 255: find the key again
+                    uint4 e[4];
+                    rec_entry(P, rec[u], e);
+                    const uint32_t key[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                                              e[2].y & 0xFFFFu};
+                    j = lds_find<6, kCombSlots>(L.tab, key, e[3].w);
+                }
+                if (j != ~0u && L.f[j * kCombF + kCfRecs] >= 2u) v[u] = kRecFlowCombined | (id0 + L.f[j * kCombF + kCfId]);
+                else ++nk;
+            }
+            uint32_t kept;
+            uint32_t pos = cursor + block_excl_scan(nk, L.wsum, kept);
+#pragma unroll
+            for (uint32_t u = 0; u < kCombU; ++u) {
+                const uint32_t k = t + u * kCombThreads + threadIdx.x;
+                if (k >= cnt) continue;
+                if (v[u] == ~0u) {
+                    v[u] = (uint32_t)(s0 + pos);  // the entry moved
+                    E[s0 + pos] = rec[u];
+                    ++pos;
+                }
+                const uint32_t rc = min((eo[u] & kEntRecMask) - chunk * kFlowChunk, kFlowChunk - 1u);
+                const uint32_t rank = L.bmp[rc >> 6] + (uint32_t)__popcll(L.bm[rc >> 6] & ((1ull << (rc & 63u)) - 1ull));
+                P.e_sort[s0 + min(rank, cnt - 1u)] = make_uint2(eo[u], v[u]);
+            }
+            cursor += kept;
+        }
+        // the combined entries (two units each in P.comb) and their index words behind the kept ones
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+            const uint32_t j = threadIdx.x * kPer + u;
+            const uint32_t* f = L.f + j * kCombF;
+            if (f[kCfRecs] < 2u) continue;
+            const uint32_t id = id0 + f[kCfId];
+            const unsigned long long* tw = L.tab + j * 6;
+            const unsigned long long* by = L.bytes + j * 4;
+            uint4* o = CE + (size_t)id * 8u;
+            o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
+            o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
+            o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
+            o[3] = make_uint4(id, f[kCfEnd] == ~0u ? ~0u : f[kCfEnd] >> 5, f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
+            o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
+            o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
+            o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
+            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta] | (f[kCfEnd] & 31u) << 8);
+            E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
+        }
+        if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_sort, and
+                                 // the group's original row from rows_h)
+            *rowp = (row & 0x7FFFu) | 0x8000u | ((cursor + n_comb) << 16);
+            P.rows_h[(size_t)chunk * P.parts + part] = row;
         }
         __syncthreads();  // the table is re-initialised for the next group
-        if (!more) break;
-        grp = gn;
-        row = rown;
-        w0 = wn;
-#pragma unroll
-        for (uint32_t u = 0; u < 4u; ++u) r0[u] = rn[u];
-        hn = hn2;
-        gn = gn2;
     }
 }
 
