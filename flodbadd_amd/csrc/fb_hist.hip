@@ -302,7 +302,7 @@ struct HistLds {
     uint32_t bm[kBmWords], bmp[kBmWords];    // a long run's records as a bitmap, prefix popcounts
     uint32_t cursor[kFlowSlots], bcnt[kFlowSlots];
     uint32_t rs[kHistRuns];      // run r (chunk c0 + r): its first entry position
-    uint32_t rn[kHistRuns];      // its entries to read (bit 31: a combined group, e_orig)
+    uint32_t rn[kHistRuns];      // its entries to read (bit 31: a combined group, e_sort)
     uint32_t rp[kHistRuns + 1];  // exclusive prefix of rn
     uint32_t rq[kHistRuns];      // the history word of its first applied entry
     uint32_t lst[kHistRuns];     // the batch's runs of more than 64 entries (then of 17..64: from the back)
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist_general(const FlowPara
         auto round = [&](uint32_t c0, uint32_t nr) {
             const uint32_t c = c0 + tid;
             const bool comb = tid < nr && (vp & 0x8000u) != 0u;
-            // a combined group's original row (its records in e_orig): rows_h, read only for those
+            // a combined group's original row (its records in e_sort): rows_h, read only for those
             const uint32_t vh = comb ? P.rows_h[(size_t)c * P.parts + q] : 0u;
             const uint32_t lp = tid < nr ? vp >> 16 : 0u, lv = comb ? vh >> 16 : lp;  // applied / read entries
             L.rs[tid] = c * kFlowChunk + (vp & 0x7FFFu);  // (k_flow_combine packs a group in place)

@@ -246,7 +246,7 @@ struct FlowParams {
     uint32_t chunk_stride;      // >= ceil(max_recs / kFlowChunk)
     uint32_t batch;             // update call number since create / clear (positions' high word)
     uint32_t* rows_h;           // [chunks][parts] a combined group's row before k_flow_combine (K1c;
-                                // the history reads its records from e_orig); a combined group's
+                                // the history reads its records from e_sort); a combined group's
                                 // row in rows / cols has bit 15 set
     uint32_t* e_orig;           // [max_recs] K1c scratch: a combined group's original entry words
     uint2* e_sort;              // [max_recs] a combined group's records in record order (K1c): the
