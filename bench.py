@@ -470,6 +470,27 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                      "fb_flow_merge_dev on each owner, all_gather of the merged records (left on the device)")
 
 
+def stream_copy(device, nbytes=1 << 30, reps=20):
+    """the measured stream-copy bandwidth beside the 8 TB/s spec -- a 16-B-per-lane
+    copy kernel (libfb_bwref.so, fb_bwref.hip) over `nbytes` (well past the 256 MB Infinity Cache),
+    timed with events on the stream it runs on; read + written bytes / time.
+    `roofline.frac_of_copy` relates the dominant kernel to what a plain copy reaches on the same GPU
+    (a reference point, not the product path; hipMemcpyAsync device to device reached only
+    ~4.7 TB/s, so it is not the yardstick)."""
+    from flodbadd_amd import _native as N
+    lib = C.CDLL(os.path.join(N.PKG, "libfb_bwref.so"))
+    lib.fb_bwref_copy.restype = C.c_int
+    lib.fb_bwref_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_float)]
+    N.check(N.gpu_lib().fb_set_device(device))
+    src, dst = N.DeviceBuffer(nbytes), N.DeviceBuffer(nbytes)
+    ms = C.c_float()
+    rc = lib.fb_bwref_copy(dst.ptr, src.ptr, nbytes, reps, C.byref(ms))
+    del src, dst
+    if rc != 0:
+        raise RuntimeError("fb_bwref_copy failed: %d" % rc)
+    return round(2.0 * nbytes * reps / (ms.value / 1e3) / 1e9, 1)
+
+
 def usable_cores():
     """Host cores this process may use: the CPU affinity set, capped by the cgroup CPU quota (the
     GPU box's CPU share) and by OMP_NUM_THREADS when the harness sets it to that share.  Returns
@@ -743,6 +764,7 @@ def main():
                     help="output layout: per-wavefront segments (default) or one batch-wide compaction")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
     ap.add_argument("--no-single-launch", action="store_true", help="skip timing one batch per launch")
+    ap.add_argument("--no-copy-ref", action="store_true", help="skip the stream-copy bandwidth reference")
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
                          "default = the rotated batches (C2 / C3 32), 1 for C4")
@@ -888,6 +910,12 @@ def main():
         except Exception as e:  # the exchange is reported, never allowed to break the bench line
             extra["c5_flow_reduce"] = {"error": repr(e)[:300]}
 
+    copy_gbs = None
+    if rank == 0 and not args.no_copy_ref:  # (after the timed region)
+        try:
+            copy_gbs = stream_copy(device)
+        except Exception as e:  # a reference point: reported, never allowed to break the bench line
+            print("stream copy reference failed: %r" % (e,), file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(main_r["frames"], main_r["offs"], args.cpu_seconds)
@@ -929,7 +957,9 @@ def main():
                          "algo_bytes_per_launch": int(algo_per_launch),
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 5),
                          "launches": main_r["launches"],
-                         "timed_region_host_us_outside_kernels": main_r["host_us"]},
+                         "timed_region_host_us_outside_kernels": main_r["host_us"],
+                         "stream_copy_GBs": copy_gbs,
+                         "frac_of_copy": round(achieved / copy_gbs, 4) if copy_gbs else None},
             "cpu_baseline": cpu,
             "batch_stats": main_r["stats"],
         }

@@ -114,3 +114,16 @@ def test_bench_launch_plan():
             p = bench.plan_launches(k, bpl)
             assert sum(p) == k and all(1 <= c <= bpl for c in p)
             assert len(p) == -(-k // bpl) and (not p or max(p) - min(p) <= 1)
+
+
+def test_bandwidth_reference_is_outside_the_product():
+    """bench.py's stream-copy reference lives in its own library (libfb_bwref.so), not in the C ABI."""
+    from flodbadd_amd.build import build_bwref
+    path = build_bwref()
+    lib = C.CDLL(path)
+    assert hasattr(lib, "fb_bwref_copy")
+    out = subprocess.run(["nm", "-D", "--defined-only", N.GPU_LIB_PATH], capture_output=True, text=True).stdout
+    assert "fb_bwref" not in out
+    lib.fb_bwref_copy.restype = C.c_int
+    lib.fb_bwref_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    assert lib.fb_bwref_copy(None, None, 16, 1, None) != 0  # invalid arguments: an error, no launch
