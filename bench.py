@@ -791,6 +791,8 @@ def main():
         return world_check(args, world, rank)
     dist = None
     if world > 1:
+        # (torch is imported before the library initialises HIP: imported after it, torch saw no GPU
+        # on the box -- tools/experiments/torch_after_lib.py -- and the C5 exchange needs its tensors)
         import torch.distributed as tdist
         tdist.init_process_group("gloo")
         dist = tdist
