@@ -119,7 +119,6 @@ struct fb_ctx {
     // fb_process_seg_async_dev: updates on the context's own stream, one batch behind the parses
     hipStream_t upd = nullptr;
     hipEvent_t ev_parsed = nullptr;
-    hipEvent_t ev_k1 = nullptr;      // (pipelined) the batch's K1 is done: a K1c helper may start
     // after the last fb_flow_history_dev: it reads the last update's shared scratch (history words,
     // partials, slot counts, combined-entry slots), which the next update rewrites -- that update
     // waits for it on every stream it uses, whichever stream the history ran on
@@ -519,7 +518,6 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_agg_slot);
     if (c->upd) hipStreamDestroy(c->upd);
     if (c->ev_parsed) hipEventDestroy(c->ev_parsed);
-    if (c->ev_k1) hipEventDestroy(c->ev_k1);
     if (c->ev_hist) hipEventDestroy(c->ev_hist);
     for (hipEvent_t e : c->ev_upd)
         if (e) hipEventDestroy(e);
@@ -1118,10 +1116,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
     p.char_call = c->d_char_call;
     c->part_recs = nullptr;
-    HIP_TRY(launch_flow_bucket(p, chunks, s_bucket, split ? c->ev_k1 : nullptr));
+    HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
     if (split) {
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_k1, 0));
-        HIP_TRY(launch_flow_combine_helper(p, s));
         // (K1t stays on the update stream: beside the next batch's parse it takes ~95 us instead of
         // 10, but on the parse stream it delays that parse instead -- C4 12.85 vs 12.57 Gpps)
         HIP_TRY(hipEventRecord(c->ev_parsed, s_bucket));
@@ -1189,7 +1185,6 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     if (!c->upd) {
         if (hipStreamCreateWithFlags(&c->upd, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_parsed, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_upd[0], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_upd[1], hipEventDisableTiming) != hipSuccess)
             return set_err(FB_ERR_HIP, "update stream / events");

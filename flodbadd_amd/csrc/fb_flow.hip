@@ -809,10 +809,6 @@ constexpr uint32_t kCombSlots = FB_COMB_SLOTS;  // keys past a full table stay p
 #endif
 constexpr uint32_t kCombThreads = FB_COMB_THREADS;
 constexpr uint32_t kCombGrid = FB_COMB_GRID;
-#ifndef FB_COMB_HELP
-#define FB_COMB_HELP 0
-#endif
-constexpr uint32_t kCombHelp = FB_COMB_HELP;  // workgroups of the helper launch (0: none)
 static_assert(kCombSlots % kCombThreads == 0, "each thread numbers kCombSlots / kCombThreads keys");
 constexpr uint32_t kCfPk = 0, kCfFirst = 1, kCfLast = 2, kCfEnd = 3, kCfHcnt = 4, kCfMask = 5, kCfChar = 6,
                    kCfRecs = 10, kCfId = 11, kCfHash = 12, kCfMeta = 13, kCombF = 14;  // u32 fields of a key (kCfChar..+3)
@@ -849,7 +845,7 @@ static_assert(sizeof(CombLds) <= 40u * 1024u, "four K1c workgroups per CU");
 static_assert(kFlowChunk % 64u == 0u, "whole bitmap words");
 constexpr uint32_t kCombBmPer = (kCombBm + kCombThreads - 1u) / kCombThreads;  // bitmap words per thread
 
-__global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P, uint32_t helper) {
+__global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams P) {
     __shared__ CombLds L;
     const uint32_t n_hot = min(P.ctl[0], P.hot_cap);
     // combined-entry ids: a workgroup reserves them `pool` at a time (one returned atomic per group on
@@ -865,14 +861,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     // K1c -5 us, K1 +7 us; not kept.)
     // The first group of a workgroup is its block index (a batch with few hot groups costs no
     // atomics in the workgroups that have none: 1,024 grabs on an empty list took 9 us).
-    // A helper launch (FB_COMB_HELP, on the update stream of the pipelined call) takes every group
-    // from the counter, beside the main launch's workgroups; it has nothing to take unless the list
-    // is longer than the main grid.
-    if (helper && n_hot <= kCombGrid) return;
     for (uint32_t it = 0;; ++it) {
         uint32_t h = blockIdx.x;
-        if (it != 0u || helper) {
-            if (threadIdx.x == 0) L.grp_next = kCombGrid + atomicAdd(P.ctl + 3, 1u);
+        if (it != 0u) {
+            if (threadIdx.x == 0) L.grp_next = gridDim.x + atomicAdd(P.ctl + 3, 1u);
             __syncthreads();  // (every thread read the previous value before the last group's barriers)
             h = L.grp_next;
         }
@@ -1372,7 +1364,7 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
     if (threadIdx.x == 0 && c) atomicAdd(d_n, c);
 }
 
-hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s, hipEvent_t ev_k1) {
+hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
     static const hipError_t attr = hipFuncSetAttribute(
         (const void*)k_flow_bucket, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1380,18 +1372,12 @@ hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t 
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), k1_lds_bytes(p.parts), s, p);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && ev_k1) e = hipEventRecord(ev_k1, s);
     if (e != hipSuccess) return e;
     if (p.hot) {
-        hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p, 0u);
+        hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p);
         e = hipGetLastError();
     }
     return e;
-}
-hipError_t launch_flow_combine_helper(const FlowParams& p, hipStream_t s) {
-    if (!p.hot || kCombHelp == 0u) return hipSuccess;
-    hipLaunchKernelGGL(k_flow_combine, dim3(kCombHelp), dim3(kCombThreads), 0, s, p, 1u);
-    return hipGetLastError();
 }
 hipError_t launch_flow_transpose(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;
