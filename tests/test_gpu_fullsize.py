@@ -104,3 +104,33 @@ def test_full_size_c4_session_table(gpu_capture):
     assert np.array_equal(_void_sorted(gflows), _void_sorted(rflows))
     cap.clear_all_sessions()
     assert cap.flow_count() == 0
+
+
+def test_full_size_c4_zipf_session_table(gpu_capture):
+    """The bench's skewed line at full size: 10M + 2M IMIX frames under Zipf(1.1) flow popularity,
+    so ~19K hot (chunk, partition) groups per batch go through k_flow_combine (combined-entry ids
+    from its pool, groups past its key table, the hottest flow at ~12 % of the records) -- every
+    flow row, counters and ordered fields, equals the oracle's."""
+    cap = gpu_capture
+    cap.clear_all_sessions()
+    cfg = coracle.make_cfg(int(SessionFilter.All))
+    flows = coracle.Flows()
+    n_records = 0
+    for n, first in ((10 * FULL, 0), (2 * FULL, 10 * FULL)):
+        frames, offs = synth.generate(4, n, first=first, zipf=1, zipf_s=1.1)
+        g = cap.process_frames_seg(frames, offs)
+        r_out = coracle.parse_classify(cfg, frames, offs)[0]
+        assert g.records.tobytes() == r_out.tobytes(), "session records differ"
+        st = np.zeros(1, dtype=N.STATS_DTYPE)
+        flows.update(r_out, st)
+        assert g.stats["new_sessions"] == int(st[0]["new_sessions"])
+        assert g.stats["updated_sessions"] == int(st[0]["updated_sessions"])
+        n_records += len(r_out)
+        del frames, offs, g, r_out
+    gflows = cap.export_flows()
+    rflows = flows.export_sorted()
+    assert len(gflows) == len(rflows) == cap.flow_count()
+    assert int(gflows["orig_pkts"].sum() + gflows["resp_pkts"].sum()) == n_records
+    assert int(max(gflows["orig_pkts"] + gflows["resp_pkts"])) > n_records // 20  # the skew is there
+    assert np.array_equal(_void_sorted(gflows), _void_sorted(rflows))
+    cap.clear_all_sessions()
