@@ -215,3 +215,14 @@ def test_history_split_list_overflow():
     del recs, keys, uniq
     gf = _run([big, tail], seg=True, capacity=1 << 18)
     assert len(gf) > 90_000 and (gf["hist_len"] > 20).any()
+
+
+def test_history_full_size_zipf():
+    """The bench's skewed C4 batch at full size (10,485,760 IMIX frames, Zipf(1.1)) and a 1M
+    follow-up: every flow's history string, conn_state and ordered fields equal the oracle's --
+    the hottest flows' partitions split by chunk blocks, thousands of combined groups read back in
+    record order through e_sort."""
+    batches = [synth.generate(4, 10 * (1 << 20), first=0, zipf=1, zipf_s=1.1),
+               synth.generate(4, 1 << 20, first=10 * (1 << 20), zipf=1, zipf_s=1.1)]
+    gf = _run(batches, seg=True, capacity=1 << 22)
+    assert (gf["hist_len"] > 100000).any()
