@@ -2,7 +2,7 @@
 # Round 4, closing run at HEAD: every GPU test, smoke(), then the driver's default bench line.
 set -u
 cd "${GRAFT_REPO_ROOT}"
-R=$(pwd); OUT=$R/gpurun_out/r4f2; rm -rf "$OUT"; mkdir -p "$OUT"
+R=$(pwd); OUT=$R/gpurun_out/${RUN_TAG:-r4f2}; rm -rf "$OUT"; mkdir -p "$OUT"
 step() { echo "== $(date +%T) $1" >&2; shift; "$@"; rc=$?; echo "rc=$rc" >&2; [ $rc -eq 0 ] || exit $rc; }
 step tests timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputests.log" 2>&1
 tail -1 "$OUT/gputests.log"
