@@ -119,7 +119,6 @@ struct fb_ctx {
     // fb_process_seg_async_dev: updates on the context's own stream, one batch behind the parses
     hipStream_t upd = nullptr;
     hipEvent_t ev_parsed = nullptr;
-    bool k1_on_upd = false;          // (experiment) the pipelined call buckets on the update stream
     // after the last fb_flow_history_dev: it reads the last update's shared scratch (history words,
     // partials, slot counts, combined-entry slots), which the next update rewrites -- that update
     // waits for it on every stream it uses, whichever stream the history ran on
@@ -439,7 +438,6 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         if (occupancy_parse_dense(&db) != hipSuccess || db < 1) db = 1;
         c->dense_grid = std::min<uint32_t>((uint32_t)(db * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
         if (const char* e = getenv("FB_DENSE_STEAL_POLLS")) c->steal_polls = (uint32_t)strtoul(e, nullptr, 10);
-        if (const char* e = getenv("FB_K1_ON_UPD")) c->k1_on_upd = e[0] == '1';
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -1118,12 +1116,6 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
     p.char_call = c->d_char_call;
     c->part_recs = nullptr;
-    if (split && c->k1_on_upd) {
-        HIP_TRY(hipEventRecord(c->ev_parsed, s_bucket));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_parsed, 0));
-        split = false;
-        s_bucket = s;
-    }
     HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
     if (split) {
         // (K1t stays on the update stream: beside the next batch's parse it takes ~95 us instead of
