@@ -96,8 +96,8 @@ def test_ip_lookup_random_tables(gpu_capture, seed):
 
 @pytest.mark.parametrize("n4,n6", [(3000, 1500), (60000, 6000)])
 def test_flow_enrich_vs_oracle(gpu_capture, n4, n6):
-    """The kernel keeps the top 12 (v4) / 10 (v6) levels of each search in LDS: the small tables
-    fit those trees, the large ones also probe the tables in memory below them."""
+    """Small tables and larger ones (deeper searches, more overlapping ranges); two batches, all
+    flows and only the new ones."""
     from flodbadd_amd.capture import lan_v6_table, own_ip_table
     v4, v6, recs, cidrs, names = _random_tables(7, n4, n6)
     gpu_capture.clear_all_sessions()
@@ -136,3 +136,31 @@ def test_flow_enrich_vs_oracle(gpu_capture, n4, n6):
         gpu_capture.set_blacklists(np.zeros(0, dtype=N.CIDR_DTYPE))
         gpu_capture.clear_all_sessions()
         gpu_capture.set_filter(SessionFilter.All)
+
+
+def test_flow_enrich_full_size(gpu_capture):
+    """The bench's enrichment scale: a 10,485,760-frame C4 batch (~1.45M flows) against IPtoASN-sized
+    tables (500k v4 + 100k v6 ranges) and the blacklists -- every flow's flags, ASN records and
+    blacklist masks equal the oracle's."""
+    v4, v6, recs, cidrs, names = _random_tables(11, 500000, 100000)
+    gpu_capture.clear_all_sessions()
+    gpu_capture.set_asn_tables(v4, v6)
+    gpu_capture.set_blacklists(cidrs)
+    cfg = coracle.make_cfg(2)
+    try:
+        frames, offs = synth.generate(4, 10 * (1 << 20))
+        gpu_capture.process_frames_seg(frames, offs)
+        del frames, offs
+        flows = gpu_capture.export_flows()
+        by_slot = {int(f["slot"]): i for i, f in enumerate(flows)}
+        e = gpu_capture.enrich(new_only=False)
+        assert len(e) == len(flows) > 1_000_000
+        ref = coracle.enrich_keys(cfg, coracle.asn_prepare(v4, 2), coracle.asn_prepare(v6, 10), cidrs,
+                                  flows[[by_slot[int(s)] for s in e["slot"]]])
+        for f in ("flags", "src_asn", "dst_asn", "src_blacklists", "dst_blacklists"):
+            assert np.array_equal(e[f], ref[f]), f
+        assert (e["dst_asn"] >= 0).sum() > 1000
+    finally:
+        gpu_capture.set_asn_tables(np.zeros(0, dtype=N.ASN_RANGE_DTYPE), np.zeros(0, dtype=N.ASN_RANGE_DTYPE))
+        gpu_capture.set_blacklists(np.zeros(0, dtype=N.CIDR_DTYPE))
+        gpu_capture.clear_all_sessions()
