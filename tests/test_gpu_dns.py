@@ -162,3 +162,21 @@ def test_dns_end_to_end_from_frames(gpu_capture):
     assert gres.resolutions == ores.resolutions
     assert {str(k): v for k, v in gres.resolutions.items()} == {
         "198.51.100.7": "video.example.com", "2001:db8::7": "video.example.com", "203.0.113.9": "tcp.example.com"}
+
+
+def test_dns_parse_full_size():
+    """The bench's DNS workload at full size (synth.dns_workload: 1,048,576 port-53 payloads,
+    queries and compressed responses): the parse of every 8th message (131,072) and of the first
+    and last 4,096 equals the oracle's, and the batch holds no rejected message."""
+    from flodbadd_amd import synth
+    payload, recs = synth.dns_workload(1 << 20)
+    g_msgs, g_names, g_addrs = parse_dns(payload, recs)
+    assert len(g_msgs) == len(recs) == 1 << 20
+    idx = sorted(set(range(0, len(recs), 8)) | set(range(4096)) | set(range(len(recs) - 4096, len(recs))))
+    for i in idx:
+        o, ln = int(recs[i]["payload_offset"]), int(recs[i]["payload_length"])
+        r, nm, ad = coracle.dns_parse(payload[o: o + ln].tobytes(), int(recs[i]["pkt_index"]))
+        assert g_msgs[i].tobytes() == r.tobytes(), (i, g_msgs[i], r)
+        assert bytes(g_names[i][: len(nm)]) == nm
+        assert g_addrs[i][: len(ad)].tobytes() == ad.tobytes()
+    assert (g_msgs["status"] == 0).all()
