@@ -437,10 +437,11 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     cnt = C.c_uint64()
     N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
 
-    def export_merge():
+    def export_merge(timing=None):
         # the library exports the owner groups into a device tensor, the collectives move them
         # (RCCL with device tensors; gloo via host memory), the library merges each owner's records
-        merged = global_flow_table(dist, ctx, shard_first=shard_first, device=device, group=group, as_tensor=True)
+        merged = global_flow_table(dist, ctx, shard_first=shard_first, device=device, group=group, as_tensor=True,
+                                   timing=timing)
         if device.type == "cuda":
             import torch
             torch.cuda.synchronize(device)
@@ -453,6 +454,10 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     t0 = time.perf_counter()
     local, merged = export_merge()
     el = time.perf_counter() - t0
+    # a third pass with every stage drained and timed apart: the collectives' time and bytes beside the
+    # library's export and merge kernels
+    stages = {}
+    export_merge(stages)
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
     t = np.array([flow_ms], dtype=np.float64)
@@ -465,6 +470,10 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
                 local_flows=local, global_flows=int(len(merged)),
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),
+                stages_ms={k: round(v, 3) for k, v in stages.items() if k.endswith("_ms")},
+                collective_bytes={k: int(v) for k, v in stages.items() if k.endswith("_bytes")},
+                collective_GBs=round((stages.get("a2a_bytes", 0) + stages.get("gather_bytes", 0)) /
+                                     max(stages.get("a2a_ms", 0) + stages.get("gather_ms", 0), 1e-9) / 1e6, 2),
                 note="per-rank fused parse+flow upsert of the rank's shard, then the global session table: "
                      "fb_flow_export_merge_dev (owner groups, device tensor), all_to_all to the owners, "
                      "fb_flow_merge_dev on each owner, all_gather of the merged records (left on the device)")
@@ -727,6 +736,31 @@ def _emit(obj):
     out.flush()
 
 
+def c5_checked(run, world, gpus, dist):
+    """Run the C5 exchange (`run()` -> its extra dict) on every rank of a world > 1 and agree on the
+    outcome: an exception, or a group that does not hold --gpus ranks, fails it.  Every rank then
+    learns over the default group whether all succeeded (a rank whose peer failed inside a collective
+    leaves it by the C5 group's timeout).  Returns (extra dict, ok on every rank)."""
+    import torch
+    try:
+        res = run()
+        ok = res.get("ranks_in_group") == gpus
+        if not ok:
+            res["error"] = "the C5 group holds %s ranks, --gpus %d" % (res.get("ranks_in_group"), gpus)
+    except Exception as e:
+        res, ok = {"error": repr(e)[:300]}, False
+    t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+    flags = [t]
+    if world > 1:
+        flags = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(flags, t)
+    failed = [r for r, f in enumerate(flags) if int(f[0])]
+    if failed:
+        res["failed_ranks"] = failed
+        res.setdefault("error", "the C5 exchange failed on rank(s) %s" % failed)
+    return res, not failed
+
+
 def world_check(args, world, rank):
     """--world-check: the launch plumbing only (no GPU): every rank joins the gloo group, the ranks
     all-reduce their rank numbers, rank 0 prints what the group saw."""
@@ -737,11 +771,27 @@ def world_check(args, world, rank):
     t = torch.tensor([rank, 1], dtype=torch.int64)
     if world > 1:
         tdist.all_reduce(t)
+    line = {"n_gpus": world, "requested_gpus": args.gpus, "group_size": int(t[1]),
+            "rank_sum": int(t[0]), "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))}
+    c5_ok = True
+    if world > 1:
+        # the C5 outcome plumbing with a stand-in exchange (FB_C5_INJECT=fail: rank 1 raises;
+        # =group: the group reports fewer ranks than --gpus)
+        inject = os.environ.get("FB_C5_INJECT", "")
+
+        def run():
+            if inject == "fail" and rank == 1:
+                raise RuntimeError("injected C5 merge failure")
+            return {"ranks_in_group": world - 1 if inject == "group" else tdist.get_world_size()}
+        res, c5_ok = c5_checked(run, world, args.gpus, tdist)
+        line["extra"] = {"c5_flow_reduce": res}
+        line["c5_ok"] = c5_ok
     if rank == 0:
-        _emit({"n_gpus": world, "requested_gpus": args.gpus, "group_size": int(t[1]),
-               "rank_sum": int(t[0]), "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))})
+        _emit(line)
     if world > 1:
         tdist.destroy_process_group()
+    if not c5_ok:
+        raise SystemExit("C5 exchange failed on some rank")
 
 
 def main():
@@ -897,6 +947,7 @@ def main():
         except Exception as e:  # reported, never allowed to break the bench line
             extra["host_ring_c2"] = {"error": repr(e)[:300]}
 
+    c5_ok = True
     if world > 1 and not args.no_flow_reduce:
         try:
             import torch
@@ -906,11 +957,19 @@ def main():
             backend = os.environ.get("FB_C5_BACKEND", "nccl")
             dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
             torch.cuda.set_device(torch.device("cuda", device))  # the library's exports land on this GPU
-            g = tdist.new_group(backend=backend)
-            extra["c5_flow_reduce"] = c5_flow_reduce(N, lib, ctx, args.c5_frames, rank, world, tdist, g, dev)
-            extra["c5_flow_reduce"]["backend"] = "rccl" if backend == "nccl" else backend
-        except Exception as e:  # the exchange is reported, never allowed to break the bench line
-            extra["c5_flow_reduce"] = {"error": repr(e)[:300]}
+            import datetime
+            g = tdist.new_group(backend=backend, timeout=datetime.timedelta(seconds=180))
+        except Exception as e:
+            g, setup_error = None, repr(e)[:300]
+
+        def run():
+            if g is None:
+                raise RuntimeError("C5 group setup failed: %s" % setup_error)
+            r = c5_flow_reduce(N, lib, ctx, args.c5_frames, rank, world, tdist, g, dev)
+            r["backend"] = "rccl" if backend == "nccl" else backend
+            return r
+        # a failed exchange or a short group fails the run (non-zero exit after the line is printed)
+        extra["c5_flow_reduce"], c5_ok = c5_checked(run, world, args.gpus, dist)
 
     copy_gbs = None
     if rank == 0 and not args.no_copy_ref:  # (after the timed region)
@@ -965,6 +1024,8 @@ def main():
             "cpu_baseline": cpu,
             "batch_stats": main_r["stats"],
         }
+        if world > 1:
+            line["c5_ok"] = c5_ok
         if per_rank:
             line["per_rank"] = per_rank
             line["roofline"]["note"] = "rank 0's GPU; every rank's own fraction in per_rank"
@@ -973,6 +1034,8 @@ def main():
         _emit(line)
     if dist:
         dist.destroy_process_group()
+    if not c5_ok:
+        raise SystemExit("C5 exchange failed on some rank (c5_ok false in the line)")
 
 
 if __name__ == "__main__":

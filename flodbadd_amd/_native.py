@@ -12,7 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 GPU_LIB_PATH = os.environ.get("FLODBADD_GPU_LIB") or os.path.join(PKG, "libflodbadd_gpu.so")  # override: tools/
 SYNTH_LIB_PATH = os.path.join(PKG, "libfb_synth.so")
 
-FB_ABI_VERSION = 3
+FB_ABI_VERSION = 4
 FB_MAX_BATCH_PACKETS = (1 << 27) - 1
 FB_MAX_LAN_V6 = 64
 FB_MAX_OWN_IPS = 64
@@ -45,7 +45,8 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
     ("outbound_bytes", "<u8"), ("inbound_bytes", "<u8"), ("orig_pkts", "<u8"), ("resp_pkts", "<u8"),
     ("orig_ip_bytes", "<u8"), ("resp_ip_bytes", "<u8"),
     ("first_seen", "<u8"), ("last_seen", "<u8"), ("end_seen", "<u8"), ("hist_len", "<u4"),
-    ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("session_flags", "<u4")])
+    ("hist_mask", "<u2"), ("conn_state", "u1"), ("end_mask", "u1"), ("slot", "<u4"), ("session_flags", "<u4"),
+    ("segment_count", "<u4"), ("in_segment", "u1"), ("reserved", "u1", (3,))])
 # fb_flow_mrec: a flow record exported for the multi-GPU merge (positions global, slot = the rank) and
 # the update call of the flow's first S, s, H, h (FB_CALL_NONE: none)
 FLOW_MREC_DTYPE = np.dtype([("rec", FLOW_REC_DTYPE), ("char_call", "<u4", (4,))])
@@ -108,7 +109,7 @@ def seg_unpack(out_bytes, seg):
 
 
 assert PKT_OUT_DTYPE.itemsize == 56 and DNS_OUT_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 56
-assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 128
+assert STATS_DTYPE.itemsize == 128 and FLOW_REC_DTYPE.itemsize == 136 and FLOW_MREC_DTYPE.itemsize == 152
 assert LAN_V6_DTYPE.itemsize == 32 and FB_IP_DTYPE.itemsize == 32
 assert ASN_RANGE_DTYPE.itemsize == 48 and CIDR_DTYPE.itemsize == 32 and FLOW_ENRICH_DTYPE.itemsize == 32
 assert DNS_MSG_DTYPE.itemsize == 16
@@ -225,6 +226,7 @@ GPU_SYMBOLS = [
     ("fb_event_spin", _I, [_P]),
     ("fb_device_count", _I, [C.POINTER(C.c_int)]),
     ("fb_set_device", _I, [_I]),
+    ("fb_ctx_device", _I, [_P, C.POINTER(C.c_int)]),
 ]
 
 _gpu = None

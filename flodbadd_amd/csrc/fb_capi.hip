@@ -78,6 +78,7 @@ struct fb_ctx {
     uint32_t dense_epoch = 0;                 // epoch of the last launch (0: status needs zeroing)
     uint32_t dense_grid = 0;
     uint32_t steal_polls = 1u << 12;
+    unsigned long long dn_skew = 0ull;  // FB_DENSE_OFFSET_SKEW: fault injection (k_parse_dense copy bounds)
     hipEvent_t stage_event = nullptr;  // fb_set_stage_event (caller-owned): recorded between the
                                        // parse and the update of fb_process[_seg]_dev
     // flow table
@@ -101,6 +102,8 @@ struct fb_ctx {
     uint32_t* d_remap = nullptr;    // the last growth's old -> new slot map
     uint4* d_char_call = nullptr;   // [table_cap] first update call of S s H h per slot (the merge's)
     void* d_mscratch = nullptr;     // multi-GPU merge scratch (export owner counts / merge tables)
+    hipEvent_t ev_mscratch = nullptr;  // after the last export / merge that used d_mscratch (either may
+                                       // run on any stream: the next use waits for it)
     uint64_t mscratch_bytes = 0;
     uint64_t remap_n = 0;
     unsigned long long* d_n = nullptr;
@@ -172,7 +175,8 @@ int fbk::ctx_report_error(fb_ctx* c, uint64_t e) {
     c->need_reset = true;
     if (e & 4u) return set_err(FB_ERR_TABLE_FULL, "flow table full (error word %llu)", (unsigned long long)e);
     return set_err(FB_ERR_INTERNAL, "device error word %llu (2: offset scan expired, 8: update scratch "
-                   "overflow, 16: table-update spin expired)", (unsigned long long)e);
+                   "overflow, 16: table-update spin expired, 32: dense tile offset past the batch)",
+                   (unsigned long long)e);
 }
 
 // Entry points that read or write the table or the update scratch first order their stream after
@@ -397,6 +401,12 @@ int fb_device_count(int* n) {
     return FB_OK;
 }
 
+int fb_ctx_device(const fb_ctx* ctx, int* device) {
+    if (!ctx || !device) return set_err(FB_ERR_INVAL, "ctx or device is NULL");
+    *device = ctx->device;
+    return FB_OK;
+}
+
 fb_ctx* fb_create(int device, const fb_config* cfg) {
     if (!cfg) { set_err(FB_ERR_INVAL, "cfg is NULL"); return nullptr; }
     if (cfg->abi_version != FB_ABI_VERSION) {
@@ -438,6 +448,8 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         if (occupancy_parse_dense(&db) != hipSuccess || db < 1) db = 1;
         c->dense_grid = std::min<uint32_t>((uint32_t)(db * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
         if (const char* e = getenv("FB_DENSE_STEAL_POLLS")) c->steal_polls = (uint32_t)strtoul(e, nullptr, 10);
+        // fault injection (tests/test_gpu_dense.py): a skew added to every dense tile offset
+        if (const char* e = getenv("FB_DENSE_OFFSET_SKEW")) c->dn_skew = strtoull(e, nullptr, 10);
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -508,6 +520,7 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_remap);
     hipFree(c->d_char_call);
     hipFree(c->d_mscratch);
+    if (c->ev_mscratch) hipEventDestroy(c->ev_mscratch);
     if (c->h_mbox) hipHostFree(c->h_mbox);
     hipFree(c->d_n);
     hipFree(c->d_hword);
@@ -773,6 +786,7 @@ static int parse_dense_single(fb_ctx* c, const uint8_t* d_frames, uint64_t frame
     p.dense_dns = d_dns;
     p.dstatus = c->d_dstatus;
     p.steal_polls = c->steal_polls;
+    p.dn_skew = c->dn_skew;
     p.dep = ++c->dense_epoch;
     p.ntiles = (nseg + parse_dense_tile_segs() - 1) / parse_dense_tile_segs();
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->dense_grid, p.ntiles));
@@ -1404,8 +1418,14 @@ int fb_flow_export_dev(fb_ctx* c, fb_flow_rec* d_out, uint64_t cap, uint64_t* d_
 }
 
 // ---- multi-GPU merge (fb_merge.hip) ---------------------------------------------------------------
+// The export and the merge share d_mscratch and may be called on different streams: each use waits
+// on the event the previous use recorded (mscratch_use / mscratch_done), and a reallocation waits for
+// that use on the host before the old buffer is freed.
 static int ensure_mscratch(fb_ctx* c, uint64_t bytes, hipStream_t s) {
+    if (!c->ev_mscratch) HIP_TRY(hipEventCreateWithFlags(&c->ev_mscratch, hipEventDisableTiming));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_mscratch, 0));  // (an event never recorded is complete)
     if (bytes <= c->mscratch_bytes) return FB_OK;
+    HIP_TRY(hipEventSynchronize(c->ev_mscratch));
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(c->d_mscratch);
     c->d_mscratch = nullptr;
@@ -1428,6 +1448,7 @@ int fb_flow_export_merge_dev(fb_ctx* c, uint32_t world, uint32_t rank, uint64_t 
     if (rc) return rc;
     HIP_TRY(launch_merge_export(c->d_table, c->d_char_call, c->table_cap, world, rank, shard_first, d_out, cap,
                                 (unsigned long long*)d_counts, c->d_mscratch, s));
+    HIP_TRY(hipEventRecord(c->ev_mscratch, s));
     return FB_OK;
 }
 
@@ -1440,6 +1461,7 @@ int fb_flow_merge_dev(fb_ctx* c, const fb_flow_mrec* d_in, uint64_t n, fb_flow_r
     const int rc = ensure_mscratch(c, n ? merge_scratch_bytes(n) : 0, s);
     if (rc) return rc;
     HIP_TRY(launch_merge(d_in, n, d_out, (unsigned long long*)d_n, c->d_mscratch, s));
+    HIP_TRY(hipEventRecord(c->ev_mscratch, s));
     return FB_OK;
 }
 

@@ -465,7 +465,7 @@ __device__ __forceinline__ int lds_upsert(unsigned long long* tab, const uint32_
                 s[3] = kw2;
                 s[4] = kw3;
                 s[5] = kw4;
-                __hip_atomic_store(s, flow_hash_words(key) | 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(s, (unsigned long long)want32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 result = 1;
                 break;
             }
@@ -607,7 +607,7 @@ __device__ __forceinline__ int k2_upsert(uint32_t* tags, unsigned long long* tab
                 s[3] = kw2;
                 s[4] = kw3;
                 s[5] = kw4;
-                s[0] = flow_hash_words(key) | 2ull;
+                s[0] = (unsigned long long)want;  // slot tag | segment_count 0 << 32
                 __hip_atomic_store(tags + i, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 result = 1;
                 break;
@@ -665,8 +665,13 @@ __device__ __forceinline__ int apply_entry(unsigned long long* slice, uint32_t* 
     uint32_t* q = scr + (size_t)i * kScrU32;
     const uint32_t rec = e3.y;
     const unsigned long long pos = (unsigned long long)rec << 32 | e3.x;  // rec, pkt_index
+    // a TCP packet with PSH ends a segment (src/packets.rs:140-160, 414-420): segment_count += 1 in
+    // the slot head's high word, and the last packet's key carries the bit (in_segment = !PSH of the
+    // flow's latest packet); pkt_index < 2^27 leaves bit 31 free
+    const uint32_t psh = (e3.z & 0x10000u) && ((e3.z >> 8) & kTcpPsh) && (e2.y & 0xFFu) == 6u ? 1u : 0u;
+    if (psh) atomicAdd(s, 1ull << 32);
     atomicMin(sc64(q, kScFirst), pos);
-    atomicMax(sc64(q, kScLast), pos);
+    atomicMax(sc64(q, kScLast), pos | (unsigned long long)psh << 31);
     // inserted by this batch: bit 16, and the session flags the reference stores at insert
     // (is_local_src/dst, is_self_src/dst of the canonical key, src/packets.rs:429-435) in bits 20-23
     // dst_service (src/packets.rs:441-466) in bit 15
@@ -715,7 +720,8 @@ __device__ __forceinline__ int apply_combined(unsigned long long* slice, uint32_
     // the group's first / last / end records: their pkt_index (and the end's character) read here
     // -- combined entries are few
     atomicMin(sc64(q, kScFirst), (unsigned long long)e2.z << 32 | rec_pkt(P, e2.z));
-    atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | rec_pkt(P, e2.w));
+    atomicMax(sc64(q, kScLast), (unsigned long long)e2.w << 32 | rec_pkt(P, e2.w) | (unsigned long long)((t3.w >> 15) & 1u) << 31);
+    if (t3.w >> 16) atomicAdd(s, (unsigned long long)(t3.w >> 16) << 32);  // the group's PSH packets: segment_count
     const uint32_t hc = e3.z & 0xFFFFu;
     const uint32_t m = (e3.z >> 16) | (result == 1 ? (1u << 16) | ((t3.w & 0xFu) << 20) | ((t3.w >> 4) & 1u) << 15 : 0u);
     if (m) atomicOr(q + kScMask, m);
@@ -746,8 +752,10 @@ __device__ __forceinline__ void finish_slot(uint32_t* q, uint32_t batch, const u
     unsigned long long end_seen = fresh ? FB_SEEN_NONE : (o1.x | (unsigned long long)o1.y << 32);
     // hist_state: hist_mask 0-12 | dst_service 15 | conn_state 16-19 | session flags 20-23 | end_mask 24-31
     const uint32_t state = fresh ? (flags & 0x00F00000u) : o1.w, len = fresh ? 0u : o1.z;
-    const unsigned long long last_seen = hi | (uint32_t)last;
-    const uint32_t mask = state & 0xFFFFu;
+    const unsigned long long last_seen = hi | ((uint32_t)last & 0x7FFFFFFFu);
+    // in_segment: the flow's latest packet was not a TCP PSH (bit 31 of the last key's low word)
+    const uint32_t in_seg = ((uint32_t)last >> 31) ? 0u : kStateInSegment;
+    const uint32_t mask = state & 0xFFFFu & ~kStateInSegment;
     // the update call of the first S, s, H, h of the flow (FB_CALL_NONE: none yet), kept beside the
     // table for the multi-GPU merge (it decides which of a rank's characters precede another rank's
     // end packet): written when a character first appears -- its mask bit was clear -- and whole at
@@ -777,7 +785,7 @@ __device__ __forceinline__ void finish_slot(uint32_t* q, uint32_t batch, const u
     const uint4 t0 = make_uint4((uint32_t)first_seen, (uint32_t)(first_seen >> 32), (uint32_t)last_seen,
                                 (uint32_t)(last_seen >> 32));
     const uint4 t1 = make_uint4((uint32_t)end_seen, (uint32_t)(end_seen >> 32), len + q[kScCount],
-                                (mask | (flags & 0xFFFFu)) | (cs << 16));
+                                (mask | (flags & 0xFFFFu) | in_seg) | (cs << 16));
     uint4* t = reinterpret_cast<uint4*>(q + kScOrd);  // bytes 96..127 of the slot
     t[0] = t0;
     t[1] = t1;
@@ -928,9 +936,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 f[kCfHash] = e[3].w;  // every lane of the key stores the same word
                 f[kCfMeta] = (e[3].z >> 20) & 0x1Fu;  // session flags + dst_service: a function of the key and the configuration
                 atomicMin(f + kCfFirst, rec);
-                atomicMax(f + kCfLast, rec);
+                const uint32_t psh = (e[3].z & 0x10000u) && ((e[3].z >> 8) & kTcpPsh) && (e[2].y & 0xFFu) == 6u ? 1u : 0u;
+                atomicMax(f + kCfLast, rec << 1 | psh);  // (rec < 2^27) the last record and its PSH bit
                 if (e[3].z & 0x10000u) {
-                    atomicAdd(f + kCfHcnt, 1u);
+                    atomicAdd(f + kCfHcnt, 1u | psh << 16);  // history count | PSH count << 16 (< kFlowChunk each)
                     const uint32_t b = hist_bit(e[3].z & 0xFFu);
                     if (b < 16u) atomicOr(f + kCfMask, 1u << b);
                     if (b < 4u) atomicMin(f + kCfChar + b, rec);
@@ -1041,12 +1050,13 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             uint4* o = CE + (size_t)id * 8u;
             o[0] = make_uint4((uint32_t)tw[1], (uint32_t)(tw[1] >> 32), (uint32_t)tw[2], (uint32_t)(tw[2] >> 32));
             o[1] = make_uint4((uint32_t)tw[3], (uint32_t)(tw[3] >> 32), (uint32_t)tw[4], (uint32_t)(tw[4] >> 32));
-            o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast]);
-            o[3] = make_uint4(id, f[kCfEnd] == ~0u ? ~0u : f[kCfEnd] >> 5, f[kCfHcnt] | (f[kCfMask] << 16), f[kCfHash]);
+            o[2] = make_uint4((uint32_t)tw[5], (uint32_t)(tw[5] >> 32) | kEntCombined, f[kCfFirst], f[kCfLast] >> 1);
+            o[3] = make_uint4(id, f[kCfEnd] == ~0u ? ~0u : f[kCfEnd] >> 5, (f[kCfHcnt] & 0xFFFFu) | (f[kCfMask] << 16), f[kCfHash]);
             o[4] = make_uint4((uint32_t)by[0], (uint32_t)(by[0] >> 32), (uint32_t)by[1], (uint32_t)(by[1] >> 32));
             o[5] = make_uint4((uint32_t)by[2], (uint32_t)(by[2] >> 32), (uint32_t)by[3], (uint32_t)(by[3] >> 32));
             o[6] = make_uint4(f[kCfPk], kEntTail, f[kCfChar], f[kCfChar + 1]);
-            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs], f[kCfMeta] | (f[kCfEnd] & 31u) << 8);
+            o[7] = make_uint4(f[kCfChar + 2], f[kCfChar + 3], f[kCfRecs],
+                              f[kCfMeta] | (f[kCfEnd] & 31u) << 8 | (f[kCfLast] & 1u) << 15 | (f[kCfHcnt] >> 16) << 16);
             E[s0 + cursor + f[kCfId]] = kIdxCombined | id;
         }
         if (threadIdx.x == 0) {  // bit 15: a combined group (the history reads e_sort, and

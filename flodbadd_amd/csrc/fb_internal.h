@@ -54,6 +54,9 @@ struct ParseParams {
     uint32_t dep;
     uint32_t ntiles;
     uint32_t steal_polls;
+    // fault injection for the tests (FB_DENSE_OFFSET_SKEW at fb_create, 0 otherwise): added to every
+    // tile offset k_parse_dense hands its copies, as a corrupted look-back word would be
+    unsigned long long dn_skew;
 };
 // 16 / 8 bytes at a 4-B aligned address: 56-B records (fb_pkt_out, fb_parsed_pkt) are only 8-B
 // aligned at odd indices, so a uint4 dereference there would claim an alignment the data lacks
@@ -128,10 +131,11 @@ struct SegBatches {
 //   64-bit hash, its home slot inside the partition the low bits (linear probing wraps inside
 //   the partition).  One workgroup owns one partition per batch and updates it in LDS, so the
 //   upsert needs no global atomics.
-//   Slot (128 B): tag (0 empty, 1 being inserted [LDS only], else hash | 2), 40-B key,
-//   6 counters in fb_flow_rec order, then the ordered state: first / last / end positions
-//   ((update call << 32) | pkt_index, FB_SEEN_NONE), hist_len, hist_mask | conn_state << 16 |
-//   session flags << 20 | end_mask << 24.
+//   Slot (128 B): tag (0 empty, 1 being inserted [LDS only], else the hash's low word | 2) and
+//   segment_count in one u64 (so K2 adds PSH packets to the high half with one LDS atomic), 40-B
+//   key, 6 counters in fb_flow_rec order, then the ordered state: first / last / end positions
+//   ((update call << 32) | pkt_index, FB_SEEN_NONE), hist_len, hist_mask | in_segment << 14 |
+//   dst_service << 15 | conn_state << 16 | session flags << 20 | end_mask << 24.
 #ifndef FB_FLOW_SLOTS
 #define FB_FLOW_SLOTS 512
 #endif
@@ -155,16 +159,19 @@ constexpr uint32_t kFlowK1Threads = FB_K1_THREADS;
 constexpr uint32_t kFlowK2Threads = FB_K2_THREADS;
 constexpr uint64_t kFlowMaxCapacity = (uint64_t)kFlowSlots * kFlowMaxParts;
 struct FlowSlot {
-    unsigned long long tag;
+    uint32_t tag;               // 0 empty, else (uint32_t)fb_flow_hash | 2
+    uint32_t segment_count;     // SessionStats.segment_count (TCP packets with PSH, src/packets.rs:140-160, 414-420)
     uint32_t key[10];
     unsigned long long cnt[6];  // outbound_bytes, inbound_bytes, orig_pkts, resp_pkts,
                                 // orig_ip_bytes, resp_ip_bytes
     unsigned long long first_seen, last_seen, end_seen;
     uint32_t hist_len;
-    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | dst_service << 15 | conn_state << 16
-                                // (4 bits) | session flags << 20 (fb_session_flags 0-3, set at insert) |
-                                // end_mask << 24
+    uint32_t hist_state;        // hist_mask (FB_HIST_CHARS bits) | in_segment << 14 | dst_service << 15 |
+                                // conn_state << 16 (4 bits) | session flags << 20 (fb_session_flags 0-3,
+                                // set at insert) | end_mask << 24
 };
+constexpr uint32_t kStateInSegment = 1u << 14;  // hist_state: SessionStats.in_segment
+constexpr uint32_t kTcpPsh = 0x08u;             // TCP_PSH, src/packets.rs:26
 static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
 // word 9 (the key's padding), L4 payload bytes, IP bytes, then the record's pkt_index, its
@@ -184,7 +191,8 @@ static_assert(sizeof(FlowEntry) == 64, "flow entry is 64 B");
 // consecutive FlowEntry units.  Head: key[0..8], key[9] | kEntCombined, first rec, last rec,
 // combined id, end rec (first FIN/RST, ~0 none), hist count | hist mask << 16, hash_lo.  Tail:
 // outbound, inbound, orig ip, resp ip bytes (u64), orig | resp pkts << 16, kEntTail, first rec
-// of S s H h (~0 none), records, 0.
+// of S s H h (~0 none), records, session flags | end char bit << 8 | last record's PSH << 15 |
+// PSH records << 16.
 constexpr uint32_t kEntCombined = 1u << 17;  // in key[9] (bit 16 is the originator)
 constexpr uint32_t kEntTail = 1u << 18;
 constexpr uint32_t kRecFlowCombined = 0x80000000u;  // e_sort position word: combined id, slot in agg_slot
@@ -299,6 +307,9 @@ __device__ __forceinline__ fb_flow_rec flow_rec_of(const FlowSlot& t, uint32_t s
     r.end_mask = (uint8_t)(t.hist_state >> 24);
     r.slot = slot;
     r.session_flags = ((t.hist_state >> 20) & 0xFu) | ((t.hist_state >> 15) & 1u) << 4;
+    r.segment_count = t.segment_count;
+    r.in_segment = (t.hist_state & kStateInSegment) ? 1u : 0u;
+    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0u;
     return r;
 }
 

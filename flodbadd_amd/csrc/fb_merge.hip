@@ -8,7 +8,9 @@
 //           its hash), slot order inside a group, positions made global (+ the shard's first packet
 //           index), rec.slot = the rank, and the update call of the flow's first S / s / H / h;
 //   merge   the records one owner received (each rank's group, rank order) -> one record per key:
-//           integer counter sums, MIN first_seen, MAX last_seen, hist_len SUM, hist_mask OR, and
+//           integer counter sums (segment_count too), MIN first_seen, MAX last_seen, hist_len SUM,
+//           hist_mask OR, in_segment of the record holding the latest packet and the session flags
+//           of the one holding the earliest (the flow's insert: src/packets.rs:429-466), and
 //           the ordered state at the GLOBAL first FIN/RST (src/packets.rs:187-198, 422-426,
 //           539-559): end_seen = the smallest end over the ranks; end_mask = the ending rank's own
 //           end_mask (the characters its history held at that packet) OR, for every other rank, the
@@ -174,6 +176,9 @@ struct MergeScratch {
     uint32_t* mask;                 // [n] hist_mask or
     uint32_t* emask;                // [n] end characters or
     uint32_t* r0;                   // [n] the ending rank
+    uint32_t* seg;                  // [n] segment_count sum
+    uint32_t* inseg;                // [n] in_segment of the latest packet's record
+    uint32_t* sflags;               // [n] session_flags of the earliest packet's record
     uint32_t* blk;                  // [blocks + 1] output counts per block, then offsets
     unsigned long long tcap;
 };
@@ -188,7 +193,7 @@ static size_t al(size_t b) { return (b + 255) & ~size_t(255); }
 
 uint64_t merge_scratch_bytes(unsigned long long n) {
     const unsigned long long blocks = (n + kMgThreads - 1) / kMgThreads;
-    return al(merge_tcap(n) * 4) + 3 * al(n * 4) + al(n * 48) + 3 * al(n * 8) + 4 * al(n * 4) + al((blocks + 1) * 4);
+    return al(merge_tcap(n) * 4) + 3 * al(n * 4) + al(n * 48) + 3 * al(n * 8) + 7 * al(n * 4) + al((blocks + 1) * 4);
 }
 
 static MergeScratch carve(void* base, unsigned long long n) {
@@ -208,6 +213,9 @@ static MergeScratch carve(void* base, unsigned long long n) {
     m.len = (uint32_t*)take(n * 4);
     m.mask = (uint32_t*)take(n * 4);
     m.emask = (uint32_t*)take(n * 4);
+    m.seg = (uint32_t*)take(n * 4);
+    m.inseg = (uint32_t*)take(n * 4);
+    m.sflags = (uint32_t*)take(n * 4);
     m.blk = (uint32_t*)take((blocks + 1) * 4);
     (void)take(0);
     return m;
@@ -262,6 +270,7 @@ __global__ __launch_bounds__(kMgThreads) void k_mg_reduce(const fb_flow_mrec* in
     if (r.end_seen != FB_SEEN_NONE) atomicMin(m.end + hd, (unsigned long long)r.end_seen);
     atomicAdd(m.len + hd, r.hist_len);
     atomicOr(m.mask + hd, (uint32_t)r.hist_mask);
+    atomicAdd(m.seg + hd, r.segment_count);
 }
 
 // The ending rank: the record whose end is the key's smallest (positions are global, so exactly
@@ -276,6 +285,10 @@ __global__ __launch_bounds__(kMgThreads) void k_mg_end(const fb_flow_mrec* in, u
         m.r0[hd] = r.slot;  // (the exporting rank)
         atomicOr(m.emask + hd, (uint32_t)r.end_mask);
     }
+    // global positions are distinct per packet: exactly one record holds the key's latest packet
+    // (in_segment follows it) and one its earliest (the insert, whose flags the session keeps)
+    if (r.last_seen == m.last[hd]) m.inseg[hd] = r.in_segment;
+    if (r.first_seen == m.first[hd]) m.sflags[hd] = r.session_flags;
 }
 
 // The other ranks' S s H h that precede the end packet: first occurrence in an earlier update
@@ -361,7 +374,10 @@ __global__ __launch_bounds__(kMgThreads) void k_mg_write(const fb_flow_mrec* in,
     o.conn_state = (uint8_t)(E != FB_SEEN_NONE ? conn_state_of(em) : FB_CONN_NONE);
     o.end_mask = (uint8_t)em;
     o.slot = 0u;
-    o.session_flags = r.session_flags;
+    o.session_flags = m.sflags[hd];
+    o.segment_count = m.seg[hd];
+    o.in_segment = (uint8_t)m.inseg[hd];
+    o.reserved[0] = o.reserved[1] = o.reserved[2] = 0u;
     out[pos] = o;
 }
 
@@ -381,6 +397,7 @@ hipError_t launch_merge(const fb_flow_mrec* in, unsigned long long n, fb_flow_re
     if ((e = hipMemsetAsync(m.len, 0, n * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(m.mask, 0, n * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(m.emask, 0, n * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(m.seg, 0, n * 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_mg_claim, dim3(blocks), dim3(kMgThreads), 0, s, in, n, m);
     hipLaunchKernelGGL(k_mg_reduce, dim3(blocks), dim3(kMgThreads), 0, s, in, n, m);
     hipLaunchKernelGGL(k_mg_end, dim3(blocks), dim3(kMgThreads), 0, s, in, n, m);

@@ -1018,7 +1018,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
             // are visible before the round is marked ready -- with relaxed orders the compiler
             // may put the base store after the flag, and a parse wave copied to a stale offset)
             if (lane == 0u) {
-                L.base[p] = excl;
+                L.base[p] = excl + P.dn_skew;
                 __hip_atomic_store(&L.ready_round[p], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
@@ -1045,14 +1045,26 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         const unsigned long long bp = L.base[p];
         const uint32_t cs = cw & 0xFFFFu, cd = cw >> 16;
         // records at batch-wide record bs (56 bs is 16-B aligned when bs is even; otherwise the
-        // first 8-B word goes alone and the 16-B body stays aligned), DNS records at bd
-        const uint32_t bs = (uint32_t)bp + (pw & 0xFFFFu), bd = (uint32_t)(bp >> 32) + (pw >> 16);
+        // first 8-B word goes alone and the 16-B body stays aligned), DNS records at bd.  The buffer
+        // resources are based at the slot's destination, so their range check only covers the slot's
+        // own records: a destination past the batch's n records (the caller's buffers hold n) would
+        // be written outside them.  That needs a corrupted tile offset -- round 4's no-look-back
+        // ablation added the real prefix to a fixed one and faulted here -- and drops the slot with
+        // error bit 32 instead (checked in 64 bits: a bad offset must not wrap into range).
+        const unsigned long long bs64 = (bp & 0xFFFFFFFFull) + (pw & 0xFFFFu), bd64 = (bp >> 32) + (pw >> 16);
+        const bool in_range = bs64 + cs <= (unsigned long long)n && bd64 + cd <= (unsigned long long)n;
+        if (!in_range && lane == 0u) {  // (the returned value is waited for: the bit is in L2 before this wave
+                                        // reports its stats, so the block that writes the batch stats reads it)
+            const uint32_t old = __hip_atomic_fetch_or(P.error, 32u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" ::"v"(old));
+        }
+        const uint32_t bs = in_range ? (uint32_t)bs64 : 0u, bd = in_range ? (uint32_t)bd64 : 0u;
         const uint32_t words = cs * 7u, head = cs ? (bs & 1u) : 0u, body = (words - head) >> 1;
         const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<uint8_t*>(P.dense_out) + (size_t)bs * 56u, (short)0, P.dense_out ? (int)(words * 8u) : 0,
-            0x00020000);
+            reinterpret_cast<uint8_t*>(P.dense_out) + (size_t)bs * 56u, (short)0,
+            P.dense_out && in_range ? (int)(words * 8u) : 0, 0x00020000);
         const __amdgpu_buffer_rsrc_t r_dns = __builtin_amdgcn_make_buffer_rsrc(
-            P.dense_dns + bd, (short)0, P.dense_dns ? (int)(cd * 16u) : 0, 0x00020000);
+            P.dense_dns + bd, (short)0, P.dense_dns && in_range ? (int)(cd * 16u) : 0, 0x00020000);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t cc = lane + 64u * k;

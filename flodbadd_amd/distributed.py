@@ -10,16 +10,17 @@ session table -- the reference's single DashMap that every capture task updates
      call of each flow's first S / s / H / h);
   2. all_to_all of the groups (RCCL over xGMI with device tensors; gloo on the CPU);
   3. each owner merges what it received (fb_flow_merge_dev, flodbadd_amd/csrc/fb_merge.hip):
-     integer sums, MIN first_seen, MAX last_seen, hist_len SUM, hist_mask OR, and end_seen /
+     integer sums (segment_count too), MIN first_seen, MAX last_seen, hist_len SUM, hist_mask OR,
+     in_segment from the latest packet's record, session flags from the earliest's, and end_seen /
      end_mask / conn_state at the globally first FIN/RST -- exact for any number of update calls
-     per rank (call k of every rank = its shard of global batch k);
+     per rank (call k of every rank = its shard of global batch k, at the same offset in each);
   4. all_gather of the merged records.
 BASELINE configs[4] names an all-reduce of per-flow counters; an all-reduce needs the same dense
 flow index on every rank (a dictionary step: all-gather of every rank's keys and a global sort),
 and its payload is the whole F-flow counter matrix on every rank.  The owner exchange moves each
 flow's record once each way instead and reduces every counter exactly once (integer sums, so the
 result is bit-identical to an all-reduce), with no global sort.
-Bytes per rank: 144 B x its flows out (x (W-1)/W) and ~the same in, 128 B x the global flows
+Bytes per rank: 152 B x its flows out (x (W-1)/W) and ~the same in, 136 B x the global flows
 gathered.
 """
 import ctypes as C
@@ -28,8 +29,9 @@ import numpy as np
 
 from ._native import FLOW_MREC_DTYPE, FLOW_REC_DTYPE
 
-MREC_WORDS = FLOW_MREC_DTYPE.itemsize // 8  # 18 u64 words per exported record
-REC_WORDS = FLOW_REC_DTYPE.itemsize // 8    # 16
+MREC_WORDS = FLOW_MREC_DTYPE.itemsize // 8  # 19 u64 words per exported record
+REC_WORDS = FLOW_REC_DTYPE.itemsize // 8    # 17
+assert MREC_WORDS * 8 == FLOW_MREC_DTYPE.itemsize and REC_WORDS * 8 == FLOW_REC_DTYPE.itemsize
 
 
 def shard_range(total, rank, world):
@@ -61,12 +63,29 @@ def sort_by_ord(flows):
     return flows[sort_keys(_key_words(flows))] if len(flows) else flows
 
 
-def exchange_merge(dist, mrecs, counts, merge, device=None, group=None):
+def _mark(timing, dev, key, t0):
+    """timing[key] += milliseconds since t0 (the device drained first for a cuda `dev`); returns now."""
+    import time
+    if timing is None:
+        return t0
+    if dev.type == "cuda":
+        import torch
+        torch.cuda.synchronize(dev)
+    now = time.perf_counter()
+    timing[key] = timing.get(key, 0.0) + (now - t0) * 1e3
+    return now
+
+
+def exchange_merge(dist, mrecs, counts, merge, device=None, group=None, timing=None):
     """Steps 2-4 of the global session table.  `mrecs`: this rank's exported records grouped by
-    owner ([n, 18] int64 tensor on `device`, FLOW_MREC_DTYPE rows), `counts`: the group sizes
-    (sequence of W ints); `merge(rows)` maps the [m, 18] int64 rows this rank received (each rank's
-    group, rank order) to the merged [k, 16] int64 FLOW_REC_DTYPE rows.  Returns the [G, 16] int64
-    global table, owners in rank order, identical on every rank."""
+    owner ([n, MREC_WORDS] int64 tensor on `device`, FLOW_MREC_DTYPE rows), `counts`: the group sizes
+    (sequence of W ints); `merge(rows)` maps the [m, MREC_WORDS] int64 rows this rank received (each
+    rank's group, rank order) to the merged [k, REC_WORDS] int64 FLOW_REC_DTYPE rows.  Returns the
+    [G, REC_WORDS] int64 global table, owners in rank order, identical on every rank.  `timing` (a dict,
+    optional): milliseconds and bytes of the collectives (a2a_ms / a2a_bytes: this rank's records sent
+    to other ranks; gather_ms / gather_bytes: merged records received from other ranks) apart from the
+    merge (merge_ms), each stage drained before the next is timed."""
+    import time
     import torch
     dev = torch.device("cpu") if device is None else torch.device(device)
     world = dist.get_world_size(group)
@@ -74,6 +93,7 @@ def exchange_merge(dist, mrecs, counts, merge, device=None, group=None):
     if len(counts) != world or sum(counts) != int(mrecs.shape[0]):
         raise ValueError("group sizes %s do not cover the %d exported records of %d ranks"
                          % (counts, int(mrecs.shape[0]), world))
+    t0 = time.perf_counter()
     if world > 1:
         send_n = torch.tensor(counts, dtype=torch.int64, device=dev)
         recv_n = torch.empty_like(send_n)
@@ -82,9 +102,14 @@ def exchange_merge(dist, mrecs, counts, merge, device=None, group=None):
         recv = torch.empty((sum(rn), MREC_WORDS), dtype=torch.int64, device=dev)
         dist.all_to_all_single(recv, mrecs.contiguous(), output_split_sizes=rn, input_split_sizes=counts,
                                group=group)
+        if timing is not None:
+            rank = dist.get_rank(group)
+            timing["a2a_bytes"] = timing.get("a2a_bytes", 0) + 8 * MREC_WORDS * (sum(counts) - counts[rank])
     else:
         recv = mrecs
+    t0 = _mark(timing, dev, "a2a_ms", t0)
     merged = merge(recv)
+    t0 = _mark(timing, dev, "merge_ms", t0)
     if world == 1:
         return merged
     n = torch.tensor([int(merged.shape[0])], dtype=torch.int64, device=dev)
@@ -95,41 +120,67 @@ def exchange_merge(dist, mrecs, counts, merge, device=None, group=None):
     pad[: merged.shape[0]] = merged
     got = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(got, pad, group=group)
-    return torch.cat([g[:sz] for g, sz in zip(got, sizes)])
+    out = torch.cat([g[:sz] for g, sz in zip(got, sizes)])
+    _mark(timing, dev, "gather_ms", t0)
+    if timing is not None:
+        timing["gather_bytes"] = timing.get("gather_bytes", 0) + 8 * REC_WORDS * (sum(sizes) - int(merged.shape[0]))
+    return out
 
 
-def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tensor=False, stream=None):
+def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tensor=False, stream=None, timing=None):
     """The global session table of every rank's context `ctx` (an fb_ctx handle) on the GPU: the
     library exports the owner groups into a device tensor, RCCL moves them (`device` a cuda device
     and `group` an nccl group; gloo with CPU tensors works too, the records then go through host
     memory), the library merges each owner's records.  `shard_first`: the global index of this
     rank's first packet (shard_range).  Returns FLOW_REC_DTYPE records in owner order, or with
-    as_tensor=True the [G, 16] int64 tensor on `device` (no download)."""
+    as_tensor=True the [G, REC_WORDS] int64 tensor on `device` (no download).
+
+    The library's kernels run on `stream` (None: the null stream); torch's copies and reads run on
+    torch's current stream of the context's device, so each hand-over between the two synchronises
+    the producing side first: the export's stream before its counts / records are read, torch's
+    stream before the merge reads the received rows, the merge's stream before its count is read.
+    `timing`: as exchange_merge, plus export_ms (the library's owner-grouped export and its copy to
+    `device`)."""
+    import time
     import torch
     from . import _native as N
     lib = N.gpu_lib()
     dev = torch.device("cpu") if device is None else torch.device(device)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    gpu = torch.device("cuda", torch.cuda.current_device()) if dev.type != "cuda" else dev
+    cdev = C.c_int(-1)
+    N.check(lib.fb_ctx_device(ctx, C.byref(cdev)))
+    gpu = torch.device("cuda", cdev.value)  # buffers on the context's device
+    if dev.type == "cuda" and dev.index is not None and dev.index != gpu.index:
+        raise ValueError("device %s is not the context's device %s" % (dev, gpu))
+
+    def stream_sync():
+        N.check(lib.fb_stream_sync(stream))
+
+    t0 = time.perf_counter()
     cnt = C.c_uint64()
     N.check(lib.fb_flow_count(ctx, C.byref(cnt), stream))
     mrecs = torch.empty((max(cnt.value, 1), MREC_WORDS), dtype=torch.int64, device=gpu)
     counts = torch.zeros(world, dtype=torch.int64, device=gpu)
+    torch.cuda.current_stream(gpu).synchronize()  # the buffers' allocation / zeroing before the export
     N.check(lib.fb_flow_export_merge_dev(ctx, world, rank, int(shard_first), C.c_void_p(mrecs.data_ptr()), cnt.value,
                                          C.c_void_p(counts.data_ptr()), stream))
-    counts = counts.tolist()  # (synchronises: the split sizes go to the collective as host ints)
+    stream_sync()  # the group sizes and records are complete before torch reads them
+    counts = counts.tolist()  # (host ints: the collective's split sizes)
     mrecs = mrecs[: sum(counts)].to(dev)
+    _mark(timing, gpu, "export_ms", t0)
 
     def merge(rows):
         m = int(rows.shape[0])
         src = rows.to(gpu).contiguous()
         out = torch.empty((max(m, 1), REC_WORDS), dtype=torch.int64, device=gpu)
         d_n = torch.zeros(1, dtype=torch.int64, device=gpu)
+        torch.cuda.current_stream(gpu).synchronize()  # the received rows' copy lands before the merge reads it
         N.check(lib.fb_flow_merge_dev(ctx, C.c_void_p(src.data_ptr()), m, C.c_void_p(out.data_ptr()),
                                       C.c_void_p(d_n.data_ptr()), stream))
+        stream_sync()  # the merged records and their count are complete
         return out[: int(d_n.item())].to(dev)
 
-    table = exchange_merge(dist, mrecs, counts, merge, device=dev, group=group)
+    table = exchange_merge(dist, mrecs, counts, merge, device=dev, group=group, timing=timing)
     if as_tensor:
         return table
     return np.ascontiguousarray(table.cpu().numpy()).view(FLOW_REC_DTYPE).reshape(-1)

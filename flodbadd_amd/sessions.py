@@ -111,6 +111,10 @@ class SessionStats:
     last_seen: int = 0
     end_seen: Optional[int] = None
     hist_len: int = 0
+    # segment detection (src/sessions.rs:88-93; src/packets.rs:137-160, 370-376, 414-420) under the
+    # no-timeout model: TCP packets with PSH counted, in a segment unless the latest packet had PSH
+    segment_count: int = 0
+    in_segment: bool = False
 
     @property
     def average_packet_size(self):
@@ -253,7 +257,8 @@ def flows_to_sessions(flows, histories=None):
                           int(r["resp_pkts"]), int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]),
                           histories.get(int(r["slot"]), "") if histories is not None else "",
                           CONN_STATES[int(r["conn_state"])], int(r["first_seen"]), int(r["last_seen"]),
-                          None if end == FB_SEEN_NONE else end, int(r["hist_len"]))
+                          None if end == FB_SEEN_NONE else end, int(r["hist_len"]), int(r["segment_count"]),
+                          bool(r["in_segment"]))
         s = Session.from_key(r)
         f = int(r["session_flags"])
         svc = (service_name(s.dst_port) or str(s.dst_port)) if f & SESSION_DST_SERVICE else None

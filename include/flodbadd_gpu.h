@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define FB_ABI_VERSION 3u /* 3: fb_flow_rec.session_flags, error-word bit 16, fb_flow_export_sessions* */
+#define FB_ABI_VERSION 4u /* 4: fb_flow_rec.segment_count / in_segment (136 B); 3: session_flags, error-word
+                              bit 16, fb_flow_export_sessions* */
 #define FB_MAX_BATCH_PACKETS ((1u << 27) - 1u)
 #define FB_MAX_LAN_V6 64u  /* interface IPv6 (prefix, network) pairs, src/ip.rs:164-191 */
 #define FB_MAX_OWN_IPS 64u /* per-interface own addresses, src/capture.rs:964-970      */
@@ -160,7 +161,10 @@ typedef struct fb_batch_stats {
                                   that follows skips them; FB_ERR_INTERNAL, not expected),
                                   4 flow-table partition full (FB_ERR_TABLE_FULL), 8 more records
                                   than the update scratch of the last parse launch holds,
-                                  16 a table-update LDS spin expired (FB_ERR_INTERNAL)       */
+                                  16 a table-update LDS spin expired (FB_ERR_INTERNAL),
+                                  32 a dense tile offset put records past the batch (those
+                                  records dropped, never written outside the buffers;
+                                  FB_ERR_INTERNAL, not expected)                          */
     uint64_t reserved[3];
 } fb_batch_stats; /* 128 bytes */
 
@@ -249,7 +253,16 @@ typedef struct fb_flow_rec {
                                 (src/packets.rs:429-435: is_local_src/dst, is_self_src/dst of the
                                 canonical key under the configuration of that update call; and
                                 dst_service is Some, src/packets.rs:441-466)                      */
-} fb_flow_rec;               /* 128 bytes */
+    uint32_t segment_count;  /* 128: SessionStats.segment_count -- TCP packets with PSH: 1 for a
+                                PSH first packet (src/packets.rs:414-420), +1 per later one
+                                (140-160)                                                          */
+    uint8_t in_segment;      /* 132: SessionStats.in_segment -- 0 right after a TCP PSH packet, 1
+                                after any other (src/packets.rs:151-159, 376, 418)                 */
+    uint8_t reserved[3];     /* 133 */
+} fb_flow_rec;               /* 136 bytes.  Segment state under the no-timeout model: the
+                                reference also ends a segment when a packet arrives >= 5 s of wall
+                                clock after the flow's last one (segment_timeout, src/packets.rs:
+                                137-149, 182-185); positions carry no clock.        */
 
 /* fb_flow_rec.session_flags (SessionInfo.is_local_src / is_local_dst / is_self_src / is_self_dst,
  * src/sessions.rs:40-61, set once at insert, src/packets.rs:429-435; bits 0-3 have the same values
@@ -582,15 +595,19 @@ uint64_t fb_flow_hash(const fb_session_key* key);
  *   4. all-gather of the owners' merged records.
  * The result equals the table ONE context builds from the same packets in global order (call k of
  * every rank = its shard of global batch k; global batch k is the ranks' shards in rank order) --
- * integer sums, MIN first_seen / end_seen, MAX last_seen, hist_len SUM, hist_mask OR, session flags
- * (a function of key and configuration) -- and conn_state / end_mask re-decided at the global first
- * FIN/RST: the ending rank's end_mask OR the S s H h of the other ranks that precede it (their
- * first occurrence in an earlier call, or in the same call on a lower rank).  Exact for any number
- * of update calls per rank.  Positions become global: (call << 32) | (shard_first + pkt_index). */
+ * integer sums (segment_count too), MIN first_seen / end_seen, MAX last_seen, hist_len SUM,
+ * hist_mask OR, in_segment and session flags from the records holding the key's latest / earliest
+ * packet -- and conn_state / end_mask re-decided at the global first FIN/RST: the ending rank's
+ * end_mask OR the S s H h of the other ranks that precede it (their first occurrence in an earlier
+ * call, or in the same call on a lower rank).  Exact for any number of update calls per rank, given
+ * the shard layout this assumes: in every call a rank's shard starts at the same packet index of the
+ * global batch (shard_first), as equal contiguous shards of equal-size global batches do; a call
+ * whose global batch differs in size (a short tail batch) needs its own export with that call's
+ * offset.  Positions become global: (call << 32) | (shard_first + pkt_index). */
 typedef struct fb_flow_mrec {
     fb_flow_rec rec;        /* positions global; rec.slot = the exporting rank                    */
     uint32_t char_call[4];  /* update call of the flow's first S, s, H, h (FB_CALL_NONE: none)     */
-} fb_flow_mrec;             /* 144 bytes */
+} fb_flow_mrec;             /* 152 bytes */
 /* Every flow of the table, grouped by owner rank (slot order inside a group), into d_out (room for
  * cap records); d_counts: `world` device u64 group sizes.  1 <= world <= 64, rank < world.
  * DEVICE pointers, asynchronous. */
@@ -669,6 +686,7 @@ int fb_event_query(void* ev); /* FB_OK once the event completed, 1 while pending
 int fb_event_spin(void* ev);
 int fb_device_count(int* n);
 int fb_set_device(int device);
+int fb_ctx_device(const fb_ctx* ctx, int* device); /* the device fb_create bound the context to */
 
 #ifdef __cplusplus
 } /* extern "C" */

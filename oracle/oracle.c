@@ -479,6 +479,14 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
             s->rec.resp_pkts += 1;
             s->rec.resp_ip_bytes += r->ip_packet_length;
         }
+        /* segment detection without the wall-clock timeout (src/packets.rs:137-160 update, 370-376 and
+           414-420 insert): a TCP packet with PSH ends the segment -- segment_count += 1, in_segment =
+           false --; any other packet leaves the flow in a segment (a new one starts when it was not) */
+        {
+            const int psh = (r->meta & FB_META_HAS_FLAGS) && r->key.protocol == 6 && (r->tcp_flags & TCP_PSH);
+            if (psh) s->rec.segment_count += 1;
+            s->rec.in_segment = psh ? 0 : 1;
+        }
         if (r->meta & FB_META_HAS_FLAGS) { /* history push, src/packets.rs:187-198, 410-426 */
             if (s->hist_len + 1 > s->hist_cap) {
                 s->hist_cap = s->hist_cap ? s->hist_cap * 2 : 16;
@@ -651,6 +659,7 @@ uint64_t orc_flow_merge(const fb_flow_mrec* in, uint64_t n, fb_flow_rec* out) {
         o.last_seen = 0;
         o.hist_len = 0;
         o.hist_mask = 0;
+        o.segment_count = 0;
         uint32_t present = 0; /* FB_HIST_CHARS bits present at the end packet */
         for (uint64_t i = a; i < b; ++i) {
             const fb_flow_mrec* x = v[i].r;
@@ -660,8 +669,11 @@ uint64_t orc_flow_merge(const fb_flow_mrec* in, uint64_t n, fb_flow_rec* out) {
             o.resp_pkts += x->rec.resp_pkts;
             o.orig_ip_bytes += x->rec.orig_ip_bytes;
             o.resp_ip_bytes += x->rec.resp_ip_bytes;
-            if (x->rec.first_seen < o.first_seen) o.first_seen = x->rec.first_seen;
-            if (x->rec.last_seen > o.last_seen) o.last_seen = x->rec.last_seen;
+            /* the session keeps what its first packet's insert stored (src/packets.rs:429-466); the
+               segment state follows its latest packet (src/packets.rs:151-159) */
+            if (x->rec.first_seen < o.first_seen) { o.first_seen = x->rec.first_seen; o.session_flags = x->rec.session_flags; }
+            if (x->rec.last_seen > o.last_seen) { o.last_seen = x->rec.last_seen; o.in_segment = x->rec.in_segment; }
+            o.segment_count += x->rec.segment_count;
             o.hist_len += x->rec.hist_len;
             o.hist_mask |= x->rec.hist_mask;
             if (end == FB_SEEN_NONE) continue;

@@ -169,7 +169,8 @@ class SessionTable:
         if s is None:
             # is_local_src/dst and is_self_src/dst are stored once, at insert (src/packets.rs:429-435)
             s = dict(outbound_bytes=0, inbound_bytes=0, orig_pkts=0, resp_pkts=0, orig_ip_bytes=0,
-                     resp_ip_bytes=0, history="", conn_state=None, is_local_src=c["local_src"],
+                     resp_ip_bytes=0, history="", conn_state=None, segment_count=0, in_segment=True,
+                     is_local_src=c["local_src"],
                      is_local_dst=c["local_dst"], is_self_src=c["self_src"], is_self_dst=c["self_dst"])
             self.sessions[key] = s
             self.new += 1
@@ -180,6 +181,10 @@ class SessionTable:
         s[side[0]] += c["plen"]
         s[side[1]] += 1
         s[side[2]] += c["iplen"]
+        # segment end on TCP PSH (src/packets.rs:140-160 / 414-420; no wall-clock timeout here)
+        psh = c["flags"] is not None and c["key"][0] == 6 and bool(c["flags"] & PSH)
+        s["segment_count"] += 1 if psh else 0
+        s["in_segment"] = not psh
         if c["flags"] is not None:
             s["history"] += c["hist"]
             if c["flags"] & (FIN | RST) and s["conn_state"] is None:
@@ -240,3 +245,35 @@ def record_to_row(c, family_of=lambda ip: 2 if ip.version == 4 else 10):
                 family=family_of(src), padding=0, packet_length=c["plen"], ip_packet_length=c["iplen"],
                 tcp_flags=c["flags"] or 0, meta=meta, hist_char=ord(c["hist"]) if c["hist"] else 0,
                 reserved=0, pkt_index=c["pkt_index"])
+
+
+def table_rows(table):
+    """SessionTable -> {canonical key tuple: counters + ordered state}, comparable with fb_flow_rec
+    rows (see rows_of_flow_recs): the integer counters, history length, conn_state and the segment
+    state."""
+    out = {}
+    for k, s in table.sessions.items():
+        out[k] = (s["outbound_bytes"], s["inbound_bytes"], s["orig_pkts"], s["resp_pkts"], s["orig_ip_bytes"],
+                  s["resp_ip_bytes"], len(s["history"]), s["conn_state"], s["segment_count"], s["in_segment"])
+    return out
+
+
+def rows_of_flow_recs(flows):
+    """fb_flow_rec records (numpy, FLOW_REC_DTYPE) -> the same form as table_rows."""
+    conn = {0: None, 1: "SF", 2: "S0", 3: "REJ", 4: "S1", 5: "-"}
+    out = {}
+    for r in flows:
+        fam = int(r["family"])
+        def ip(w):
+            if fam == 2:
+                return ipaddress.IPv4Address(int(w[0]))
+            v = 0
+            for x in w:
+                v = (v << 32) | int(x)
+            return ipaddress.IPv6Address(v)
+        k = (int(r["protocol"]), ip(r["src_ip"]), int(r["src_port"]), ip(r["dst_ip"]), int(r["dst_port"]))
+        out[k] = (int(r["outbound_bytes"]), int(r["inbound_bytes"]), int(r["orig_pkts"]), int(r["resp_pkts"]),
+                  int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]), int(r["hist_len"]), conn[int(r["conn_state"])],
+                  int(r["segment_count"]), bool(r["in_segment"]))
+    return out
+

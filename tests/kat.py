@@ -59,6 +59,14 @@ def check_case(case, records, flows, histories=None):
         for f in ("average_packet_size", "inbound_outbound_ratio"):
             if f in e:
                 assert abs(getattr(st, f) - e[f]) <= tol, (name, f, getattr(st, f), e[f])
+        # segment state (src/packets.rs:137-160, 370-376, 414-420): last_segment_end is Some exactly
+        # when a segment has ended, i.e. segment_count > 0
+        if "segment_count" in e:
+            assert st.segment_count == e["segment_count"], (name, "segment_count", st.segment_count, e["segment_count"])
+        if "in_segment" in e:
+            assert st.in_segment == e["in_segment"], (name, "in_segment", st.in_segment)
+        if "last_segment_end_set" in e:
+            assert (st.segment_count > 0) == e["last_segment_end_set"], (name, "last_segment_end", st.segment_count)
         h, cs = hist.get(k, ("", None))
         if "history" in e:
             assert h == e["history"], (name, h)

@@ -77,12 +77,40 @@ def test_record_layouts():
     assert N.PKT_OUT_DTYPE.fields["packet_length"][1] == 40
     assert N.PKT_OUT_DTYPE.fields["pkt_index"][1] == 52
     assert N.FLOW_REC_DTYPE.fields["outbound_bytes"][1] == 40
-    assert N.FLOW_REC_DTYPE.itemsize == 128
+    assert N.FLOW_REC_DTYPE.itemsize == 136
     for f, off in (("first_seen", 88), ("last_seen", 96), ("end_seen", 104), ("hist_len", 112),
-                   ("hist_mask", 116), ("conn_state", 118), ("slot", 120)):
+                   ("hist_mask", 116), ("conn_state", 118), ("slot", 120), ("segment_count", 128),
+                   ("in_segment", 132)):
         assert N.FLOW_REC_DTYPE.fields[f][1] == off, f
     assert N.DNS_OUT_DTYPE.itemsize == 16
     assert N.STATS_DTYPE.itemsize == 128
+
+
+def test_record_layouts_match_the_header(tmp_path):
+    """The numpy dtypes the host side uses are the C header's structs: offsetof / sizeof of
+    include/flodbadd_gpu.h compiled by gcc here."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    checks = [("fb_flow_rec", N.FLOW_REC_DTYPE), ("fb_flow_mrec", N.FLOW_MREC_DTYPE), ("fb_pkt_out", N.PKT_OUT_DTYPE),
+              ("fb_batch_stats", N.STATS_DTYPE), ("fb_dns_out", N.DNS_OUT_DTYPE)]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s/include/flodbadd_gpu.h"' % root, "int main(void) {"]
+    want = []
+    for st, dt in checks:
+        src.append('printf("%%zu\\n", sizeof(%s));' % st)
+        want.append(dt.itemsize)
+        for f in dt.names:
+            if f in ("src_ip", "dst_ip", "src_port", "dst_port", "protocol", "family", "padding") or f.startswith("reserved"):
+                continue  # the key's fields (fb_session_key: its size below) and reserved words
+            src.append('printf("%%zu\\n", offsetof(%s, %s));' % (st, f))
+            want.append(dt.fields[f][1])
+    src.append('printf("%zu\\n", sizeof(fb_session_key)); return 0; }')
+    want.append(40)
+    c = tmp_path / "lay.c"
+    c.write_text("\n".join(src) + "\n")
+    subprocess.run(["gcc", "-o", str(tmp_path / "lay"), str(c)], check=True)
+    got = [int(x) for x in subprocess.run([str(tmp_path / "lay")], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert got == want
 
 
 def test_flow_hash_is_deterministic_and_host_side():

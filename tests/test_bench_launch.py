@@ -44,3 +44,25 @@ def test_world_mismatch_is_an_error():
     p = _run(["--gpus", "4", "--world-check"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "launcher started 2 ranks" in (p.stderr + p.stdout)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("inject", ["fail", "group"])
+def test_c5_failure_fails_the_run(inject):
+    """At N > 1 the C5 exchange's outcome is agreed by every rank: a rank whose merge raises, or a
+    group smaller than --gpus, puts "c5_ok": false in the line and the run exits non-zero (the line
+    used to keep the error in extra.c5_flow_reduce and exit 0)."""
+    p = _run(["--gpus", "2", "--world-check"], env={"FB_C5_INJECT": inject})
+    assert p.returncode != 0, p.stdout
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    c5 = d["extra"]["c5_flow_reduce"]
+    assert d["c5_ok"] is False and "error" in c5
+    assert c5["failed_ranks"] == ([1] if inject == "fail" else [0, 1])
+
+
+@pytest.mark.timeout(240)
+def test_c5_success_keeps_rc_zero():
+    p = _run(["--gpus", "2", "--world-check"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert d["c5_ok"] is True and d["extra"]["c5_flow_reduce"]["ranks_in_group"] == 2

@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from flodbadd_amd import _native as N
-from flodbadd_amd.distributed import MREC_WORDS, _key_words, exchange_merge, shard_range, sort_by_ord, sort_keys
+from flodbadd_amd.distributed import MREC_WORDS, REC_WORDS, _key_words, exchange_merge, shard_range, sort_by_ord, sort_keys
 
 TOTAL = 9000   # frames per global batch
 CALLS = 3      # update calls (global batches) per rank
@@ -63,7 +63,7 @@ def _oracle_merge(rows):
     from oracle import coracle
     m = np.ascontiguousarray(rows.numpy()).view(N.FLOW_MREC_DTYPE).reshape(-1)
     merged = coracle.flow_merge(m)
-    return torch.from_numpy(np.ascontiguousarray(merged).view(np.int64).reshape(len(merged), 16).copy())
+    return torch.from_numpy(np.ascontiguousarray(merged).view(np.int64).reshape(len(merged), REC_WORDS).copy())
 
 
 def _worker(rank, world, port, outdir, empty_rank=-1):
@@ -123,8 +123,8 @@ def test_gloo_global_flow_table(tmp_path, world):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
         assert len(got) == len(ref), (len(got), len(ref))
         g, e = _rows(got), _rows(ref)
-        bad = np.flatnonzero(g.view(np.uint8).reshape(len(g), 128).any(axis=1) &
-                             (g.view(np.uint8).reshape(len(g), 128) != e.view(np.uint8).reshape(len(e), 128)).any(axis=1))
+        bad = np.flatnonzero(g.view(np.uint8).reshape(len(g), N.FLOW_REC_DTYPE.itemsize).any(axis=1) &
+                             (g.view(np.uint8).reshape(len(g), N.FLOW_REC_DTYPE.itemsize) != e.view(np.uint8).reshape(len(e), N.FLOW_REC_DTYPE.itemsize)).any(axis=1))
         assert g.tobytes() == e.tobytes(), (r, bad[:5], g[bad[:2]], e[bad[:2]])
 
 

@@ -62,3 +62,19 @@ def test_samples_c_oracle_and_generator(cid):
     assert fl.export_sorted().tobytes() == g["flows_all"].tobytes()
     gout, _, gcls, gst = coracle.parse_classify(coracle.make_cfg(1), frames, offs)
     assert gout.tobytes() == g["records_global"].tobytes()
+
+
+@pytest.mark.parametrize("cid", [2, 3])
+def test_samples_flow_table_matches_python_restatement(cid):
+    """The C oracle's session table (counters, history length, conn_state, segment state) equals the
+    independent Python restatement's dict table on the sample batches."""
+    g = load("c%d_sample.npz" % cid)
+    fl = coracle.Flows()
+    fl.update(g["records_all"])
+    pcfg = pyoracle.Config.from_bitmap(coracle.default_bitmap(), session_filter=2)
+    table = pyoracle.SessionTable()
+    pyoracle.run_batch(pcfg, g["frames"], g["offsets"], table)
+    got = pyoracle.rows_of_flow_recs(fl.export_sorted())
+    assert got == pyoracle.table_rows(table)
+    segs = [v[8] for v in got.values()]
+    assert sum(segs) > 0 and any(not v[9] for v in got.values())  # the mix has PSH packets

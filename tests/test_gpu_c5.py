@@ -98,8 +98,8 @@ def test_device_export_and_merge_equal_one_table(world):
                 a = m[int(counts[:o].sum()): int(counts[: o + 1].sum())]
                 b = em[int(ecounts[:o].sum()): int(ecounts[: o + 1].sum())]
                 assert np.all(a["rec"]["slot"] == r)
-                ka = np.ascontiguousarray(a).view(np.uint8).reshape(len(a), 144)
-                kb = np.ascontiguousarray(b).view(np.uint8).reshape(len(b), 144)
+                ka = np.ascontiguousarray(a).view(np.uint8).reshape(len(a), N.FLOW_MREC_DTYPE.itemsize)
+                kb = np.ascontiguousarray(b).view(np.uint8).reshape(len(b), N.FLOW_MREC_DTYPE.itemsize)
                 ka, kb = ka[np.lexsort(ka[:, :40].T[::-1])], kb[np.lexsort(kb[:, :40].T[::-1])]
                 assert ka.tobytes() == kb.tobytes(), (r, o)
             groups.append((m, counts))

@@ -135,3 +135,34 @@ def test_dense_lookback_fallback_forced(monkeypatch):
                 b.check()
     finally:
         cap.close()
+
+
+def test_dense_corrupted_tile_offset_drops_instead_of_faulting(monkeypatch):
+    """A corrupted look-back offset (FB_DENSE_OFFSET_SKEW: half a batch added to every tile's
+    batch-wide offset -- what round 4's no-look-back ablation did by adding the real prefix to a
+    fixed one, and faulted with an illegal memory access) must not write outside the caller's
+    buffers: the slots whose destination passes the batch's n records are dropped and the batch's
+    error word has bit 32; a context without the skew is bit-exact again on the same batch."""
+    n = 65536
+    frames, offs = synth.generate(3, n, first=7)
+    monkeypatch.setenv("FB_DENSE_OFFSET_SKEW", str(n // 2))
+    cap = _ctx()
+    monkeypatch.delenv("FB_DENSE_OFFSET_SKEW")
+    try:
+        b = _Dense(frames, offs)
+        b.run(cap)
+        N.check(N.gpu_lib().fb_stream_sync(None))
+        st = b.st.download(np.zeros(1, dtype=N.STATS_DTYPE))
+        assert int(st[0]["error"]) & 32
+        out = b.out.download(np.zeros(n * 56 + 64, dtype=np.uint8))
+        dns = b.dns.download(np.zeros(n * 16 + 64, dtype=np.uint8))
+        assert (out[n * 56:] == 0x5A).all() and (dns[n * 16:] == 0x5A).all(), "written past the buffers"
+        assert int(st[0]["n_session"]) == len(b.ref[0])  # the counts themselves are right
+    finally:
+        cap.close()
+    cap = _ctx()
+    try:
+        b.run(cap)
+        b.check()
+    finally:
+        cap.close()

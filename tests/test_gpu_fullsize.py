@@ -134,3 +134,72 @@ def test_full_size_c4_zipf_session_table(gpu_capture):
     assert int(max(gflows["orig_pkts"] + gflows["resp_pkts"])) > n_records // 20  # the skew is there
     assert np.array_equal(_void_sorted(gflows), _void_sorted(rflows))
     cap.clear_all_sessions()
+
+
+def test_full_size_c4_pipelined_table_only_bench_path():
+    """bench.py's `extra.c4` timed path exactly (bench.py run_config / c4_line): a context with the
+    bench's configuration (GlobalOnly, FB_CFG_FIXED_TABLE at 2^21 slots, 2^24 packets per batch),
+    `fb_set_session_records(ctx, 0)` (the table is the only output), two device-resident buffer sets
+    of 10,485,760 IMIX frames, and five back-to-back `fb_process_seg_async_dev` calls alternating
+    between them with no join in between -- each update overlapping the next call's parse on the
+    context's own stream -- then `fb_flow_join` and the export.  The two sets hold DIFFERENT batches
+    (the bench rotates one batch), so the table must fold five calls of two batches in call order:
+    every row, counters, positions, ordered state and segment state, equals the oracle fed the same
+    five batches in order (src/packets.rs:329-343, 105-198), and every call's batch stats are clean."""
+    import ctypes as C
+    lib = N.gpu_lib()
+    cfg = N.FbConfig()
+    cfg.abi_version = N.FB_ABI_VERSION
+    cfg.filter = N.FB_FILTER_GLOBAL_ONLY
+    cfg.max_batch_packets = 1 << 24
+    cfg.flow_capacity = 1 << 21
+    cfg.flags = N.FB_CFG_FIXED_TABLE
+    ctx = lib.fb_create(0, C.byref(cfg))
+    assert ctx, lib.fb_last_error()
+    ctx = C.c_void_p(ctx)
+    n = 10 * FULL
+    try:
+        stream = N.Stream()
+        sets, expect = [], []
+        for k in range(2):
+            frames, offs = synth.generate(4, n, first=k * n)
+            nseg = (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES
+            sets.append((N.DeviceBuffer(frames.nbytes).upload(frames), frames.nbytes,
+                         N.DeviceBuffer(offs.nbytes).upload(offs), N.DeviceBuffer(nseg * N.SEG_BYTES),
+                         N.DeviceBuffer(nseg * 4)))
+            out, _, _, st = coracle.parse_classify(coracle.make_cfg(int(SessionFilter.GlobalOnly)), frames, offs)
+            expect.append((out, st))
+            del frames, offs
+        N.check(lib.fb_set_session_records(ctx, 0))
+        calls = [0, 1, 0, 1, 0]
+        stats = [N.DeviceBuffer(N.STATS_DTYPE.itemsize) for _ in calls]
+        for i, k in enumerate(calls):
+            d_fr, nb, d_off, d_out, d_seg = sets[k]
+            N.check(lib.fb_process_seg_async_dev(ctx, d_fr.ptr, nb, d_off.ptr, n, d_out.ptr, d_seg.ptr, None,
+                                                 stats[i].ptr, stream.ptr))
+        N.check(lib.fb_flow_join(ctx, stream.ptr))
+        stream.sync()
+        flows = coracle.Flows()
+        for i, k in enumerate(calls):
+            out, est = expect[k]
+            ost = np.zeros(1, dtype=N.STATS_DTYPE)
+            flows.update(out, ost)
+            g = stats[i].download(np.zeros(1, dtype=N.STATS_DTYPE))
+            _conserved(g, n)
+            for f in ("total_processed", "tcp_processed", "udp_processed", "ipv4_processed", "ipv6_processed",
+                      "n_session", "n_dns", "n_drop", "n_filtered"):
+                assert int(g[0][f]) == int(est[0][f]), (i, f)
+            assert int(g[0]["new_sessions"]) == int(ost[0]["new_sessions"]), i
+            assert int(g[0]["updated_sessions"]) == int(ost[0]["updated_sessions"]), i
+        cnt = C.c_uint64(0)
+        N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
+        gflows = np.zeros(max(cnt.value, 1), dtype=N.FLOW_REC_DTYPE)
+        got = C.c_uint64(0)
+        N.check(lib.fb_flow_export(ctx, N.ptr(gflows), cnt.value, C.byref(got), None))
+        gflows = gflows[: got.value]
+        rflows = flows.export_sorted()
+        assert len(gflows) == len(rflows) == cnt.value
+        assert int(gflows["segment_count"].sum()) > 0 and int((gflows["in_segment"] == 0).sum()) > 0
+        assert np.array_equal(_void_sorted(gflows), _void_sorted(rflows))
+    finally:
+        lib.fb_destroy(ctx)

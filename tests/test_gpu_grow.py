@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 def _key_order(a):
     """Row order of flow records by the derived Ord of Session (the oracle's export order)."""
-    w = np.ascontiguousarray(a).view(np.uint8).reshape(len(a), 128)[:, :40].copy().view(np.uint32).reshape(len(a), 10)
+    w = np.ascontiguousarray(a).view(np.uint8).reshape(len(a), N.FLOW_REC_DTYPE.itemsize)[:, :40].copy().view(np.uint32).reshape(len(a), 10)
     ports, pf = w[:, 8], w[:, 9]
     return np.lexsort([ports >> 16, w[:, 7], w[:, 6], w[:, 5], w[:, 4], ports & 0xFFFF, w[:, 3], w[:, 2], w[:, 1],
                        w[:, 0], (pf >> 8) & 0xFF, pf & 0xFF])
@@ -31,7 +31,7 @@ def _same_table(g, r):
     g["slot"] = 0
     r = r.copy()
     r["slot"] = 0
-    bad = np.flatnonzero((g.view(np.uint8).reshape(len(g), 128) != r.view(np.uint8).reshape(len(r), 128)).any(axis=1))
+    bad = np.flatnonzero((g.view(np.uint8).reshape(len(g), N.FLOW_REC_DTYPE.itemsize) != r.view(np.uint8).reshape(len(r), N.FLOW_REC_DTYPE.itemsize)).any(axis=1))
     assert g.tobytes() == r.tobytes(), "first differing rows: %s" % bad[:5]
 
 
