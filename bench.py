@@ -249,6 +249,63 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
                 launches=n_launch, stats={k: int(st[0][k]) for k in ("n_session", "n_dns", "n_drop", "n_filtered")})
 
 
+def queue_line(N, lib, ctx, config_id, n, steps, warmup, rotate, depth=8):
+    """One batch per call without a launch per batch: the resident queue-fed parse (fb_seg_queue_*,
+    k_parse_seg_queue).  The same device-resident workload as the main line (rotate distinct batch
+    buffer sets); the host submits one batch per call and the timed region runs from the first
+    submission to the observed completion of the last (host wall clock: the queue's kernel runs on
+    its own stream).  Every batch's stats are checked against a plain fb_parse_classify_seg_dev."""
+    from flodbadd_amd import synth
+    frames, offs = synth.generate(config_id, n, first=0)
+    nseg = (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES
+    sets, descs = [], []
+    for _ in range(rotate):
+        b = (N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+             N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize))
+        d = np.zeros(1, dtype=N.SEG_BATCH_DTYPE)
+        d[0] = (b[0].ptr.value, frames.nbytes, b[1].ptr.value, n, 0, b[2].ptr.value, b[3].ptr.value, 0, b[4].ptr.value)
+        sets.append(b)
+        descs.append(d)
+    # the expected stats: one plain launch into the first set
+    ref = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+    b = sets[0]
+    N.check(lib.fb_parse_classify_seg_dev(ctx, b[0].ptr, frames.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr, None, ref.ptr, None))
+    expect = ref.download(np.zeros(1, dtype=N.STATS_DTYPE))
+    N.check(lib.fb_stream_sync(None))
+    q = lib.fb_seg_queue_create(ctx, depth, 0)
+    if not q:
+        raise RuntimeError("fb_seg_queue_create: %s" % lib.fb_last_error().decode())
+    q = C.c_void_p(q)
+    ptrs = [C.c_void_p(d.ctypes.data) for d in descs]
+    t = C.c_uint64()
+    submit, wait = lib.fb_seg_queue_submit, lib.fb_seg_queue_wait
+    try:
+        for i in range(warmup):
+            N.check(submit(q, ptrs[i % rotate], C.byref(t)))
+        N.check(wait(q, t.value))
+        t0 = time.perf_counter()
+        for i in range(steps):
+            rc = submit(q, ptrs[i % rotate], C.byref(t))
+            if rc:
+                N.check(rc)
+        N.check(wait(q, t.value))
+        t1 = time.perf_counter()
+    finally:
+        N.check(lib.fb_seg_queue_destroy(q))
+    for k in range(min(rotate, steps)):
+        got = sets[k][4].download(np.zeros(1, dtype=N.STATS_DTYPE))
+        if got.tobytes() != expect.tobytes():
+            raise RuntimeError("queue batch %d stats differ: %s vs %s" % (k, got, expect))
+    for b in sets:
+        for x in b:
+            x.free()
+    el = t1 - t0
+    return dict(value=round(n * steps / el / 1e6, 2), unit="Mpackets/s", ms_per_step=round(el * 1e3 / steps, 4),
+                steps=steps, depth=depth,
+                note="fb_seg_queue_submit per batch into the resident k_parse_seg_queue kernel; host wall clock "
+                     "from the first submission to the last batch's completion word")
+
+
 def enrich_timing(N, lib, ctx, flows, stream, reps=5):
     """New-session enrichment (fb_flow_enrich_dev) over every flow of the C4 table against
     IPtoASN-sized synthetic tables: 500k IPv4 + 100k IPv6 ASN ranges, 50k blacklist ranges in 32
@@ -814,6 +871,7 @@ def main():
                     help="output layout: per-wavefront segments (default) or one batch-wide compaction")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other output layout")
     ap.add_argument("--no-single-launch", action="store_true", help="skip timing one batch per launch")
+    ap.add_argument("--no-queue", action="store_true", help="skip timing one batch per call through fb_seg_queue")
     ap.add_argument("--no-copy-ref", action="store_true", help="skip the stream-copy bandwidth reference")
     ap.add_argument("--batches-per-launch", type=int, default=None,
                     help="seg mode: batches (steps) per kernel launch (fb_parse_classify_seg_batches_dev); "
@@ -913,6 +971,13 @@ def main():
                                             unit="Mpackets/s", ms_per_step=round(r1["elapsed"] * 1e3 / st_1, 4),
                                             roofline_achieved_GBs=round(r1["algo_bytes"] / pl1 / 1e9, 1),
                                             roofline_frac=round(r1["algo_bytes"] / pl1 / 1e9 / HBM_PEAK_GBS, 4))
+        if not args.no_queue:  # one batch per call through the resident queue-fed kernel
+            try:
+                qr = queue_line(N, lib, ctx, args.config, n, max(args.steps, 256), max(args.warmup // 2, 8), rotate)
+                qr["value"] = round(qr["value"] * world, 2)
+                extra["single_batch_queue"] = qr
+            except Exception as e:  # reported beside the line; the headline does not depend on it
+                extra["single_batch_queue"] = {"error": repr(e)[:300]}
     # N > 1: the scaling line needs only the headline path (the other layout is timed at N = 1)
     if not args.no_other_mode and world == 1:
         other = "dense" if args.mode == "seg" else "seg"

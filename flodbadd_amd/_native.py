@@ -82,6 +82,7 @@ FB_IP_DTYPE = np.dtype([("addr", "<u4", (4,)), ("family", "<u4"), ("reserved", "
 FB_SEG_FRAMES = 64
 SEG_BYTES = FB_SEG_FRAMES * 56
 FB_MAX_SEG_BATCHES = 32
+FB_QUEUE_MAX_DEPTH = 32
 # fb_seg_batch: one batch of fb_parse_classify_seg_batches_dev (device pointers as integers)
 SEG_BATCH_DTYPE = np.dtype([("d_frames", "<u8"), ("frames_bytes", "<u8"), ("d_offsets", "<u8"), ("n", "<u4"),
                             ("reserved", "<u4"), ("d_out", "<u8"), ("d_seg", "<u8"), ("d_class", "<u8"),
@@ -227,6 +228,11 @@ GPU_SYMBOLS = [
     ("fb_device_count", _I, [C.POINTER(C.c_int)]),
     ("fb_set_device", _I, [_I]),
     ("fb_ctx_device", _I, [_P, C.POINTER(C.c_int)]),
+    ("fb_seg_queue_create", _P, [_P, _U32, _U32]),
+    ("fb_seg_queue_submit", _I, [_P, _P, _PU64]),
+    ("fb_seg_queue_query", _I, [_P, _U64]),
+    ("fb_seg_queue_wait", _I, [_P, _U64]),
+    ("fb_seg_queue_destroy", _I, [_P]),
 ]
 
 _gpu = None

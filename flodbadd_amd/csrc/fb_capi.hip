@@ -694,6 +694,211 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, ui
     return launch_seg(c, sb, n_max, nullptr, (hipStream_t)stream);
 }
 
+// ---- resident queue-fed parse (k_parse_seg_queue, fb_parse.hip) ------------------------------------
+#ifdef FB_QUEUE_TRACE
+static unsigned long long g_qtrace[kQTraceAll];
+#endif
+struct fb_seg_queue {
+    int device = 0;
+    uint32_t depth = 0;  // batches in flight at most
+    uint32_t slots = 0;  // ring slots: depth rounded up to a power of two (the kernel masks)
+    hipStream_t stream = nullptr;
+    QueueHost* h = nullptr;      // pinned, coherent host memory (the kernel's ring and completion words)
+    QueueHost* h_dev = nullptr;  // its device alias
+    QueueDev* d_ring = nullptr;  // the device side of the ring
+    DevConfig* d_cfg = nullptr;  // the context's configuration when the queue was created
+    unsigned long long* d_tick = nullptr;
+    uint32_t* d_blk = nullptr;
+    uint32_t* d_head = nullptr;
+    uint32_t* d_err = nullptr;
+    unsigned long long* d_trace = nullptr;  // -DFB_QUEUE_TRACE builds
+    uint64_t submitted = 0;
+    bool launched = false;
+    hipError_t gone = hipSuccess;  // what the stream reported when the kernel was found gone
+};
+
+static void queue_free(fb_seg_queue* q) {
+    if (q->stream) hipStreamDestroy(q->stream);
+    hipFree(q->d_cfg);
+    hipFree(q->d_tick);
+    hipFree(q->d_blk);
+    hipFree(q->d_head);
+    hipFree(q->d_err);
+    hipFree(q->d_ring);
+    hipFree(q->d_trace);
+    if (q->h) hipHostFree(q->h);
+    delete q;
+}
+
+static uint64_t hload(const unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+// FB_OK once the kernel is gone or going (a block expired, or -- every `every` calls, a runtime call --
+// the kernel has ended), 1 while it runs
+static int queue_kernel_gone(fb_seg_queue* q, uint64_t spin, uint64_t every) {
+    if (hload(&q->h->status) & kQueueExpired) return FB_OK;
+    if (spin % every != every - 1u) return 1;
+    const hipError_t e = hipStreamQuery(q->stream);
+    if (e == hipErrorNotReady) return 1;
+    q->gone = e;
+    return FB_OK;
+}
+
+static int queue_gone_error(fb_seg_queue* q) {
+    const QueueHost* h = q->h;
+    return set_err(FB_ERR_INTERNAL,
+                   "the queue kernel has stopped (status %llu, stream: %s; a block left after %llu ticks idle "
+                   "waiting for batch %llu (block %llu), tail %llu): destroy the queue",
+                   (unsigned long long)hload(&h->status), hipGetErrorString(q->gone), (unsigned long long)hload(&h->pad[0]),
+                   (unsigned long long)(hload(&h->pad[1]) & 0xFFFFFFFFu), (unsigned long long)(hload(&h->pad[1]) >> 32),
+                   (unsigned long long)hload(&h->pad[2]));
+}
+
+fb_seg_queue* fb_seg_queue_create(fb_ctx* c, uint32_t depth, uint32_t idle_ms) {
+    if (!c) {
+        set_err(FB_ERR_INVAL, "ctx is NULL");
+        return nullptr;
+    }
+    if (depth == 0u) depth = 8u;
+    if (depth > kQueueMax) {
+        set_err(FB_ERR_INVAL, "depth %u > FB_QUEUE_MAX_DEPTH", depth);
+        return nullptr;
+    }
+    DeviceGuard g(c->device);
+    fb_seg_queue* q = new (std::nothrow) fb_seg_queue();
+    if (!q) {
+        set_err(FB_ERR_NOMEM, "queue");
+        return nullptr;
+    }
+    q->device = c->device;
+    q->depth = depth;
+    q->slots = 1u;
+    while (q->slots < depth) q->slots <<= 1;
+    bool ok = hipHostMalloc((void**)&q->h, sizeof(QueueHost), hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess;
+    if (ok) {
+        memset(q->h, 0, sizeof(QueueHost));
+        ok = hipHostGetDevicePointer((void**)&q->h_dev, q->h, 0) == hipSuccess;
+    }
+    ok = ok && hipMalloc(&q->d_cfg, sizeof(DevConfig)) == hipSuccess &&
+         hipMemcpy(q->d_cfg, c->h_cfg, sizeof(DevConfig), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMalloc(&q->d_tick, kQueueMax * 8u * 8u) == hipSuccess && hipMemset(q->d_tick, 0, kQueueMax * 64u) == hipSuccess;
+    ok = ok && hipMalloc(&q->d_blk, kQueueMax * 4u) == hipSuccess && hipMemset(q->d_blk, 0, kQueueMax * 4u) == hipSuccess;
+    ok = ok && hipMalloc(&q->d_head, kQueueMax * kQueueHeadWords * 4u) == hipSuccess &&
+         hipMemset(q->d_head, 0, kQueueMax * kQueueHeadWords * 4u) == hipSuccess;
+    ok = ok && hipMalloc(&q->d_err, 4) == hipSuccess && hipMemset(q->d_err, 0, 4) == hipSuccess;
+    ok = ok && hipMalloc(&q->d_ring, sizeof(QueueDev)) == hipSuccess && hipMemset(q->d_ring, 0, sizeof(QueueDev)) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) == hipSuccess;
+#ifdef FB_QUEUE_TRACE
+    if (ok) {
+        std::vector<unsigned long long> t0((size_t)kQTraceAll, 0ull);
+        std::fill(t0.begin() + kQtFirst * kQTraceN, t0.begin() + (kQtArr0 + 1) * kQTraceN, ~0ull);
+        ok = hipMalloc(&q->d_trace, t0.size() * 8u) == hipSuccess &&
+             hipMemcpy(q->d_trace, t0.data(), t0.size() * 8u, hipMemcpyHostToDevice) == hipSuccess;
+    }
+#endif
+    if (!ok) {
+        queue_free(q);
+        set_err(FB_ERR_NOMEM, "queue resources");
+        return nullptr;
+    }
+    QueueParams p;
+    p.cfg = q->d_cfg;
+    p.h = q->h_dev;
+    p.d = q->d_ring;
+    p.tick = q->d_tick;
+    p.blk_done = q->d_blk;
+    p.head = q->d_head;
+    p.error = q->d_err;
+    p.depth = q->slots;
+    p.idle_ticks = (unsigned long long)(idle_ms ? idle_ms : 5000u) * 100000ull;  // s_memrealtime: 100 MHz
+    p.trace = q->d_trace;
+    // two blocks per CU, not k_parse_seg's three: the resident kernel must leave room on every CU for
+    // the work the host issues while it runs -- blit kernels of pageable copies (a capture loop reads
+    // its results back), other streams' kernels; at three blocks (80 VGPRs x 6 waves per SIMD) a D2H
+    // copy into pageable memory waited until the queue's kernel had left (round-5 probe)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus < 1) cus = 1;
+    // every block must be resident at once: a batch completes when every block has passed it
+    int occ = 0;
+    if (occupancy_parse_seg_queue(&occ) != hipSuccess || occ < 1) occ = 1;
+    const uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(FB_QUEUE_BPC, occ) * cus));
+    if (launch_parse_seg_queue(p, grid, q->stream) != hipSuccess) {
+        queue_free(q);
+        set_err(FB_ERR_HIP, "queue kernel launch");
+        return nullptr;
+    }
+    q->launched = true;
+    return q;
+}
+
+int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* x, uint64_t* ticket) {
+    if (!q || !x) return set_err(FB_ERR_INVAL, "queue and batch are required");
+    if (!x->d_stats) return set_err(FB_ERR_INVAL, "d_stats is required");
+    if (x->n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n > FB_MAX_BATCH_PACKETS");
+    if (x->frames_bytes > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "frames_bytes must be < 4 GiB");
+    if (!x->d_offsets || (x->n && (!x->d_out || !x->d_seg))) return set_err(FB_ERR_INVAL, "d_offsets, d_out and d_seg are required");
+    if (x->n && x->frames_bytes && !x->d_frames) return set_err(FB_ERR_INVAL, "d_frames is NULL");
+    const uint64_t k = q->submitted, S = q->slots;
+    // at most `depth` batches in flight, and a slot is reused only once its previous batch (k - S) is
+    // complete -- its completion word is stored after the kernel has reset the slot's state
+    const uint64_t back[2] = {q->depth, S};
+    for (const uint64_t b : back) {
+        if (k < b) continue;  // (no such batch yet)
+        const uint64_t prev = k - b;
+        for (uint64_t spin = 0; hload(&q->h->cdone[prev & (S - 1u)]) != prev + 1u; ++spin) {
+            if (queue_kernel_gone(q, spin, 4096u) == FB_OK && hload(&q->h->cdone[prev & (S - 1u)]) != prev + 1u)
+                return queue_gone_error(q);
+            __builtin_ia32_pause();
+        }
+    }
+    QueueHost* h = q->h;
+    memcpy((void*)&h->desc[k & (S - 1u)], x, sizeof(fb_seg_batch));
+    __atomic_store_n(&h->tail, (unsigned long long)(k + 1u), __ATOMIC_RELEASE);  // after the descriptor
+    q->submitted = k + 1u;
+    if (ticket) *ticket = k;
+    return FB_OK;
+}
+
+static int queue_poll(fb_seg_queue* q, uint64_t t, uint64_t spin, uint64_t every) {
+    if (!q) return set_err(FB_ERR_INVAL, "queue is NULL");
+    if (t >= q->submitted) return set_err(FB_ERR_INVAL, "ticket %llu was not issued", (unsigned long long)t);
+    if (t + q->depth < q->submitted) return FB_OK;  // a later submission waited for it
+    const uint64_t slot = t & (q->slots - 1u);
+    if (hload(&q->h->cdone[slot]) == t + 1u) return FB_OK;
+    if (queue_kernel_gone(q, spin, every) == FB_OK && hload(&q->h->cdone[slot]) != t + 1u)
+        return queue_gone_error(q);
+    return 1;
+}
+
+int fb_seg_queue_query(fb_seg_queue* q, uint64_t t) { return queue_poll(q, t, 0u, 1u); }
+
+int fb_seg_queue_wait(fb_seg_queue* q, uint64_t t) {
+    for (uint64_t spin = 0;; ++spin) {
+        const int rc = queue_poll(q, t, spin, 4096u);
+        if (rc != 1) return rc;
+        __builtin_ia32_pause();
+    }
+}
+
+int fb_seg_queue_destroy(fb_seg_queue* q) {
+    if (!q) return set_err(FB_ERR_INVAL, "queue is NULL");
+    DeviceGuard g(q->device);
+    __atomic_store_n(&q->h->stop, 1ull, __ATOMIC_RELEASE);  // the kernel leaves once the submitted batches are done
+    int rc = FB_OK;
+    if (q->launched && hipStreamSynchronize(q->stream) != hipSuccess) rc = set_err(FB_ERR_HIP, "queue kernel");
+#ifdef FB_QUEUE_TRACE
+    if (q->d_trace) hipMemcpy(g_qtrace, q->d_trace, sizeof(g_qtrace), hipMemcpyDeviceToHost);
+#endif
+    queue_free(q);
+    return rc;
+}
+#ifdef FB_QUEUE_TRACE
+// diagnostic builds only: the last destroyed queue's trace (kQTraceAll words: QTrace order, then per block)
+extern "C" __attribute__((visibility("default"))) int fb_seg_queue_trace_last(unsigned long long* out) {
+    memcpy(out, g_qtrace, sizeof(g_qtrace));
+    return (int)kQTraceAll;
+}
+#endif
+
 static int parse_seg(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, const uint32_t* d_offsets, uint32_t n,
                      fb_pkt_out* d_out, uint32_t* d_seg, uint8_t* d_class, fb_batch_stats* d_stats, void* stream,
                      bool want_parts) {

@@ -348,6 +348,60 @@ constexpr uint32_t kEntV6 = 1u << 28;               // index word: an IPv6 key (
 constexpr uint32_t kRecUnitShift = 16, kRecV6 = 1u << 23;  // rec_part fields
 __host__ __device__ inline bool upd_ent_v6(uint32_t a_w) { return ((a_w >> 8) & 0xFFu) == 10u; }
 
+// Resident queue-fed parse (fb_seg_queue_*, k_parse_seg_queue): the host control block lives in
+// pinned, coherent host memory (the kernel reads it with system-scope loads); per ring slot the
+// device keeps the batch's stats words (tick, 8 per slot) and the count of blocks done with it.
+constexpr uint32_t kQueueMax = FB_QUEUE_MAX_DEPTH;
+struct QueueHost {
+    unsigned long long tail;    // batches submitted (host store, after the slot's descriptor)
+    unsigned long long stop;    // host: no batch follows the submitted ones; the kernel exits when idle
+    unsigned long long status;  // device: kQueueExpired -- a block waited idle_ticks for a batch and left
+    unsigned long long pad[5];
+    unsigned long long cdone[kQueueMax];  // slot k % depth: k + 1 once batch k is complete (system store)
+    fb_seg_batch desc[kQueueMax];         // slot k % depth: batch k (host stores)
+};
+constexpr unsigned long long kQueueExpired = 1ull;
+constexpr uint32_t kQueueHeadWords = 128u;  // per slot: up to 8 counters, one 64-B line each
+// The device side of the ring: ONE block at a time reads the host's tail over PCIe (poller: 0 free,
+// else the polling block + 1) and copies the new descriptors here; every block reads these.
+struct QueueDev {
+    unsigned long long tail;   // batches whose descriptors are in desc[]
+    unsigned long long stop;   // the host's stop word, as the last poll saw it with nothing left
+    uint32_t poller;
+    uint32_t pad[3];
+    fb_seg_batch desc[kQueueMax];
+};
+struct QueueParams {
+    const DevConfig* cfg;
+    QueueHost* h;                  // device alias of the host control block
+    QueueDev* d;                   // the device side (zeroed at create)
+    unsigned long long* tick;      // [kQueueMax * 8] packed stats words per slot (k_parse_seg's format)
+    uint32_t* blk_done;            // [kQueueMax] blocks that have finished the slot's batch
+    uint32_t* head;                // [kQueueMax * kQueueHeadWords] the slot's chunk counters (k_parse_seg_queue)
+    uint32_t* error;               // the queue's error word (copied into every batch's stats)
+    uint32_t depth;                // ring slots: a power of two <= kQueueMax
+    unsigned long long idle_ticks; // s_memrealtime ticks (100 MHz) a block waits for a batch before it leaves
+    unsigned long long* trace;     // diagnostic builds (-DFB_QUEUE_TRACE): kQTraceWords x kQTraceN timings
+};
+// -DFB_QUEUE_TRACE (tools/build_variants.sh, never the product): per batch (k % kQTraceN) the
+// real-time ticks of its publication in the device ring, the first block's descriptor load, the first
+// and the last block's completion, and counts of the waves that drained and blocked before it and of
+// the poller's host reads while it was awaited.
+constexpr uint32_t kQTraceN = 1024u, kQTraceWords = 6u;
+// then per block (up to kQTraceN blocks, 4 words): its completion ticks of batches kQtB0 and kQtB1,
+// its HW_ID and XCC_ID registers
+constexpr uint32_t kQtB0 = 100u, kQtB1 = 164u, kQTraceAll = kQTraceWords * kQTraceN + 4u * kQTraceN;
+enum QTrace : uint32_t { kQtPub = 0, kQtFirst, kQtArr0, kQtDone, kQtDrain, kQtPolls };
+// Workgroups per CU of the queue kernel (fb_seg_queue_create's note), and its waves per SIMD as the
+// register budget is set: five at two workgroups (<= 102 VGPRs: no spills in the streaming loop, and a
+// fifth wave's registers stay free on every SIMD for the blit and other kernels issued meanwhile)
+#ifndef FB_QUEUE_BPC
+#define FB_QUEUE_BPC 2
+#endif
+constexpr int kQueueWavesPerSimd = FB_QUEUE_BPC * 8 / 4 + 1;
+hipError_t launch_parse_seg_queue(const QueueParams& q, uint32_t grid, hipStream_t s);
+hipError_t occupancy_parse_seg_queue(int* blocks_per_cu);
+
 // Launchers (fb_parse.hip / fb_compact.hip / fb_flow.hip).
 // Which k_parse_seg instance: the segmented output; dense pass 1 (segment counts, classes, stats);
 // dense pass 2 (records to batch-wide positions from the scanned counts, ParseParams::pre).

@@ -1258,4 +1258,558 @@ hipError_t occupancy_parse_seg(int* blocks_per_cu) {
 }
 uint32_t parse_seg_block_threads() { return kSegThreads; }
 
+// ============================================================================================
+// k_parse_seg_queue -- k_parse_seg's segmented output as ONE resident kernel fed batch by batch
+// (fb_seg_queue_*).  A single-batch launch pays its prologue (configuration, then the first offsets,
+// then the first headers: two dependent round trips before a wave has work) and the tail of the
+// batch's last segments on every call: 27.8 us of kernel per 1M-frame C2 batch against 22.4 us per
+// batch inside a multi-batch launch (profiles/r05_single_batch_trace.txt).  Here the waves stream
+// from one batch into the next as k_parse_seg's multi-batch instance does, but the batches arrive
+// while the kernel runs: the host writes batch k into slot k % depth of a ring in pinned host memory
+// and then its tail word; a block learns batch k's descriptor once (the first wave that needs it
+// copies it from the device side of the ring into the block's LDS, the others wait on the LDS copy;
+// one block at a time reads the host's ring over PCIe into the device side) and takes batch k's
+// segments in chunks from the slot's device counter, handing them to its waves through an LDS
+// counter.  A wave never blocks while it holds unprocessed segments: when the next batch is not
+// published yet it drains its pipeline and only then waits.
+// Completion without a grid barrier (blocks need not be resident together): each wave, before it
+// counts itself done with a batch (LDS arrival per batch), has waited for its own stores; the
+// block's last wave adds the block's counters into the batch's stats words (the block completing a
+// word writes its stats fields), writes the XCD's L2 back (agent release) and counts the block in
+// the batch's device counter; the last block resets that counter and stores k + 1 into the slot's
+// completion word in host memory (system release), which fb_seg_queue_query polls.  The host never
+// reuses a slot before its batch completed, so per-slot LDS and device state is reset by the batch's
+// last user.  A block that waits idle_ticks for a batch, or sees the host's stop word with nothing
+// left, leaves; an expired queue reports it in the control block's status word.
+// ============================================================================================
+// The queue kernel's output stores are write-through (sc1): a batch is complete when the waves that
+// wrote it have their stores acknowledged (s_waitcnt vmcnt(0) before each wave counts itself done),
+// with no dirty line left in an XCD's L2 -- an agent-scope release per block per batch (an L2
+// write-back, buffer_wbl2) took ~1.2 ms per batch for 512 blocks in the first build.  (16-B sc1
+// stores stream at the plain rate, MI355X_MICROARCH.md.)
+#ifndef FB_QUEUE_ST_AUX
+#define FB_QUEUE_ST_AUX 16
+#endif
+constexpr int kQSt = FB_QUEUE_ST_AUX;  // cache-policy bits: sc1
+// A batch's segments are handed to blocks in chunks from the slot's device counter (Q.head), each
+// block holding its current chunk and the next: with a static share per block (k_parse_seg's rows)
+// the blocks drifted apart by up to the ring's depth -- a batch took 362 us from its first block's
+// start to its last block's end at depth 8 (tools/experiments/queue_trace.py) -- and the blocks
+// ahead drained and waited while the ones behind ran on half a CU.
+#ifndef FB_QUEUE_CHUNK
+#define FB_QUEUE_CHUNK 16
+#endif
+constexpr uint32_t kQChunk = FB_QUEUE_CHUNK;  // segments per chunk
+constexpr uint32_t kQRing = 8u;               // chunk ids per slot in the block's LDS (tagged)
+// The chunk counters of a slot (kQHeads, each on its own 64-B line): with more than one, a block
+// takes its XCD's chunks (c = j * kQHeads + x) and, once they are gone, the other XCDs'.  One counter
+// carries 1,024 returning atomics per 24-us batch, about half a word's rate (MI355X_MICROARCH.md:
+// ~88 per us), yet eight measured no faster (41.5 vs 41.8 Gpps over 512 batches) and the stealing at
+// each batch's end lengthened its completion (profiles/r05_queue_ab.txt); chunks of 8 segments (2,048
+// atomics per batch) cost 22 %, of 32 (coarser balance) 7 %.
+#ifndef FB_QUEUE_HEADS
+#define FB_QUEUE_HEADS 1
+#endif
+constexpr uint32_t kQHeads = FB_QUEUE_HEADS;
+static_assert(kQHeads >= 1u && kQHeads <= 8u && (kQHeads & (kQHeads - 1u)) == 0u, "1, 2, 4 or 8 chunk counters");
+static_assert(kQueueHeadWords >= kQHeads * 16u, "fb_internal.h: kQueueHeadWords");
+
+struct QDesc {  // a ring slot's batch, cached in the block's LDS
+    unsigned long long frames, offsets, out, seg, cls, stats;
+    uint32_t frames_bytes, n, nseg, seq;  // seq: batch + 1 once the fields are valid
+};
+struct QLds {  // the block's queue state (per ring slot unless noted)
+    QDesc desc[kQueueMax];
+    uint32_t claim[kQueueMax];  // batch + 1 whose descriptor a wave has taken on to load
+    uint32_t next[kQueueMax];   // the block's next position in the slot's batch (chunk i = L / kQChunk)
+    unsigned long long chunk[kQueueMax * kQRing];  // (i + 1) << 32 | the batch's chunk number, or ~0u: none left
+    uint32_t arr[kQueueMax];    // waves done with the slot's batch
+    uint32_t acc[kQueueMax * 10u];
+    uint32_t stop;              // the block leaves (host stop with nothing left, or idle)
+    uint32_t tail;              // batches the block has seen published (one PCIe peek serves its waves)
+};
+
+__device__ __forceinline__ uint32_t u1st(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// The 100-MHz real-time counter, waited for in the same statement: s_memrealtime returns through
+// lgkmcnt out of order with LDS operations, so a compiler-placed lgkmcnt(N) after the builtin form
+// can read the register before it is written (the first queue build expired at once on garbage).
+__device__ __forceinline__ unsigned long long rt_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ __forceinline__ unsigned long long u1st64(unsigned long long x) {
+    return (unsigned long long)u1st((uint32_t)x) | ((unsigned long long)u1st((uint32_t)(x >> 32)) << 32);
+}
+#ifdef FB_QUEUE_TRACE
+#define QTRACE(stmt) do { stmt; } while (0)
+__device__ __forceinline__ unsigned long long* qt(const QueueParams& Q, uint32_t what, uint64_t k) {
+    return Q.trace + what * kQTraceN + (k % kQTraceN);
+}
+#else
+#define QTRACE(stmt) do { } while (0)
+#endif
+
+// A chunk of the slot's batch for this block (~0u: none left): its XCD's counter, then the others'.
+__device__ __forceinline__ uint32_t q_grab(const QueueParams& Q, uint32_t slot, uint32_t nch) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t x = kQHeads > 1u ? u1st(__builtin_amdgcn_s_getreg((31 << 11) | 20)) & (kQHeads - 1u) : 0u;  // XCC_ID
+    for (uint32_t h = 0u; h < kQHeads; ++h) {
+        const uint32_t y = (x + h) & (kQHeads - 1u);
+        uint32_t r = 0u;
+        if (lane == 0u)
+            r = __hip_atomic_fetch_add(Q.head + slot * kQueueHeadWords + y * 16u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t c = u1st(r) * kQHeads + y;
+        if (c < nch) return c;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// One block at a time (whichever takes the poller word) reads the host's tail over PCIe and copies
+// the new descriptors into the device ring -- 512 blocks polling the host each had every host access
+// wait ~1 ms.  Returns the device ring's tail as this wave last saw it.  The host's stop word is read
+// before its tail (the host stores them in the other order), so a stop seen with nothing new is final.
+__device__ __forceinline__ unsigned long long q_refill(const QueueParams& Q, uint32_t k) {
+    const uint32_t lane = threadIdx.x & 63u, R = Q.depth;
+    unsigned long long dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t got = 0u;
+    if (lane == 0u) got = atomicCAS(&Q.d->poller, 0u, blockIdx.x + 1u) == 0u ? 1u : 0u;
+    if (!u1st(got)) return dt;
+    dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hs =
+        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+    const unsigned long long tl =
+        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+    QTRACE(if (lane == 0u) atomicAdd(qt(Q, kQtPolls, k), 1ull));
+    if (tl > dt) {  // descriptors dt .. tl-1 (at most R: the host waits for slot reuse)
+        const uint32_t words = (uint32_t)min(tl - dt, (unsigned long long)R) * 8u;
+        for (uint32_t w = lane; w < words; w += 64u) {
+            const unsigned long long j = dt + w / 8u;
+            const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&Q.h->desc[j & (R - 1u)]) + (w & 7u);
+            unsigned long long* dst = reinterpret_cast<unsigned long long*>(&Q.d->desc[j & (R - 1u)]) + (w & 7u);
+            *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (lane == 0u) __hip_atomic_store(&Q.d->tail, tl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        QTRACE(const unsigned long long now_ = rt_now();
+               for (unsigned long long j = dt + lane; j < tl; j += 64u) *qt(Q, kQtPub, j) = now_);
+        dt = tl;
+    } else if (lane == 0u && hs != 0ull) {
+        __hip_atomic_store(&Q.d->stop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0u) __hip_atomic_store(&Q.d->poller, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return dt;
+}
+
+// Batch k's descriptor into the block's LDS, with the block's first chunk of it (false: the queue
+// stops -- no batch k will come).
+__device__ __forceinline__ bool q_ensure(const QueueParams& Q, QLds* L, uint32_t k) {
+    const uint32_t lane = threadIdx.x & 63u, R = Q.depth, slot = k & (R - 1u);
+    for (;;) {
+        if (__hip_atomic_load(&L->desc[slot].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k + 1u) return true;
+        if (__hip_atomic_load(&L->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        uint32_t won = 0u;
+        if (lane == 0u) {
+            const uint32_t expect = k >= R ? k - R + 1u : 0u;  // the slot's previous batch, or none
+            won = atomicCAS(&L->claim[slot], expect, k + 1u) == expect ? 1u : 0u;
+        }
+        if (!u1st(won)) {  // another wave of the block loads it
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        // wait until batch k's descriptor is in the device ring
+        const unsigned long long t0 = rt_now();
+        unsigned long long dt;
+        for (uint32_t spins = 0u;; ++spins) {
+            dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (dt <= k) dt = q_refill(Q, k);
+            if (dt > k) {
+                if (lane == 0u) atomicMax(&L->tail, (uint32_t)dt);
+                break;
+            }
+            const bool stop = __hip_atomic_load(&Q.d->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull;
+            const unsigned long long now = rt_now();
+            if (stop || now - t0 > Q.idle_ticks) {
+                if (!stop && lane == 0u) {
+                    // what the block saw when it left (pad words: diagnostics for the host)
+                    __hip_atomic_store(&Q.h->pad[0], now - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&Q.h->pad[1], (unsigned long long)k | (unsigned long long)blockIdx.x << 32,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&Q.h->pad[2], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&Q.h->status, kQueueExpired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (lane == 0u) __hip_atomic_store(&L->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+            if (spins < 256u) __builtin_amdgcn_s_sleep(2);
+            else __builtin_amdgcn_s_sleep(127);  // (~3.4 us per poll once idle)
+        }
+        // lane j < 8 reads word j of the 64-B descriptor (fb_seg_batch) from the device ring
+        const unsigned long long v =
+            lane < 8u ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&Q.d->desc[slot]) + lane,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0ull;
+        QDesc& d = L->desc[slot];
+        if (lane == 0u) d.frames = v;
+        if (lane == 1u) d.frames_bytes = (uint32_t)v;
+        if (lane == 2u) d.offsets = v;
+        if (lane == 3u) {
+            d.n = (uint32_t)v;
+            d.nseg = ((uint32_t)v + 63u) / 64u;
+        }
+        if (lane == 4u) d.out = v;
+        if (lane == 5u) d.seg = v;
+        if (lane == 6u) d.cls = v;
+        if (lane == 7u) d.stats = v;
+        // the block's first chunk (its waves take the next ones, q_take)
+        const uint32_t nseg0 = ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 3) + 63u) / 64u;
+        const uint32_t c0 = q_grab(Q, slot, (nseg0 + kQChunk - 1u) / kQChunk);
+        if (lane == 0u) L->chunk[slot * kQRing] = (1ull << 32) | c0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0u) __hip_atomic_store(&d.seq, k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        QTRACE(if (lane == 0u) atomicMin(qt(Q, kQtFirst, k), rt_now()));
+        // the batch's first block keeps the device ring ahead of the waves: the descriptors the host
+        // has published since are copied in now, before any wave runs out of batches
+        if (c0 == 0u && dt < (unsigned long long)k + R) q_refill(Q, k);
+        return true;
+    }
+}
+
+// The block's next segment of the slot's batch (false: the batch has none left for this block).
+// Position L of the block is offset L % kQChunk of the block's chunk L / kQChunk; the wave that
+// takes a chunk's first position fetches the block's next chunk from the slot's device counter (after
+// its own chunk is known, so the chunks of a block increase), or marks it empty once its own is.
+__device__ __forceinline__ bool q_take(const QueueParams& Q, QLds* L, uint32_t slot, uint32_t* sg) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t v = 0u;
+    if (lane == 0u) v = __hip_atomic_fetch_add(&L->next[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t pos = u1st(v), i = pos / kQChunk, o = pos % kQChunk;
+    unsigned long long* ring = L->chunk + slot * kQRing;
+    uint32_t c;
+    for (;;) {
+        const unsigned long long w = __hip_atomic_load(ring + i % kQRing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((uint32_t)u1st64(w >> 32) == i + 1u) {
+            c = u1st((uint32_t)w);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const uint32_t nseg = u1st(L->desc[slot].nseg), nch = (nseg + kQChunk - 1u) / kQChunk;
+    if (o == 0u) {
+        uint32_t cn = 0xFFFFFFFFu;
+        if (c < nch) cn = q_grab(Q, slot, nch);
+        if (lane == 0u) __hip_atomic_store(ring + (i + 1u) % kQRing, ((unsigned long long)(i + 2u) << 32) | cn,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (c >= nch) return false;
+    *sg = c * kQChunk + o;
+    return *sg < nseg;
+}
+
+// This wave is done with batches [*arr_next, upto) -- its stores of them are complete (the caller
+// waited) and its counters are in the block's LDS.  The block's last wave for a batch publishes the
+// block's counters, resets the slot, writes the XCD's L2 back and counts the block; the batch's last
+// block stores the completion word.
+__device__ __forceinline__ void q_arrive(const QueueParams& Q, QLds* L, uint32_t* arr_next, uint32_t upto) {
+    const uint32_t lane = threadIdx.x & 63u, R = Q.depth, G = gridDim.x;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the counters' LDS adds first)
+    for (uint32_t j = *arr_next; j < upto; ++j) {
+        const uint32_t slot = j & (R - 1u);
+        uint32_t old = 0u;
+        if (lane == 0u) old = __hip_atomic_fetch_add(&L->arr[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (u1st(old) != (uint32_t)kSegWaves - 1u) continue;
+        if (lane < 5u) {  // the block's counters into the batch's five packed stats words (k_parse_seg's format)
+            const unsigned long long lo = L->acc[slot * 10u + 2u * lane], hi = L->acc[slot * 10u + 2u * lane + 1u];
+            unsigned long long* word = Q.tick + slot * 8u + lane;
+            const unsigned long long add = (1ull << 54) | (hi << 27) | lo;
+            const unsigned long long o = __hip_atomic_fetch_add(word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((o >> 54) == (unsigned long long)G - 1u) {  // this block completed the word: its fields
+                const unsigned long long tot = o + add, m27 = (1ull << 27) - 1ull;
+                const unsigned long long f_lo = tot & m27, f_hi = (tot >> 27) & m27;
+                __hip_atomic_store(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fb_batch_stats* S = reinterpret_cast<fb_batch_stats*>(L->desc[slot].stats);
+                // (system-scope stores: written through, like the records)
+                auto put = [](uint64_t* p, unsigned long long v) {
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                };
+                if (lane == 0u) {
+                    put(&S->n_session, f_lo);
+                    put(&S->n_filtered, f_hi);
+                    put(&S->new_sessions, 0ull);
+                    put(&S->updated_sessions, 0ull);
+                    put(&S->error, __hip_atomic_load(Q.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    put(&S->reserved[0], 0ull);
+                    put(&S->reserved[1], 0ull);
+                    put(&S->reserved[2], 0ull);
+                } else if (lane == 1u) {
+                    put(&S->n_dns, f_lo);
+                    put(&S->bad_offsets, f_hi);
+                } else if (lane == 2u) {
+                    put(&S->tcp_processed, f_lo);
+                    put(&S->udp_processed, f_hi);
+                } else if (lane == 3u) {
+                    put(&S->ipv4_processed, f_lo);
+                    put(&S->ipv6_processed, f_hi);
+                } else {
+                    put(&S->total_processed, f_lo);
+                    put(&S->n_drop, f_hi);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // acknowledged before the block is counted
+            }
+        }
+        if (lane < 10u) L->acc[slot * 10u + lane] = 0u;  // the slot's next batch starts from zero
+        if (lane < kQRing) L->chunk[slot * kQRing + lane] = 0ull;
+        if (lane == 0u) {
+            L->next[slot] = 0u;
+            L->arr[slot] = 0u;
+        }
+        // every wave of the block has its (write-through) stores of batch j acknowledged: count the block
+        uint32_t ob = 0u;
+        if (lane == 0u) ob = __hip_atomic_fetch_add(Q.blk_done + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        QTRACE(if (lane == 0u) {
+            const unsigned long long now_ = rt_now();
+            atomicMin(qt(Q, kQtArr0, j), now_);
+            unsigned long long* b_ = Q.trace + kQTraceWords * kQTraceN + 4u * blockIdx.x;
+            if (j == kQtB0 || j == kQtB1) b_[j == kQtB1] = now_;
+            if (j == kQtB0) {
+                b_[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+                b_[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+            }
+        });
+        if (u1st(ob) == G - 1u) {  // the batch's last block (resets the slot's counters first)
+            if (lane < kQHeads)
+                __hip_atomic_store(Q.head + slot * kQueueHeadWords + lane * 16u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            QTRACE(if (lane == 0u) *qt(Q, kQtDone, j) = rt_now());
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (lane == 0u) {
+                __hip_atomic_store(Q.blk_done + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&Q.h->cdone[slot], (unsigned long long)j + 1ull, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    *arr_next = upto > *arr_next ? upto : *arr_next;
+}
+
+// A wave's positions: (batch, segment) in increasing order -- batch gk, the wave's position count gt
+// inside it (two static per wave, then the block's counter, as k_parse_seg hands them out).  block:
+// wait for the batch to be published; otherwise a batch the host has not published ends it.
+struct QPos {
+    uint32_t k, sg, ok;
+};
+struct QGen {
+    uint32_t gk, gt, known;
+};
+__device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* g, bool block, uint32_t* arr_next) {
+    const uint32_t lane = threadIdx.x & 63u, R = Q.depth;
+    for (;;) {
+        if (g->gk >= g->known) {
+            g->known = u1st(__hip_atomic_load(&L->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (g->gk >= g->known) {  // a peek at the device ring's tail (the poller keeps it current)
+                uint32_t t = 0u;
+                if (lane == 0u) {
+                    t = (uint32_t)__hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicMax(&L->tail, t);
+                }
+                g->known = u1st(t);
+                if (g->gk >= g->known) {
+                    if (!block) return QPos{g->gk, 0u, 0u};
+                    QTRACE(if (lane == 0u) atomicAdd(qt(Q, kQtDrain, g->gk), 1ull));
+                    // about to wait for a batch the host has not published: this wave (pipeline empty,
+                    // counters flushed, stores complete -- the caller's drain) is done with every batch
+                    // before it, including those it passed without a segment here; the host may be
+                    // waiting for them before it publishes more
+                    q_arrive(Q, L, arr_next, g->gk);
+                }
+            }
+        }
+        if (!q_ensure(Q, L, g->gk)) return QPos{g->gk, 0u, 0u};
+        if (g->known <= g->gk) g->known = g->gk + 1u;
+        g->gt = 1u;  // (inside batch gk: the main loop's fast path takes its positions)
+        uint32_t sg;
+        if (q_take(Q, L, g->gk & (R - 1u), &sg)) return QPos{g->gk, sg, 1u};
+        ++g->gk;
+        g->gt = 0u;
+    }
+}
+
+__global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_queue(const QueueParams Q) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = u1st(tid >> 6), R = Q.depth;
+    __shared__ uint4 s_cfg4[sizeof(DevConfig) / 16];
+    __shared__ __attribute__((aligned(16))) unsigned long long s_stage[kSegWaves][64u * 7u];
+    __shared__ QLds L;
+    const DevConfig* cfg = reinterpret_cast<const DevConfig*>(s_cfg4);
+    unsigned long long* stage = s_stage[wave];
+    const unsigned long long lmask = (1ull << lane) - 1ull;
+    constexpr uint32_t kOob = 0x80000000u;
+    for (uint32_t k = tid; k < kQueueMax; k += kSegThreads) {
+        L.desc[k].seq = 0u;
+        L.claim[k] = 0u;
+        L.next[k] = 0u;
+        L.arr[k] = 0u;
+    }
+    for (uint32_t k = tid; k < kQueueMax * kQRing; k += kSegThreads) L.chunk[k] = 0ull;
+    for (uint32_t k = tid; k < kQueueMax * 10u; k += kSegThreads) L.acc[k] = 0u;
+    if (tid == 0u) {
+        L.stop = 0u;
+        L.tail = 0u;
+    }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(Q.cfg);
+        constexpr uint32_t kCfg16 = kCfgLdsBytes / 16;
+        for (uint32_t k = tid; k < kCfg16; k += kSegThreads) s_cfg4[k] = src[k];
+        constexpr uint32_t kLanOff = offsetof(DevConfig, lan_v6) / 16, kOwnOff = offsetof(DevConfig, own) / 16;
+        const uint32_t nl = Q.cfg->n_lan_v6 * (sizeof(LanV6) / 16), no = Q.cfg->n_own * (sizeof(fb_ip) / 16);
+        for (uint32_t k = tid; k < nl; k += kSegThreads) s_cfg4[kLanOff + k] = src[kLanOff + k];
+        for (uint32_t k = tid; k < no; k += kSegThreads) s_cfg4[kOwnOff + k] = src[kOwnOff + k];
+    }
+    __syncthreads();
+
+    QGen g{0u, 0u, 0u};
+    auto frames_rsrc = [&](uint32_t k) {
+        const QDesc& d = L.desc[k & (R - 1u)];
+        return __builtin_amdgcn_make_buffer_rsrc((void*)u1st64(d.frames), (short)0, (int)u1st(d.frames_bytes), 0x00020000);
+    };
+    auto load_q = [&](const QPos& p, uint2& q) {  // frame offsets of p's segment (invalid p: offsets[0])
+        const QDesc& d = L.desc[p.k & (R - 1u)];
+        const uint32_t* off = reinterpret_cast<const uint32_t*>(u1st64(d.offsets));
+        const uint32_t n = u1st(d.n);
+        const uint32_t i = p.ok ? p.sg * 64u + lane : 0u;
+        q = make_uint2(off[min(i, n)], off[min(i + 1u, n)]);
+    };
+    auto vmov = [](uint32_t x) {
+        uint32_t y;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+        return y;
+    };
+    // counters of batch a_k (wave-uniform)
+    uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u, a_k = 0u, arr_next = 0u;
+    auto flush = [&]() {
+        const uint32_t a_tot = a_s + a_f;
+        const uint32_t mine[10] = {a_s, a_f, a_d, a_b, a_t, a_tot - a_t, a_4, a_tot - a_4, a_tot, a_n - a_tot - a_d};
+        if (lane < 10u) {
+            uint32_t v = 0u;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v = lane == (uint32_t)k ? mine[k] : v;
+            if (v) __hip_atomic_fetch_add(&L.acc[(a_k & (R - 1u)) * 10u + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        a_s = a_d = a_f = a_t = a_4 = a_b = a_n = 0u;
+    };
+
+    Hdr h;
+    uint2 c = make_uint2(0u, 0u), q = make_uint2(0u, 0u);
+    QPos cur{0u, 0u, 0u}, nxt{0u, 0u, 0u};
+    for (;;) {
+        if (!cur.ok) {
+            // pipeline empty: everything this wave generated is processed; it is done with every batch
+            // before g.gk; then wait for work (the only place a wave blocks)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            flush();
+            q_arrive(Q, &L, &arr_next, g.gk);
+            cur = q_gen_slow(Q, &L, &g, true, &arr_next);
+            if (!cur.ok) break;
+            nxt = q_gen_slow(Q, &L, &g, false, &arr_next);
+            load_q(cur, q);
+            load_headers1(frames_rsrc(cur.k), q.x, h);
+            c = make_uint2(vmov(q.x), vmov(q.y));
+            load_q(nxt.ok ? nxt : cur, q);
+        }
+        // the position after next: the fast path is a static position or a grab inside a known batch
+        QPos aft{nxt.k, 0u, 0u};
+        if (nxt.ok) {
+            bool fast = false;
+            if (g.gt) {  // a position inside the batch this wave is in
+                uint32_t sg;
+                if (q_take(Q, &L, g.gk & (R - 1u), &sg)) {
+                    aft = QPos{g.gk, sg, 1u};
+                    fast = true;
+                } else {
+                    ++g.gk;
+                    g.gt = 0u;
+                }
+            }
+            if (!fast) aft = q_gen_slow(Q, &L, &g, false, &arr_next);
+        }
+        if (cur.k != a_k) {  // the first segment of a later batch: the earlier ones are done here
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            flush();
+            a_k = cur.k;
+            q_arrive(Q, &L, &arr_next, cur.k);
+        }
+        const QDesc& D = L.desc[cur.k & (R - 1u)];
+        const uint32_t n = u1st(D.n), fbytes = u1st(D.frames_bytes);
+        const uint32_t ls = cur.sg, i = ls * 64u + lane;
+        const bool valid = i < n;
+        Pkt kk;
+        process_frame(frames_rsrc(cur.k), cfg, cfg, h, valid ? c.x : 1u, valid ? c.y : 0u, fbytes, i, kk);
+        const bool is_s = valid && kk.cls == FB_CLASS_SESSION;
+        const bool is_d = valid && kk.cls == FB_CLASS_DNS;
+        const bool is_f = valid && kk.cls == FB_CLASS_FILTERED;
+        const bool counted = is_s || is_f;
+        const unsigned long long m_sess = __ballot(is_s), m_dns = __ballot(is_d);
+        const uint32_t cs = (uint32_t)__popcll(m_sess), cd = (uint32_t)__popcll(m_dns);
+        if (is_s) {
+            unsigned long long* dd = stage + (size_t)__popcll(m_sess & lmask) * 7;
+#pragma unroll
+            for (int w = 0; w < 7; ++w) dd[w] = (unsigned long long)kk.w[2 * w] | ((unsigned long long)kk.w[2 * w + 1] << 32);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // prefetch: the next segment's headers (offsets already here), the offsets of the one after
+        // (an invalid position reads its batch's offsets[0] / the frame at 0: harmless, never used)
+        load_headers1(frames_rsrc(nxt.ok ? nxt.k : cur.k), nxt.ok ? q.x : 0u, h);
+        c = make_uint2(vmov(q.x), vmov(q.y));
+        load_q(aft.ok ? aft : cur, q);
+        {   // stores (as k_parse_seg): 4 x 16 B of records, the 8-B tail, one DNS record, the count, the class
+            uint8_t* out = reinterpret_cast<uint8_t*>(u1st64(D.out)) + (size_t)ls * kSegBytes;
+            const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)kSegBytes, 0x00020000);
+            uint32_t* segw = reinterpret_cast<uint32_t*>(u1st64(D.seg));
+            uint8_t* clsp = reinterpret_cast<uint8_t*>(u1st64(D.cls));
+            const __amdgpu_buffer_rsrc_t r_seg =
+                __builtin_amdgcn_make_buffer_rsrc(segw, (short)0, (int)(((n + 63u) / 64u) * 4u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t r_cls = __builtin_amdgcn_make_buffer_rsrc(clsp, (short)0, clsp ? (int)n : 0, 0x00020000);
+            const uint32_t words = cs * 7u, body = words >> 1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t cc = lane + 64u * j;
+                const uint32_t src = min(cc, 223u);
+                const unsigned long long x = stage[2u * src], y = stage[2u * src + 1u];
+                const u32x4 v = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r_out, cc < body ? cc * 16u : kOob, 0, kQSt);
+            }
+            {
+                const bool tail = (words & 1u) && lane == 0u;
+                const unsigned long long x = stage[words ? words - 1u : 0u];
+                const u32x2 v = {(uint32_t)x, (uint32_t)(x >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(v, r_out, tail ? (words - 1u) * 8u : kOob, 0, kQSt);
+            }
+            {
+                const u32x4 v = {kk.w[0], kk.w[1], kk.w[2], kk.w[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    v, r_out, is_d ? kSegBytes - 16u * (1u + (uint32_t)__popcll(m_dns & lmask)) : kOob, 0, kQSt);
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(cs | (cd << 16), r_seg, lane == 0u ? ls * 4u : kOob, 0, kQSt);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)kk.cls, r_cls, valid ? i : kOob, 0, kQSt);
+        }
+        __builtin_amdgcn_wave_barrier();  // stage reads of this segment before the next writes
+        a_s += cs;
+        a_d += cd;
+        a_f += __popcll(__ballot(is_f));
+        a_t += __popcll(__ballot(counted && kk.tcp));
+        a_4 += __popcll(__ballot(counted && kk.v4));
+        a_b += __popcll(__ballot(valid && kk.bad));
+        a_n += __popcll(__ballot(valid));
+        cur = nxt;
+        nxt = aft;
+    }
+}
+
+hipError_t occupancy_parse_seg_queue(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_parse_seg_queue, kSegThreads, 0);
+}
+hipError_t launch_parse_seg_queue(const QueueParams& q, uint32_t grid, hipStream_t s) {
+    if (q.depth == 0u || q.depth > kQueueMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_parse_seg_queue, dim3(grid), dim3(kSegThreads), 0, s, q);
+    return hipGetLastError();
+}
+
 }  // namespace fbk

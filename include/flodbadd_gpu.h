@@ -399,6 +399,30 @@ typedef struct fb_seg_batch {
 } fb_seg_batch;                /* 64 bytes */
 int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, uint32_t count, void* stream);
 
+/* ---- resident queue-fed parse: one batch per call without a launch per batch ----------------
+ * A capture loop that hands over one batch at a time (src/capture.rs:1036-1061 runs the pair per
+ * packet; a GPU capture engine fills one device buffer at a time) pays a kernel launch per call
+ * above: its prologue and the tail of the last segments.  fb_seg_queue_create launches ONE
+ * resident parse kernel on an internal stream; fb_seg_queue_submit hands it a batch through a
+ * ring in pinned host memory (no launch, no stream operation) and returns a ticket; the batch's
+ * outputs (segmented layout and stats, exactly as fb_parse_classify_seg_dev writes them) are
+ * complete once fb_seg_queue_query(ticket) returns FB_OK.  Not stream-ordered: the batch's frames
+ * and offsets must be in device memory when it is submitted, and stay untouched (like its output
+ * buffers) until its ticket completes.  The context's configuration is captured at create.  While
+ * a queue lives its kernel holds two workgroups on every CU (every one must be resident: the grid is
+ * sized by the occupancy query); what it leaves free -- the registers of a fifth wave per SIMD, a third
+ * of the LDS -- runs copies and small kernels beside it, and a kernel that needs more of a CU waits
+ * until fb_seg_queue_destroy.  A queue left idle for idle_ms (0 = 5,000 ms) stops itself; its calls
+ * then fail with FB_ERR_INTERNAL (destroy it and create a new one). */
+#define FB_QUEUE_MAX_DEPTH 32u
+typedef struct fb_seg_queue fb_seg_queue;
+fb_seg_queue* fb_seg_queue_create(fb_ctx* ctx, uint32_t depth /* 1..FB_QUEUE_MAX_DEPTH, 0 = 8 */, uint32_t idle_ms);
+/* Blocks only while `depth` batches are in flight (until the oldest of them completes). */
+int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* batch, uint64_t* ticket);
+int fb_seg_queue_query(fb_seg_queue* q, uint64_t ticket); /* FB_OK done, 1 pending, < 0 error */
+int fb_seg_queue_wait(fb_seg_queue* q, uint64_t ticket);  /* polls until done (no blocking wait) */
+int fb_seg_queue_destroy(fb_seg_queue* q);                /* after the submitted batches complete */
+
 /* Dense records from a segmented batch of n frames (d_seg_out / d_seg of the calls above): the
  * SESSION records into d_out and the DNS side records into d_dns, batch-wide packet order, as
  * fb_parse_classify_dev lays them out (either may be NULL).  The counts are those of the

@@ -1,0 +1,166 @@
+"""The resident queue-fed parse (fb_seg_queue_*, k_parse_seg_queue): batches handed one call at a
+time to ONE running kernel through a ring in pinned host memory, each batch's segmented outputs,
+classes and stats bit-exact against the oracle (the layout fb_parse_classify_seg_dev writes) --
+ragged and empty batches, more batches than ring slots, an idle gap between submissions, the
+configuration captured at create, and an expired queue reporting an error instead of hanging."""
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+from flodbadd_amd import _native as N
+from flodbadd_amd import synth
+from flodbadd_amd.capture import FlodbaddGpuCapture
+from flodbadd_amd.sessions import SessionFilter
+from test_gpu_segmented import _check
+
+pytestmark = pytest.mark.gpu
+
+
+class _Batch:
+    """Device buffers of one batch and its fb_seg_batch descriptor."""
+
+    def __init__(self, frames, offs, with_cls=True):
+        self.frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        self.offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        self.n = n = len(self.offs) - 1
+        nseg = max((n + 63) // 64, 1)
+        self.fr = N.DeviceBuffer(max(self.frames.nbytes, 1))
+        if self.frames.nbytes:
+            self.fr.upload(self.frames)
+        self.of = N.DeviceBuffer(self.offs.nbytes).upload(self.offs)
+        self.out, self.seg = N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4)
+        self.cls = N.DeviceBuffer(max(n, 1)) if with_cls else None
+        self.st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        self.desc = np.zeros(1, dtype=N.SEG_BATCH_DTYPE)
+        self.desc[0] = (self.fr.ptr.value, self.frames.nbytes, self.of.ptr.value, n, 0, self.out.ptr.value,
+                        self.seg.ptr.value, self.cls.ptr.value if self.cls else 0, self.st.ptr.value)
+
+    def reset(self):
+        # bytes outside a segment's records must stay untouched.  The fills are copies from the host
+        # (DMA engine), not memset kernels: while a queue lives its kernel holds the CUs, and a fill
+        # kernel would wait for it (fb_seg_queue_create's note); upload() also completes before the submit
+        self.out.upload(np.full(self.out.nbytes, 0xA5, dtype=np.uint8))
+        self.st.upload(np.full(self.st.nbytes, 0xEE, dtype=np.uint8))
+
+    def result(self):
+        n, nseg = self.n, max((self.n + 63) // 64, 1)
+        raw = self.out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8))
+        seg = self.seg.download(np.zeros(nseg, dtype=np.uint32))[: (n + 63) // 64]
+        cls = self.cls.download(np.zeros(max(n, 1), dtype=np.uint8))[:n] if self.cls else None
+        st = self.st.download(np.zeros(1, dtype=N.STATS_DTYPE))
+        return raw, seg, cls, st
+
+
+class _Queue:
+    def __init__(self, cap, depth, idle_ms=3000):
+        self.lib = N.gpu_lib()
+        q = self.lib.fb_seg_queue_create(cap.ctx, depth, idle_ms)
+        assert q, self.lib.fb_last_error()
+        self.q = C.c_void_p(q)
+
+    def submit(self, b):
+        t = C.c_uint64()
+        N.check(self.lib.fb_seg_queue_submit(self.q, N.ptr(b.desc), C.byref(t)))
+        return t.value
+
+    def wait(self, t):
+        N.check(self.lib.fb_seg_queue_wait(self.q, t))
+
+    def close(self):
+        if self.q:
+            rc = self.lib.fb_seg_queue_destroy(self.q)
+            self.q = None
+            N.check(rc)
+
+
+def _verify(b, flt):
+    from oracle import coracle
+    from test_gpu_segmented import _expected_seg
+    raw, seg, cls, st = b.result()
+    r_out, r_dns, r_cls, r_st = coracle.parse_classify(coracle.make_cfg(int(flt)), b.frames, b.offs)
+    if cls is None:  # no class output asked for
+        cls = r_cls
+    # compact diagnostics first (a failing bytes comparison of a 1M-frame batch makes pytest diff for minutes)
+    es = _expected_seg(r_out, r_dns, b.n)
+    bad = np.flatnonzero(seg != es)
+    assert bad.size == 0, ("n=%d: %d segment counts differ, first %d: %x vs %x" %
+                           (b.n, bad.size, bad[0], int(seg[bad[0]]), int(es[bad[0]])))
+    badc = np.flatnonzero(cls != r_cls)
+    assert badc.size == 0, ("n=%d: %d classes differ, first at %d" % (b.n, badc.size, badc[0]))
+    g_out, g_dns = N.seg_unpack(raw, seg)
+    if g_out.tobytes() != r_out.tobytes():
+        d = np.flatnonzero(g_out.view(np.uint8).reshape(-1, 56).any(axis=1) != r_out.view(np.uint8).reshape(-1, 56).any(axis=1)
+                           if len(g_out) != len(r_out) else
+                           (g_out.view(np.uint8).reshape(-1, 56) != r_out.view(np.uint8).reshape(-1, 56)).any(axis=1))
+        raise AssertionError("n=%d: %d of %d records differ, first %s" % (b.n, d.size, len(r_out), d[:5]))
+    _check(None, b.frames, b.offs, flt=int(flt), res=(raw, seg, cls, st))
+
+
+@pytest.mark.parametrize("depth", [4, 3, 1])
+def test_queue_ragged_batches_more_than_slots(depth):
+    """depth 3: four ring slots with at most three batches in flight (the kernel's slot ring is a
+    power of two); depth 1: every submission waits for the previous batch."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=0)
+    sizes = [(3, 65537), (2, 64), (3, 1), (2, 0), (3, 6401), (2, 1 << 20), (3, 63), (3, 300001), (2, 65),
+             (3, 12345), (2, 128), (3, 70001)]
+    batches = [_Batch(*synth.generate(cid, n, first=7 * k), with_cls=k % 3 != 1) for k, (cid, n) in enumerate(sizes)]
+    q = _Queue(cap, depth=depth)
+    try:
+        for b in batches:
+            b.reset()
+        tickets = [q.submit(b) for b in batches]  # the later submits wait for slots
+        for t in tickets:
+            q.wait(t)
+        for b in batches:
+            _verify(b, SessionFilter.All)
+        # the same buffers again, twice round the ring, checked after each wait
+        for rnd in range(2):
+            for b in batches[:6]:
+                b.reset()
+                q.wait(q.submit(b))
+                _verify(b, SessionFilter.All)
+    finally:
+        q.close()
+        cap.close()
+
+
+def test_queue_idle_gap_and_captured_configuration():
+    """GlobalOnly (the FlodbaddCapture default) captured at create; submissions resume after the
+    kernel has drained and waited idle (below its limit)."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.GlobalOnly, flow_capacity=0)
+    batches = [_Batch(*synth.generate(3, n, first=3 + k)) for k, n in enumerate((40000, 99999, 1 << 18))]
+    q = _Queue(cap, depth=2)
+    try:
+        for rep in range(3):
+            for b in batches:
+                b.reset()
+            ts = [q.submit(b) for b in batches]
+            q.wait(ts[-1])
+            for t in ts:
+                q.wait(t)
+            for b in batches:
+                _verify(b, SessionFilter.GlobalOnly)
+            time.sleep(0.2)  # every wave drains and waits for the next batch
+    finally:
+        q.close()
+        cap.close()
+
+
+def test_queue_expired_reports_error():
+    """A queue idle past idle_ms stops its kernel; a later submission fails instead of hanging."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=0)
+    b = _Batch(*synth.generate(2, 4096))
+    q = _Queue(cap, depth=2, idle_ms=100)
+    try:
+        b.reset()
+        q.wait(q.submit(b))  # within the limit: fine
+        _verify(b, SessionFilter.All)
+        time.sleep(1.0)
+        with pytest.raises(N.FbError) as e:
+            q.wait(q.submit(b))
+        assert e.value.code == N.FB_ERR_INTERNAL
+    finally:
+        q.close()
+        cap.close()

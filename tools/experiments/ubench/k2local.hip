@@ -28,9 +28,12 @@ static unsigned long long sm(unsigned long long& s) {
     return z ^ (z >> 31);
 }
 
+template <int U>
 __global__ __launch_bounds__(512) void k_gather(const uint4* __restrict__ units, const uint32_t* __restrict__ idx,
                                                 const uint32_t* __restrict__ pstart, uint32_t P, uint32_t S,
                                                 uint32_t xcd_map, uint4* out) {
+    extern __shared__ uint32_t pad[];  // launched with K2's 72 KB to get its two workgroups per CU
+    if (threadIdx.x == 1023u) pad[0] = 0u;
     const uint32_t i = blockIdx.x;
     uint32_t p = i;
     if (xcd_map) {
@@ -40,14 +43,23 @@ __global__ __launch_bounds__(512) void k_gather(const uint4* __restrict__ units,
     }
     const uint32_t a = pstart[p], b = pstart[p + 1];
     uint4 acc = make_uint4(0, 0, 0, 0);
-    for (uint32_t e = a + threadIdx.x; e < b; e += 2u * 512u) {
-        const uint32_t u0 = idx[e];
-        const uint32_t u1 = e + 512u < b ? idx[e + 512u] : u0;
-        const uint4 x0 = units[2ull * u0], y0 = units[2ull * u0 + 1], x1 = units[2ull * u1], y1 = units[2ull * u1 + 1];
-        acc.x ^= x0.x + y0.y + x1.z;
-        acc.y += x0.w ^ y1.x;
-        acc.z ^= y0.z + x1.y;
-        acc.w += y1.w;
+    for (uint32_t e = a + threadIdx.x; e < b; e += U * 512u) {
+        uint32_t u[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) u[k] = e + k * 512u < b ? idx[e + k * 512u] : idx[e];
+        uint4 x[U], y[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            x[k] = units[2ull * u[k]];
+            y[k] = units[2ull * u[k] + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            acc.x ^= x[k].x + y[k].y;
+            acc.y += x[k].w ^ y[k].x;
+            acc.z ^= y[k].z + x[k].y;
+            acc.w += y[k].w;
+        }
     }
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) out[blockIdx.x * 512u + threadIdx.x] = acc;
 }
@@ -69,6 +81,8 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    CK(hipFuncSetAttribute((const void*)k_gather<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 1024));
+    CK(hipFuncSetAttribute((const void*)k_gather<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 1024));
     const uint32_t Ss[] = {0u, 64u, 128u, 256u, 4096u};  // 0: packed layout; P: contiguous per partition
     for (uint32_t S : Ss) {
         // the layout: position of each record's unit
@@ -90,19 +104,30 @@ int main(int argc, char** argv) {
         for (uint32_t u = 0; u < N; ++u) idx[cur[part[u]]++] = pos[u];
         CK(hipMemcpy(d_idx, idx.data(), (size_t)N * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(d_ps, ps.data(), (size_t)(P + 1) * 4, hipMemcpyHostToDevice));
-        for (uint32_t xm = 0; xm < (S ? 2u : 1u); ++xm) {
+        for (uint32_t v = 0; v < (S ? 2u : 5u); ++v) {
+          const uint32_t xm = S ? v : 0u;
+          // packed layout variants: units in flight per thread (2 / 4) x free occupancy / K2's 72 KB LDS
+          const int U = (S || v == 0 || v == 1 || v == 3) ? 2 : 4;
+          const size_t lds = (!S && v >= 3) ? 72u * 1024u : 0u;
+          if (!S && v == 1) continue;
+          {
             float best = 1e9f, sum = 0.f;
             for (int r = 0; r < reps + 2; ++r) {
                 CK(hipEventRecord(e0));
-                hipLaunchKernelGGL(k_gather, dim3(P), dim3(512), 0, 0, d_units, d_idx, d_ps, P, S ? S : 1u, xm, d_out);
+                if (U == 2)
+                    hipLaunchKernelGGL(k_gather<2>, dim3(P), dim3(512), lds, 0, d_units, d_idx, d_ps, P, S ? S : 1u, xm, d_out);
+                else
+                    hipLaunchKernelGGL(k_gather<4>, dim3(P), dim3(512), lds, 0, d_units, d_idx, d_ps, P, S ? S : 1u, xm, d_out);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 if (r >= 2) { best = std::min(best, ms); sum += ms; }
             }
-            printf("%-7s S=%-4u map=%-5s  units %u  best %.1f us  mean %.1f us  %.1f G units/s\n", S ? "super" : "packed",
-                   S, xm ? "xcd" : "ident", N, best * 1e3f, sum / reps * 1e3f, N / (best * 1e-3f) / 1e9f);
+            printf("%-7s S=%-4u map=%-5s inflight=%d lds=%zuK  units %u  best %.1f us  mean %.1f us  %.1f G units/s\n",
+                   S ? "super" : "packed", S, xm ? "xcd" : "ident", U, lds >> 10, N, best * 1e3f, sum / reps * 1e3f,
+                   N / (best * 1e-3f) / 1e9f);
+          }
         }
     }
     return 0;
