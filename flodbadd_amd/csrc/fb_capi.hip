@@ -694,6 +694,14 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* c, const fb_seg_batch* batches, ui
     return launch_seg(c, sb, n_max, nullptr, (hipStream_t)stream);
 }
 
+#ifdef FB_DN_TRACE
+static unsigned long long* g_dtrace = nullptr;
+// diagnostic builds only: the last dense launch's trace (4 x (8192 + 1024) words), after a device sync
+extern "C" __attribute__((visibility("default"))) int fb_dense_trace_last(unsigned long long* out) {
+    if (!g_dtrace || hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpy(out, g_dtrace, 8u * 4u * (8192u + 1024u), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 // ---- resident queue-fed parse (k_parse_seg_queue, fb_parse.hip) ------------------------------------
 #ifdef FB_QUEUE_TRACE
 static unsigned long long g_qtrace[kQTraceAll];
@@ -992,6 +1000,13 @@ static int parse_dense_single(fb_ctx* c, const uint8_t* d_frames, uint64_t frame
     p.dstatus = c->d_dstatus;
     p.steal_polls = c->steal_polls;
     p.dn_skew = c->dn_skew;
+#ifdef FB_DN_TRACE
+    if (!g_dtrace) {
+        if (hipMalloc(&g_dtrace, 8u * 4u * (8192u + 1024u)) != hipSuccess) return set_err(FB_ERR_NOMEM, "trace");
+    }
+    HIP_TRY(hipMemsetAsync(g_dtrace, 0, 8u * 4u * (8192u + 1024u), s));
+    p.dtrace = g_dtrace;
+#endif
     p.dep = ++c->dense_epoch;
     p.ntiles = (nseg + parse_dense_tile_segs() - 1) / parse_dense_tile_segs();
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->dense_grid, p.ntiles));

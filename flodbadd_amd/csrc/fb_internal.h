@@ -57,6 +57,10 @@ struct ParseParams {
     // fault injection for the tests (FB_DENSE_OFFSET_SKEW at fb_create, 0 otherwise): added to every
     // tile offset k_parse_dense hands its copies, as a corrupted look-back word would be
     unsigned long long dn_skew;
+#ifdef FB_DN_TRACE
+    // diagnostic builds: k_parse_dense timings (fb_parse.hip, kDnTr*)
+    unsigned long long* dtrace;
+#endif
 };
 // 16 / 8 bytes at a 4-B aligned address: 56-B records (fb_pkt_out, fb_parsed_pkt) are only 8-B
 // aligned at odd indices, so a uint4 dereference there would claim an alignment the data lacks

@@ -811,6 +811,21 @@ __device__ __forceinline__ unsigned long long dn_word(uint32_t ep, unsigned long
 __device__ __forceinline__ unsigned long long dn_pair(unsigned long long w) {
     return (w & kDn27) | (((w >> 27) & kDn27) << 32);
 }
+#ifdef FB_DN_TRACE
+// -DFB_DN_TRACE (never the product): per tile t the real-time ticks (100 MHz) when the store wave saw
+// it written, published its offset, and when its last slot was copied out; per block its start,
+// the end of its parse waves' segment loops (max) and its end (max).  Words: [tile 4 x kDnTrTiles |
+// block 4 x kDnTrBlocks] (tools/experiments/dense_trace.py).
+constexpr uint32_t kDnTrTiles = 8192u, kDnTrBlocks = 1024u;
+__device__ __forceinline__ unsigned long long dn_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define DNTR(stmt) do { stmt; } while (0)
+#else
+#define DNTR(stmt) do { } while (0)
+#endif
 struct DnLds {
     unsigned long long buf[kDnBufs][kDnTileSegs][kDnSlotU64];  // tile buffers, one slot per segment
     unsigned long long base[kDnBufs];                     // the buffer's tile: batch-wide offset (pair)
@@ -853,6 +868,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
     }
     if (tid <= 10u) L.acc[tid] = 0u;
     if (tid == 0u) L.next = 2u * kDnWaves;  // the first two segments of each wave are static
+    DNTR(if (tid == 0u && b < kDnTrBlocks) P.dtrace[4u * kDnTrTiles + 4u * b] = dn_now());
 
     // block-local segment number Ls -> global segment: round Ls / T of the block (tile b + round G),
     // slot Ls % T of the tile
@@ -925,6 +941,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
             while (__hip_atomic_load(&L.free_round[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != r ||
                    __hip_atomic_load(&L.done[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != segs)
                 __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
+            DNTR(if (lane == 0u && t < kDnTrTiles) P.dtrace[4u * t] = dn_now());
             // per slot exclusive prefixes inside the tile (lane j: slot j), and the tile's sums
             const uint32_t cw = lane < segs ? L.cnt[p][lane] : 0u;
             uint32_t incl = cw;  // n_session | n_dns << 16 never carries (<= 64 per slot, 16 slots)
@@ -1017,6 +1034,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
             // the offset for the parse waves, which copy their slots out (release: pre and base
             // are visible before the round is marked ready -- with relaxed orders the compiler
             // may put the base store after the flag, and a parse wave copied to a stale offset)
+            DNTR(if (lane == 0u && t < kDnTrTiles) P.dtrace[4u * t + 1u] = dn_now());
             if (lane == 0u) {
                 L.base[p] = excl + P.dn_skew;
                 __hip_atomic_store(&L.ready_round[p], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1091,6 +1109,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
             const uint32_t t = b + rnd * G, segs = min(kDnTileSegs, nseg - t * kDnTileSegs);
             const uint32_t old = __hip_atomic_fetch_add(&L.copied[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old + 1u == segs) {  // the tile's last copy: the buffer serves round rnd + kDnBufs
+                DNTR(if (t < kDnTrTiles) P.dtrace[4u * t + 2u] = dn_now());
                 L.done[p] = 0u;
                 L.copied[p] = 0u;
                 __hip_atomic_store(&L.free_round[p], rnd + kDnBufs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1161,6 +1180,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         Ln = La;
         sg = g_next;
     }
+    DNTR(if (lane == 0u && b < kDnTrBlocks) atomicMax(P.dtrace + 4u * kDnTrTiles + 4u * b + 1u, dn_now()));
     for (uint32_t k = 0; k < 2u; ++k) {  // the last pending slots
         if (pend0 == ~0u) break;
         while (!ready_of(pend0)) __builtin_amdgcn_s_sleep(FB_DN_SLEEP);
@@ -1168,6 +1188,7 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
         pend0 = pend1;
         pend1 = ~0u;
     }
+    DNTR(if (lane == 0u && b < kDnTrBlocks) atomicMax(P.dtrace + 4u * kDnTrTiles + 4u * b + 2u, dn_now()));
     // batch stats: as k_parse_seg (one batch): wave counters into LDS, the block's last parse wave
     // adds the block's into the five packed device words; the block completing a word writes its
     // fields
