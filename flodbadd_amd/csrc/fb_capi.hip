@@ -599,6 +599,14 @@ int fb_set_own_ips(fb_ctx* c, const fb_ip* ips, uint32_t n) {
 // `want_parts`: one frame batch whose session table update follows (fb_process_seg_dev) -- the
 // kernel also writes each SESSION record slot's table partition, so the update's histogram pass
 // reads 4 B per record instead of the record.
+#ifdef FB_SEG_TRACE
+static unsigned long long* g_strace = nullptr;
+// diagnostic builds only: the last k_parse_seg launch's per-block trace (4 x 2048 words), after a sync
+extern "C" __attribute__((visibility("default"))) int fb_seg_trace_last(unsigned long long* out) {
+    if (!g_strace || hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpy(out, g_strace, 8u * 4u * 2048u, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_parsed_pkt* parsed, hipStream_t s,
                       bool want_parts = false, SegPass pass = SegPass::kSegments, fb_pkt_out* dense_out = nullptr,
                       fb_dns_out* dense_dns = nullptr) {
@@ -637,6 +645,11 @@ static int launch_seg(fb_ctx* c, const SegBatches& sb, uint32_t n_max, const fb_
     p.error_next = c->d_error + ((launch + 1u) & 3u);
     const uint32_t waves = parse_seg_block_threads() / 64u;
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(c->seg_grid, (sb.total_segs + waves - 1) / waves));
+#ifdef FB_SEG_TRACE
+    if (!g_strace && hipMalloc(&g_strace, 8u * 4u * 2048u) != hipSuccess) return set_err(FB_ERR_NOMEM, "trace");
+    HIP_TRY(hipMemsetAsync(g_strace, 0, 8u * 4u * 2048u, s));
+    p.dtrace = g_strace;
+#endif
     HIP_TRY(launch_parse_seg(p, sb, grid, s, pass));
     return FB_OK;
 }

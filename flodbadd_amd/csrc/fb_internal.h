@@ -57,8 +57,8 @@ struct ParseParams {
     // fault injection for the tests (FB_DENSE_OFFSET_SKEW at fb_create, 0 otherwise): added to every
     // tile offset k_parse_dense hands its copies, as a corrupted look-back word would be
     unsigned long long dn_skew;
-#ifdef FB_DN_TRACE
-    // diagnostic builds: k_parse_dense timings (fb_parse.hip, kDnTr*)
+#if defined(FB_DN_TRACE) || defined(FB_SEG_TRACE)
+    // diagnostic builds: k_parse_dense / k_parse_seg timings (fb_parse.hip, kDnTr* / kSegTr*)
     unsigned long long* dtrace;
 #endif
 };

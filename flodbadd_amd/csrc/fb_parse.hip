@@ -319,6 +319,20 @@ constexpr int kSegDepth = FB_SEG_DEPTH;  // segments of header loads in flight p
 constexpr int kSegThreads = 64 * kSegWaves;
 constexpr uint32_t kSegBytes = 64u * 56u;  // one segment of output: 64 record slots
 
+#ifdef FB_SEG_TRACE
+// -DFB_SEG_TRACE (never the product): per block (up to kSegTrBlocks) the real-time ticks of its
+// start, its waves' last segment loop end (max), its segments, and its end (max)
+// (tools/experiments/seg_trace.py)
+constexpr uint32_t kSegTrBlocks = 2048u;
+__device__ __forceinline__ unsigned long long seg_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define SEGTR(stmt) do { stmt; } while (0)
+#else
+#define SEGTR(stmt) do { } while (0)
+#endif
 template <bool PARSED, uint32_t FLAGS = kFlagsProduct, bool MULTI = false>
 __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_parse_seg(const ParseParams P,
                                                                                       const SegBatches SB) {
@@ -340,6 +354,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     uint32_t a_s = 0u, a_d = 0u, a_f = 0u, a_t = 0u, a_4 = 0u, a_b = 0u, a_n = 0u;  // wave-uniform
     uint32_t a_k = 0u;  // the batch the counters belong to
     if (tid <= kAcc) s_acc[tid] = 0u;  // published by the prologue barrier
+    SEGTR(if (tid == 0u && b < kSegTrBlocks) P.dtrace[4u * b] = seg_now());
 
     // Batch of global segment g.  A wave visits its segments in increasing order, and so do its
     // header fetches and its offsets loads, so each keeps a monotone cursor (wave-uniform scalar
@@ -375,6 +390,12 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
     // takes the block's next L from an LDS counter, one step ahead of use: a wave that is
     // served faster processes more segments, and the block finishes when its work is done, not
     // when its slowest wave is.  A wave's L (hence its segments) still increase monotonically.
+    // Across blocks the share stays fixed: in a 20-batch C2 launch the blocks end between 257 and
+    // 469 us with equal shares, but dealing the launch in chunks from a device counter (round 5,
+    // tools/experiments/seg_dynamic_chunks.diff) evened them out (459-495 us) and ran slower --
+    // 42.4 vs 43.2 Gpps, and 24.3 vs 36.9 for one batch per launch: the memory system's total rate
+    // is fixed, the blocks left running go faster, and the counter's round trips cost
+    // (profiles/r05_seg_trace_static.txt, r05_seg_trace_dynamic.txt, r05_seg_dynamic_ab.txt).
     // One segment of header loads in flight per wave: X.h = headers of the current segment,
     // X.c its offsets, X.q the offsets of the wave's next segment.  After a segment:
     // X.h <- headers of the next segment from X.q, X.c <- X.q (explicit v_mov: no back-edge copy
@@ -680,6 +701,9 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             a_b += __popcll(__ballot(valid && kk.bad));
             a_n += __popcll(__ballot(valid));
     };
+#ifdef FB_SEG_TRACE
+    uint32_t steps_ = 0u;
+#endif
     while (sg < nseg) {
         const uint32_t La = grab();
         const uint32_t g_next = seg_of(Ln);
@@ -687,7 +711,12 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
         Lc = Ln;
         Ln = La;
         sg = g_next;
+        SEGTR(++steps_);
     }
+    SEGTR(if (lane == 0u && b < kSegTrBlocks) {
+        atomicMax(P.dtrace + 4u * b + 1u, seg_now());
+        atomicAdd(P.dtrace + 4u * b + 2u, (unsigned long long)steps_);
+    });
     if constexpr ((FLAGS & kDense) != 0u) return;  // pass 1 of the dense call published the stats
     // ---- batch stats, no barrier and no partials read-back:
     // every wave adds its counters into LDS (per batch); the block's last wave (LDS arrival
@@ -740,6 +769,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWaves * FB_SEG_BPC / 4) void k_par
             }
         }
     }
+    SEGTR(if (lane == 0u && b < kSegTrBlocks) atomicMax(P.dtrace + 4u * b + 3u, seg_now()));
 }
 
 // ============================================================================================
