@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -736,9 +737,22 @@ struct fb_seg_queue {
     uint64_t submitted = 0;
     bool launched = false;
     hipError_t gone = hipSuccess;  // what the stream reported when the kernel was found gone
+    uint32_t grid = 0;             // the kernel's blocks (all must be resident at once)
+    uint64_t idle_ns = 0;          // idle_ms in ns
+    std::chrono::steady_clock::time_point created;
+    bool not_resident = false;     // its blocks were not all running idle_ms after create
+    bool counted = false;          // holds its device's live-queue count
 };
+// One live queue per device: a second one's blocks could never all be resident beside the first's
+// (two blocks per CU each), so its kernel would not start and nothing on the device could report it.
+static std::mutex g_queue_mu;
+static uint32_t g_queue_live[64];
 
 static void queue_free(fb_seg_queue* q) {
+    if (q->counted) {
+        std::lock_guard<std::mutex> lk(g_queue_mu);
+        --g_queue_live[q->device];
+    }
     if (q->stream) hipStreamDestroy(q->stream);
     hipFree(q->d_cfg);
     hipFree(q->d_tick);
@@ -759,13 +773,29 @@ static int queue_kernel_gone(fb_seg_queue* q, uint64_t spin, uint64_t every) {
     if (hload(&q->h->status) & kQueueExpired) return FB_OK;
     if (spin % every != every - 1u) return 1;
     const hipError_t e = hipStreamQuery(q->stream);
-    if (e == hipErrorNotReady) return 1;
+    if (e == hipErrorNotReady) {
+        // every block counts itself into pad[3] when it starts; a kernel some of whose blocks never
+        // ran (the CUs held by other work) cannot complete a batch, and its resident blocks are not
+        // the ones waiting -- only the host can notice
+        if (hload(&q->h->pad[3]) != q->grid &&
+            (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                          q->created).count() > q->idle_ns) {
+            q->not_resident = true;
+            return FB_OK;
+        }
+        return 1;
+    }
     q->gone = e;
     return FB_OK;
 }
 
 static int queue_gone_error(fb_seg_queue* q) {
     const QueueHost* h = q->h;
+    if (q->not_resident)
+        return set_err(FB_ERR_INTERNAL,
+                       "the queue kernel's blocks are not all running (%llu of %u started within idle_ms): the "
+                       "device's CUs are held by other work; destroy the queue",
+                       (unsigned long long)hload(&h->pad[3]), q->grid);
     return set_err(FB_ERR_INTERNAL,
                    "the queue kernel has stopped (status %llu, stream: %s; a block left after %llu ticks idle "
                    "waiting for batch %llu (block %llu), tail %llu): destroy the queue",
@@ -785,11 +815,26 @@ fb_seg_queue* fb_seg_queue_create(fb_ctx* c, uint32_t depth, uint32_t idle_ms) {
         return nullptr;
     }
     DeviceGuard g(c->device);
+    {
+        std::lock_guard<std::mutex> lk(g_queue_mu);
+        if (c->device < 0 || c->device >= 64) {
+            set_err(FB_ERR_INVAL, "device %d", c->device);
+            return nullptr;
+        }
+        if (g_queue_live[c->device]) {
+            set_err(FB_ERR_INVAL, "device %d already runs a queue (one per device: destroy it first)", c->device);
+            return nullptr;
+        }
+        ++g_queue_live[c->device];  // (released by queue_free, or below)
+    }
     fb_seg_queue* q = new (std::nothrow) fb_seg_queue();
     if (!q) {
+        std::lock_guard<std::mutex> lk(g_queue_mu);
+        --g_queue_live[c->device];
         set_err(FB_ERR_NOMEM, "queue");
         return nullptr;
     }
+    q->counted = true;
     q->device = c->device;
     q->depth = depth;
     q->slots = 1u;
@@ -842,6 +887,9 @@ fb_seg_queue* fb_seg_queue_create(fb_ctx* c, uint32_t depth, uint32_t idle_ms) {
     int occ = 0;
     if (occupancy_parse_seg_queue(&occ) != hipSuccess || occ < 1) occ = 1;
     const uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(FB_QUEUE_BPC, occ) * cus));
+    q->grid = grid;
+    q->idle_ns = (uint64_t)(idle_ms ? idle_ms : 5000u) * 1000000ull;
+    q->created = std::chrono::steady_clock::now();
     if (launch_parse_seg_queue(p, grid, q->stream) != hipSuccess) {
         queue_free(q);
         set_err(FB_ERR_HIP, "queue kernel launch");

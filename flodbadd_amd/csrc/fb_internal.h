@@ -360,7 +360,7 @@ struct QueueHost {
     unsigned long long tail;    // batches submitted (host store, after the slot's descriptor)
     unsigned long long stop;    // host: no batch follows the submitted ones; the kernel exits when idle
     unsigned long long status;  // device: kQueueExpired -- a block waited idle_ticks for a batch and left
-    unsigned long long pad[5];
+    unsigned long long pad[5];  // 0-2: an expired block's diagnostics; 3: the kernel's blocks, once all run
     unsigned long long cdone[kQueueMax];  // slot k % depth: k + 1 once batch k is complete (system store)
     fb_seg_batch desc[kQueueMax];         // slot k % depth: batch k (host stores)
 };
@@ -372,7 +372,7 @@ struct QueueDev {
     unsigned long long tail;   // batches whose descriptors are in desc[]
     unsigned long long stop;   // the host's stop word, as the last poll saw it with nothing left
     uint32_t poller;
-    uint32_t pad[3];
+    uint32_t pad[3];           // pad[0]: blocks started (the last one sets the host's pad[3])
     fb_seg_batch desc[kQueueMax];
 };
 struct QueueParams {

@@ -1704,6 +1704,9 @@ __global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_q
     if (tid == 0u) {
         L.stop = 0u;
         L.tail = 0u;
+        // count the block in; the last one tells the host that every block runs (host pad word 3)
+        if (atomicAdd(&Q.d->pad[0], 1u) == gridDim.x - 1u)
+            __hip_atomic_store(&Q.h->pad[3], (unsigned long long)gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(Q.cfg);

@@ -412,8 +412,12 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, 
  * a queue lives its kernel holds two workgroups on every CU (every one must be resident: the grid is
  * sized by the occupancy query); what it leaves free -- the registers of a fifth wave per SIMD, a third
  * of the LDS -- runs copies and small kernels beside it, and a kernel that needs more of a CU waits
- * until fb_seg_queue_destroy.  A queue left idle for idle_ms (0 = 5,000 ms) stops itself; its calls
- * then fail with FB_ERR_INTERNAL (destroy it and create a new one). */
+ * until fb_seg_queue_destroy; so does hipFree (measured: a 1-MB hipFree waited 4.8 s, until the
+ * idle limit stopped the kernel, while hipMalloc, H2D and D2H copies did not wait): free device
+ * memory only after fb_seg_queue_destroy.  One queue per device at a time (a second create fails with
+ * FB_ERR_INVAL while the first lives).  A queue left idle for idle_ms (0 = 5,000 ms) stops itself,
+ * and one whose blocks were not all running idle_ms after create (CUs held by other work) is
+ * reported the same way: its calls then fail with FB_ERR_INTERNAL (destroy it, create a new one). */
 #define FB_QUEUE_MAX_DEPTH 32u
 typedef struct fb_seg_queue fb_seg_queue;
 fb_seg_queue* fb_seg_queue_create(fb_ctx* ctx, uint32_t depth /* 1..FB_QUEUE_MAX_DEPTH, 0 = 8 */, uint32_t idle_ms);

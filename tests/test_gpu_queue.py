@@ -164,3 +164,31 @@ def test_queue_expired_reports_error():
     finally:
         q.close()
         cap.close()
+
+
+def test_one_queue_per_device():
+    """A second queue's blocks could never be resident beside the first's: its create fails (instead
+    of a kernel that never starts), and succeeds again once the first is destroyed."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=0)
+    cap2 = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=0)
+    lib = N.gpu_lib()
+    b = _Batch(*synth.generate(3, 5000, first=11))  # (device buffers before the queue: see its create)
+    b2 = _Batch(*synth.generate(2, 3000, first=5))
+    q = _Queue(cap, depth=2)
+    try:
+        assert not lib.fb_seg_queue_create(cap2.ctx, 2, 1000)
+        assert b"already runs a queue" in lib.fb_last_error()
+        b.reset()
+        q.wait(q.submit(b))  # the first queue is unaffected
+        _verify(b, SessionFilter.All)
+    finally:
+        q.close()
+    q2 = _Queue(cap2, depth=2)
+    try:  # (no device buffer is freed while a queue lives: hipFree waits for the queue's kernel)
+        b2.reset()
+        q2.wait(q2.submit(b2))
+        _verify(b2, SessionFilter.All)
+    finally:
+        q2.close()
+        cap.close()
+        cap2.close()
