@@ -9,8 +9,9 @@ from . import _native
 from ._native import (DNS_OUT_DTYPE, FB_CLASS_DNS, FB_CLASS_DROP, FB_CLASS_FILTERED, FB_CLASS_SESSION,
                       FLOW_REC_DTYPE, PKT_OUT_DTYPE, STATS_DTYPE, FbError, NativeLibraryMissing, gpu_lib)
 from .sessions import Protocol, Session, SessionFilter, SessionInfo, SessionPacketData, SessionStats
+from .queue import DeviceSegBatch, SegQueue
 
-__all__ = ["_native", "gpu_lib", "FbError", "NativeLibraryMissing", "PKT_OUT_DTYPE", "DNS_OUT_DTYPE",
+__all__ = ["_native", "DeviceSegBatch", "SegQueue", "gpu_lib", "FbError", "NativeLibraryMissing", "PKT_OUT_DTYPE", "DNS_OUT_DTYPE",
            "STATS_DTYPE", "FLOW_REC_DTYPE", "FB_CLASS_SESSION", "FB_CLASS_DNS", "FB_CLASS_DROP",
            "FB_CLASS_FILTERED", "Protocol", "Session", "SessionFilter", "SessionInfo", "SessionPacketData",
            "SessionStats"]

@@ -3,7 +3,6 @@ time to ONE running kernel through a ring in pinned host memory, each batch's se
 classes and stats bit-exact against the oracle (the layout fb_parse_classify_seg_dev writes) --
 ragged and empty batches, more batches than ring slots, an idle gap between submissions, the
 configuration captured at create, and an expired queue reporting an error instead of hanging."""
-import ctypes as C
 import time
 
 import numpy as np
@@ -12,6 +11,7 @@ import pytest
 from flodbadd_amd import _native as N
 from flodbadd_amd import synth
 from flodbadd_amd.capture import FlodbaddGpuCapture
+from flodbadd_amd.queue import DeviceSegBatch, SegQueue
 from flodbadd_amd.sessions import SessionFilter
 from test_gpu_segmented import _check
 
@@ -19,60 +19,30 @@ pytestmark = pytest.mark.gpu
 
 
 class _Batch:
-    """Device buffers of one batch and its fb_seg_batch descriptor."""
+    """A test batch: the host arrays the oracle checks against, beside the package's device buffers."""
 
     def __init__(self, frames, offs, with_cls=True):
         self.frames = np.ascontiguousarray(frames, dtype=np.uint8)
         self.offs = np.ascontiguousarray(offs, dtype=np.uint32)
-        self.n = n = len(self.offs) - 1
-        nseg = max((n + 63) // 64, 1)
-        self.fr = N.DeviceBuffer(max(self.frames.nbytes, 1))
-        if self.frames.nbytes:
-            self.fr.upload(self.frames)
-        self.of = N.DeviceBuffer(self.offs.nbytes).upload(self.offs)
-        self.out, self.seg = N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4)
-        self.cls = N.DeviceBuffer(max(n, 1)) if with_cls else None
-        self.st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
-        self.desc = np.zeros(1, dtype=N.SEG_BATCH_DTYPE)
-        self.desc[0] = (self.fr.ptr.value, self.frames.nbytes, self.of.ptr.value, n, 0, self.out.ptr.value,
-                        self.seg.ptr.value, self.cls.ptr.value if self.cls else 0, self.st.ptr.value)
+        self.n = len(self.offs) - 1
+        self.dev = DeviceSegBatch(self.frames, self.offs, with_classes=with_cls)
 
     def reset(self):
-        # bytes outside a segment's records must stay untouched.  The fills are copies from the host
-        # (DMA engine), not memset kernels: while a queue lives its kernel holds the CUs, and a fill
-        # kernel would wait for it (fb_seg_queue_create's note); upload() also completes before the submit
-        self.out.upload(np.full(self.out.nbytes, 0xA5, dtype=np.uint8))
-        self.st.upload(np.full(self.st.nbytes, 0xEE, dtype=np.uint8))
+        # bytes outside a segment's records must stay untouched (the fills are host copies: while a
+        # queue lives its kernel holds the CUs a fill kernel would wait for; upload() completes before
+        # the submit)
+        self.dev.fill_outputs()
 
     def result(self):
-        n, nseg = self.n, max((self.n + 63) // 64, 1)
-        raw = self.out.download(np.zeros(nseg * N.SEG_BYTES, dtype=np.uint8))
-        seg = self.seg.download(np.zeros(nseg, dtype=np.uint32))[: (n + 63) // 64]
-        cls = self.cls.download(np.zeros(max(n, 1), dtype=np.uint8))[:n] if self.cls else None
-        st = self.st.download(np.zeros(1, dtype=N.STATS_DTYPE))
-        return raw, seg, cls, st
+        return self.dev.raw()
 
 
-class _Queue:
+class _Queue(SegQueue):
     def __init__(self, cap, depth, idle_ms=3000):
-        self.lib = N.gpu_lib()
-        q = self.lib.fb_seg_queue_create(cap.ctx, depth, idle_ms)
-        assert q, self.lib.fb_last_error()
-        self.q = C.c_void_p(q)
+        super().__init__(cap, depth=depth, idle_ms=idle_ms)
 
     def submit(self, b):
-        t = C.c_uint64()
-        N.check(self.lib.fb_seg_queue_submit(self.q, N.ptr(b.desc), C.byref(t)))
-        return t.value
-
-    def wait(self, t):
-        N.check(self.lib.fb_seg_queue_wait(self.q, t))
-
-    def close(self):
-        if self.q:
-            rc = self.lib.fb_seg_queue_destroy(self.q)
-            self.q = None
-            N.check(rc)
+        return super().submit(b.dev)
 
 
 def _verify(b, flt):
