@@ -36,7 +36,9 @@ __global__ __launch_bounds__(512) void k_gather(const uint4* __restrict__ units,
     if (threadIdx.x == 1023u) pad[0] = 0u;
     const uint32_t i = blockIdx.x;
     uint32_t p = i;
-    if (xcd_map) {
+    if (xcd_map == 2u) {  // XCD-contiguous: XCD x (blocks i % 8 == x) takes partitions [x P/8, (x+1) P/8) in order
+        p = (i % 8u) * (P / 8u) + i / 8u;
+    } else if (xcd_map) {
         const uint32_t per = P / S, x = i % 8u, k = i / 8u;  // XCD x: supers x, x + 8, ..., in order
         const uint32_t s = x + 8u * (k / per);
         p = s * per + k % per;
@@ -128,6 +130,38 @@ int main(int argc, char** argv) {
                    S ? "super" : "packed", S, xm ? "xcd" : "ident", U, lds >> 10, N, best * 1e3f, sum / reps * 1e3f,
                    N / (best * 1e-3f) / 1e9f);
           }
+        }
+    }
+    // layouts of the fused parse: units sorted by partition inside groups of G consecutive records
+    // (G = 64: the product's per-segment sort; 256 / 1024: a wave's 4 / a block's 16 segments)
+    for (uint32_t G : {64u, 256u, 1024u}) {
+        std::vector<uint32_t> pos(N), ord(G);
+        for (uint32_t g0 = 0; g0 < N; g0 += G) {
+            const uint32_t m = std::min(G, N - g0);
+            for (uint32_t k = 0; k < m; ++k) ord[k] = g0 + k;
+            std::stable_sort(ord.begin(), ord.begin() + m, [&](uint32_t x, uint32_t y) { return part[x] < part[y]; });
+            for (uint32_t k = 0; k < m; ++k) pos[ord[k]] = g0 + k;
+        }
+        std::vector<uint32_t> ps(P + 1, 0), idx(N);
+        for (uint32_t u = 0; u < N; ++u) ps[part[u] + 1]++;
+        for (uint32_t q = 0; q < P; ++q) ps[q + 1] += ps[q];
+        std::vector<uint32_t> cur(ps.begin(), ps.end() - 1);
+        for (uint32_t u = 0; u < N; ++u) idx[cur[part[u]]++] = pos[u];
+        CK(hipMemcpy(d_idx, idx.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_ps, ps.data(), (size_t)(P + 1) * 4, hipMemcpyHostToDevice));
+        for (uint32_t xm : {0u, 2u}) {
+            float best = 1e9f, sum = 0.f;
+            for (int r = 0; r < reps + 2; ++r) {
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(k_gather<2>, dim3(P), dim3(512), 72u * 1024u, 0, d_units, d_idx, d_ps, P, 1u, xm, d_out);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r >= 2) { best = std::min(best, ms); sum += ms; }
+            }
+            printf("sorted G=%-5u map=%-6s lds=72K  units %u  best %.1f us  mean %.1f us  %.1f G units/s\n", G,
+                   xm ? "xcdrun" : "ident", N, best * 1e3f, sum / reps * 1e3f, N / (best * 1e-3f) / 1e9f);
         }
     }
     return 0;
