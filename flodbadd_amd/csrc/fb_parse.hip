@@ -1525,33 +1525,15 @@ __device__ __forceinline__ bool q_ensure(const QueueParams& Q, QLds* L, uint32_t
     }
 }
 
-// A chunk fetch whose returned value has not been read yet: the wave that issues it publishes it in
-// the ring at its next position fetch (or before it could block), so the atomic's round trip overlaps
-// a segment's work instead of draining the wave's pipeline (a returned atomic waits for every older
-// load and store of the wave).  One counter only (kQHeads 1); with more, q_grab fetches at once.
-struct QPend {
-    uint32_t where;  // L->chunk index of the entry to publish, ~0u: none
-    uint32_t tag;    // its slot + 1
-    uint32_t nch;    // chunks of its batch
-    uint32_t r;      // lane 0: the counter's returned value
-};
-__device__ __forceinline__ void q_flush(QLds* L, QPend* p) {
-    if (p->where == ~0u) return;  // (uniform)
-    const uint32_t v = u1st(p->r);
-    const uint32_t cn = v < p->nch ? v : 0xFFFFFFFFu;
-    if ((threadIdx.x & 63u) == 0u)
-        __hip_atomic_store(L->chunk + p->where, ((unsigned long long)p->tag << 32) | cn, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-    p->where = ~0u;
-}
-
 // The block's next segment of the slot's batch (false: the batch has none left for this block).
 // Position L of the block is offset L % kQChunk of the block's chunk L / kQChunk; the wave that
 // takes a chunk's first position fetches the block's next chunk from the slot's device counter (after
 // its own chunk is known, so the chunks of a block increase), or marks it empty once its own is.
-__device__ __forceinline__ bool q_take(const QueueParams& Q, QLds* L, uint32_t slot, uint32_t* sg, QPend* pend) {
+// (Publishing the fetched chunk only at the wave's next position fetch, so the returned atomic's
+// round trip overlaps a segment instead of draining the wave: 41.47 / 41.56 vs 41.45 / 41.43 Gpps
+// over 512 batches, interleaved -- no gain, not kept; tools/experiments/queue_deferred_fetch.diff.)
+__device__ __forceinline__ bool q_take(const QueueParams& Q, QLds* L, uint32_t slot, uint32_t* sg) {
     const uint32_t lane = threadIdx.x & 63u;
-    q_flush(L, pend);  // (before this wave can wait on a ring entry)
     uint32_t v = 0u;
     if (lane == 0u) v = __hip_atomic_fetch_add(&L->next[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t pos = u1st(v), i = pos / kQChunk, o = pos % kQChunk;
@@ -1567,18 +1549,10 @@ __device__ __forceinline__ bool q_take(const QueueParams& Q, QLds* L, uint32_t s
     }
     const uint32_t nseg = u1st(L->desc[slot].nseg), nch = (nseg + kQChunk - 1u) / kQChunk;
     if (o == 0u) {
-        if (kQHeads == 1u && c < nch) {  // fetched now, published at this wave's next position fetch
-            uint32_t r = 0u;
-            if (lane == 0u) r = __hip_atomic_fetch_add(Q.head + slot * kQueueHeadWords, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pend->r = r;
-            pend->where = slot * kQRing + (i + 1u) % kQRing;
-            pend->tag = i + 2u;
-            pend->nch = nch;
-        } else {
-            const uint32_t cn = c < nch ? q_grab(Q, slot, nch) : 0xFFFFFFFFu;
-            if (lane == 0u) __hip_atomic_store(ring + (i + 1u) % kQRing, ((unsigned long long)(i + 2u) << 32) | cn,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        uint32_t cn = 0xFFFFFFFFu;
+        if (c < nch) cn = q_grab(Q, slot, nch);
+        if (lane == 0u) __hip_atomic_store(ring + (i + 1u) % kQRing, ((unsigned long long)(i + 2u) << 32) | cn,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (c >= nch) return false;
     *sg = c * kQChunk + o;
@@ -1679,8 +1653,7 @@ struct QPos {
 struct QGen {
     uint32_t gk, gt, known;
 };
-__device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* g, bool block, uint32_t* arr_next,
-                                           QPend* pend) {
+__device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* g, bool block, uint32_t* arr_next) {
     const uint32_t lane = threadIdx.x & 63u, R = Q.depth;
     for (;;) {
         if (g->gk >= g->known) {
@@ -1695,7 +1668,6 @@ __device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* 
                 if (g->gk >= g->known) {
                     if (!block) return QPos{g->gk, 0u, 0u};
                     QTRACE(if (lane == 0u) atomicAdd(qt(Q, kQtDrain, g->gk), 1ull));
-                    q_flush(L, pend);  // (nothing of this wave may hold up the batches it leaves)
                     // about to wait for a batch the host has not published: this wave (pipeline empty,
                     // counters flushed, stores complete -- the caller's drain) is done with every batch
                     // before it, including those it passed without a segment here; the host may be
@@ -1708,7 +1680,7 @@ __device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* 
         if (g->known <= g->gk) g->known = g->gk + 1u;
         g->gt = 1u;  // (inside batch gk: the main loop's fast path takes its positions)
         uint32_t sg;
-        if (q_take(Q, L, g->gk & (R - 1u), &sg, pend)) return QPos{g->gk, sg, 1u};
+        if (q_take(Q, L, g->gk & (R - 1u), &sg)) return QPos{g->gk, sg, 1u};
         ++g->gk;
         g->gt = 0u;
     }
@@ -1751,7 +1723,6 @@ __global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_q
     __syncthreads();
 
     QGen g{0u, 0u, 0u};
-    QPend pend{~0u, 0u, 0u, 0u};
     auto frames_rsrc = [&](uint32_t k) {
         const QDesc& d = L.desc[k & (R - 1u)];
         return __builtin_amdgcn_make_buffer_rsrc((void*)u1st64(d.frames), (short)0, (int)u1st(d.frames_bytes), 0x00020000);
@@ -1790,12 +1761,11 @@ __global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_q
             // pipeline empty: everything this wave generated is processed; it is done with every batch
             // before g.gk; then wait for work (the only place a wave blocks)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            q_flush(&L, &pend);
             flush();
             q_arrive(Q, &L, &arr_next, g.gk);
-            cur = q_gen_slow(Q, &L, &g, true, &arr_next, &pend);
+            cur = q_gen_slow(Q, &L, &g, true, &arr_next);
             if (!cur.ok) break;
-            nxt = q_gen_slow(Q, &L, &g, false, &arr_next, &pend);
+            nxt = q_gen_slow(Q, &L, &g, false, &arr_next);
             load_q(cur, q);
             load_headers1(frames_rsrc(cur.k), q.x, h);
             c = make_uint2(vmov(q.x), vmov(q.y));
@@ -1807,7 +1777,7 @@ __global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_q
             bool fast = false;
             if (g.gt) {  // a position inside the batch this wave is in
                 uint32_t sg;
-                if (q_take(Q, &L, g.gk & (R - 1u), &sg, &pend)) {
+                if (q_take(Q, &L, g.gk & (R - 1u), &sg)) {
                     aft = QPos{g.gk, sg, 1u};
                     fast = true;
                 } else {
@@ -1815,11 +1785,10 @@ __global__ __launch_bounds__(kSegThreads, kQueueWavesPerSimd) void k_parse_seg_q
                     g.gt = 0u;
                 }
             }
-            if (!fast) aft = q_gen_slow(Q, &L, &g, false, &arr_next, &pend);
+            if (!fast) aft = q_gen_slow(Q, &L, &g, false, &arr_next);
         }
         if (cur.k != a_k) {  // the first segment of a later batch: the earlier ones are done here
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            q_flush(&L, &pend);
             flush();
             a_k = cur.k;
             q_arrive(Q, &L, &arr_next, cur.k);
