@@ -134,12 +134,17 @@ int main(int argc, char** argv) {
     }
     // layouts of the fused parse: units sorted by partition inside groups of G consecutive records
     // (G = 64: the product's per-segment sort; 256 / 1024: a wave's 4 / a block's 16 segments)
-    for (uint32_t G : {64u, 256u, 1024u}) {
+    // (BK > 1: sorted by partition / BK only -- the bucket of 64 consecutive partitions one XCD's K2
+    // workgroups hold at once under the XCD-contiguous mapping -- order inside a bucket arbitrary)
+    for (uint32_t GB : {64u, 256u, 1024u, 256u | (64u << 16), 320u | (64u << 16), 384u | (64u << 16)}) {
+        const uint32_t G = GB & 0xFFFFu, BK = GB >> 16 ? GB >> 16 : 1u;
         std::vector<uint32_t> pos(N), ord(G);
         for (uint32_t g0 = 0; g0 < N; g0 += G) {
             const uint32_t m = std::min(G, N - g0);
             for (uint32_t k = 0; k < m; ++k) ord[k] = g0 + k;
-            std::stable_sort(ord.begin(), ord.begin() + m, [&](uint32_t x, uint32_t y) { return part[x] < part[y]; });
+            std::stable_sort(ord.begin(), ord.begin() + m, [&](uint32_t x, uint32_t y) {
+                return part[x] / BK < part[y] / BK || (part[x] / BK == part[y] / BK && BK > 1u && (x * 2654435761u) < (y * 2654435761u));
+            });
             for (uint32_t k = 0; k < m; ++k) pos[ord[k]] = g0 + k;
         }
         std::vector<uint32_t> ps(P + 1, 0), idx(N);
@@ -160,8 +165,8 @@ int main(int argc, char** argv) {
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 if (r >= 2) { best = std::min(best, ms); sum += ms; }
             }
-            printf("sorted G=%-5u map=%-6s lds=72K  units %u  best %.1f us  mean %.1f us  %.1f G units/s\n", G,
-                   xm ? "xcdrun" : "ident", N, best * 1e3f, sum / reps * 1e3f, N / (best * 1e-3f) / 1e9f);
+            printf("sorted G=%-5u key=part/%-3u map=%-6s lds=72K  units %u  best %.1f us  mean %.1f us  %.1f G units/s\n", G,
+                   BK, xm ? "xcdrun" : "ident", N, best * 1e3f, sum / reps * 1e3f, N / (best * 1e-3f) / 1e9f);
         }
     }
     return 0;
