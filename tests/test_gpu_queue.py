@@ -45,11 +45,11 @@ class _Queue(SegQueue):
         return super().submit(b.dev)
 
 
-def _verify(b, flt):
+def _verify(b, flt, cfg=None):
     from oracle import coracle
     from test_gpu_segmented import _expected_seg
     raw, seg, cls, st = b.result()
-    r_out, r_dns, r_cls, r_st = coracle.parse_classify(coracle.make_cfg(int(flt)), b.frames, b.offs)
+    r_out, r_dns, r_cls, r_st = coracle.parse_classify(cfg or coracle.make_cfg(int(flt)), b.frames, b.offs)
     if cls is None:  # no class output asked for
         cls = r_cls
     # compact diagnostics first (a failing bytes comparison of a 1M-frame batch makes pytest diff for minutes)
@@ -65,7 +65,13 @@ def _verify(b, flt):
                            if len(g_out) != len(r_out) else
                            (g_out.view(np.uint8).reshape(-1, 56) != r_out.view(np.uint8).reshape(-1, 56)).any(axis=1))
         raise AssertionError("n=%d: %d of %d records differ, first %s" % (b.n, d.size, len(r_out), d[:5]))
-    _check(None, b.frames, b.offs, flt=int(flt), res=(raw, seg, cls, st))
+    if cfg is None:
+        _check(None, b.frames, b.offs, flt=int(flt), res=(raw, seg, cls, st))
+    else:  # (the stats against the same oracle run)
+        for k in N.STATS_FIELDS:
+            if k.startswith("reserved") or k in ("new_sessions", "updated_sessions", "error"):
+                continue
+            assert int(st[0][k]) == int(r_st[0][k]), k
 
 
 @pytest.mark.parametrize("depth", [4, 3, 1])
@@ -162,3 +168,33 @@ def test_one_queue_per_device():
         q2.close()
         cap.close()
         cap2.close()
+
+
+def test_queue_lan_v6_own_ips_captured_at_create():
+    """LocalOnly with IPv6 LAN prefixes and own IPs: the edge-case frames and an IMIX batch through the
+    queue match the oracle under that configuration, although the context is reset to All with no
+    prefixes or own IPs right after the queue is created (the queue keeps what it captured)."""
+    import framegen as fg
+    from flodbadd_amd.capture import lan_v6_table, own_ip_table
+    from oracle import coracle
+    lan = [("2001:db8:abcd:12::1", 64)]
+    own = ["192.168.1.1", "10.0.0.5", "2001:db8::1"]
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.LocalOnly, flow_capacity=0)
+    cap.set_lan_v6(lan)
+    cap.set_own_ips(own)
+    cfg = coracle.make_cfg(int(SessionFilter.LocalOnly), lan_v6=lan_v6_table(lan), own_ips=own_ip_table(own))
+    edge = _Batch(*fg.pack([f for _, f in fg.edge_cases()]))
+    imix = _Batch(*synth.generate(3, 70001, first=41))
+    cap.parse_classify(edge.frames, edge.offs)  # (the configuration uploaded before the queue captures it)
+    q = _Queue(cap, depth=2)
+    try:
+        cap.set_filter(SessionFilter.All)
+        cap.set_lan_v6([])
+        cap.set_own_ips([])
+        for b in (edge, imix):
+            b.reset()
+            q.wait(q.submit(b))
+            _verify(b, SessionFilter.LocalOnly, cfg=cfg)
+    finally:
+        q.close()
+        cap.close()
