@@ -198,3 +198,22 @@ def test_queue_lan_v6_own_ips_captured_at_create():
     finally:
         q.close()
         cap.close()
+
+
+def test_queue_large_batch_between_small_ones():
+    """An 8M-frame IMIX batch (131,072 segments, chunk counters far past one block's share) between
+    small batches in the ring, every one bit-exact."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.GlobalOnly, flow_capacity=0)
+    batches = [_Batch(*synth.generate(3, n, first=f)) for n, f in ((4097, 5), (1 << 23, 100), (130, 9))]
+    q = _Queue(cap, depth=3)
+    try:
+        for b in batches:
+            b.reset()
+        ts = [q.submit(b) for b in batches]
+        for t in ts:
+            q.wait(t)
+        for b in batches:
+            _verify(b, SessionFilter.GlobalOnly)
+    finally:
+        q.close()
+        cap.close()
