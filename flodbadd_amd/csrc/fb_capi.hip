@@ -50,6 +50,7 @@ struct UpdScratch {
     uint2* e_sort = nullptr;       // [flow_recs] combined groups' records in record order (history)
     uint32_t* hot = nullptr;       // [flow_recs / 16 + 16] hot groups for k_flow_combine
     uint32_t* ctl = nullptr;       // [4] its counters (FlowParams::ctl)
+    uint32_t* order = nullptr;     // [flow_parts + kK2Lead + 1] K2's partition order (FlowParams::order)
 };
 
 struct fb_ctx {
@@ -246,6 +247,7 @@ static void free_upd_scratch(UpdScratch& u) {
     hipFree(u.e_sort);
     hipFree(u.hot);
     hipFree(u.ctl);
+    hipFree(u.order);
     u = UpdScratch();
 }
 
@@ -258,7 +260,8 @@ static int alloc_upd_scratch(fb_ctx* c, UpdScratch& u, hipStream_t s) {
         hipMalloc(&u.e_orig, recs * 4ull) != hipSuccess || hipMalloc(&u.e_sort, recs * 8ull) != hipSuccess ||
         hipMalloc(&u.rows, chunks * c->flow_parts * 4ull) != hipSuccess ||
         hipMalloc(&u.cols, chunks * c->flow_parts * 4ull) != hipSuccess ||
-        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 16) != hipSuccess) {
+        hipMalloc(&u.hot, (recs / 16 + 16) * 4ull) != hipSuccess || hipMalloc(&u.ctl, 16) != hipSuccess ||
+        hipMalloc(&u.order, ((uint64_t)c->flow_parts + kK2Lead + 1u) * 4ull) != hipSuccess) {
         free_upd_scratch(u);
         return set_err(FB_ERR_NOMEM, "flow update scratch (%llu records)", (unsigned long long)recs);
     }
@@ -1405,6 +1408,10 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.hword = c->d_hword;
     p.hot = u.hot;
     p.ctl = u.ctl;
+#ifndef FB_K2_ORDER
+#define FB_K2_ORDER 1
+#endif
+    p.order = FB_K2_ORDER ? u.order : nullptr;
     p.agg_slot = c->d_agg_slot;
     p.hot_cap = (uint32_t)(c->flow_recs / 16 + 16);
     p.rec_part = (d_seg && c->part_recs == d_recs) ? c->part_buf : nullptr;  // written by this batch's parse

@@ -20,8 +20,13 @@
 //                       more than once becomes one combined entry in `comb`, its index word
 //                       kIdxCombined | id.
 //   K1t k_flow_transpose rows[chunk][part] -> cols[part][chunk] (so K2 reads its column
-//                       contiguously).
-//   K2 k_flow_apply     one workgroup per partition: loads the partition's slot heads into LDS,
+//                       contiguously), and each partition's entries summed: the partitions past
+//                       twice the mean are listed for K2's leading workgroups.
+//   K2 k_flow_apply     one workgroup per partition (the listed ones first, then the rest in
+//                       order: under Zipf(1.1) a partition holding a flow K1c leaves plain takes
+//                       up to ~210 us, and in partition order such workgroups started up to
+//                       ~280 us into the launch -- K2 405 -> 330 us, tools/experiments/
+//                       flow_trace.py, profiles/r05_k2_experiments.txt): loads the partition's slot heads into LDS,
 //                       gathers its entries' records (or combined entries) from every chunk,
 //                       finds/inserts each key in the slice, adds the counters and reduces the
 //                       ordered state with LDS atomics, folds the ordered state once per slot,
@@ -39,6 +44,24 @@
 namespace fbk {
 
 // flow_hash_words / part_of: fb_internal.h (the parse kernel computes the partition too).
+
+#ifdef FB_FLOW_TRACE
+// -DFB_FLOW_TRACE (never the product): per K2 workgroup (partition, up to kFlowTrParts) the
+// real-time ticks of its start, the end of its entry loop and its end, its entries (low word) and
+// its busiest slot's history characters (high word); per K1c workgroup its start, its end, its
+// groups and its records (tools/experiments/flow_trace.py, fb_flow_trace_last)
+constexpr uint32_t kFlowTrParts = 8192u;
+__device__ unsigned long long g_k2_trace[kFlowTrParts * 4u];
+__device__ unsigned long long g_k1c_trace[1024u * 4u];
+__device__ __forceinline__ unsigned long long flow_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define FLOWTR(stmt) do { stmt; } while (0)
+#else
+#define FLOWTR(stmt) do { } while (0)
+#endif
 
 // Inclusive wave scan + block exclusive scan of one u32 per thread (blockDim multiple of 64).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
@@ -229,6 +252,10 @@ __global__ __launch_bounds__(kFlowK1Threads) void k_flow_bucket(const FlowParams
     const uint32_t n = batch_records(P);
     if (blockIdx.x == 0 && threadIdx.x == 0 && !P.seg && P.stats->n_session > (unsigned long long)P.max_recs)
         atomicOr(P.error, 8u);  // more records than the update scratch holds: the rest is dropped
+    if (P.order)  // K2's partition order of this update (K1t sums into it)
+        for (uint32_t j = blockIdx.x * kFlowK1Threads + threadIdx.x; j < P.parts + kK2Lead + 1u;
+             j += gridDim.x * kFlowK1Threads)
+            P.order[j] = 0u;
     const uint32_t base = blockIdx.x * kFlowChunk;
     if (base >= n) return;
     const uint32_t cnt = min(kFlowChunk, n - base);
@@ -382,9 +409,33 @@ __global__ __launch_bounds__(256) void k_flow_transpose(const FlowParams P, uint
         tile[y][tx] = (c < chunks && p < P.parts) ? P.rows[(size_t)c * P.parts + p] : 0u;
     }
     __syncthreads();
+    // each partition's entries (a wave holds one partition's 64 chunks of the tile) summed into
+    // P.order; the partition whose sum passes twice the mean joins K2's leading partitions.  Only a
+    // tile holding at least its share of that (the tiles of a heavy partition do) adds with a
+    // returned value -- the others' adds are fire-and-forget, so a uniform batch waits on none
+    const uint32_t lead_min = max(64u, 2u * (uint32_t)(((unsigned long long)chunks * kFlowChunk) / P.parts));
+    const uint32_t tile_min = lead_min / ((chunks + 63u) / 64u);
     for (uint32_t y = ty; y < 64u; y += 4u) {
         const uint32_t p = p0 + y, c = c0 + tx;
-        if (p < P.parts && c < chunks) P.cols[(size_t)p * P.chunk_stride + c] = tile[tx][y];
+        const uint32_t w = tile[tx][y];
+        if (p < P.parts && c < chunks) P.cols[(size_t)p * P.chunk_stride + c] = w;
+        if (P.order && p < P.parts) {  // (uniform per wave)
+            uint32_t sum = c < chunks ? w >> 16 : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+            if (tx == 0u && sum != 0u && sum < tile_min) {
+                __hip_atomic_fetch_add(P.order + p, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (tx == 0u && sum != 0u) {
+                const uint32_t old = atomicAdd(P.order + p, sum);
+                if (old < lead_min && old + sum >= lead_min) {
+                    const uint32_t i = atomicAdd(P.order + P.parts + kK2Lead, 1u);
+                    if (i < kK2Lead) {
+                        P.order[P.parts + i] = p;
+                        atomicOr(P.order + p, 1u << 31);
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -863,6 +914,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
     if (threadIdx.x == 0) L.pool_next = L.pool_end = 0u;  // published by the group loop's first barrier
     uint32_t* E = P.entries;
     uint4* CE = reinterpret_cast<uint4*>(P.comb);
+#ifdef FB_FLOW_TRACE
+    const unsigned long long tr_t0 = flow_now();
+    uint32_t tr_groups = 0u, tr_recs = 0u;
+#endif
     // Groups are taken one at a time (ctl[3]), not by a fixed stride: their sizes vary by 50x under
     // skew (48 .. ~2,500 records), and with the stride the busiest workgroup held 2.2x the mean's
     // records (C4 Zipf(1.1) K1c 346 -> 288 us).  (Big groups first, from the back of the list:
@@ -880,6 +935,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         const uint32_t grp = P.hot[h], chunk = grp >> 16, part = grp & 0xFFFFu;
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
+        FLOWTR(++tr_groups; tr_recs += cnt);
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
         for (uint32_t j = threadIdx.x; j < kCombBm; j += kCombThreads) L.bm[j] = 0ull;
         for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
@@ -1066,6 +1122,13 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         }
         __syncthreads();  // the table is re-initialised for the next group
     }
+    FLOWTR(if (threadIdx.x == 0 && blockIdx.x < 1024u) {
+        unsigned long long* t = g_k1c_trace + 4u * blockIdx.x;
+        t[0] = tr_t0;
+        t[1] = flow_now();
+        t[2] = tr_groups;
+        t[3] = tr_recs;
+    });
 }
 
 __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_flow_apply(const FlowParams P) {
@@ -1078,10 +1141,28 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     unsigned long long* slice = reinterpret_cast<unsigned long long*>(slice4);
     uint32_t* scr = reinterpret_cast<uint32_t*>(slice + (size_t)kFlowSlots * kSlotWords);
     uint32_t* tags = scr + (size_t)kFlowSlots * kScrU32;  // FB_K2_TAGS: the slots' probe tags
-    const uint32_t part = blockIdx.x;
+    // the leading workgroups take the partitions with the most entries (K1t's list), the rest the
+    // other partitions in order; the grid has kK2Lead workgroups more than partitions with P.order
+    // (a later workgroup's check of its partition waits below, behind its first loads)
+    uint32_t part = blockIdx.x, led = 0u;
+    if (P.order) {
+        if (blockIdx.x < kK2Lead) {
+            if (blockIdx.x >= min(P.order[P.parts + kK2Lead], kK2Lead)) return;  // (uniform)
+            part = P.order[P.parts + blockIdx.x];
+        } else {
+            part = blockIdx.x - kK2Lead;
+            led = P.order[part];
+        }
+    }
     const uint32_t n = batch_records(P);
     const uint32_t chunks = (n + kFlowChunk - 1u) / kFlowChunk;
     const uint32_t* col = P.cols + (size_t)part * P.chunk_stride;
+#ifdef FB_FLOW_TRACE
+    const unsigned long long tr_t0 = flow_now();
+    unsigned long long tr_t1 = 0ull;
+    __shared__ uint32_t tr_hmax;
+    if (threadIdx.x == 0) tr_hmax = 0u;
+#endif
 
     // the first round's group rows (kept for it) and the rows past it: the partition's total
     uint32_t v0[kK2Cpt], mine = 0u;
@@ -1116,6 +1197,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
 #endif
     const bool dense = FB_K2_PREFETCH && n >= 32u * P.parts;
     if (dense) load_slice();
+    if (led >> 31) return;  // (uniform) a leading workgroup's partition
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
     uint32_t hbase_out = 0u, hc = 0u;
@@ -1231,6 +1313,7 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
             __syncthreads();
         }
         hc = scr[(size_t)threadIdx.x * kScrU32 + kScCount];  // (before the fold reuses the word)
+        FLOWTR(tr_t1 = flow_now(); atomicMax(&tr_hmax, hc));
         finish_slot(scr + (size_t)threadIdx.x * kScrU32, P.batch, ord0, ord1,
                     P.char_call ? P.char_call + (size_t)part * kFlowSlots + threadIdx.x : nullptr);
         __syncthreads();  // every slot's new ordered fields are in its scratch
@@ -1256,6 +1339,13 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
     // history characters per slot this update (the history's output offsets), and their total
     P.hcount[(size_t)part * kFlowSlots + threadIdx.x] = hc;
     const unsigned long long hcs = block_sum((unsigned long long)hc, sh);
+    FLOWTR(if (threadIdx.x == 0 && part < kFlowTrParts) {
+        unsigned long long* t = g_k2_trace + 4u * part;
+        t[0] = tr_t0;
+        t[1] = tr_t1;
+        t[2] = flow_now();
+        t[3] = total | (unsigned long long)tr_hmax << 32;
+    });
     if (threadIdx.x == 0) {
         P.partials[4 * part] = n_new;
         P.partials[4 * part + 1] = n_upd;
@@ -1403,7 +1493,7 @@ hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k_flow_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kK2Lds);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_flow_apply, dim3(p.parts), dim3(kFlowK2Threads), kK2Lds, s, p);
+    hipLaunchKernelGGL(k_flow_apply, dim3(p.parts + (p.order ? kK2Lead : 0u)), dim3(kFlowK2Threads), kK2Lds, s, p);
     return hipGetLastError();
 }
 hipError_t launch_flow_finish(fb_batch_stats* stats, const unsigned long long* partials, uint32_t nblk,
@@ -1438,6 +1528,17 @@ hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap, unsi
 }
 
 }  // namespace fbk
+
+#ifdef FB_FLOW_TRACE
+// diagnostic builds only: the last K2 launch's per-partition trace (4 x 8192 words), then the last
+// K1c launch's per-workgroup trace (4 x 1024 words), after a device sync
+extern "C" __attribute__((visibility("default"))) int fb_flow_trace_last(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fbk::g_k2_trace), sizeof(fbk::g_k2_trace)) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out + 4u * fbk::kFlowTrParts, HIP_SYMBOL(fbk::g_k1c_trace),
+                               sizeof(fbk::g_k1c_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" uint64_t fb_flow_hash(const fb_session_key* key) {
     uint32_t w[10];

@@ -280,7 +280,14 @@ struct FlowParams {
                                 // K1c / K2 read instead of the records
     uint4* char_call = nullptr; // [capacity] per slot: the update call of the flow's first S, s, H, h
                                 // (FB_CALL_NONE: none), for the multi-GPU merge (fb_flow_merge_dev)
+    uint32_t* order = nullptr;  // [parts + kK2Lead + 1] K2's partition order: per partition its entries
+                                // (K1t's sums; bit 31: one of K2's leading workgroups takes it), the
+                                // leading partitions, their count (zeroed by K1)
 };
+// K2's leading workgroups: the partitions with more than twice the mean entries (skewed popularity
+// leaves flows K1c does not combine, up to ~18K entries in one partition under Zipf(1.1)), started
+// before the rest instead of in partition order
+constexpr uint32_t kK2Lead = 256;
 
 // determine_conn_state, src/packets.rs:539-559, over FB_HIST_CHARS bits.
 __host__ __device__ inline uint32_t conn_state_of(uint32_t m) {
