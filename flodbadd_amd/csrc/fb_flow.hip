@@ -49,10 +49,13 @@ namespace fbk {
 // -DFB_FLOW_TRACE (never the product): per K2 workgroup (partition, up to kFlowTrParts) the
 // real-time ticks of its start, the end of its entry loop and its end, its entries (low word) and
 // its busiest slot's history characters (high word); per K1c workgroup its start, its end, its
-// groups and its records (tools/experiments/flow_trace.py, fb_flow_trace_last)
+// groups, its records and the ticks its groups spent in each phase (group fetch, table init,
+// reduce, numbering, order bitmap, pack, combined entries) (tools/experiments/flow_trace.py,
+// fb_flow_trace_last)
 constexpr uint32_t kFlowTrParts = 8192u;
+constexpr uint32_t kK1cTrWords = 12u;  // start, end, groups, records, 7 phase totals, 0
 __device__ unsigned long long g_k2_trace[kFlowTrParts * 4u];
-__device__ unsigned long long g_k1c_trace[1024u * 4u];
+__device__ unsigned long long g_k1c_trace[1024u * kK1cTrWords];
 __device__ __forceinline__ unsigned long long flow_now() {
     unsigned long long t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -917,6 +920,10 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
 #ifdef FB_FLOW_TRACE
     const unsigned long long tr_t0 = flow_now();
     uint32_t tr_groups = 0u, tr_recs = 0u;
+    unsigned long long tr_ph[7] = {}, tr_prev = tr_t0;
+#define K1CPH(k) FLOWTR({ const unsigned long long t_ = flow_now(); tr_ph[k] += t_ - tr_prev; tr_prev = t_; })
+#else
+#define K1CPH(k) do { } while (0)
 #endif
     // Groups are taken one at a time (ctl[3]), not by a fixed stride: their sizes vary by 50x under
     // skew (48 .. ~2,500 records), and with the stride the busiest workgroup held 2.2x the mean's
@@ -936,6 +943,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
         uint32_t* rowp = P.rows + (size_t)chunk * P.parts + part;
         const uint32_t row = *rowp, cnt = row >> 16;
         FLOWTR(++tr_groups; tr_recs += cnt);
+        K1CPH(0);
         const size_t s0 = (size_t)chunk * kFlowChunk + (row & 0xFFFFu);
         for (uint32_t j = threadIdx.x; j < kCombBm; j += kCombThreads) L.bm[j] = 0ull;
         for (uint32_t j = threadIdx.x; j < kCombSlots; j += kCombThreads) {
@@ -947,6 +955,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
                 L.f[j * kCombF + w] = (w == kCfFirst || w == kCfEnd || (w >= kCfChar && w < kCfChar + 4)) ? ~0u : 0u;
         }
         __syncthreads();
+        K1CPH(1);
         // reduce per key (a key the table cannot take stays a plain entry), kCombU records per
         // thread at a time with their loads in flight together.  (Measured and not kept: four
         // records per thread, C4 Zipf(1.1) K1c 328 -> 415 us; a thread's consecutive records of
@@ -1004,6 +1013,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             }
         }
         __syncthreads();
+        K1CPH(2);
         // number the keys met more than once; one global atomic per group for their ids
         constexpr uint32_t kPer = kCombSlots / kCombThreads;
         uint32_t nc = 0u;
@@ -1024,6 +1034,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             L.pool_end = en;
         }
         __syncthreads();
+        K1CPH(3);
         const uint32_t id0 = L.base;
         if (id0 + n_comb > P.comb_cap) continue;  // no room for its combined entries: the group stays plain
 #pragma unroll
@@ -1048,6 +1059,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             }
         }
         __syncthreads();
+        K1CPH(4);
         // pack the remaining plain entries (record indices) to the front, tile by tile of kCombU
         // records per thread (a tile is loaded before any of its stores, and stores land below the
         // next tile); every record's original word and new position (combined id or moved entry)
@@ -1094,6 +1106,7 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             }
             cursor += kept;
         }
+        K1CPH(5);
         // the combined entries (two units each in P.comb) and their index words behind the kept ones
 #pragma unroll
         for (uint32_t u = 0; u < kPer; ++u) {
@@ -1121,13 +1134,17 @@ __global__ __launch_bounds__(kCombThreads) void k_flow_combine(const FlowParams 
             P.rows_h[(size_t)chunk * P.parts + part] = row;
         }
         __syncthreads();  // the table is re-initialised for the next group
+        K1CPH(6);
     }
+#undef K1CPH
     FLOWTR(if (threadIdx.x == 0 && blockIdx.x < 1024u) {
-        unsigned long long* t = g_k1c_trace + 4u * blockIdx.x;
+        unsigned long long* t = g_k1c_trace + kK1cTrWords * blockIdx.x;
         t[0] = tr_t0;
         t[1] = flow_now();
         t[2] = tr_groups;
         t[3] = tr_recs;
+        for (uint32_t k = 0; k < 7u; ++k) t[4 + k] = tr_ph[k];
+        t[11] = 0ull;
     });
 }
 
@@ -1531,7 +1548,7 @@ hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap, unsi
 
 #ifdef FB_FLOW_TRACE
 // diagnostic builds only: the last K2 launch's per-partition trace (4 x 8192 words), then the last
-// K1c launch's per-workgroup trace (4 x 1024 words), after a device sync
+// K1c launch's per-workgroup trace (12 x 1024 words), after a device sync
 extern "C" __attribute__((visibility("default"))) int fb_flow_trace_last(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fbk::g_k2_trace), sizeof(fbk::g_k2_trace)) != hipSuccess) return -1;

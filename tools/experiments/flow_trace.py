@@ -38,7 +38,7 @@ def q(x):
 for name, kw in (("uniform", None), ("zipf1.1", dict(zipf=1, zipf_s=1.1))):
     r = bench.run_config(N, lib, ctx, 4, n, 4, 2, 1, 0, 1, None, flow=True, mode="seg", synth_kw=kw,
                          stage_extras=False, records=False)
-    tr = np.zeros(4 * TR_PARTS + 4 * 1024, dtype=np.uint64)
+    tr = np.zeros(4 * TR_PARTS + 12 * 1024, dtype=np.uint64)
     assert f(tr.ctypes.data) == 0
     k2 = tr[:4 * TR_PARTS].reshape(TR_PARTS, 4)
     k2 = k2[k2[:, 0] > 0]
@@ -64,7 +64,7 @@ for name, kw in (("uniform", None), ("zipf1.1", dict(zipf=1, zipf_s=1.1))):
         return round(max(h), 1)
     sched = dict(sum_dur_us=round(float(dur.sum()), 1), work_per_slot_us=round(float(dur.sum()) / 512, 1),
                  model_partition_order_us=makespan(dur), model_longest_first_us=makespan(np.sort(dur)[::-1]))
-    k1c = tr[4 * TR_PARTS:].reshape(1024, 4)
+    k1c = tr[4 * TR_PARTS:].reshape(1024, 12)
     k1c = k1c[k1c[:, 0] > 0]
     out = dict(workload=name, step_ms=round(r["elapsed"] * 1e3 / 4, 3), flow_ms=round(r["stage"]["flow_ms"], 4),
                k2=dict(parts=int(len(k2)), span_us=round(float(end.max()), 1),
@@ -78,5 +78,8 @@ for name, kw in (("uniform", None), ("zipf1.1", dict(zipf=1, zipf_s=1.1))):
         out["k1c"] = dict(workgroups=int(len(k1c)), span_us=round(float(ce.max()), 1), end_us=q(ce),
                           start_spread_us=round(float((k1c[:, 0].max() - c0) / 100.0), 1),
                           groups=q(k1c[:, 2].astype(np.float64)), records=q(k1c[:, 3].astype(np.float64)),
-                          groups_total=int(k1c[:, 2].sum()), records_total=int(k1c[:, 3].sum()))
+                          groups_total=int(k1c[:, 2].sum()), records_total=int(k1c[:, 3].sum()),
+                          # mean us per workgroup in each phase of its groups
+                          phases_us={nm: round(float(k1c[:, 4 + i].mean()) / 100.0, 1) for i, nm in enumerate(
+                              ("fetch", "init", "reduce", "number", "bitmap", "pack", "combined"))})
     print(json.dumps(out), flush=True)
