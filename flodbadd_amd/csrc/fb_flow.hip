@@ -116,7 +116,10 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
 // A (chunk, partition) group of at least this many records (and 4x the chunk's mean) is combined
 // per key by k_flow_combine before K2.
 #ifndef FB_COMB_MIN
-#define FB_COMB_MIN 48
+#define FB_COMB_MIN 64  // (48 until K2 started its heavy partitions first; with that order, C4 Zipf(1.1)
+                        // pipelined 10,706 -> 10,924 and one stream 10,105 -> 10,317 at 64, while 96 /
+                        // 128 gained pipelined and lost one stream -- a partition whose flow stays plain
+                        // then takes ~390 us in K2; profiles/r05_k2_experiments.txt)
 #endif
 constexpr uint32_t kCombMin = FB_COMB_MIN;
 
