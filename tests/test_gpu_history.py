@@ -217,6 +217,48 @@ def test_history_split_list_overflow():
     assert len(gf) > 90_000 and (gf["hist_len"] > 20).any()
 
 
+def test_k2_heavy_partition_list_overflow():
+    """More heavy partitions than K2's leading list holds (kK2Lead = 256, fb_flow.hip K1t / K2): a
+    2^19-slot table has 1,024 partitions; 400 warm flows carry 10K records each of a 5M-record batch
+    (~41 per bucketing chunk, under k_flow_combine's minimum, so they stay plain entries) and 100K
+    cold flows the rest, so ~330 partitions pass twice the mean -- the first 256 go to K2's leading
+    workgroups, the others stay with the later ones.  A second, cold-only batch then has no heavy
+    partition (the list and its flags must be cleared per update).  Every flow row and history
+    equals the oracle's."""
+    rnd = np.random.default_rng(5)
+    n_warm, per_warm, n_cold, n = 400, 10_000, 100_000, 5_000_000
+    tmpl = []  # two 60-byte frames per flow: ACK, PSH | ACK
+    for i in range(n_warm + n_cold):
+        src = ("10.%d.%d.%d" if i < n_warm else "172.%d.%d.%d") % (16 + (i >> 16), (i >> 8) & 255, i & 255)
+        for fl in (fg.ACK, fg.ACK | fg.PSH):
+            tmpl.append(fg.tcp_frame(src, 1024 + i % 60000, "93.184.216.34", 443, fl, 6))
+    L = len(tmpl[0])
+    assert all(len(t) == L for t in tmpl)
+    T = np.frombuffer(b"".join(tmpl), dtype=np.uint8).reshape(-1, L)
+    del tmpl
+
+    def batch(ids):
+        sel = ids * 2 + rnd.integers(0, 2, len(ids))
+        return np.ascontiguousarray(T[sel]).reshape(-1), (np.arange(len(ids) + 1, dtype=np.uint64) * L).astype(np.uint32)
+
+    ids = np.concatenate([np.repeat(np.arange(n_warm), per_warm),
+                          rnd.integers(n_warm, n_warm + n_cold, n - n_warm * per_warm)])
+    rnd.shuffle(ids)
+    big = batch(ids)
+    cold = batch(rnd.integers(n_warm, n_warm + n_cold, 1_000_000))
+    # precondition (host-side hash): more partitions than the list holds pass K1t's threshold
+    lib = N.gpu_lib()
+    cfg = coracle.make_cfg(2)
+    keys = coracle.parse_classify(cfg, T[0::2].reshape(-1), (np.arange(len(T) // 2 + 1, dtype=np.uint64) * L).astype(np.uint32))[0]
+    part = np.array([lib.fb_flow_hash(N.ptr(keys[i: i + 1])) >> 54 for i in range(len(keys))])
+    per_part = np.bincount(part, weights=np.bincount(ids, minlength=len(keys)), minlength=1024)
+    lead_min = 2 * ((n + 20479) // 20480) * 20480 // 1024
+    assert (per_part >= lead_min).sum() > 256, (per_part >= lead_min).sum()
+    del keys, ids
+    gf = _run([big, cold], seg=True, capacity=1 << 19)
+    assert len(gf) == n_warm + n_cold
+
+
 def test_history_full_size_zipf():
     """The bench's skewed C4 batch at full size (10,485,760 IMIX frames, Zipf(1.1)) and a 1M
     follow-up: every flow's history string, conn_state and ordered fields equal the oracle's --
