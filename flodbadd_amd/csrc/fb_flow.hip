@@ -1484,7 +1484,12 @@ __global__ __launch_bounds__(256) void k_flow_count(const FlowSlot* T, unsigned 
     if (threadIdx.x == 0 && c) atomicAdd(d_n, c);
 }
 
-hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s) {
+hipError_t launch_flow_combine(const FlowParams& p, hipStream_t s) {
+    if (!p.hot) return hipSuccess;
+    hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s, bool combine) {
     if (chunks == 0u) chunks = 1u;
     static const hipError_t attr = hipFuncSetAttribute(
         (const void*)k_flow_bucket, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1493,11 +1498,7 @@ hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t 
     hipLaunchKernelGGL(k_flow_bucket, dim3(chunks), dim3(kFlowK1Threads), k1_lds_bytes(p.parts), s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (p.hot) {
-        hipLaunchKernelGGL(k_flow_combine, dim3(kCombGrid), dim3(kCombThreads), 0, s, p);
-        e = hipGetLastError();
-    }
-    return e;
+    return combine ? launch_flow_combine(p, s) : e;
 }
 hipError_t launch_flow_transpose(const FlowParams& p, uint32_t chunks, hipStream_t s) {
     if (chunks == 0u) chunks = 1u;

@@ -445,8 +445,9 @@ hipError_t launch_seg_compact(const fb_pkt_out* seg_out, const uint32_t* seg, ui
 // One table update = launch_flow_bucket (K1 bucketing, K1c hot-group combine), launch_flow_transpose
 // (K1t) and launch_flow_apply (K2; with transpose = true K1t first) -- separate calls so the
 // pipelined path can put them on different streams.
-hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s);
+hipError_t launch_flow_bucket(const FlowParams& p, uint32_t chunks, hipStream_t s, bool combine = true);
 hipError_t launch_flow_transpose(const FlowParams& p, uint32_t chunks, hipStream_t s);
+hipError_t launch_flow_combine(const FlowParams& p, hipStream_t s);
 hipError_t launch_flow_apply(const FlowParams& p, uint32_t chunks, hipStream_t s, bool transpose = true);
 // Table occupancy after an update, written by k_flow_finish into host-mapped memory so the host can
 // decide to grow the table without waiting for the device: seq = the update's number (+1).
