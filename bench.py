@@ -411,22 +411,47 @@ def host_inclusive(N, lib, ctx, frames, offs, calls=20):
                 note="synchronous fb_parse_classify on pinned host buffers (H2D + kernel + D2H, no overlap)")
 
 
-def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
+def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4, copy_threads=8):
     """The host ingest ring (fb_ring_*): pinned batches, H2D on a copy
     stream overlapping the previous batch's parse + session-table upsert, only the batch stats
     (and DNS side records) back -- the session table stays in HBM.  Two producers:
       copy:     fb_ring_push_block from ordinary (pageable) memory, one host thread (the memcpy
                 into the pinned batch is the capture thread's copy, like the reference's to_vec);
+      copy_mt:  the same with the block's copy split over `copy_threads` threads
+                (fb_ring_config.copy_threads);
+      per_frame: fb_ring_push once per frame from a native loop (the reference's reader thread hands
+                over one frame per next_packet(), src/capture.rs:1088-1092);
       in_place: fb_ring_reserve_block with the frames already in the pinned batch (a capture
                 engine writing into the ring; the offsets are still written per batch).
     Reported in DESIGN.md; never the headline value."""
     n = len(offs) - 1
-    cfg = N.FbRingConfig(slots, n, frames.nbytes, 0, 0)
+    out = {}
+    for name, threads in (("copy", 1), ("copy_mt", copy_threads)):
+        if name == "copy_mt":
+            out.update(_host_ring_runs(N, lib, ctx, frames, offs, batches, slots, threads, ("copy",),
+                                       rename={"copy": "copy_mt"}))
+            out["copy_mt"]["threads"] = threads
+        else:
+            out.update(_host_ring_runs(N, lib, ctx, frames, offs, batches, slots, threads,
+                                       ("copy", "per_frame", "in_place")))
+    return dict(unit="Mpackets/s", slots=slots, batch_frames=n, **out,
+                note="fb_ring: pinned %d-batch ring, H2D (copy stream) + parse + session-table upsert "
+                     "(compute stream) + stats D2H per batch, table kept in HBM" % slots)
+
+
+def _host_ring_runs(N, lib, ctx, frames, offs, batches, slots, threads, modes, rename=None):
+    n = len(offs) - 1
+    cfg = N.FbRingConfig(slots, n, frames.nbytes, 0, threads)
     r = lib.fb_ring_create(ctx, C.byref(cfg))
     if not r:
         raise RuntimeError(lib.fb_last_error().decode())
     r = C.c_void_p(r)
     out = {}
+    hb = C.CDLL(os.path.join(N.PKG, "libfb_hostbench.so"))
+    hb.fb_hostbench_push_frames.restype = C.c_int
+    hb.fb_hostbench_push_frames.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                            C.POINTER(C.c_double)]
+    push_fn = C.cast(lib.fb_ring_push, C.c_void_p)
     try:
         N.check(lib.fb_flow_clear(ctx, None))
         rel = np.ascontiguousarray(offs[:-1], dtype=np.uint32)
@@ -444,17 +469,32 @@ def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
             o = np.ctypeslib.as_array((C.c_uint32 * n).from_address(po.value))
             np.add(rel, np.uint32(base.value), out=o)
 
-        for name, fn in (("copy", lambda i: copy_batch()), ("in_place", lambda i: in_place_batch(i < slots))):
-            for i in range(slots):  # warm-up: fill every slot once
-                fn(i)
-            N.check(lib.fb_ring_sync(r))
-            t0 = time.perf_counter()
-            for i in range(batches):
-                fn(slots + i)
-            N.check(lib.fb_ring_sync(r))
-            el = time.perf_counter() - t0
-            out[name] = dict(value=round(batches * n / el / 1e6, 2), ms_per_batch=round(el * 1e3 / batches, 3),
-                             pcie_GBs=round(batches * (frames.nbytes + offs.nbytes) / el / 1e9, 2))
+        def per_frame_batches(k):
+            sec = C.c_double()
+            N.check(hb.fb_hostbench_push_frames(push_fn, r, N.ptr(frames), N.ptr(offs), n, k, C.byref(sec)))
+
+        fns = {"copy": lambda i: copy_batch(), "in_place": lambda i: in_place_batch(i < slots)}
+        for name in modes:
+            if name == "per_frame":  # one native call per frame, `batches` batches' worth
+                per_frame_batches(slots)  # warm-up
+                N.check(lib.fb_ring_sync(r))
+                t0 = time.perf_counter()
+                per_frame_batches(batches)
+                N.check(lib.fb_ring_sync(r))
+                el = time.perf_counter() - t0
+            else:
+                fn = fns[name]
+                for i in range(slots):  # warm-up: fill every slot once
+                    fn(i)
+                N.check(lib.fb_ring_sync(r))
+                t0 = time.perf_counter()
+                for i in range(batches):
+                    fn(slots + i)
+                N.check(lib.fb_ring_sync(r))
+                el = time.perf_counter() - t0
+            out[(rename or {}).get(name, name)] = dict(
+                value=round(batches * n / el / 1e6, 2), ms_per_batch=round(el * 1e3 / batches, 3),
+                pcie_GBs=round(batches * (frames.nbytes + offs.nbytes) / el / 1e9, 2))
         tot = np.zeros(1, dtype=N.STATS_DTYPE)
         nb = C.c_uint64()
         N.check(lib.fb_ring_stats(r, N.ptr(tot), C.byref(nb), None))
@@ -464,9 +504,29 @@ def host_ring(N, lib, ctx, frames, offs, batches=16, slots=4):
     finally:
         lib.fb_ring_destroy(r)
         lib.fb_flow_clear(ctx, None)
-    return dict(unit="Mpackets/s", slots=slots, batch_frames=n, **out,
-                note="fb_ring: pinned %d-batch ring, H2D (copy stream) + parse + session-table upsert "
-                     "(compute stream) + stats D2H per batch, table kept in HBM" % slots)
+    return out
+
+
+def c5_conservation(merged, records, local_flows, global_flows, unique_keys):
+    """Invariants of the merged global session table (C5), whatever the exchange did: every SESSION
+    record the ranks' parses emitted is counted exactly once -- the table's packets (orig + resp),
+    payload bytes (outbound + inbound) and IP bytes (orig_ip + resp_ip) equal the sums over every
+    rank's records --, the global flows lie between the largest rank table and the sum of all of
+    them, and no key appears twice.  `merged` / `records`: dicts of packets, payload_bytes, ip_bytes.
+    Raises RuntimeError naming every violated invariant; returns the checked values."""
+    bad = []
+    for k in ("packets", "payload_bytes", "ip_bytes"):
+        if int(merged[k]) != int(records[k]):
+            bad.append("%s: table %d != records %d" % (k, int(merged[k]), int(records[k])))
+    if not (max(local_flows) <= global_flows <= sum(local_flows)):
+        bad.append("global flows %d outside [max %d, sum %d] of the rank tables"
+                   % (global_flows, max(local_flows), sum(local_flows)))
+    if unique_keys != global_flows:
+        bad.append("%d distinct keys in %d merged records" % (unique_keys, global_flows))
+    if bad:
+        raise RuntimeError("C5 conservation violated: " + "; ".join(bad))
+    return dict(packets=int(merged["packets"]), payload_bytes=int(merged["payload_bytes"]),
+                ip_bytes=int(merged["ip_bytes"]), local_flows=[int(x) for x in local_flows], unique_keys=unique_keys)
 
 
 def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
@@ -494,6 +554,12 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     flow_ms = ev0.elapsed_ms(ev1)
     cnt = C.c_uint64()
     N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
+    # what this rank's parse emitted (the records the table must account for, exactly once)
+    st = d_st.download(np.zeros(1, dtype=N.STATS_DTYPE))
+    ns = int(st[0]["n_session"])
+    recs = d_out.download(np.zeros(max(ns, 1), dtype=N.PKT_OUT_DTYPE))[:ns]
+    rec_sums = [ns, int(recs["packet_length"].sum(dtype=np.uint64)), int(recs["ip_packet_length"].sum(dtype=np.uint64))]
+    del recs
 
     def export_merge(timing=None):
         # the library exports the owner groups into a device tensor, the collectives move them
@@ -518,13 +584,30 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     export_merge(stages)
     for b in (d_fr, d_off, d_out, d_st):
         b.free()
+    import torch
     t = np.array([flow_ms], dtype=np.float64)
     if world > 1:  # the slowest rank's update: the aggregate rate of the concurrent shards
-        import torch
         tt = torch.tensor(t, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
         t = tt.cpu().numpy()
+    # conservation of the merged table against every rank's records (a violation fails the run)
+    rs = torch.tensor(rec_sums, dtype=torch.int64, device=device)
+    lf = torch.tensor([local], dtype=torch.int64, device=device)
+    lfs = [torch.zeros_like(lf) for _ in range(world)]
+    if world > 1:
+        dist.all_reduce(rs, group=group)
+        dist.all_gather(lfs, lf, group=group)
+    else:
+        lfs = [lf]
+    cols = merged[:, 5:11].sum(dim=0).tolist() if len(merged) else [0] * 6  # fb_flow_rec counters
+    uniq = int(torch.unique(merged[:, :5], dim=0).shape[0]) if len(merged) else 0
+    rs = rs.tolist()
+    conserved = c5_conservation(
+        dict(packets=cols[2] + cols[3], payload_bytes=cols[0] + cols[1], ip_bytes=cols[4] + cols[5]),
+        dict(packets=rs[0], payload_bytes=rs[1], ip_bytes=rs[2]),
+        [int(x.item()) for x in lfs], int(len(merged)), uniq)
     return dict(ranks_in_group=dist.get_world_size(group), frames_per_rank=n, total_frames=n * world,
+                conservation=conserved,
                 local_flows=local, global_flows=int(len(merged)),
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),
@@ -734,6 +817,19 @@ def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
                              ms_per_step=round(rr["elapsed"] * 1e3 / steps, 4),
                              note="the same pipelined calls also storing every SESSION record (fb_pkt_out) in d_out")
     out.update(c4_split(N, lib, ctx, r, n, steps, warmup, rank, world, dist, "seg", True, records=False))
+    # C4 also with Zipf(1.1) flow popularity -- the same pipelined table-only calls
+    rz = run_config(N, lib, ctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg", pipelined=True,
+                    records=False, synth_kw=dict(zipf=1, zipf_s=1.1), stage_extras=False)
+    out["c4_zipf"] = dict(value=round(world * n * steps / rz["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                          ms_per_step=round(rz["elapsed"] * 1e3 / steps, 4), steps=steps,
+                          note="Zipf(1.1) flow popularity over the 2^20 pool, otherwise as the C4 line")
+    # the batch a capture loop flushing every ~1 ms hands over: 1,048,576 frames per fused call
+    m, s1 = 1 << 20, max(steps * 5, 100)
+    r1 = run_config(N, lib, ctx, 4, m, s1, warmup * 2, 2, rank, world, dist, flow=True, mode="seg", pipelined=True,
+                    records=False, stage_extras=False)
+    out["c4_1m"] = dict(value=round(world * m * s1 / r1["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                        ms_per_call=round(r1["elapsed"] * 1e3 / s1, 4), steps=s1, frames_per_call=m,
+                        note="the C4 mix in 1M-frame fb_process_seg_async_dev calls (table-only, pipelined)")
     if rank == 0 and world == 1 and cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline_c4(r["frames"], r["offs"], cpu_seconds)
     return out
@@ -834,12 +930,16 @@ def world_check(args, world, rank):
     c5_ok = True
     if world > 1:
         # the C5 outcome plumbing with a stand-in exchange (FB_C5_INJECT=fail: rank 1 raises;
-        # =group: the group reports fewer ranks than --gpus)
+        # =group: the group reports fewer ranks than --gpus; =conservation: every rank's merged
+        # table fails c5_conservation)
         inject = os.environ.get("FB_C5_INJECT", "")
 
         def run():
             if inject == "fail" and rank == 1:
                 raise RuntimeError("injected C5 merge failure")
+            if inject == "conservation":  # a merged table that lost one packet's bytes
+                sums = dict(packets=1000, payload_bytes=64000, ip_bytes=104000)
+                c5_conservation(dict(sums, payload_bytes=63990), sums, [600, 500], 900, 900)
             return {"ranks_in_group": world - 1 if inject == "group" else tdist.get_world_size()}
         res, c5_ok = c5_checked(run, world, args.gpus, tdist)
         line["extra"] = {"c5_flow_reduce": res}
@@ -1050,7 +1150,7 @@ def main():
     lib.fb_destroy(ctx)
     if bpl > 1:
         output_desc = ("per-64-frame wavefront-compacted segments (fb_parse_classify_seg_batches_dev: "
-                       "%d batches per launch, each with its own outputs and stats)" % bpl)
+                       "up to %d batches per launch, each with its own outputs and stats)" % bpl)
     elif args.mode == "seg" and args.config == 4:
         output_desc = ("per-64-frame wavefront-compacted segments + session-table upsert " +
                        ("(fb_process_seg_async_dev: each batch's update overlaps the next batch's parse, "
@@ -1076,7 +1176,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (deterministic splitmix64 frames, SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.config] + (" (Zipf(%g) flow popularity)" % args.zipf if args.zipf else ""), "frames_per_gpu_per_step": n,
-                       "rotated_batches": rotate, "batches_per_launch": bpl, "filter": "GlobalOnly",
+                       "rotated_batches": rotate,
+                       "batches_per_launch": round(args.steps / main_r["launches"], 2),
+                       "batches_per_launch_max": bpl, "filter": "GlobalOnly",
                        "output": output_desc,
                        "parallelism": "packet-index shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

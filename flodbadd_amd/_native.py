@@ -134,7 +134,7 @@ class FlowTableInfo(C.Structure):
 
 class FbRingConfig(C.Structure):
     _fields_ = [("slots", C.c_uint32), ("max_packets", C.c_uint32), ("max_bytes", C.c_uint64),
-                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+                ("flags", C.c_uint32), ("copy_threads", C.c_uint32)]
 
 
 FB_RING_NO_FLOW = 1
@@ -156,6 +156,8 @@ class FbError(RuntimeError):
 # Every symbol include/flodbadd_gpu.h declares: (name, restype, argtypes).
 _P, _U32, _U64, _I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
 _PU32, _PU64 = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+FB_DEBUG_DENSE_STEAL_POLLS, FB_DEBUG_DENSE_OFFSET_SKEW = 1, 2
+
 GPU_SYMBOLS = [
     ("fb_abi_version", _U32, []),
     ("fb_last_error", C.c_char_p, []),
@@ -197,6 +199,7 @@ GPU_SYMBOLS = [
     ("fb_flow_slot_remap", _I, [_P, _P, _U64, _PU64]),
     ("fb_flow_hash", _U64, [_P]),
     ("fb_flow_export_merge_dev", _I, [_P, _U32, _U32, _U64, _P, _U64, _P, _P]),
+    ("fb_flow_export_merge_map_dev", _I, [_P, _U32, _U32, _P, _U32, _P, _U64, _P, _P]),
     ("fb_flow_merge_dev", _I, [_P, _P, _U64, _P, _P, _P]),
     ("fb_flow_owner", _U32, [_P, _U32]),
     ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),
@@ -233,6 +236,8 @@ GPU_SYMBOLS = [
     ("fb_seg_queue_query", _I, [_P, _U64]),
     ("fb_seg_queue_wait", _I, [_P, _U64]),
     ("fb_seg_queue_destroy", _I, [_P]),
+    ("fb_seg_queue_set_limit", _I, [_P, _U64]),
+    ("fb_debug_set", _I, [_P, _U32, _U64]),
 ]
 
 _gpu = None

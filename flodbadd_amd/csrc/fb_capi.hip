@@ -74,13 +74,13 @@ struct fb_ctx {
     uint32_t scan_epoch = 0;                  // epoch of the last scan (0: status needs zeroing)
     uint64_t cseg_cap = 0;                    // segments
     // single-pass dense output (k_parse_dense): per-tile look-back words, epoch, grid, and the
-    // look-back's polls before it computes a late predecessor's sums itself (FB_DENSE_STEAL_POLLS
-    // at fb_create; tests set 0 to force that path)
+    // look-back's polls before it computes a late predecessor's sums itself (fb_debug_set
+    // FB_DEBUG_DENSE_STEAL_POLLS; tests set 0 to force that path)
     unsigned long long* d_dstatus = nullptr;  // [cseg_cap / parse_dense_tile_segs() + 1]
     uint32_t dense_epoch = 0;                 // epoch of the last launch (0: status needs zeroing)
     uint32_t dense_grid = 0;
     uint32_t steal_polls = 1u << 12;
-    unsigned long long dn_skew = 0ull;  // FB_DENSE_OFFSET_SKEW: fault injection (k_parse_dense copy bounds)
+    unsigned long long dn_skew = 0ull;  // FB_DEBUG_DENSE_OFFSET_SKEW: fault injection (k_parse_dense copy bounds)
     hipEvent_t stage_event = nullptr;  // fb_set_stage_event (caller-owned): recorded between the
                                        // parse and the update of fb_process[_seg]_dev
     // flow table
@@ -451,9 +451,6 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
         int db = 0;
         if (occupancy_parse_dense(&db) != hipSuccess || db < 1) db = 1;
         c->dense_grid = std::min<uint32_t>((uint32_t)(db * prop.multiProcessorCount), 1023u);  // 10-bit stats tickets
-        if (const char* e = getenv("FB_DENSE_STEAL_POLLS")) c->steal_polls = (uint32_t)strtoul(e, nullptr, 10);
-        // fault injection (tests/test_gpu_dense.py): a skew added to every dense tile offset
-        if (const char* e = getenv("FB_DENSE_OFFSET_SKEW")) c->dn_skew = strtoull(e, nullptr, 10);
     }
     c->h_cfg = new (std::nothrow) DevConfig();
     bool ok = c->h_cfg != nullptr;
@@ -583,6 +580,23 @@ int fb_set_stage_event(fb_ctx* c, void* event) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     c->stage_event = (hipEvent_t)event;  // the caller's event (fb_event_create); not owned
     return FB_OK;
+}
+
+int fb_debug_set(fb_ctx* c, uint32_t knob, uint64_t value) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    switch (knob) {
+        case FB_DEBUG_DENSE_STEAL_POLLS:
+            c->steal_polls = (uint32_t)std::min<uint64_t>(value, 0xFFFFFFFFull);
+            return FB_OK;
+        case FB_DEBUG_DENSE_OFFSET_SKEW:
+            if (value > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "skew %llu >= 2^32", (unsigned long long)value);
+            c->dn_skew = value;
+            if (value) fprintf(stderr, "flodbadd_gpu: FB_DEBUG_DENSE_OFFSET_SKEW %llu active on this context (fault injection)\n",
+                               (unsigned long long)value);
+            return FB_OK;
+        default:
+            return set_err(FB_ERR_INVAL, "unknown debug knob %u", knob);
+    }
 }
 
 int fb_set_session_records(fb_ctx* c, int emit) {
@@ -738,6 +752,7 @@ struct fb_seg_queue {
     uint32_t* d_err = nullptr;
     unsigned long long* d_trace = nullptr;  // -DFB_QUEUE_TRACE builds
     uint64_t submitted = 0;
+    uint64_t limit = FB_QUEUE_MAX_SUBMISSIONS;  // the kernel's batch numbers are 32-bit (k_parse_seg_queue)
     bool launched = false;
     hipError_t gone = hipSuccess;  // what the stream reported when the kernel was found gone
     uint32_t grid = 0;             // the kernel's blocks (all must be resident at once)
@@ -910,6 +925,12 @@ int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* x, uint64_t* ticket
     if (!x->d_offsets || (x->n && (!x->d_out || !x->d_seg))) return set_err(FB_ERR_INVAL, "d_offsets, d_out and d_seg are required");
     if (x->n && x->frames_bytes && !x->d_frames) return set_err(FB_ERR_INVAL, "d_frames is NULL");
     const uint64_t k = q->submitted, S = q->slots;
+    // the kernel carries batch numbers, ring claims and completion words in 32 bits: past 2^32 a
+    // claim's expected value and a slot's completion word would repeat an old batch's, so a queue
+    // takes at most `limit` batches and is then recycled by the host
+    if (k >= q->limit)
+        return set_err(FB_ERR_INVAL, "the queue took its %llu batches (32-bit batch numbers): destroy it and create a "
+                       "new one", (unsigned long long)q->limit);
     // at most `depth` batches in flight, and a slot is reused only once its previous batch (k - S) is
     // complete -- its completion word is stored after the kernel has reset the slot's state
     const uint64_t back[2] = {q->depth, S};
@@ -927,6 +948,15 @@ int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* x, uint64_t* ticket
     __atomic_store_n(&h->tail, (unsigned long long)(k + 1u), __ATOMIC_RELEASE);  // after the descriptor
     q->submitted = k + 1u;
     if (ticket) *ticket = k;
+    return FB_OK;
+}
+
+int fb_seg_queue_set_limit(fb_seg_queue* q, uint64_t limit) {
+    if (!q) return set_err(FB_ERR_INVAL, "queue is NULL");
+    if (limit > FB_QUEUE_MAX_SUBMISSIONS || limit < q->submitted)
+        return set_err(FB_ERR_INVAL, "limit %llu outside [%llu, FB_QUEUE_MAX_SUBMISSIONS]", (unsigned long long)limit,
+                       (unsigned long long)q->submitted);
+    q->limit = limit;
     return FB_OK;
 }
 
@@ -1724,20 +1754,56 @@ static int ensure_mscratch(fb_ctx* c, uint64_t bytes, hipStream_t s) {
     return FB_OK;
 }
 
-int fb_flow_export_merge_dev(fb_ctx* c, uint32_t world, uint32_t rank, uint64_t shard_first, fb_flow_mrec* d_out,
-                             uint64_t cap, uint64_t* d_counts, void* stream) {
+static int export_merge(fb_ctx* c, uint32_t world, uint32_t rank, uint64_t shard_first, const uint64_t* call_map,
+                        uint32_t n_calls, fb_flow_mrec* d_out, uint64_t cap, uint64_t* d_counts, void* stream) {
     if (!c || !d_counts || (cap && !d_out)) return set_err(FB_ERR_INVAL, "ctx, d_counts and d_out are required");
     if (world == 0 || world > 64 || rank >= world) return set_err(FB_ERR_INVAL, "1 <= world <= 64, rank < world");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
+    if (call_map) {  // every position the table holds names a call below flow_batch
+        if (n_calls < c->flow_batch)
+            return set_err(FB_ERR_INVAL, "call map has %u entries, the table holds %u update calls", n_calls,
+                           c->flow_batch);
+        for (uint32_t k = 0; k < c->flow_batch; ++k) {
+            const uint64_t gb = call_map[k] >> 32, first = call_map[k] & 0xFFFFFFFFull;
+            if (gb >= 0xFFFFFFFFull || (k && gb <= (call_map[k - 1] >> 32)))
+                return set_err(FB_ERR_INVAL, "call map: global batches must increase with the calls (call %u)", k);
+            if (first + FB_MAX_BATCH_PACKETS > 0xFFFFFFFFull)
+                return set_err(FB_ERR_INVAL, "call map: call %u's shard starts past 2^32 - FB_MAX_BATCH_PACKETS", k);
+        }
+    }
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
+    const uint64_t cnt_bytes = merge_export_scratch_bytes(c->table_cap, world);
     int rc = join_updates(c, s);
-    if (!rc) rc = ensure_mscratch(c, merge_export_scratch_bytes(c->table_cap, world), s);
+    if (!rc) rc = ensure_mscratch(c, cnt_bytes + (call_map ? 8ull * std::max<uint32_t>(c->flow_batch, 1u) : 0ull), s);
     if (rc) return rc;
-    HIP_TRY(launch_merge_export(c->d_table, c->d_char_call, c->table_cap, world, rank, shard_first, d_out, cap,
-                                (unsigned long long*)d_counts, c->d_mscratch, s));
+    unsigned long long* d_map = nullptr;
+    if (call_map && c->flow_batch) {
+        d_map = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->d_mscratch) + cnt_bytes);
+        HIP_TRY(hipMemcpyAsync(d_map, call_map, 8ull * c->flow_batch, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(launch_merge_export(c->d_table, c->d_char_call, c->table_cap, world, rank, shard_first,
+                                call_map ? d_map : nullptr, d_out, cap, (unsigned long long*)d_counts,
+                                c->d_mscratch, s));
     HIP_TRY(hipEventRecord(c->ev_mscratch, s));
     return FB_OK;
+}
+
+int fb_flow_export_merge_dev(fb_ctx* c, uint32_t world, uint32_t rank, uint64_t shard_first, fb_flow_mrec* d_out,
+                             uint64_t cap, uint64_t* d_counts, void* stream) {
+    if (shard_first + FB_MAX_BATCH_PACKETS > 0xFFFFFFFFull)
+        return set_err(FB_ERR_INVAL, "shard_first past 2^32 - FB_MAX_BATCH_PACKETS");
+    return export_merge(c, world, rank, shard_first, nullptr, 0u, d_out, cap, d_counts, stream);
+}
+
+int fb_flow_export_merge_map_dev(fb_ctx* c, uint32_t world, uint32_t rank, const uint64_t* call_map, uint32_t n_calls,
+                                 fb_flow_mrec* d_out, uint64_t cap, uint64_t* d_counts, void* stream) {
+    if (!call_map && n_calls) return set_err(FB_ERR_INVAL, "call_map is NULL");
+    if (!call_map) {  // (a table that took no update call holds no flow)
+        static const uint64_t none = 0ull;
+        call_map = &none;
+    }
+    return export_merge(c, world, rank, 0ull, call_map, n_calls, d_out, cap, d_counts, stream);
 }
 
 int fb_flow_merge_dev(fb_ctx* c, const fb_flow_mrec* d_in, uint64_t n, fb_flow_rec* d_out, uint64_t* d_n,

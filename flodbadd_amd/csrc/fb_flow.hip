@@ -1216,8 +1216,10 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
 #define FB_K2_PREFETCH 1
 #endif
     const bool dense = FB_K2_PREFETCH && n >= 32u * P.parts;
+    // (uniform) a leading workgroup's partition: leave before its 64-KB slice is loaded a second
+    // time (the order word was issued before the group rows, so this waits for it alone)
+    if (led >> 31) return;
     if (dense) load_slice();
-    if (led >> 31) return;  // (uniform) a leading workgroup's partition
     const unsigned long long total = block_sum(mine, sh);
     unsigned long long n_new = 0ull, n_upd = 0ull;
     uint32_t hbase_out = 0u, hc = 0u;

@@ -477,9 +477,12 @@ hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
 // (flow_owner), slot order inside each group, positions made global (+ shard_first), rec.slot = rank;
 // d_counts[world] (u64) receives the group sizes.  scratch: merge_export_scratch_bytes(cap, world).
 uint64_t merge_export_scratch_bytes(unsigned long long cap, uint32_t world);
+// cmap (device, optional): per update call of this rank, global batch << 32 | the global index of its
+// shard's first packet (fb_flow_export_merge_map_dev); null: call k = global batch k at shard_first.
 hipError_t launch_merge_export(const FlowSlot* table, const uint4* char_call, unsigned long long cap, uint32_t world,
-                               uint32_t rank, unsigned long long shard_first, fb_flow_mrec* out,
-                               unsigned long long out_cap, unsigned long long* d_counts, void* scratch, hipStream_t s);
+                               uint32_t rank, unsigned long long shard_first, const unsigned long long* cmap,
+                               fb_flow_mrec* out, unsigned long long out_cap, unsigned long long* d_counts,
+                               void* scratch, hipStream_t s);
 // Merge: n records of one owner (every rank's group, rank order) -> one record per key in d_out (in
 // the order of each key's first record), *d_n (u64) = keys.  scratch: merge_scratch_bytes(n).
 uint64_t merge_scratch_bytes(unsigned long long n);

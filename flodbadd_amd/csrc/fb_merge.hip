@@ -105,9 +105,20 @@ __global__ __launch_bounds__(1024) void k_mx_scan(uint32_t* cnt, uint32_t chunks
     }
 }
 
+// A table position (update call << 32 | pkt_index) made global: with a call map, call k of this rank
+// was its shard of global batch cmap[k] >> 32 starting at global packet cmap[k] & 0xFFFFFFFF; without
+// one, call k is global batch k with the shard at shard_first in each.
+__device__ __forceinline__ unsigned long long global_pos(unsigned long long p, unsigned long long shard_first,
+                                                         const unsigned long long* cmap) {
+    const unsigned long long lo = 0xFFFFFFFFull;
+    const unsigned long long m = cmap ? cmap[p >> 32] : ((p & ~lo) | shard_first);
+    return (m & ~lo) | ((m & lo) + (p & lo));
+}
+
 __global__ __launch_bounds__(64) void k_mx_write(const FlowSlot* T, const uint4* cc, unsigned long long cap,
                                                  uint32_t world, uint32_t rank, unsigned long long shard_first,
-                                                 const uint32_t* off, fb_flow_mrec* out, unsigned long long out_cap) {
+                                                 const unsigned long long* cmap, const uint32_t* off,
+                                                 fb_flow_mrec* out, unsigned long long out_cap) {
     const uint32_t lane = threadIdx.x;
     const unsigned long long c0 = (unsigned long long)blockIdx.x * kMxChunk;
     uint32_t next = lane < world ? off[(size_t)blockIdx.x * world + lane] : 0u;  // lane o: owner o's cursor
@@ -126,17 +137,16 @@ __global__ __launch_bounds__(64) void k_mx_write(const FlowSlot* T, const uint4*
         if (occ && pos < out_cap) {
             fb_flow_mrec r;
             r.rec = flow_rec_of(T[i], rank);
-            // positions (call << 32 | pkt_index) -> global packet index; end None stays None
-            const unsigned long long lo = 0xFFFFFFFFull;
-            r.rec.first_seen = (r.rec.first_seen & ~lo) | ((r.rec.first_seen & lo) + shard_first);
-            r.rec.last_seen = (r.rec.last_seen & ~lo) | ((r.rec.last_seen & lo) + shard_first);
-            if (r.rec.end_seen != FB_SEEN_NONE)
-                r.rec.end_seen = (r.rec.end_seen & ~lo) | ((r.rec.end_seen & lo) + shard_first);
+            // positions (call << 32 | pkt_index) -> (global batch << 32 | global packet index); end
+            // None stays None; the calls of the first S s H h -> their global batches
+            r.rec.first_seen = global_pos(r.rec.first_seen, shard_first, cmap);
+            r.rec.last_seen = global_pos(r.rec.last_seen, shard_first, cmap);
+            if (r.rec.end_seen != FB_SEEN_NONE) r.rec.end_seen = global_pos(r.rec.end_seen, shard_first, cmap);
             const uint4 c = cc ? cc[i] : make_uint4(FB_CALL_NONE, FB_CALL_NONE, FB_CALL_NONE, FB_CALL_NONE);
-            r.char_call[0] = c.x;
-            r.char_call[1] = c.y;
-            r.char_call[2] = c.z;
-            r.char_call[3] = c.w;
+            const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                r.char_call[b] = (cw[b] == FB_CALL_NONE || !cmap) ? cw[b] : (uint32_t)(cmap[cw[b]] >> 32);
             out[pos] = r;
         }
     }
@@ -144,19 +154,20 @@ __global__ __launch_bounds__(64) void k_mx_write(const FlowSlot* T, const uint4*
 
 uint64_t merge_export_scratch_bytes(unsigned long long cap, uint32_t world) {
     const unsigned long long chunks = (cap + kMxChunk - 1) / kMxChunk;
-    return chunks * world * 4ull;
+    return (chunks * world * 4ull + 255ull) & ~255ull;
 }
 
 hipError_t launch_merge_export(const FlowSlot* table, const uint4* char_call, unsigned long long cap, uint32_t world,
-                               uint32_t rank, unsigned long long shard_first, fb_flow_mrec* out,
-                               unsigned long long out_cap, unsigned long long* d_counts, void* scratch, hipStream_t s) {
+                               uint32_t rank, unsigned long long shard_first, const unsigned long long* cmap,
+                               fb_flow_mrec* out, unsigned long long out_cap, unsigned long long* d_counts,
+                               void* scratch, hipStream_t s) {
     if (world == 0u || world > kMxMaxWorld) return hipErrorInvalidValue;
     const uint32_t chunks = (uint32_t)((cap + kMxChunk - 1) / kMxChunk);
     uint32_t* cnt = static_cast<uint32_t*>(scratch);
     hipLaunchKernelGGL(k_mx_count, dim3(chunks), dim3(64), 0, s, table, cap, world, cnt);
     hipLaunchKernelGGL(k_mx_scan, dim3(1), dim3(1024), 0, s, cnt, chunks, world, d_counts);
-    hipLaunchKernelGGL(k_mx_write, dim3(chunks), dim3(64), 0, s, table, char_call, cap, world, rank, shard_first, cnt,
-                       out, out_cap);
+    hipLaunchKernelGGL(k_mx_write, dim3(chunks), dim3(64), 0, s, table, char_call, cap, world, rank, shard_first, cmap,
+                       cnt, out, out_cap);
     return hipGetLastError();
 }
 

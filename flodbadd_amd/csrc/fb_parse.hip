@@ -1066,7 +1066,8 @@ __global__ __launch_bounds__(kDnThreads, (FB_DN_BPC * kDnThreads + 255) / 256) v
             // may put the base store after the flag, and a parse wave copied to a stale offset)
             DNTR(if (lane == 0u && t < kDnTrTiles) P.dtrace[4u * t + 1u] = dn_now());
             if (lane == 0u) {
-                L.base[p] = excl + P.dn_skew;
+                // (a fault-injection skew moves the session half only, wrapping inside it)
+                L.base[p] = P.dn_skew ? ((excl & ~0xFFFFFFFFull) | ((excl + P.dn_skew) & 0xFFFFFFFFull)) : excl;
                 __hip_atomic_store(&L.ready_round[p], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }

@@ -127,12 +127,22 @@ def exchange_merge(dist, mrecs, counts, merge, device=None, group=None, timing=N
     return out
 
 
-def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tensor=False, stream=None, timing=None):
+def call_map_entry(global_batch, shard_first):
+    """One entry of an export call map: this rank's update call was its shard of `global_batch`,
+    starting at global packet index `shard_first` of that batch."""
+    return (int(global_batch) << 32) | int(shard_first)
+
+
+def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tensor=False, stream=None, timing=None,
+                      call_map=None):
     """The global session table of every rank's context `ctx` (an fb_ctx handle) on the GPU: the
     library exports the owner groups into a device tensor, RCCL moves them (`device` a cuda device
     and `group` an nccl group; gloo with CPU tensors works too, the records then go through host
     memory), the library merges each owner's records.  `shard_first`: the global index of this
-    rank's first packet (shard_range).  Returns FLOW_REC_DTYPE records in owner order, or with
+    rank's first packet (shard_range) when call k of every rank was its shard of equal-size global
+    batch k; `call_map` (a sequence of call_map_entry per update call of this rank) for any other
+    layout -- unequal per-call batches, a short tail batch, no call for an empty shard
+    (fb_flow_export_merge_map_dev).  Returns FLOW_REC_DTYPE records in owner order, or with
     as_tensor=True the [G, REC_WORDS] int64 tensor on `device` (no download).
 
     The library's kernels run on `stream` (None: the null stream); torch's copies and reads run on
@@ -162,8 +172,14 @@ def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tens
     mrecs = torch.empty((max(cnt.value, 1), MREC_WORDS), dtype=torch.int64, device=gpu)
     counts = torch.zeros(world, dtype=torch.int64, device=gpu)
     torch.cuda.current_stream(gpu).synchronize()  # the buffers' allocation / zeroing before the export
-    N.check(lib.fb_flow_export_merge_dev(ctx, world, rank, int(shard_first), C.c_void_p(mrecs.data_ptr()), cnt.value,
-                                         C.c_void_p(counts.data_ptr()), stream))
+    if call_map is None:
+        N.check(lib.fb_flow_export_merge_dev(ctx, world, rank, int(shard_first), C.c_void_p(mrecs.data_ptr()),
+                                             cnt.value, C.c_void_p(counts.data_ptr()), stream))
+    else:
+        cm = np.ascontiguousarray(np.asarray(list(call_map), dtype=np.uint64).reshape(-1))
+        N.check(lib.fb_flow_export_merge_map_dev(ctx, world, rank, N.ptr(cm) if cm.size else None, int(cm.size),
+                                                 C.c_void_p(mrecs.data_ptr()), cnt.value,
+                                                 C.c_void_p(counts.data_ptr()), stream))
     stream_sync()  # the group sizes and records are complete before torch reads them
     counts = counts.tolist()  # (host ints: the collective's split sizes)
     mrecs = mrecs[: sum(counts)].to(dev)

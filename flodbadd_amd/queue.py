@@ -103,6 +103,11 @@ class SegQueue:
         self._live[t.value] = batch
         return t.value
 
+    def set_limit(self, limit):
+        """Lower the queue's submission limit (fb_seg_queue_set_limit): the submit past it fails with
+        FB_ERR_INVAL, as the one past FB_QUEUE_MAX_SUBMISSIONS does."""
+        N.check(self._lib.fb_seg_queue_set_limit(self._q, int(limit)))
+
     def done(self, ticket):
         rc = self._lib.fb_seg_queue_query(self._q, int(ticket))
         if rc < 0:

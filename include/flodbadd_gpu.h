@@ -293,6 +293,13 @@ int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
  * (from fb_event_create, caller-owned; NULL clears) is set, fb_process_dev / fb_process_seg_dev
  * record it on their stream between the parse and the session-table update. */
 int fb_set_stage_event(fb_ctx* ctx, void* event);
+/* Test / diagnostic knobs of one context (never needed in production; each takes effect for the
+ * next call): FB_DEBUG_DENSE_STEAL_POLLS -- the polls a dense look-back waits for a predecessor's
+ * word before computing that tile's sums itself (default 4096; 0 forces the fallback path);
+ * FB_DEBUG_DENSE_OFFSET_SKEW -- fault injection, added (mod 2^32) to the session half of every
+ * dense tile offset, as a corrupted look-back word would be (< 2^32; logged on stderr when set). */
+enum fb_debug_knob { FB_DEBUG_DENSE_STEAL_POLLS = 1, FB_DEBUG_DENSE_OFFSET_SKEW = 2 };
+int fb_debug_set(fb_ctx* ctx, uint32_t knob, uint64_t value);
 /* Whether the fused parse + upsert calls (fb_process_seg_dev, fb_process_seg_async_dev) store the
  * SESSION records in d_out (default 1).  With 0 the session table is their only per-packet output,
  * as in the reference's capture loop, which drops each ParsedPacket once process_parsed_packet has
@@ -412,17 +419,29 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, 
  * a queue lives its kernel holds two workgroups on every CU (every one must be resident: the grid is
  * sized by the occupancy query); what it leaves free -- the registers of a fifth wave per SIMD, a third
  * of the LDS -- runs copies and small kernels beside it, and a kernel that needs more of a CU waits
- * until fb_seg_queue_destroy; so does hipFree (measured: a 1-MB hipFree waited 4.8 s, until the
- * idle limit stopped the kernel, while hipMalloc, H2D and D2H copies did not wait): free device
- * memory only after fb_seg_queue_destroy.  One queue per device at a time (a second create fails with
+ * until fb_seg_queue_destroy.  One queue per device at a time (a second create fails with
  * FB_ERR_INVAL while the first lives).  A queue left idle for idle_ms (0 = 5,000 ms) stops itself,
  * and one whose blocks were not all running idle_ms after create (CUs held by other work) is
- * reported the same way: its calls then fail with FB_ERR_INTERNAL (destroy it, create a new one). */
+ * reported the same way: its calls then fail with FB_ERR_INTERNAL (destroy it, create a new one).
+ * HARD RULES while a queue lives:
+ *   - never hipFree / fb_dev_free device memory on its device: the free waits for the resident
+ *     kernel (measured: a 1-MB hipFree waited 4.8 s, until the idle limit stopped the kernel, while
+ *     hipMalloc, H2D and D2H copies did not wait) -- free only after fb_seg_queue_destroy;
+ *   - one producer thread: submit / query / wait / destroy of one queue are not synchronised with
+ *     each other (two concurrent submits would write the same ring slot and hand out one ticket);
+ *   - at most FB_QUEUE_MAX_SUBMISSIONS batches over the queue's life (the kernel numbers batches in
+ *     32 bits): the submit after that fails with FB_ERR_INVAL -- destroy the queue and create a new
+ *     one (at ~24 us per 1M-frame batch that is ~28 h of continuous capture). */
 #define FB_QUEUE_MAX_DEPTH 32u
+#define FB_QUEUE_MAX_SUBMISSIONS (0xFFFFFFFFull - FB_QUEUE_MAX_DEPTH)
 typedef struct fb_seg_queue fb_seg_queue;
 fb_seg_queue* fb_seg_queue_create(fb_ctx* ctx, uint32_t depth /* 1..FB_QUEUE_MAX_DEPTH, 0 = 8 */, uint32_t idle_ms);
 /* Blocks only while `depth` batches are in flight (until the oldest of them completes). */
 int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* batch, uint64_t* ticket);
+/* Lower this queue's submission limit below FB_QUEUE_MAX_SUBMISSIONS (tests of the limit; a host
+ * that wants to recycle its queue earlier).  FB_ERR_INVAL if `limit` is above the maximum or below
+ * the batches already submitted. */
+int fb_seg_queue_set_limit(fb_seg_queue* q, uint64_t limit);
 int fb_seg_queue_query(fb_seg_queue* q, uint64_t ticket); /* FB_OK done, 1 pending, < 0 error */
 int fb_seg_queue_wait(fb_seg_queue* q, uint64_t ticket);  /* polls until done (no blocking wait) */
 int fb_seg_queue_destroy(fb_seg_queue* q);                /* after the submitted batches complete */
@@ -627,11 +646,16 @@ uint64_t fb_flow_hash(const fb_session_key* key);
  * hist_mask OR, in_segment and session flags from the records holding the key's latest / earliest
  * packet -- and conn_state / end_mask re-decided at the global first FIN/RST: the ending rank's
  * end_mask OR the S s H h of the other ranks that precede it (their first occurrence in an earlier
- * call, or in the same call on a lower rank).  Exact for any number of update calls per rank, given
- * the shard layout this assumes: in every call a rank's shard starts at the same packet index of the
- * global batch (shard_first), as equal contiguous shards of equal-size global batches do; a call
- * whose global batch differs in size (a short tail batch) needs its own export with that call's
- * offset.  Positions become global: (call << 32) | (shard_first + pkt_index). */
+ * call, or in the same call on a lower rank).  Exact for any number of update calls per rank.  The
+ * shard layout: global batch k is split into contiguous packet-index ranges, rank r's before rank
+ * r+1's.  fb_flow_export_merge_dev takes the layout of equal shards of equal-size batches -- call k
+ * of every rank is its shard of global batch k, starting at the same index `shard_first` in each --
+ * and makes positions (k << 32) | (shard_first + pkt_index).  fb_flow_export_merge_map_dev takes
+ * any layout -- unequal per-call batches, a short tail batch, a rank that makes no call for a batch
+ * whose shard is empty -- as a call map: call_map[k] = (global batch of this rank's update call k)
+ * << 32 | (global index of that shard's first packet), global batches increasing with k; positions
+ * become (call_map[k] >> 32) << 32 | ((call_map[k] & 0xFFFFFFFF) + pkt_index) and char_call the
+ * global batch numbers. */
 typedef struct fb_flow_mrec {
     fb_flow_rec rec;        /* positions global; rec.slot = the exporting rank                    */
     uint32_t char_call[4];  /* update call of the flow's first S, s, H, h (FB_CALL_NONE: none)     */
@@ -641,6 +665,10 @@ typedef struct fb_flow_mrec {
  * DEVICE pointers, asynchronous. */
 int fb_flow_export_merge_dev(fb_ctx* ctx, uint32_t world, uint32_t rank, uint64_t shard_first, fb_flow_mrec* d_out,
                              uint64_t cap, uint64_t* d_counts, void* stream);
+/* The same with a host call map (n_calls >= the context's update calls since create / clear; the
+ * map is copied before the call returns). */
+int fb_flow_export_merge_map_dev(fb_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* call_map, uint32_t n_calls,
+                                 fb_flow_mrec* d_out, uint64_t cap, uint64_t* d_counts, void* stream);
 /* Merge n records received by one owner (each rank's group, in rank order; a key at most once per
  * rank) into one fb_flow_rec per key (slot 0), in the order of each key's first record; *d_n
  * (device u64) = keys.  d_out: room for n records.  DEVICE pointers, asynchronous. */
@@ -663,7 +691,9 @@ typedef struct fb_ring_config {
     uint32_t max_packets; /* frames per batch                                    */
     uint64_t max_bytes;   /* frame bytes per batch, < 4 GiB                      */
     uint32_t flags;       /* FB_RING_*                                           */
-    uint32_t reserved;
+    uint32_t copy_threads; /* threads of fb_ring_push_block's copy into the pinned batch (the
+                              producer + copy_threads - 1 helpers the ring owns; 0 or 1 = the
+                              producer alone; at most 64); other calls are unaffected */
 } fb_ring_config;
 #define FB_RING_NO_FLOW 1u /* parse + classify only, no session-table update */
 typedef struct fb_ring_dns {

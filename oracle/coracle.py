@@ -74,6 +74,8 @@ def lib():
         L.orc_flow_hash.argtypes = [P]
         L.orc_flows_export_merge.restype = U64
         L.orc_flows_export_merge.argtypes = [P, U32, U32, U64, P, P]
+        L.orc_flows_export_merge_map.restype = U64
+        L.orc_flows_export_merge_map.argtypes = [P, U32, U32, P, P, P]
         L.orc_flow_merge.restype = U64
         L.orc_flow_merge.argtypes = [P, U64, P]
         _lib = L
@@ -214,12 +216,21 @@ class Flows:
             return None, None
         return self._buf.raw[:n].decode(), (self._cs.value.decode() or None)
 
-    def export_merge(self, world, rank, shard_first):
-        """orc_flows_export_merge: FLOW_MREC_DTYPE records grouped by owner rank, and the group sizes."""
+    def export_merge(self, world, rank, shard_first=0, call_map=None):
+        """orc_flows_export_merge (orc_flows_export_merge_map with `call_map`, a sequence of
+        global batch << 32 | shard start per update call): FLOW_MREC_DTYPE records grouped by owner
+        rank, and the group sizes."""
         n = self.count()
         out = np.zeros(max(n, 1), dtype=N.FLOW_MREC_DTYPE)
         counts = np.zeros(world, dtype=np.uint64)
-        m = lib().orc_flows_export_merge(self.h, world, rank, shard_first, out.ctypes.data, counts.ctypes.data)
+        if call_map is None:
+            m = lib().orc_flows_export_merge(self.h, world, rank, shard_first, out.ctypes.data, counts.ctypes.data)
+        else:
+            cm = np.ascontiguousarray(np.asarray(call_map, dtype=np.uint64).reshape(-1))
+            if cm.size == 0:
+                cm = np.zeros(1, dtype=np.uint64)
+            m = lib().orc_flows_export_merge_map(self.h, world, rank, cm.ctypes.data, out.ctypes.data,
+                                                 counts.ctypes.data)
         return out[:m], counts
 
     def clear(self):

@@ -589,12 +589,29 @@ static uint32_t owner_of(const fb_session_key* k, uint32_t world) {
     return (uint32_t)(((orc_flow_hash(k) >> 32) * (uint64_t)world) >> 32);
 }
 
-static uint64_t globalize(uint64_t pos, uint64_t shard_first) {
-    return (pos & 0xFFFFFFFF00000000ull) | ((pos & 0xFFFFFFFFull) + shard_first);
+/* A position (update call << 32 | pkt_index) made global: call k was this rank's shard of global
+ * batch map[k] >> 32 starting at global packet map[k] & 0xFFFFFFFF (without a map: batch k, the
+ * shard at shard_first). */
+static uint64_t globalize(uint64_t pos, uint64_t shard_first, const uint64_t* map) {
+    const uint64_t m = map ? map[pos >> 32] : ((pos & 0xFFFFFFFF00000000ull) | shard_first);
+    return (m & 0xFFFFFFFF00000000ull) | ((m & 0xFFFFFFFFull) + (pos & 0xFFFFFFFFull));
 }
+
+static uint64_t export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
+                             const uint64_t* map, fb_flow_mrec* out, uint64_t* counts);
 
 uint64_t orc_flows_export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
                                 fb_flow_mrec* out, uint64_t* counts) {
+    return export_merge(f, world, rank, shard_first, NULL, out, counts);
+}
+
+uint64_t orc_flows_export_merge_map(const orc_flows* f, uint32_t world, uint32_t rank, const uint64_t* call_map,
+                                    fb_flow_mrec* out, uint64_t* counts) {
+    return export_merge(f, world, rank, 0, call_map, out, counts);
+}
+
+static uint64_t export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
+                             const uint64_t* map, fb_flow_mrec* out, uint64_t* counts) {
     /* the table in Ord order, then stably grouped by owner */
     const uint64_t n = f->count;
     fb_flow_rec* recs = (fb_flow_rec*)malloc((n ? n : 1) * sizeof(fb_flow_rec));
@@ -611,11 +628,12 @@ uint64_t orc_flows_export_merge(const orc_flows* f, uint32_t world, uint32_t ran
             if (owner_of(&recs[i].key, world) != o) continue;
             fb_flow_mrec* x = &out[w++];
             x->rec = recs[i];
-            x->rec.first_seen = globalize(x->rec.first_seen, shard_first);
-            x->rec.last_seen = globalize(x->rec.last_seen, shard_first);
-            if (x->rec.end_seen != FB_SEEN_NONE) x->rec.end_seen = globalize(x->rec.end_seen, shard_first);
+            x->rec.first_seen = globalize(x->rec.first_seen, shard_first, map);
+            x->rec.last_seen = globalize(x->rec.last_seen, shard_first, map);
+            if (x->rec.end_seen != FB_SEEN_NONE) x->rec.end_seen = globalize(x->rec.end_seen, shard_first, map);
             x->rec.slot = rank;
-            memcpy(x->char_call, calls[i], sizeof(x->char_call));
+            for (int b = 0; b < 4; ++b) /* the update call of the first S s H h -> its global batch */
+                x->char_call[b] = (calls[i][b] == FB_CALL_NONE || !map) ? calls[i][b] : (uint32_t)(map[calls[i][b]] >> 32);
             counts[o]++;
         }
     }

@@ -103,6 +103,10 @@ int64_t orc_flows_history(const orc_flows* f, const fb_session_key* key, char* b
 uint64_t orc_flow_hash(const fb_session_key* key);
 uint64_t orc_flows_export_merge(const orc_flows* f, uint32_t world, uint32_t rank, uint64_t shard_first,
                                 fb_flow_mrec* out, uint64_t* counts);
+/* The same under a call map (fb_flow_export_merge_map_dev): call_map[k] = global batch of update call
+ * k << 32 | global index of that shard's first packet. */
+uint64_t orc_flows_export_merge_map(const orc_flows* f, uint32_t world, uint32_t rank, const uint64_t* call_map,
+                                    fb_flow_mrec* out, uint64_t* counts);
 /* One owner's received records (rank order) -> one record per key, in the order of each key's first
  * record.  Returns the keys written (`out` must hold n). */
 uint64_t orc_flow_merge(const fb_flow_mrec* in, uint64_t n, fb_flow_rec* out);

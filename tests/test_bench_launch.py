@@ -47,7 +47,7 @@ def test_world_mismatch_is_an_error():
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("inject", ["fail", "group"])
+@pytest.mark.parametrize("inject", ["fail", "group", "conservation"])
 def test_c5_failure_fails_the_run(inject):
     """At N > 1 the C5 exchange's outcome is agreed by every rank: a rank whose merge raises, or a
     group smaller than --gpus, puts "c5_ok": false in the line and the run exits non-zero (the line
@@ -58,6 +58,8 @@ def test_c5_failure_fails_the_run(inject):
     c5 = d["extra"]["c5_flow_reduce"]
     assert d["c5_ok"] is False and "error" in c5
     assert c5["failed_ranks"] == ([1] if inject == "fail" else [0, 1])
+    if inject == "conservation":
+        assert "conservation violated: payload_bytes" in c5["error"]
 
 
 @pytest.mark.timeout(240)
@@ -66,3 +68,18 @@ def test_c5_success_keeps_rc_zero():
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
     assert d["c5_ok"] is True and d["extra"]["c5_flow_reduce"]["ranks_in_group"] == 2
+
+
+def test_c5_conservation_checks():
+    sys.path.insert(0, ROOT)
+    import bench
+    sums = dict(packets=10, payload_bytes=640, ip_bytes=1040)
+    ok = bench.c5_conservation(sums, dict(sums), [6, 5], 9, 9)
+    assert ok["packets"] == 10 and ok["local_flows"] == [6, 5]
+    for merged, local, g, u, what in ((dict(sums, packets=9), [6, 5], 9, 9, "packets"),
+                                      (sums, [6, 5], 12, 12, "outside"),
+                                      (sums, [6, 5], 5, 5, "outside"),
+                                      (sums, [6, 5], 9, 8, "distinct keys")):
+        with pytest.raises(RuntimeError) as e:
+            bench.c5_conservation(merged, sums, local, g, u)
+        assert what in str(e.value)

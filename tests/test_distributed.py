@@ -66,14 +66,56 @@ def _oracle_merge(rows):
     return torch.from_numpy(np.ascontiguousarray(merged).view(np.int64).reshape(len(merged), REC_WORDS).copy())
 
 
-def _worker(rank, world, port, outdir, empty_rank=-1):
+# Unequal global batches (a capture loop flushing every MAX_BATCH frames or every 1 ms): the last one
+# a short tail whose shard is empty on the lower ranks of a 3-rank world.
+SIZES = (9000, 4097, 6001, 2)
+BASE = 100000  # global batch k's frames are synth frames [k * BASE, k * BASE + size)
+
+
+def _sched_batch(k, first, count):
+    from flodbadd_amd import synth
+    return synth.generate(4, count, first=k * BASE + first, n_flows=POOL)
+
+
+def _rank_table_sched(rank, world, skip_empty):
+    """Rank `rank`'s table over SIZES, one update call per global batch (none for an empty shard
+    when skip_empty), and its call map (global batch << 32 | shard start per call)."""
+    from oracle import coracle
+    fl = coracle.Flows()
+    cmap = []
+    for k, size in enumerate(SIZES):
+        first, count = shard_range(size, rank, world)
+        if count == 0 and skip_empty:
+            continue
+        frames, offs = _sched_batch(k, first, count)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
+        fl.update(out)
+        cmap.append((k << 32) | first)
+    return fl, cmap
+
+
+def single_table_sched():
+    from oracle import coracle
+    fl = coracle.Flows()
+    for k, size in enumerate(SIZES):
+        frames, offs = _sched_batch(k, 0, size)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), frames, offs)
+        fl.update(out)
+    return fl.export_sorted()
+
+
+def _worker(rank, world, port, outdir, empty_rank=-1, sched=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        fl, first = _rank_table(rank, world)
-        if rank == empty_rank:
-            fl.clear()
-        mrecs, counts = fl.export_merge(world, rank, first)
+        if sched is None:
+            fl, first = _rank_table(rank, world)
+            if rank == empty_rank:
+                fl.clear()
+            mrecs, counts = fl.export_merge(world, rank, first)
+        else:
+            fl, cmap = _rank_table_sched(rank, world, skip_empty=sched == "skip")
+            mrecs, counts = fl.export_merge(world, rank, call_map=cmap)
         rows = torch.from_numpy(np.ascontiguousarray(mrecs).view(np.int64).reshape(len(mrecs), MREC_WORDS).copy())
         table = exchange_merge(dist, rows, counts.tolist(), _oracle_merge)
         np.save(os.path.join(outdir, "r%d.npy" % rank), table.numpy().view(np.uint8))
@@ -151,3 +193,40 @@ def test_oracle_merge_of_one_rank_is_its_table():
     assert int(counts[0]) == len(m) == fl.count()
     merged = coracle.flow_merge(m)
     assert _rows(merged).tobytes() == _rows(fl.export_sorted()).tobytes()
+
+
+def test_unequal_batches_fixture_has_an_empty_shard():
+    assert shard_range(SIZES[-1], 0, 3)[1] == 0 and shard_range(SIZES[-1], 2, 3)[1] == 2
+    assert len(set(SIZES)) == len(SIZES)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,sched", [(2, "skip"), (3, "skip"), (3, "call")])
+def test_gloo_global_flow_table_unequal_batches(tmp_path, world, sched):
+    """Global batches of different sizes and a 2-frame tail: each rank's export takes a call map
+    (global batch << 32 | its shard's start, per update call; "skip": no call for an empty shard,
+    "call": an empty call) and the merged table equals ONE table of the global stream, byte for
+    byte (include/flodbadd_gpu.h fb_flow_export_merge_map_dev)."""
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), -1, sched), nprocs=world,
+                       start_method="spawn")
+    ref = single_table_sched()
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
+        assert len(got) == len(ref), (len(got), len(ref))
+        assert _rows(got).tobytes() == _rows(ref).tobytes(), r
+
+
+def test_shard_first_layout_breaks_on_unequal_batches():
+    """Why the call map exists: the single shard_first layout assumes every global batch has the
+    rank's shard at the same index; with unequal batches its positions (and so last_seen / end_seen)
+    are wrong for rank 1."""
+    from oracle import coracle
+    world = 2
+    recs = []
+    for r in range(world):
+        fl, cmap = _rank_table_sched(r, world, skip_empty=False)
+        m_map, _ = fl.export_merge(1, r, call_map=cmap)
+        m_old, _ = fl.export_merge(1, r, shard_range(SIZES[0], r, world)[0])
+        recs.append((m_map, m_old))
+    assert recs[0][0].tobytes() == recs[0][1].tobytes()  # rank 0: shard start 0 in every batch
+    assert recs[1][0].tobytes() != recs[1][1].tobytes()

@@ -188,3 +188,76 @@ def test_rccl_world1_global_flow_table(tmp_path):
     merged = np.load(out).view(N.FLOW_REC_DTYPE)
     ref = _single(pool=1 << 20)
     assert len(merged) == len(ref) and _rows(merged).tobytes() == _rows(ref).tobytes()
+
+
+# Unequal global batches and a 1-frame tail (rank 0's shard of it is empty: it makes no call for it).
+SIZES = (60000, 20001, 35555, 1)
+BASE = 1 << 20
+
+
+def _sched_batch(k, first, count):
+    return synth.generate(4, count, first=k * BASE + first, n_flows=POOL)
+
+
+def _gloo_child(rank, world, port, outdir, layout):
+    """Rank `rank` of a gloo group on GPU 0: its own context parses + upserts its shards on the
+    device, then global_flow_table runs the library's export / merge kernels (the collectives move
+    the records through host memory)."""
+    import torch
+    import torch.distributed as dist
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.distributed import call_map_entry, global_flow_table
+    from flodbadd_amd.sessions import SessionFilter
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 16)
+    try:
+        if layout == "equal":
+            first, count = shard_range(TOTAL, rank, world)
+            for k in range(CALLS):
+                fr, of = _batch(k, first, count)
+                g = cap.process_frames_seg(fr, of) if k % 2 else cap.process_frames(fr, of)
+                assert g.stats["error"] == 0
+            merged = global_flow_table(dist, cap.ctx, shard_first=first)
+        else:
+            cmap = []
+            for k, size in enumerate(SIZES):
+                first, count = shard_range(size, rank, world)
+                if count == 0:
+                    continue  # no call for an empty shard: the call map skips the batch
+                fr, of = _sched_batch(k, first, count)
+                g = cap.process_frames(fr, of) if k % 2 else cap.process_frames_seg(fr, of)
+                assert g.stats["error"] == 0
+                cmap.append(call_map_entry(k, first))
+            merged = global_flow_table(dist, cap.ctx, call_map=cmap)
+        np.save(os.path.join(outdir, "r%d.npy" % rank), merged.view(np.uint8))
+    finally:
+        cap.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("layout", ["equal", "unequal"])
+def test_two_process_gloo_device_merge(tmp_path, layout):
+    """Two processes (ranks of a gloo group, both on GPU 0): the device export (fb_flow_export_merge_dev,
+    or fb_flow_export_merge_map_dev for unequal batches and a short tail batch) and the device merge
+    (fb_flow_merge_dev) through flodbadd_amd.distributed.global_flow_table.  Both ranks' tables equal
+    ONE oracle table fed the same packets in global order, byte for byte."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.start_processes(_gloo_child, args=(world, _free_port(), str(tmp_path), layout), nprocs=world,
+                       start_method="spawn")
+    if layout == "equal":
+        ref = _single()
+    else:
+        fl = coracle.Flows()
+        for k, size in enumerate(SIZES):
+            fr, of = _sched_batch(k, 0, size)
+            out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+            fl.update(out)
+        ref = fl.export_sorted()
+    assert shard_range(SIZES[-1], 0, world)[1] == 0  # (the fixture's empty shard)
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
+        assert len(got) == len(ref), (r, len(got), len(ref))
+        assert _rows(got).tobytes() == _rows(ref).tobytes(), r

@@ -120,12 +120,11 @@ def test_dense_full_size(cid):
 
 
 def test_dense_lookback_fallback_forced(monkeypatch):
-    """FB_DENSE_STEAL_POLLS=0: every look-back that meets a predecessor's unpublished word at once
+    """fb_debug_set(FB_DEBUG_DENSE_STEAL_POLLS, 0): every look-back that meets a predecessor's unpublished word at once
     computes that tile's sums itself (the path that keeps the kernel safe when some workgroups are
     not running) and CASes them in -- the outputs stay bit-identical."""
-    monkeypatch.setenv("FB_DENSE_STEAL_POLLS", "0")
     cap = _ctx()
-    monkeypatch.delenv("FB_DENSE_STEAL_POLLS")
+    N.check(N.gpu_lib().fb_debug_set(cap.ctx, N.FB_DEBUG_DENSE_STEAL_POLLS, 0))
     try:
         for k, n in enumerate((1025, 65536, 300001)):
             frames, offs = synth.generate(3, n, first=91 + k)
@@ -138,16 +137,15 @@ def test_dense_lookback_fallback_forced(monkeypatch):
 
 
 def test_dense_corrupted_tile_offset_drops_instead_of_faulting(monkeypatch):
-    """A corrupted look-back offset (FB_DENSE_OFFSET_SKEW: half a batch added to every tile's
+    """A corrupted look-back offset (FB_DEBUG_DENSE_OFFSET_SKEW: half a batch added to every tile's
     batch-wide offset -- what round 4's no-look-back ablation did by adding the real prefix to a
     fixed one, and faulted with an illegal memory access) must not write outside the caller's
     buffers: the slots whose destination passes the batch's n records are dropped and the batch's
     error word has bit 32; a context without the skew is bit-exact again on the same batch."""
     n = 65536
     frames, offs = synth.generate(3, n, first=7)
-    monkeypatch.setenv("FB_DENSE_OFFSET_SKEW", str(n // 2))
     cap = _ctx()
-    monkeypatch.delenv("FB_DENSE_OFFSET_SKEW")
+    N.check(N.gpu_lib().fb_debug_set(cap.ctx, N.FB_DEBUG_DENSE_OFFSET_SKEW, n // 2))
     try:
         b = _Dense(frames, offs)
         b.run(cap)

@@ -142,6 +142,32 @@ def test_queue_expired_reports_error():
         cap.close()
 
 
+def test_queue_submission_limit():
+    """The kernel numbers batches in 32 bits, so a queue takes at most FB_QUEUE_MAX_SUBMISSIONS
+    batches; the submit past its limit fails with FB_ERR_INVAL (here a lowered limit: the same check)
+    instead of wrapping, and the batches before it stay exact."""
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=0)
+    b = _Batch(*synth.generate(2, 5000))
+    q = _Queue(cap, depth=2)
+    try:
+        with pytest.raises(N.FbError) as e:
+            q.set_limit((1 << 32))  # above FB_QUEUE_MAX_SUBMISSIONS
+        assert e.value.code == N.FB_ERR_INVAL
+        q.set_limit(3)
+        for _ in range(3):
+            b.reset()
+            q.wait(q.submit(b))
+            _verify(b, SessionFilter.All)
+        with pytest.raises(N.FbError) as e:
+            q.submit(b)
+        assert e.value.code == N.FB_ERR_INVAL
+        with pytest.raises(N.FbError):
+            q.set_limit(2)  # below the batches already submitted
+    finally:
+        q.close()
+        cap.close()
+
+
 def test_one_queue_per_device():
     """A second queue's blocks could never be resident beside the first's: its create fails (instead
     of a kernel that never starts), and succeeds again once the first is destroyed."""

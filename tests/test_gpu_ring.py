@@ -17,8 +17,8 @@ from test_gpu_parity import rows_sorted
 pytestmark = pytest.mark.gpu
 
 
-def _ring(cap, slots, max_packets, max_bytes, flags=0):
-    cfg = N.FbRingConfig(slots, max_packets, max_bytes, flags, 0)
+def _ring(cap, slots, max_packets, max_bytes, flags=0, copy_threads=0):
+    cfg = N.FbRingConfig(slots, max_packets, max_bytes, flags, copy_threads)
     r = N.gpu_lib().fb_ring_create(cap.ctx, C.byref(cfg))
     assert r, N.gpu_lib().fb_last_error()
     return C.c_void_p(r)
@@ -55,23 +55,26 @@ def _oracle_batches(frames, offs, per_batch, flows):
     return tot, dns
 
 
-@pytest.mark.parametrize("how", ["block", "push", "reserve"])
+@pytest.mark.parametrize("how", ["block", "push", "reserve", "block_mt"])
 def test_ring_vs_oracle(gpu_capture, how):
-    frames, offs = synth.generate(3, 20000, first=11)
+    """block_mt: 150k frames in blocks split over 5 copy threads (fb_ring_config.copy_threads; runs of
+    more than 1 MB are copied by frame ranges, a block of 65,536+ frames is validated by ranges)."""
+    frames, offs = synth.generate(3, 150000 if how == "block_mt" else 20000, first=11)
     extra, eo = fg.pack([f for _, f in fg.edge_cases()])
     frames = np.concatenate([frames, extra])
     offs = np.concatenate([offs, offs[-1] + eo[1:]]).astype(np.uint32)
     n = len(offs) - 1
-    per = 3000  # 7 batches through 3 pinned slots
+    per = 3000 if how != "block_mt" else 40000  # 7 (4) batches through 3 pinned slots
     lib = N.gpu_lib()
     gpu_capture.clear_all_sessions()
-    r = _ring(gpu_capture, 3, per, 64 << 20)
+    r = _ring(gpu_capture, 3, per, 64 << 20, copy_threads=5 if how == "block_mt" else 0)
     try:
-        if how == "block":
-            N.check(lib.fb_ring_push_block(r, N.ptr(frames), N.ptr(offs), 5000))
-            rest = np.ascontiguousarray(offs[5000:] - offs[5000], dtype=np.uint32)  # kept alive for the call
-            tail = frames[offs[5000]:]
-            N.check(lib.fb_ring_push_block(r, N.ptr(tail), N.ptr(rest), n - 5000))
+        if how in ("block", "block_mt"):
+            cut = 5000 if how == "block" else 70001
+            N.check(lib.fb_ring_push_block(r, N.ptr(frames), N.ptr(offs), cut))
+            rest = np.ascontiguousarray(offs[cut:] - offs[cut], dtype=np.uint32)  # kept alive for the call
+            tail = frames[offs[cut]:]
+            N.check(lib.fb_ring_push_block(r, N.ptr(tail), N.ptr(rest), n - cut))
         elif how == "push":
             for i in range(n):
                 f = np.ascontiguousarray(frames[offs[i]: offs[i + 1]])
@@ -114,6 +117,22 @@ def test_ring_bad_arguments(gpu_capture):
         nb = C.c_uint64()
         N.check(lib.fb_ring_stats(r, None, C.byref(nb), None))
         assert nb.value == 0
+    finally:
+        lib.fb_ring_destroy(r)
+    # the range-split validation of a multi-threaded ring: a decrease deep in a large block is
+    # found and nothing of the block is taken
+    r = _ring(gpu_capture, 2, 1 << 17, 1 << 24, copy_threads=4)
+    try:
+        n = 100000
+        offs = np.arange(n + 1, dtype=np.uint32) * 64
+        offs[77777] = offs[77776] - 1
+        fr = np.zeros(n * 64, dtype=np.uint8)
+        assert lib.fb_ring_push_block(r, N.ptr(fr), N.ptr(offs), n) == N.FB_ERR_INVAL
+        assert b"77776" in lib.fb_last_error()
+        N.check(lib.fb_ring_sync(r))
+        nb, nf = C.c_uint64(), C.c_uint64()
+        N.check(lib.fb_ring_stats(r, None, C.byref(nb), C.byref(nf)))
+        assert nb.value == 0 and nf.value == 0
     finally:
         lib.fb_ring_destroy(r)
 
