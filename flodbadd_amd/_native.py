@@ -51,6 +51,15 @@ FLOW_REC_DTYPE = np.dtype(KEY_FIELDS + [
 # the update call of the flow's first S, s, H, h (FB_CALL_NONE: none)
 FLOW_MREC_DTYPE = np.dtype([("rec", FLOW_REC_DTYPE), ("char_call", "<u4", (4,))])
 FB_CALL_NONE = 0xFFFFFFFF
+# fb_flow_time: a flow's capture-time state on a timed context (FB_CFG_TIMED)
+FLOW_TIME_DTYPE = np.dtype([
+    ("start_time_ns", "<u8"), ("last_activity_ns", "<u8"), ("end_time_ns", "<u8"),
+    ("current_segment_start_ns", "<u8"), ("last_segment_end_ns", "<u8"),
+    ("total_segment_interarrival_ms", "<i8"), ("segment_interarrival_div", "<u4"), ("segment_count", "<u4"),
+    ("in_segment", "u1"), ("reserved", "u1", (3,)), ("slot", "<u4")])
+assert FLOW_TIME_DTYPE.itemsize == 64
+FB_SEGMENT_TIMEOUT_MS = 5000
+FB_CFG_TIMED = 2
 # fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst and
 # dst_service is Some, at insert)
 SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST, SESSION_DST_SERVICE = 1, 2, 4, 8, 16
@@ -201,6 +210,8 @@ GPU_SYMBOLS = [
     ("fb_flow_export_merge_dev", _I, [_P, _U32, _U32, _U64, _P, _U64, _P, _P]),
     ("fb_flow_export_merge_map_dev", _I, [_P, _U32, _U32, _P, _U32, _P, _U64, _P, _P]),
     ("fb_flow_merge_dev", _I, [_P, _P, _U64, _P, _P, _P]),
+    ("fb_flow_update_records_dev", _I, [_P, _P, _U32, _P, _P]),
+    ("fb_route_records_dev", _I, [_P, _P, _P, _U32, _U32, _U64, _P, _P, _P, _P, _P]),
     ("fb_flow_owner", _U32, [_P, _U32]),
     ("fb_ring_create", _P, [_P, C.POINTER(FbRingConfig)]),
     ("fb_ring_destroy", _I, [_P]),
@@ -238,6 +249,9 @@ GPU_SYMBOLS = [
     ("fb_seg_queue_destroy", _I, [_P]),
     ("fb_seg_queue_set_limit", _I, [_P, _U64]),
     ("fb_debug_set", _I, [_P, _U32, _U64]),
+    ("fb_set_frame_times", _I, [_P, _P]),
+    ("fb_flow_export_times_dev", _I, [_P, _P, _U64, _P, _P]),
+    ("fb_flow_export_times", _I, [_P, _P, _U64, _PU64, _P]),
 ]
 
 _gpu = None

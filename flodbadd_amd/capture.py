@@ -52,7 +52,10 @@ def stats_dict(arr):
 class FlodbaddGpuCapture:
     def __init__(self, device=0, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 20,
                  service_bitmap=None, lan_v6=(), own_ips=(), max_batch_packets=1 << 20, track_history=False,
-                 grow=True):
+                 grow=True, timed=False):
+        """timed: capture-time session state (FB_CFG_TIMED): every batch then comes with its frames'
+        capture timestamps (`ts`, ns) and the sessions carry start / last / end times and the
+        segment state with the reference's 5-s timeout (src/packets.rs:137-200)."""
         lib = N.gpu_lib()
         self._keep = []
         cfg = N.FbConfig()
@@ -73,7 +76,7 @@ class FlodbaddGpuCapture:
         cfg.n_own_ips = len(ot)
         cfg.flow_capacity = int(flow_capacity)
         cfg.max_batch_packets = int(max_batch_packets)
-        cfg.flags = 0 if grow else N.FB_CFG_FIXED_TABLE  # the reference's session map is unbounded
+        cfg.flags = (0 if grow else N.FB_CFG_FIXED_TABLE) | (N.FB_CFG_TIMED if timed else 0)  # (the map is unbounded)
         ctx = lib.fb_create(int(device), C.byref(cfg))
         if not ctx:
             raise N.FbError(N.FB_ERR_NODEV, lib.fb_last_error().decode(errors="replace"))
@@ -81,6 +84,7 @@ class FlodbaddGpuCapture:
         self.filter = SessionFilter(session_filter)
         self.device = device
         self.flow_capacity = flow_capacity
+        self.timed = bool(timed)
         # history strings (src/packets.rs:187-198, 410-426) per table slot, appended batch by batch
         # from fb_flow_history_dev when track_history is set
         self.track_history = bool(track_history) and flow_capacity > 0
@@ -110,6 +114,24 @@ class FlodbaddGpuCapture:
         N.check(N.gpu_lib().fb_set_own_ips(self.ctx, N.ptr(t) if len(t) else None, len(t)))
 
     # ---- packet path -----------------------------------------------------------------------
+    def _frame_times(self, ts, n):
+        """Upload a batch's capture timestamps and hand them to the next update call (timed
+        contexts); returns the device buffer (kept alive by the caller until the call is done)."""
+        if not self.timed:
+            if ts is not None:
+                raise ValueError("capture timestamps need a timed capture (timed=True)")
+            return None
+        if ts is None:
+            raise ValueError("a timed capture needs each batch's capture timestamps (ts)")
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        if ts.size < n:
+            raise ValueError("%d timestamps for %d frames" % (ts.size, n))
+        d = N.DeviceBuffer(max(ts.nbytes, 8))
+        if ts.size:
+            d.upload(ts)
+        N.check(N.gpu_lib().fb_set_frame_times(self.ctx, d.ptr))
+        return d
+
     def parse_classify(self, frames, offsets):
         """Host-memory batch: parse_packet_pcap + per-packet classification for every frame."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
@@ -125,7 +147,7 @@ class FlodbaddGpuCapture:
                                               N.ptr(cls), N.ptr(st), None))
         return BatchResult(out[: n_out.value], dns[: n_dns.value], cls[:n], stats_dict(st))
 
-    def process_parsed(self, packets):
+    def process_parsed(self, packets, ts=None):
         """process_parsed_packet (src/packets.rs:202-537) for a batch of SessionPacketData (list)
         or PARSED_DTYPE records: canonical keys + filter on the GPU, then the session-table upsert
         when the capture has a flow table.  Returns a BatchResult (records, cls, stats)."""
@@ -137,13 +159,15 @@ class FlodbaddGpuCapture:
         cls = np.zeros(max(n, 1), dtype=np.uint8)
         st = np.zeros(1, dtype=N.STATS_DTYPE)
         n_out = C.c_uint32(0)
+        d_ts = self._frame_times(ts, n) if self.flow_capacity else None  # (indexed by pkt_index)
         N.check(N.gpu_lib().fb_process_parsed(self.ctx, N.ptr(arr) if n else None, n, N.ptr(out), C.byref(n_out),
                                               N.ptr(cls), N.ptr(st), None))
         self._pull_history(n)
         return BatchResult(out[: n_out.value], np.zeros(0, dtype=N.DNS_OUT_DTYPE), cls[:n], stats_dict(st))
 
-    def process_frames(self, frames, offsets):
-        """parse + classify + flow-table upsert (the whole process_parsed_packet per frame)."""
+    def process_frames(self, frames, offsets, ts=None):
+        """parse + classify + flow-table upsert (the whole process_parsed_packet per frame); ts: the
+        frames' capture timestamps (ns) on a timed capture."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
         n = offsets.size - 1
@@ -154,6 +178,7 @@ class FlodbaddGpuCapture:
         d_dns = N.DeviceBuffer(max(n, 1) * N.DNS_OUT_DTYPE.itemsize)
         d_cls = N.DeviceBuffer(max(n, 1))
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        d_ts = self._frame_times(ts, n)  # noqa: F841 (alive until the call's results are read)
         N.check(lib.fb_process_dev(self.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, d_dns.ptr,
                                    d_cls.ptr, d_st.ptr, None))
         st = d_st.download(np.zeros(1, dtype=N.STATS_DTYPE))
@@ -170,7 +195,7 @@ class FlodbaddGpuCapture:
         self._pull_history(n)
         return BatchResult(out, dns, cls, sd)
 
-    def process_frames_seg(self, frames, offsets, flow=True):
+    def process_frames_seg(self, frames, offsets, flow=True, ts=None):
         """The segmented streaming path (fb_process_seg_dev / fb_parse_classify_seg_dev): same
         classification and session-table update, records left in per-wavefront segments on the
         device; returned here densified (packet order) for comparison with process_frames."""
@@ -185,6 +210,7 @@ class FlodbaddGpuCapture:
         d_seg = N.DeviceBuffer(nseg * 4)
         d_cls = N.DeviceBuffer(max(n, 1))
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
+        d_ts = self._frame_times(ts, n) if flow else None  # noqa: F841
         fn = lib.fb_process_seg_dev if flow else lib.fb_parse_classify_seg_dev
         N.check(fn(self.ctx, d_fr.ptr, frames.nbytes, d_off.ptr, n, d_out.ptr, d_seg.ptr, d_cls.ptr, d_st.ptr, None))
         sd = stats_dict(d_st.download(np.zeros(1, dtype=N.STATS_DTYPE)))
@@ -262,11 +288,20 @@ class FlodbaddGpuCapture:
         N.check(N.gpu_lib().fb_flow_export_sessions(self.ctx, int(session_filter), N.ptr(out), cnt, C.byref(n), None))
         return out[: n.value]
 
+    def export_times(self):
+        """fb_flow_export_times: every flow's FLOW_TIME_DTYPE record (timed captures), with its slot."""
+        cnt = self.flow_count()
+        out = np.zeros(max(cnt, 1), dtype=N.FLOW_TIME_DTYPE)
+        n = C.c_uint64(0)
+        N.check(N.gpu_lib().fb_flow_export_times(self.ctx, N.ptr(out), cnt, C.byref(n), None))
+        return out[: n.value]
+
     def get_sessions(self):
         """get_sessions (src/capture.rs:1578-1612): the sessions that pass the CURRENT filter,
         is_local_session! evaluated at query time on the GPU (capture.rs:1603-1608), sorted by the
         derived Ord of Session (integer counters + derived f64s)."""
-        return flows_to_sessions(self.export_flows(self.filter), self.histories if self.track_history else None)
+        return flows_to_sessions(self.export_flows(self.filter), self.histories if self.track_history else None,
+                                 times=self.export_times() if self.timed else None)
 
     # ---- new-session enrichment (src/packets.rs:429-485) -------------------------------------
     def set_asn_tables(self, v4, v6):

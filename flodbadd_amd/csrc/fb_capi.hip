@@ -103,6 +103,14 @@ struct fb_ctx {
     bool grow = true;               // FB_CFG_FIXED_TABLE clears it
     uint32_t* d_remap = nullptr;    // the last growth's old -> new slot map
     uint4* d_char_call = nullptr;   // [table_cap] first update call of S s H h per slot (the merge's)
+    // timed contexts (FB_CFG_TIMED, fb_time.hip): the time plane, the next update's frame times, the
+    // capture-time pass's scratch (its last use: ev_tscratch)
+    bool timed = false;
+    FlowTime* d_time = nullptr;               // [table_cap]
+    const unsigned long long* next_ts = nullptr;
+    void* d_tscratch = nullptr;
+    uint64_t tscratch_bytes = 0;
+    hipEvent_t ev_tscratch = nullptr;
     void* d_mscratch = nullptr;     // multi-GPU merge scratch (export owner counts / merge tables)
     hipEvent_t ev_mscratch = nullptr;  // after the last export / merge that used d_mscratch (either may
                                        // run on any stream: the next use waits for it)
@@ -492,6 +500,11 @@ fb_ctx* fb_create(int device, const fb_config* cfg) {
              hipHostGetDevicePointer((void**)&c->d_mbox, c->h_mbox, 0) == hipSuccess;
         if (ok) memset(c->h_mbox, 0, sizeof(FlowMailbox));
         c->grow = (cfg->flags & FB_CFG_FIXED_TABLE) == 0u;
+        c->timed = (cfg->flags & FB_CFG_TIMED) != 0u;
+        if (ok && c->timed)
+            ok = hipMalloc(&c->d_time, cap * sizeof(FlowTime)) == hipSuccess &&
+                 hipMemset(c->d_time, 0, cap * sizeof(FlowTime)) == hipSuccess &&
+                 hipEventCreateWithFlags(&c->ev_tscratch, hipEventDisableTiming) == hipSuccess;
         ok = ok && ensure_flow_scratch(c, cfg->max_batch_packets, nullptr) == FB_OK;
     }
     ok = ok && upload_cfg(c, nullptr) == FB_OK;
@@ -520,6 +533,9 @@ int fb_destroy(fb_ctx* c) {
     hipFree(c->d_partials);
     hipFree(c->d_remap);
     hipFree(c->d_char_call);
+    hipFree(c->d_time);
+    hipFree(c->d_tscratch);
+    if (c->ev_tscratch) hipEventDestroy(c->ev_tscratch);
     hipFree(c->d_mscratch);
     if (c->ev_mscratch) hipEventDestroy(c->ev_mscratch);
     if (c->h_mbox) hipHostFree(c->h_mbox);
@@ -579,6 +595,21 @@ int fb_set_lan_v6(fb_ctx* c, const fb_lan_v6* nets, uint32_t n) {
 int fb_set_stage_event(fb_ctx* c, void* event) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     c->stage_event = (hipEvent_t)event;  // the caller's event (fb_event_create); not owned
+    return FB_OK;
+}
+
+int fb_set_frame_times(fb_ctx* c, const uint64_t* d_ts) {
+    if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
+    if (!c->timed) return set_err(FB_ERR_INVAL, "the context was created without FB_CFG_TIMED");
+    c->next_ts = reinterpret_cast<const unsigned long long*>(d_ts);
+    return FB_OK;
+}
+
+// Every update call of a timed context consumes the frame times set before it (checked before the
+// call's parse, so a refused call changes nothing).
+static int timed_ready(fb_ctx* c) {
+    if (c->timed && !c->next_ts)
+        return set_err(FB_ERR_INVAL, "a timed context needs fb_set_frame_times before each update call");
     return FB_OK;
 }
 
@@ -1233,6 +1264,9 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n too large");
     if (n && !in) return set_err(FB_ERR_INVAL, "NULL input");
+    if (c->d_table) {
+        if (int rc = timed_ready(c)) return rc;
+    }
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     int rc = ensure_staging(c, n, (uint64_t)n * sizeof(fb_parsed_pkt));
@@ -1263,6 +1297,7 @@ int fb_process_parsed(fb_ctx* c, const fb_parsed_pkt* in, uint32_t n, fb_pkt_out
 // An update call without records still counts as one (the high word of flow positions).
 static int empty_update(fb_ctx* c) {
     ++c->flow_batch;
+    c->next_ts = nullptr;
     c->last_recs = nullptr;
     c->last_part = nullptr;
     return FB_OK;
@@ -1311,7 +1346,22 @@ static int grow_table(fb_ctx* c, hipStream_t s, uint32_t k) {
     }
     HIP_TRY(launch_flow_grow(c->d_table, c->flow_parts, k, c->flow_shift - k, nw, c->d_remap, c->d_char_call, nw_cc,
                              s));
+    FlowTime* nw_time = nullptr;
+    if (c->timed) {  // the time records follow their flows' new slots
+        if (hipMalloc(&nw_time, cap * sizeof(FlowTime)) != hipSuccess) {
+            hipFree(nw);
+            hipFree(nw_cc);
+            free_new();
+            return set_err(FB_ERR_NOMEM, "grown time plane");
+        }
+        HIP_TRY(hipMemsetAsync(nw_time, 0, cap * sizeof(FlowTime), s));
+        HIP_TRY(launch_time_remap(c->d_time, c->d_remap, c->table_cap, nw_time, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
+    if (c->timed) {
+        hipFree(c->d_time);
+        c->d_time = nw_time;
+    }
     hipFree(c->d_table);
     hipFree(c->d_partials);
     hipFree(c->d_hcount);
@@ -1458,6 +1508,25 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     HIP_TRY(launch_flow_apply(p, chunks, s));
     HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), c->d_mbox,
                                ++c->upd_seq, s));
+    if (c->timed) {  // the capture-time pass over the placed records (fb_time.hip)
+        const uint32_t slots = p.max_recs < n_slots ? p.max_recs : n_slots;
+        uint32_t bits = 0;
+        while ((1ull << bits) < c->table_cap) ++bits;
+        const uint64_t need = time_scratch_bytes(slots, bits);
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_tscratch, 0));
+        if (need > c->tscratch_bytes) {
+            HIP_TRY(hipEventSynchronize(c->ev_tscratch));
+            hipFree(c->d_tscratch);
+            c->d_tscratch = nullptr;
+            c->tscratch_bytes = 0;
+            if (hipMalloc(&c->d_tscratch, need) != hipSuccess)
+                return set_err(FB_ERR_NOMEM, "capture-time scratch (%llu bytes)", (unsigned long long)need);
+            c->tscratch_bytes = need;
+        }
+        HIP_TRY(launch_time_update(p, slots, c->table_cap, c->d_time, c->next_ts, c->d_tscratch, s));
+        HIP_TRY(hipEventRecord(c->ev_tscratch, s));
+        c->next_ts = nullptr;
+    }
     ++c->flow_batch;
     c->last_set = set;
     c->last_recs = d_recs;
@@ -1472,13 +1541,24 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
 
 int fb_flow_update_dev(fb_ctx* c, const fb_pkt_out* d_recs, fb_batch_stats* d_stats, void* stream) {
     if (!c || !d_recs || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_recs and d_stats are required");
+    if (int rc = timed_ready(c)) return rc;
     return flow_update(c, d_recs, nullptr, c->last_n, d_stats, (hipStream_t)stream);
+}
+
+int fb_flow_update_records_dev(fb_ctx* c, const fb_pkt_out* d_recs, uint32_t max_n, fb_batch_stats* d_stats,
+                               void* stream) {
+    if (!c || !d_stats || (max_n && !d_recs)) return set_err(FB_ERR_INVAL, "ctx, d_recs and d_stats are required");
+    if (max_n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "max_n %u > FB_MAX_BATCH_PACKETS", max_n);
+    if (int rc = timed_ready(c)) return rc;
+    if (max_n == 0) return empty_update(c);
+    return flow_update(c, d_recs, nullptr, max_n, d_stats, (hipStream_t)stream);
 }
 
 int fb_flow_update_seg_dev(fb_ctx* c, const fb_pkt_out* d_out, const uint32_t* d_seg, uint32_t n,
                            fb_batch_stats* d_stats, void* stream) {
     if (!c || !d_out || !d_seg || !d_stats) return set_err(FB_ERR_INVAL, "ctx, d_out, d_seg and d_stats are required");
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (int rc = timed_ready(c)) return rc;
     if (n == 0) return empty_update(c);
     const uint32_t slots = (n + FB_SEG_FRAMES - 1) / FB_SEG_FRAMES * FB_SEG_FRAMES;
     return flow_update(c, d_out, d_seg, slots, d_stats, (hipStream_t)stream);
@@ -1489,7 +1569,8 @@ int fb_process_seg_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes
                        void* stream) {
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
-    int rc;
+    int rc = timed_ready(c);
+    if (rc) return rc;
     {
         DeviceGuard g(c->device);
         rc = maybe_grow(c, (hipStream_t)stream);  // before the parse writes partitions of this geometry
@@ -1512,6 +1593,7 @@ int fb_process_seg_async_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     if (n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "n %u > FB_MAX_BATCH_PACKETS", n);
+    if (int rc = timed_ready(c)) return rc;
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     if (!c->upd) {
@@ -1575,6 +1657,7 @@ int fb_process_dev(fb_ctx* c, const uint8_t* d_frames, uint64_t frames_bytes, co
     if (!c) return set_err(FB_ERR_INVAL, "ctx is NULL");
     if (!c->d_table) return set_err(FB_ERR_INVAL, "context was created without a flow table");
     if (!d_out) return set_err(FB_ERR_INVAL, "d_out is required");
+    if (int rc = timed_ready(c)) return rc;
     int rc = fb_parse_classify_dev(c, d_frames, frames_bytes, d_offsets, n, d_out, d_dns, d_class, d_stats, stream);
     if (rc) return rc;
     if (c->stage_event) HIP_TRY(hipEventRecord(c->stage_event, (hipStream_t)stream));
@@ -1727,7 +1810,43 @@ int fb_flow_export_sessions_dev(fb_ctx* c, uint32_t filter, fb_flow_rec* d_out, 
     int rc = join_updates(c, s);
     if (!rc && filter != FB_FILTER_ALL) rc = upload_cfg(c, s);  // the LAN configuration as of now
     if (rc) return rc;
-    HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s, filter, c->d_cfg));
+    HIP_TRY(launch_flow_export(c->d_table, c->table_cap, d_out, cap, (unsigned long long*)d_n, s, filter, c->d_cfg,
+                               c->d_time));
+    return FB_OK;
+}
+
+int fb_flow_export_times_dev(fb_ctx* c, fb_flow_time* d_out, uint64_t cap, uint64_t* d_n, void* stream) {
+    if (!c || !d_n || (cap && !d_out)) return set_err(FB_ERR_INVAL, "bad arguments");
+    if (!c->timed) return set_err(FB_ERR_INVAL, "the context was created without FB_CFG_TIMED");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(d_n, 0, 8, s));
+    int rc = join_updates(c, s);
+    if (rc) return rc;
+    HIP_TRY(launch_time_export(c->d_table, c->d_time, c->table_cap, d_out, cap, (unsigned long long*)d_n, s));
+    return FB_OK;
+}
+
+int fb_flow_export_times(fb_ctx* c, fb_flow_time* out, uint64_t cap, uint64_t* n, void* stream) {
+    if (!c || !n || (cap && !out)) return set_err(FB_ERR_INVAL, "bad arguments");
+    *n = 0;
+    if (!c->timed) return set_err(FB_ERR_INVAL, "the context was created without FB_CFG_TIMED");
+    if (cap == 0) return FB_OK;
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    fb_flow_time* d_out = nullptr;
+    if (hipMalloc(&d_out, cap * sizeof(fb_flow_time)) != hipSuccess) return set_err(FB_ERR_NOMEM, "export buffer");
+    unsigned long long h = 0;
+    int rc = fb_flow_export_times_dev(c, d_out, cap, reinterpret_cast<uint64_t*>(c->d_n), stream);
+    hipError_t e = rc ? hipSuccess : hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s);
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint64_t got = std::min<uint64_t>(h, cap);
+    if (!rc && e == hipSuccess && got) e = hipMemcpyAsync(out, d_out, got * sizeof(fb_flow_time), hipMemcpyDeviceToHost, s);
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(d_out);
+    if (rc) return rc;
+    if (e != hipSuccess) return set_err(FB_ERR_HIP, "time export: %s", hipGetErrorString(e));
+    *n = got;
     return FB_OK;
 }
 
@@ -1806,6 +1925,26 @@ int fb_flow_export_merge_map_dev(fb_ctx* c, uint32_t world, uint32_t rank, const
     return export_merge(c, world, rank, 0ull, call_map, n_calls, d_out, cap, d_counts, stream);
 }
 
+int fb_route_records_dev(fb_ctx* c, const fb_pkt_out* d_recs, const fb_batch_stats* d_stats, uint32_t max_n,
+                         uint32_t world, uint64_t shard_first, const uint64_t* d_ts, fb_pkt_out* d_out,
+                         uint64_t* d_ts_out, uint64_t* d_counts, void* stream) {
+    if (!c || !d_stats || !d_counts || (max_n && (!d_recs || !d_out)))
+        return set_err(FB_ERR_INVAL, "ctx, d_stats, d_counts, d_recs and d_out are required");
+    if (world == 0 || world > 64) return set_err(FB_ERR_INVAL, "1 <= world <= 64");
+    if (max_n > FB_MAX_BATCH_PACKETS) return set_err(FB_ERR_INVAL, "max_n > FB_MAX_BATCH_PACKETS");
+    if (shard_first + FB_MAX_BATCH_PACKETS > 0xFFFFFFFFull) return set_err(FB_ERR_INVAL, "shard_first too large");
+    if ((d_ts == nullptr) != (d_ts_out == nullptr)) return set_err(FB_ERR_INVAL, "d_ts and d_ts_out go together");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = ensure_mscratch(c, route_scratch_bytes(max_n, world), s);
+    if (rc) return rc;
+    HIP_TRY(launch_route(d_recs, d_stats, max_n, world, shard_first, reinterpret_cast<const unsigned long long*>(d_ts),
+                         d_out, reinterpret_cast<unsigned long long*>(d_ts_out), (unsigned long long*)d_counts,
+                         c->d_mscratch, s));
+    HIP_TRY(hipEventRecord(c->ev_mscratch, s));
+    return FB_OK;
+}
+
 int fb_flow_merge_dev(fb_ctx* c, const fb_flow_mrec* d_in, uint64_t n, fb_flow_rec* d_out, uint64_t* d_n,
                       void* stream) {
     if (!c || !d_n || (n && (!d_in || !d_out))) return set_err(FB_ERR_INVAL, "ctx, d_in, d_out and d_n are required");
@@ -1835,7 +1974,7 @@ int fb_flow_export_sessions(fb_ctx* c, uint32_t filter, fb_flow_rec* out, uint64
     if (hipMalloc(&d_out, m * sizeof(fb_flow_rec)) != hipSuccess) return set_err(FB_ERR_NOMEM, "export buffer");
     unsigned long long h = 0;
     hipError_t e = hipMemsetAsync(c->d_n, 0, 8, s);
-    if (e == hipSuccess) e = launch_flow_export(c->d_table, c->table_cap, d_out, m, c->d_n, s, filter, c->d_cfg);
+    if (e == hipSuccess) e = launch_flow_export(c->d_table, c->table_cap, d_out, m, c->d_n, s, filter, c->d_cfg, c->d_time);
     if (e == hipSuccess) e = hipMemcpyAsync(&h, c->d_n, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     const uint64_t got = std::min<uint64_t>(h, m);

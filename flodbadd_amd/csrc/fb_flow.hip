@@ -100,19 +100,6 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
     return t;
 }
 
-// Record slots of the batch: dense -> n_session of the parse launch (read on the device);
-// segmented -> every slot of every segment (invalid slots are skipped by slot_valid).
-__device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
-    // dense records whose offset scan expired (error bit 2, set only by k_seg_scan, which completes
-    // before K1 starts: every workgroup of K1 / K1c / K2 reads the same value) never reach the table
-    if (!P.seg && (__hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return 0u;
-    const unsigned long long n = P.seg ? (unsigned long long)P.n_slots : P.stats->n_session;
-    return (uint32_t)min(n, (unsigned long long)P.max_recs);
-}
-__device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
-    return !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
-}
-
 // A (chunk, partition) group of at least this many records (and 4x the chunk's mean) is combined
 // per key by k_flow_combine before K2.
 #ifndef FB_COMB_MIN
@@ -123,61 +110,6 @@ __device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
 #endif
 constexpr uint32_t kCombMin = FB_COMB_MIN;
 
-// An entry word's record as the four uint4 of a plain FlowEntry (fb_internal.h): key words, key word
-// 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char | tcp_flags
-// << 8 | has_flags << 16 | session flags << 20, the low word of the key's hash.  `rec` orders a
-// flow's packets: the record slot (entry word & kEntRecMask), or -- update entries from the fused
-// parse (P.ent; the word is unit index | IPv6 << 28) -- the pkt_index.  Records are 56 B, so only
-// 8-B aligned at odd slots: loaded through ld_u4 / ld_u2; an entry is one aligned 32-B unit (two
-// for an IPv6 key).  The raw words are loaded first (raw_entry) and decoded when applied
-// (entry_of), so K2 can keep loads in flight.
-__device__ __forceinline__ void raw_entry(const FlowParams& P, uint32_t w, uint4 (&r)[4]) {
-    if (P.ent) {
-        const uint4* u = P.ent + (size_t)(w & kEntUnitMask) * 2u;
-        r[0] = u[0];
-        r[1] = u[1];
-        if (w & kEntV6) {
-            r[2] = u[2];
-            r[3] = u[3];
-        } else {
-            r[2] = r[3] = make_uint4(0u, 0u, 0u, 0u);
-        }
-    } else {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (w & kEntRecMask));
-        r[0] = ld_u4(q);
-        r[1] = ld_u4(q + 4);
-        r[2] = ld_u4(q + 8);
-        const uint2 m = ld_u2(q + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
-        r[3] = make_uint4(m.x, m.y, 0u, 0u);
-    }
-}
-__device__ __forceinline__ void entry_of(bool ent, const uint4 (&r)[4], uint32_t w, uint4 (&e)[4]) {
-    if (ent) {  // UpdEnt units: A = r[0], B = r[1]; IPv6: r[2], r[3] (zero words for IPv4)
-        const uint4 A = r[0], Bw = r[1], C = r[2], D = r[3];
-        const uint32_t key[10] = {A.x, C.x, C.y, C.z, A.y, C.w, D.x, D.y, A.z, A.w & 0xFFFFu};
-        e[0] = make_uint4(key[0], key[1], key[2], key[3]);
-        e[1] = make_uint4(key[4], key[5], key[6], key[7]);
-        e[2] = make_uint4(A.z, A.w & 0x1FFFFu, Bw.x, Bw.y);
-        e[3] = make_uint4(Bw.z, Bw.z, Bw.w & 0x03FFFFFFu, (uint32_t)flow_hash_words(key));
-    } else {
-        const uint4 a = r[0], b = r[1], c = r[2];
-        const uint32_t mx = r[3].x, my = r[3].y;
-        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
-        const uint32_t meta = (mx >> 8) & 0xFFu;
-        const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
-        const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
-                               ((meta >> 3) & 0x1Fu) << 20;  // FB_META_LOCAL_SRC .. DST_SERVICE -> fb_session_flags
-        e[0] = a;
-        e[1] = b;
-        e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
-        e[3] = make_uint4(my, w & kEntRecMask, hinfo, (uint32_t)flow_hash_words(key));
-    }
-}
-__device__ __forceinline__ void rec_entry(const FlowParams& P, uint32_t w, uint4 (&e)[4]) {
-    uint4 r[4];
-    raw_entry(P, w, r);
-    entry_of(P.ent != nullptr, r, w, e);
-}
 // pkt_index of a combined group's first / last record `rec` (with entries rec IS the pkt_index)
 __device__ __forceinline__ uint32_t rec_pkt(const FlowParams& P, uint32_t rec) {
     if (P.ent) return rec;
@@ -1450,7 +1382,8 @@ __device__ __forceinline__ bool slot_local(const DevConfig* cfg, const FlowSlot&
 
 __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned long long cap,
                                                      fb_flow_rec* out, unsigned long long out_cap,
-                                                     unsigned long long* d_n, uint32_t filter, const DevConfig* cfg) {
+                                                     unsigned long long* d_n, uint32_t filter, const DevConfig* cfg,
+                                                     const FlowTime* plane) {
     __shared__ unsigned long long sh[4];
     __shared__ unsigned long long s_base;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
@@ -1470,7 +1403,14 @@ __global__ __launch_bounds__(256) void k_flow_export(const FlowSlot* T, unsigned
         __syncthreads();
         unsigned long long pos = s_base + __popcll(m & ((1ull << lane) - 1ull));
         for (uint32_t w = 0; w < wave; ++w) pos += sh[w];
-        if (occ && pos < out_cap) out[pos] = flow_rec_of(T[i], (uint32_t)i);
+        if (occ && pos < out_cap) {
+            fb_flow_rec r = flow_rec_of(T[i], (uint32_t)i);
+            if (plane) {  // a timed context: the segment state with the 5-s timeout (fb_time.hip)
+                r.segment_count = plane[i].segment_count;
+                r.in_segment = plane[i].in_segment;
+            }
+            out[pos] = r;
+        }
         __syncthreads();
     }
 }
@@ -1533,12 +1473,13 @@ hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k,
 }
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,
                               unsigned long long out_cap, unsigned long long* d_n, hipStream_t s, uint32_t filter,
-                              const DevConfig* cfg) {
+                              const DevConfig* cfg, const FlowTime* plane) {
     unsigned long long g = (cap + 255ull) / 256ull;
     if (g > 1024ull) g = 1024ull;
     if (g == 0ull) g = 1ull;
     if (!cfg) filter = FB_FILTER_ALL;
-    hipLaunchKernelGGL(k_flow_export, dim3((uint32_t)g), dim3(256), 0, s, table, cap, out, out_cap, d_n, filter, cfg);
+    hipLaunchKernelGGL(k_flow_export, dim3((uint32_t)g), dim3(256), 0, s, table, cap, out, out_cap, d_n, filter, cfg,
+                       plane);
     return hipGetLastError();
 }
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap, unsigned long long* d_n,

@@ -177,6 +177,9 @@ struct FlowSlot {
 constexpr uint32_t kStateInSegment = 1u << 14;  // hist_state: SessionStats.in_segment
 constexpr uint32_t kTcpPsh = 0x08u;             // TCP_PSH, src/packets.rs:26
 static_assert(sizeof(FlowSlot) == 128, "flow slot is 128 B");
+// Capture-time state per table slot on a timed context (the "time plane", fb_time.hip).
+using FlowTime = fb_flow_time;
+static_assert(sizeof(FlowTime) == 64, "one 64-B time record per slot");
 // Bucketed update entry (K1 -> K2): canonical key with the originator flag in bit 16 of
 // word 9 (the key's padding), L4 payload bytes, IP bytes, then the record's pkt_index, its
 // record slot (the batch order K2 orders the history by), hist_char | tcp_flags << 8 |
@@ -359,6 +362,75 @@ constexpr uint32_t kEntV6 = 1u << 28;               // index word: an IPv6 key (
 constexpr uint32_t kRecUnitShift = 16, kRecV6 = 1u << 23;  // rec_part fields
 __host__ __device__ inline bool upd_ent_v6(uint32_t a_w) { return ((a_w >> 8) & 0xFFu) == 10u; }
 
+// (shared by the table update, fb_flow.hip, and its capture-time pass, fb_time.hip)
+// Record slots of the batch: dense -> n_session of the parse launch (read on the device);
+// segmented -> every slot of every segment (invalid slots are skipped by slot_valid).
+__device__ __forceinline__ uint32_t batch_records(const FlowParams& P) {
+    // dense records whose offset scan expired (error bit 2, set only by k_seg_scan, which completes
+    // before K1 starts: every workgroup of K1 / K1c / K2 reads the same value) never reach the table
+    if (!P.seg && (__hip_atomic_load(P.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return 0u;
+    const unsigned long long n = P.seg ? (unsigned long long)P.n_slots : P.stats->n_session;
+    return (uint32_t)min(n, (unsigned long long)P.max_recs);
+}
+__device__ __forceinline__ bool slot_valid(const FlowParams& P, uint32_t i) {
+    return !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
+}
+
+// An entry word's record as the four uint4 of a plain FlowEntry (fb_internal.h): key words, key word
+// 9 | originator << 16, packet_length, ip_packet_length, then pkt_index, rec, hist_char | tcp_flags
+// << 8 | has_flags << 16 | session flags << 20, the low word of the key's hash.  `rec` orders a
+// flow's packets: the record slot (entry word & kEntRecMask), or -- update entries from the fused
+// parse (P.ent; the word is unit index | IPv6 << 28) -- the pkt_index.  Records are 56 B, so only
+// 8-B aligned at odd slots: loaded through ld_u4 / ld_u2; an entry is one aligned 32-B unit (two
+// for an IPv6 key).  The raw words are loaded first (raw_entry) and decoded when applied
+// (entry_of), so K2 can keep loads in flight.
+__device__ __forceinline__ void raw_entry(const FlowParams& P, uint32_t w, uint4 (&r)[4]) {
+    if (P.ent) {
+        const uint4* u = P.ent + (size_t)(w & kEntUnitMask) * 2u;
+        r[0] = u[0];
+        r[1] = u[1];
+        if (w & kEntV6) {
+            r[2] = u[2];
+            r[3] = u[3];
+        } else {
+            r[2] = r[3] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    } else {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + (w & kEntRecMask));
+        r[0] = ld_u4(q);
+        r[1] = ld_u4(q + 4);
+        r[2] = ld_u4(q + 8);
+        const uint2 m = ld_u2(q + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
+        r[3] = make_uint4(m.x, m.y, 0u, 0u);
+    }
+}
+__device__ __forceinline__ void entry_of(bool ent, const uint4 (&r)[4], uint32_t w, uint4 (&e)[4]) {
+    if (ent) {  // UpdEnt units: A = r[0], B = r[1]; IPv6: r[2], r[3] (zero words for IPv4)
+        const uint4 A = r[0], Bw = r[1], C = r[2], D = r[3];
+        const uint32_t key[10] = {A.x, C.x, C.y, C.z, A.y, C.w, D.x, D.y, A.z, A.w & 0xFFFFu};
+        e[0] = make_uint4(key[0], key[1], key[2], key[3]);
+        e[1] = make_uint4(key[4], key[5], key[6], key[7]);
+        e[2] = make_uint4(A.z, A.w & 0x1FFFFu, Bw.x, Bw.y);
+        e[3] = make_uint4(Bw.z, Bw.z, Bw.w & 0x03FFFFFFu, (uint32_t)flow_hash_words(key));
+    } else {
+        const uint4 a = r[0], b = r[1], c = r[2];
+        const uint32_t mx = r[3].x, my = r[3].y;
+        const uint32_t key[10] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y & 0xFFFFu};
+        const uint32_t meta = (mx >> 8) & 0xFFu;
+        const uint32_t orig = (meta & FB_META_ORIGINATOR) ? 1u : 0u;
+        const uint32_t hinfo = ((mx >> 16) & 0xFFu) | ((mx & 0xFFu) << 8) | ((meta & FB_META_HAS_FLAGS) ? 1u << 16 : 0u) |
+                               ((meta >> 3) & 0x1Fu) << 20;  // FB_META_LOCAL_SRC .. DST_SERVICE -> fb_session_flags
+        e[0] = a;
+        e[1] = b;
+        e[2] = make_uint4(c.x, (c.y & 0xFFFFu) | (orig << 16), c.z, c.w);
+        e[3] = make_uint4(my, w & kEntRecMask, hinfo, (uint32_t)flow_hash_words(key));
+    }
+}
+__device__ __forceinline__ void rec_entry(const FlowParams& P, uint32_t w, uint4 (&e)[4]) {
+    uint4 r[4];
+    raw_entry(P, w, r);
+    entry_of(P.ent != nullptr, r, w, e);
+}
 // Resident queue-fed parse (fb_seg_queue_*, k_parse_seg_queue): the host control block lives in
 // pinned, coherent host memory (the kernel reads it with system-scope loads); per ring slot the
 // device keeps the batch's stats words (tick, 8 per slot) and the count of blocks done with it.
@@ -467,9 +539,11 @@ hipError_t launch_flow_grow(const FlowSlot* old, uint32_t old_parts, uint32_t k,
                             uint32_t* remap, const uint4* old_cc, uint4* new_cc, hipStream_t s);
 // filter: fb_filter evaluated per flow at export time against `cfg` (is_local_session!,
 // src/sessions.rs:660-672); FB_FILTER_ALL (cfg may be null) exports every flow.
+// plane (timed contexts): segment_count / in_segment come from the flows' time records.
 hipError_t launch_flow_export(const FlowSlot* table, unsigned long long cap, fb_flow_rec* out,
                               unsigned long long out_cap, unsigned long long* d_n,
-                              hipStream_t s, uint32_t filter = FB_FILTER_ALL, const DevConfig* cfg = nullptr);
+                              hipStream_t s, uint32_t filter = FB_FILTER_ALL, const DevConfig* cfg = nullptr,
+                              const FlowTime* plane = nullptr);
 hipError_t launch_flow_count(const FlowSlot* table, unsigned long long cap,
                              unsigned long long* d_n, hipStream_t s);
 
@@ -483,11 +557,28 @@ hipError_t launch_merge_export(const FlowSlot* table, const uint4* char_call, un
                                uint32_t rank, unsigned long long shard_first, const unsigned long long* cmap,
                                fb_flow_mrec* out, unsigned long long out_cap, unsigned long long* d_counts,
                                void* scratch, hipStream_t s);
+// Routing: a rank's dense SESSION records (n_session of *stats, at most max_n) grouped by owner rank,
+// stable, pkt_index += shard_first; ts_out[j] = ts[the record's frame] when ts is given.
+uint64_t route_scratch_bytes(uint32_t max_n, uint32_t world);
+hipError_t launch_route(const fb_pkt_out* recs, const fb_batch_stats* stats, uint32_t max_n, uint32_t world,
+                        unsigned long long shard_first, const unsigned long long* ts, fb_pkt_out* out,
+                        unsigned long long* ts_out, unsigned long long* d_counts, void* scratch, hipStream_t s);
 // Merge: n records of one owner (every rank's group, rank order) -> one record per key in d_out (in
 // the order of each key's first record), *d_n (u64) = keys.  scratch: merge_scratch_bytes(n).
 uint64_t merge_scratch_bytes(unsigned long long n);
 hipError_t launch_merge(const fb_flow_mrec* in, unsigned long long n, fb_flow_rec* out, unsigned long long* d_n,
                         void* scratch, hipStream_t s);
+
+// Capture-time pass of a timed context's update (fb_time.hip): after K2, over the same FlowParams
+// (its record slots, n_slots of them), brings each touched flow's FlowTime forward; ts = the batch's
+// capture timestamps by frame index; scratch: time_scratch_bytes(n_slots, log2(cap)).
+uint64_t time_scratch_bytes(uint32_t n_slots, uint32_t cap_bits);
+hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t cap, FlowTime* plane,
+                              const unsigned long long* ts, void* scratch, hipStream_t s);
+hipError_t launch_time_remap(const FlowTime* old, const uint32_t* remap, unsigned long long old_cap, FlowTime* nw,
+                             hipStream_t s);
+hipError_t launch_time_export(const FlowSlot* table, const FlowTime* plane, unsigned long long cap, fb_flow_time* out,
+                              unsigned long long out_cap, unsigned long long* d_n, hipStream_t s);
 
 // Per-flow history characters of the last update (fb_hist.hip): the update's FlowParams (its
 // entries, transposed original rows, combined-group maps, per-slot counts) and the outputs.

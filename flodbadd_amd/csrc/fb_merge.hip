@@ -21,6 +21,8 @@
 // Every reduction is a sum / min / max / or, so the result does not depend on the order in which
 // the atomics land; each key's record is placed at the position of its first input record (a
 // prefix sum over "first record of its key" flags), so the output order is deterministic too.
+#include <algorithm>
+
 #include "fb_internal.h"
 
 namespace fbk {
@@ -168,6 +170,82 @@ hipError_t launch_merge_export(const FlowSlot* table, const uint4* char_call, un
     hipLaunchKernelGGL(k_mx_scan, dim3(1), dim3(1024), 0, s, cnt, chunks, world, d_counts);
     hipLaunchKernelGGL(k_mx_write, dim3(chunks), dim3(64), 0, s, table, char_call, cap, world, rank, shard_first, cmap,
                        cnt, out, out_cap);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Record routing (fb_route_records_dev): a rank's dense SESSION records grouped by the owner of their
+// key (stable: packet order inside a group), pkt_index made global (+ shard_first) and, with frame
+// times, each record's capture time beside it.  The same count / scan / write structure as the
+// export above, over records instead of table slots.
+__device__ __forceinline__ uint32_t rec_owner(const fb_pkt_out* R, unsigned long long i, uint32_t world) {
+    uint32_t key[10];
+    __builtin_memcpy(key, &R[i].key, 40);
+    key[9] &= 0xFFFFu;
+    return flow_owner(flow_hash_words(key), world);
+}
+
+__global__ __launch_bounds__(64) void k_rt_count(const fb_pkt_out* R, const fb_batch_stats* st, uint32_t max_n,
+                                                 uint32_t world, uint32_t* cnt) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long n = min((unsigned long long)st->n_session, (unsigned long long)max_n);
+    const unsigned long long c0 = (unsigned long long)blockIdx.x * kMxChunk;
+    uint32_t mine = 0u;
+    for (uint32_t j = 0; j < kMxChunk; j += 64u) {
+        const unsigned long long i = c0 + j + lane;
+        const uint32_t o = i < n ? rec_owner(R, i, world) : ~0u;
+        for (uint32_t w = 0; w < world; ++w) {
+            const uint32_t k = (uint32_t)__popcll(__ballot(o == w));
+            if (lane == w) mine += k;
+        }
+    }
+    if (lane < world) cnt[(size_t)blockIdx.x * world + lane] = mine;
+}
+
+__global__ __launch_bounds__(64) void k_rt_write(const fb_pkt_out* R, const fb_batch_stats* st, uint32_t max_n,
+                                                 uint32_t world, unsigned long long shard_first,
+                                                 const unsigned long long* ts, const uint32_t* off, fb_pkt_out* out,
+                                                 unsigned long long* ts_out) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long n = min((unsigned long long)st->n_session, (unsigned long long)max_n);
+    const unsigned long long c0 = (unsigned long long)blockIdx.x * kMxChunk;
+    uint32_t next = lane < world ? off[(size_t)blockIdx.x * world + lane] : 0u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t j = 0; j < kMxChunk; j += 64u) {
+        const unsigned long long i = c0 + j + lane;
+        const bool in = i < n;
+        const uint32_t o = in ? rec_owner(R, i, world) : ~0u;
+        uint32_t pos = 0u;
+        for (uint32_t w = 0; w < world; ++w) {
+            const unsigned long long m = __ballot(o == w);
+            const uint32_t base = (uint32_t)__shfl((int)next, (int)w, 64);
+            if (o == w) pos = base + (uint32_t)__popcll(m & lt);
+            if (lane == w) next += (uint32_t)__popcll(m);
+        }
+        if (in) {
+            fb_pkt_out r = R[i];
+            if (ts_out) ts_out[pos] = ts[r.pkt_index];
+            r.pkt_index = (uint32_t)(r.pkt_index + shard_first);
+            out[pos] = r;
+        }
+    }
+}
+
+uint64_t route_scratch_bytes(uint32_t max_n, uint32_t world) {
+    const unsigned long long chunks = ((unsigned long long)max_n + kMxChunk - 1) / kMxChunk;
+    return (std::max(chunks, 1ull) * world * 4ull + 255ull) & ~255ull;
+}
+
+hipError_t launch_route(const fb_pkt_out* recs, const fb_batch_stats* stats, uint32_t max_n, uint32_t world,
+                        unsigned long long shard_first, const unsigned long long* ts, fb_pkt_out* out,
+                        unsigned long long* ts_out, unsigned long long* d_counts, void* scratch, hipStream_t s) {
+    if (world == 0u || world > kMxMaxWorld) return hipErrorInvalidValue;
+    const uint32_t chunks = std::max<uint32_t>((uint32_t)(((unsigned long long)max_n + kMxChunk - 1) / kMxChunk), 1u);
+    uint32_t* cnt = static_cast<uint32_t*>(scratch);
+    hipLaunchKernelGGL(k_rt_count, dim3(chunks), dim3(64), 0, s, recs, stats, max_n, world, cnt);
+    hipLaunchKernelGGL(k_mx_scan, dim3(1), dim3(1024), 0, s, cnt, chunks, world, d_counts);
+    hipLaunchKernelGGL(k_rt_write, dim3(chunks), dim3(64), 0, s, recs, stats, max_n, world, shard_first, ts, cnt, out,
+                       ts_out);
     return hipGetLastError();
 }
 

@@ -342,6 +342,19 @@ uint8_t* fb_ring_reserve_block(fb_ring* r, uint32_t n, uint64_t bytes, uint32_t*
 
 int fb_ring_push(fb_ring* r, const uint8_t* frame, uint32_t caplen) {
     if (!r || (caplen && !frame)) return set_err(FB_ERR_INVAL, "bad arguments");
+    {
+        // the per-frame fast path: room in the filling batch -- no device call, so no device guard
+        // (hipGetDevice / hipSetDevice cost more than the 64-B copy)
+        RingSlot& s = r->slots[r->cur];
+        if (s.n < r->cfg.max_packets && s.bytes + caplen <= r->cfg.max_bytes) {
+            uint8_t* p = s.h_frames + s.bytes;
+            s.h_offsets[s.n++] = (uint32_t)s.bytes;
+            s.bytes += caplen;
+            r->seq++;
+            if (caplen) memcpy(p, frame, caplen);
+            return FB_OK;
+        }
+    }
     uint8_t* p = fb_ring_reserve(r, caplen);
     if (!p) return FB_ERR_INVAL;
     if (caplen) memcpy(p, frame, caplen);

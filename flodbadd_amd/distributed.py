@@ -200,3 +200,147 @@ def global_flow_table(dist, ctx, shard_first=0, device=None, group=None, as_tens
     if as_tensor:
         return table
     return np.ascontiguousarray(table.cpu().numpy()).view(FLOW_REC_DTYPE).reshape(-1)
+
+
+class RoutedSessionTable:
+    """The global session table with EVERY kind of session state exact -- the ordered history and
+    conn_state, and on a timed context the 5-s segment timeout and capture times, whose decisions
+    depend on each flow's previous packet wherever it was captured: records are routed to their key's
+    owner rank BEFORE the update (fb_route_records_dev), and each owner runs one update call per global
+    batch over every rank's records in rank (= global packet) order.  Owner o's table is then exactly
+    the single-table state of the flows o owns; `global_table` gathers them.
+
+    Per global batch: parse the rank's shard (fb_parse_classify_dev, dense records, no update), route
+    (owner groups, pkt_index made global, capture times beside them), all_to_all of the groups (RCCL
+    with device tensors, or gloo through host memory), the owner's update on what it received (frame
+    times scattered into a global-batch array by pkt_index).  Bytes per rank and batch: 56 B (+8 B of
+    time) per SESSION record out x (W-1)/W and about as much in -- a per-batch exchange of records,
+    where the merge of global_flow_table moves each flow once at the end; the price of exact ordered
+    state across ranks."""
+
+    def __init__(self, dist, capture, group=None, device=None):
+        import torch
+        self.dist, self.cap, self.group = dist, capture, group
+        self.dev = torch.device("cpu") if device is None else torch.device(device)
+        cdev = C.c_int(-1)
+        from . import _native as N
+        self.N, self.lib = N, N.gpu_lib()
+        N.check(self.lib.fb_ctx_device(capture.ctx, C.byref(cdev)))
+        self.gpu = torch.device("cuda", cdev.value)
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+
+    def process(self, frames, offsets, shard_first, global_n, ts=None, timing=None):
+        """One global batch: this rank's shard (host arrays `frames` / `offsets`, the frames
+        [shard_first, shard_first + n) of a global batch of `global_n` frames; ts: the shard's capture
+        times on a timed capture).  Every rank must call it for every global batch (an empty shard
+        too).  Returns this rank's batch stats (its parse's PACKET_STATS) as a dict."""
+        import time
+        import torch
+        N, lib, gpu = self.N, self.lib, self.gpu
+        t0 = time.perf_counter()
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n = offsets.size - 1
+        ctx = self.cap.ctx
+        d_fr = torch.from_numpy(frames if frames.size else np.zeros(1, np.uint8)).to(gpu)
+        d_of = torch.from_numpy(offsets.view(np.int32)).to(gpu)
+        recs = torch.empty((max(n, 1), 7), dtype=torch.int64, device=gpu)      # fb_pkt_out, 56 B
+        grouped = torch.empty_like(recs)
+        st = torch.zeros(N.STATS_DTYPE.itemsize // 8, dtype=torch.int64, device=gpu)
+        counts = torch.zeros(self.world, dtype=torch.int64, device=gpu)
+        timed = bool(getattr(self.cap, "timed", False))
+        if timed:
+            if ts is None or len(ts) < n:
+                raise ValueError("a timed capture needs the shard's capture times")
+            d_ts = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.uint64).view(np.int64)).to(gpu) if n else \
+                torch.zeros(1, dtype=torch.int64, device=gpu)
+            ts_out = torch.empty(max(n, 1), dtype=torch.int64, device=gpu)
+        torch.cuda.current_stream(gpu).synchronize()
+        p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        N.check(lib.fb_parse_classify_dev(ctx, p(d_fr), frames.nbytes, p(d_of), n, p(recs), None, None, p(st), None))
+        N.check(lib.fb_route_records_dev(ctx, p(recs), p(st), n, self.world, int(shard_first),
+                                         p(d_ts) if timed else None, p(grouped), p(ts_out) if timed else None,
+                                         p(counts), None))
+        N.check(lib.fb_stream_sync(None))
+        stats = np.frombuffer(st.cpu().numpy().tobytes(), dtype=N.STATS_DTYPE)
+        cnt = [int(x) for x in counts.tolist()]
+        m = sum(cnt)
+        t0 = _mark(timing, gpu, "route_ms", t0)
+        # all_to_all of the groups (and their capture times)
+        dev = self.dev
+        send = grouped[:m].to(dev)
+        if self.world > 1:
+            send_n = torch.tensor(cnt, dtype=torch.int64, device=dev)
+            recv_n = torch.empty_like(send_n)
+            self.dist.all_to_all_single(recv_n, send_n, group=self.group)
+            rn = [int(x) for x in recv_n.tolist()]
+            recv = torch.empty((sum(rn), 7), dtype=torch.int64, device=dev)
+            self.dist.all_to_all_single(recv, send, output_split_sizes=rn, input_split_sizes=cnt, group=self.group)
+            if timed:
+                rts = torch.empty(sum(rn), dtype=torch.int64, device=dev)
+                self.dist.all_to_all_single(rts, ts_out[:m].to(dev), output_split_sizes=rn, input_split_sizes=cnt,
+                                            group=self.group)
+        else:
+            recv = send
+            rts = ts_out[:m].to(dev) if timed else None
+        t0 = _mark(timing, dev if dev.type == "cuda" else gpu, "a2a_ms", t0)
+        # the owner's update: one call per global batch, its flows' packets in global order
+        k = int(recv.shape[0])
+        r_gpu = recv.to(gpu).contiguous() if k else torch.zeros((1, 7), dtype=torch.int64, device=gpu)
+        ust = torch.zeros(N.STATS_DTYPE.itemsize // 8, dtype=torch.int64, device=gpu)
+        ust[list(N.STATS_DTYPE.names).index("n_session")] = k  # (every stats field is a u64)
+        keep = None
+        if timed:
+            g_ts = torch.zeros(max(int(global_n), 1), dtype=torch.int64, device=gpu)
+            if k:
+                idx = (r_gpu[:, 6] >> 32) & 0xFFFFFFFF  # pkt_index: bytes 52..55 = the high half of word 6
+                g_ts[idx] = rts.to(gpu)
+            keep = g_ts
+        torch.cuda.current_stream(gpu).synchronize()
+        if timed:
+            N.check(lib.fb_set_frame_times(ctx, p(keep)))
+        N.check(lib.fb_flow_update_records_dev(ctx, p(r_gpu), k, p(ust), None))
+        N.check(lib.fb_stream_sync(None))
+        out = np.frombuffer(ust.cpu().numpy().tobytes(), dtype=N.STATS_DTYPE)
+        if int(out[0]["error"]):
+            raise N.FbError(N.FB_ERR_TABLE_FULL if int(out[0]["error"]) & 4 else N.FB_ERR_INTERNAL,
+                            "owner update error word %d" % int(out[0]["error"]))
+        _mark(timing, gpu, "update_ms", t0)
+        if timing is not None:
+            timing["records_out"] = timing.get("records_out", 0) + m - cnt[self.rank]
+        res = {k2: int(stats[0][k2]) for k2 in N.STATS_FIELDS if not k2.startswith("reserved")}
+        res["owner_new_sessions"] = int(out[0]["new_sessions"])
+        res["owner_records"] = k
+        return res
+
+    def global_table(self, with_times=False):
+        """Every owner's flows (fb_flow_rec; and with_times, fb_flow_time joined by slot), gathered on
+        every rank: owners in rank order."""
+        import torch
+        recs = self.cap.export_flows()
+        rows = [np.ascontiguousarray(recs).view(np.int64).reshape(len(recs), REC_WORDS)]
+        if with_times:
+            t = self.cap.export_times()
+            by = {int(x["slot"]): x for x in t}
+            tt = np.array([by[int(r["slot"])] for r in recs], dtype=self.N.FLOW_TIME_DTYPE) if len(recs) else \
+                np.zeros(0, dtype=self.N.FLOW_TIME_DTYPE)
+            rows.append(np.ascontiguousarray(tt).view(np.int64).reshape(len(tt), 8))
+        mine = torch.from_numpy(np.concatenate(rows, axis=1) if len(rows) > 1 else rows[0])
+        width = mine.shape[1]
+        if self.world == 1:
+            allr = mine
+        else:
+            n = torch.tensor([mine.shape[0]], dtype=torch.int64)
+            sizes = [torch.zeros_like(n) for _ in range(self.world)]
+            self.dist.all_gather(sizes, n, group=self.group)
+            sizes = [int(x.item()) for x in sizes]
+            pad = torch.zeros((max(sizes + [1]), width), dtype=torch.int64)
+            pad[: mine.shape[0]] = mine
+            got = [torch.zeros_like(pad) for _ in range(self.world)]
+            self.dist.all_gather(got, pad, group=self.group)
+            allr = torch.cat([g[:sz] for g, sz in zip(got, sizes)])
+        a = allr.numpy()
+        flows = np.ascontiguousarray(a[:, :REC_WORDS]).view(FLOW_REC_DTYPE).reshape(-1)
+        if not with_times:
+            return flows
+        return flows, np.ascontiguousarray(a[:, REC_WORDS:]).view(self.N.FLOW_TIME_DTYPE).reshape(-1)

@@ -115,6 +115,35 @@ class SessionStats:
     # no-timeout model: TCP packets with PSH counted, in a segment unless the latest packet had PSH
     segment_count: int = 0
     in_segment: bool = False
+    # timed contexts (fb_flow_time, FB_CFG_TIMED): capture times in ns since the epoch (the
+    # reference's DateTime<Utc> start_time / last_activity / end_time / current_segment_start /
+    # last_segment_end, src/sessions.rs:74-92) and the exact interarrival sum in ms; None untimed
+    start_time_ns: Optional[int] = None
+    last_activity_ns: Optional[int] = None
+    end_time_ns: Optional[int] = None
+    current_segment_start_ns: Optional[int] = None
+    last_segment_end_ns: Optional[int] = None
+    total_segment_interarrival_ms: int = 0
+    segment_interarrival_div: int = 0
+    segment_timeout: float = 5.0  # src/packets.rs:379
+
+    @property
+    def total_segment_interarrival(self):
+        """Seconds (f64), as src/packets.rs:166 accumulates it (from the exact integer ms sum)."""
+        return self.total_segment_interarrival_ms / 1000.0
+
+    @property
+    def segment_interarrival(self):
+        """src/packets.rs:167-171: the total over segment_count - 1 at the last accepted term."""
+        d = self.segment_interarrival_div
+        return self.total_segment_interarrival / d if d > 0 else 0.0
+
+    @property
+    def last_segment_end_set(self):
+        """last_segment_end.is_some(): timed, from the capture times; untimed, a segment has ended."""
+        if self.start_time_ns is not None:
+            return self.last_segment_end_ns is not None
+        return self.segment_count > 0
 
     @property
     def average_packet_size(self):
@@ -242,16 +271,23 @@ def histories_from_records(recs):
     return {k: (h, state.get(k)) for k, h in hist.items()}
 
 
-def flows_to_sessions(flows, histories=None):
+def flows_to_sessions(flows, histories=None, times=None):
     """fb_flow_rec records -> SessionInfo list sorted by the derived Ord of Session.  `histories`
     ({table slot: str}, FlodbaddGpuCapture.histories) supplies the history strings; the locality
     flags and dst_service come from fb_flow_rec.session_flags (stored at insert, src/packets.rs:
     429-466; dst_service = the key's dst port name, or its number for a port only a service table
-    set at run time names)."""
+    set at run time names).  `times` (timed contexts): FLOW_TIME_DTYPE records, either joined by
+    table slot (fb_flow_export_times) or, when every slot field is 0, one per flow in `flows` order."""
     if flows.dtype != FLOW_REC_DTYPE:
         raise TypeError("expected fb_flow_rec records (FLOW_REC_DTYPE), got %s" % flows.dtype)
+    tmap = None
+    if times is not None:
+        if len(times) == len(flows) and (len(times) == 0 or not times["slot"].any()):
+            tmap = {i: t for i, t in enumerate(times)}
+        else:
+            tmap = {int(t["slot"]): t for t in times}
     out = []
-    for r in flows:
+    for idx, r in enumerate(flows):
         end = int(r["end_seen"])
         st = SessionStats(int(r["inbound_bytes"]), int(r["outbound_bytes"]), int(r["orig_pkts"]),
                           int(r["resp_pkts"]), int(r["orig_ip_bytes"]), int(r["resp_ip_bytes"]),
@@ -259,6 +295,15 @@ def flows_to_sessions(flows, histories=None):
                           CONN_STATES[int(r["conn_state"])], int(r["first_seen"]), int(r["last_seen"]),
                           None if end == FB_SEEN_NONE else end, int(r["hist_len"]), int(r["segment_count"]),
                           bool(r["in_segment"]))
+        if tmap is not None:
+            t = tmap[idx] if (len(times) == len(flows) and (len(times) == 0 or not times["slot"].any())) \
+                else tmap[int(r["slot"])]
+            none = lambda v: None if int(v) == FB_SEEN_NONE else int(v)  # noqa: E731
+            st.start_time_ns, st.last_activity_ns = int(t["start_time_ns"]), int(t["last_activity_ns"])
+            st.end_time_ns, st.last_segment_end_ns = none(t["end_time_ns"]), none(t["last_segment_end_ns"])
+            st.current_segment_start_ns = int(t["current_segment_start_ns"])
+            st.total_segment_interarrival_ms = int(t["total_segment_interarrival_ms"])
+            st.segment_interarrival_div = int(t["segment_interarrival_div"])
         s = Session.from_key(r)
         f = int(r["session_flags"])
         svc = (service_name(s.dst_port) or str(s.dst_port)) if f & SESSION_DST_SERVICE else None

@@ -45,6 +45,8 @@ extern "C" {
 #define FB_SERVICE_BITMAP_BYTES 8192u
 #define FB_MAX_FLOW_CAPACITY (1ull << 25) /* slots: 65,536 partitions of 512 (4 GiB of table)   */
 #define FB_CFG_FIXED_TABLE 1u             /* fb_config.flags: never grow the flow table         */
+#define FB_CFG_TIMED 2u                   /* fb_config.flags: capture-time state (fb_flow_time);
+                                             every update call then needs fb_set_frame_times   */
 
 /* Return codes. */
 enum fb_err {
@@ -264,6 +266,34 @@ typedef struct fb_flow_rec {
                                 clock after the flow's last one (segment_timeout, src/packets.rs:
                                 137-149, 182-185); positions carry no clock.        */
 
+/* Capture-time state of a flow on a timed context (fb_config.flags FB_CFG_TIMED; per-frame capture
+ * timestamps handed to every update call with fb_set_frame_times).  The reference samples the wall
+ * clock per packet (`now = Utc::now()`, src/packets.rs:230) and keeps, per session, start_time,
+ * last_activity, end_time and the segment state (src/packets.rs:137-186 update, 352-380 + 414-426
+ * insert): a TCP packet with PSH ends a segment, and so does any packet arriving >= 5 s
+ * (segment_timeout, src/packets.rs:379) after the flow's previous one while a segment is open, which
+ * then opens a new segment at that packet.  Here `now` is the frame's capture timestamp (ns), so the
+ * state is a deterministic function of the input; chrono's num_milliseconds (truncation toward zero)
+ * is applied to the same differences.  segment_count / in_segment of fb_flow_rec carry the timed state
+ * on a timed context.  The reference accumulates total_segment_interarrival as an f64 running sum of
+ * (ms / 1000.0) terms; this keeps the exact integer sum of the ms terms (the f64 running sum differs
+ * from total_ms / 1000.0 by its own rounding, at most ~n ulp) and the divisor of the last accepted
+ * term, so segment_interarrival = total_ms / 1000.0 / div (0.0 when div is 0). */
+typedef struct fb_flow_time {
+    uint64_t start_time_ns;            /*  0: SessionStats.start_time (the insert packet's time)      */
+    uint64_t last_activity_ns;         /*  8: the flow's latest packet's time (arrival order)         */
+    uint64_t end_time_ns;              /* 16: first FIN/RST packet's time; FB_SEEN_NONE = None          */
+    uint64_t current_segment_start_ns; /* 24 */
+    uint64_t last_segment_end_ns;      /* 32: FB_SEEN_NONE = None                                       */
+    int64_t total_segment_interarrival_ms; /* 40: sum of the accepted segment interarrivals (ms)   */
+    uint32_t segment_interarrival_div; /* 48: segment_count - 1 when the last term was accepted      */
+    uint32_t segment_count;            /* 52: SessionStats.segment_count (timed)                       */
+    uint8_t in_segment;                /* 56 */
+    uint8_t reserved[3];               /* 57 */
+    uint32_t slot;                     /* 60: table slot (joins fb_flow_rec.slot)                      */
+} fb_flow_time;                        /* 64 bytes */
+#define FB_SEGMENT_TIMEOUT_MS 5000 /* segment_timeout: 5.0 s, src/packets.rs:379 */
+
 /* fb_flow_rec.session_flags (SessionInfo.is_local_src / is_local_dst / is_self_src / is_self_dst,
  * src/sessions.rs:40-61, set once at insert, src/packets.rs:429-435; bits 0-3 have the same values
  * as fb_enrich_bits) and FB_SESSION_DST_SERVICE: SessionInfo.dst_service is Some, i.e. the
@@ -293,6 +323,14 @@ int fb_set_own_ips(fb_ctx* ctx, const fb_ip* ips, uint32_t n);
  * (from fb_event_create, caller-owned; NULL clears) is set, fb_process_dev / fb_process_seg_dev
  * record it on their stream between the parse and the session-table update. */
 int fb_set_stage_event(fb_ctx* ctx, void* event);
+/* Timed contexts (FB_CFG_TIMED): the per-frame capture timestamps of the NEXT update call
+ * (fb_flow_update*_dev, fb_process*_dev incl. the async and parsed-packet forms, fb_process_parsed):
+ * d_ts[i] = frame i's capture time in ns since the Unix epoch (pcap header time, as the reference's
+ * Utc::now() would read it), indexed by the records' pkt_index -- a DEVICE pointer that must stay
+ * valid until that call's work completes on its stream (for fb_process_seg_async_dev: until
+ * fb_flow_join or a later call's wait on it).  Consumed by that call; an update call on a timed
+ * context without it fails with FB_ERR_INVAL before doing anything. */
+int fb_set_frame_times(fb_ctx* ctx, const uint64_t* d_ts);
 /* Test / diagnostic knobs of one context (never needed in production; each takes effect for the
  * next call): FB_DEBUG_DENSE_STEAL_POLLS -- the polls a dense look-back waits for a predecessor's
  * word before computing that tile's sums itself (default 4096; 0 forces the fallback path);
@@ -346,6 +384,12 @@ int fb_parse_classify(fb_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes,
  */
 int fb_flow_update_dev(fb_ctx* ctx, const fb_pkt_out* d_recs, fb_batch_stats* d_stats,
                        void* stream);
+/* The same for dense records that did not come from this context's last parse (records routed from
+ * other ranks, fb_route_records_dev; a host's own record buffer): max_n = a host bound of the count,
+ * the count itself is d_stats->n_session on the device (min with max_n).  max_n = 0 is an update
+ * call without records. */
+int fb_flow_update_records_dev(fb_ctx* ctx, const fb_pkt_out* d_recs, uint32_t max_n, fb_batch_stats* d_stats,
+                               void* stream);
 
 /*
  * Batched process_parsed_packet (src/packets.rs:202-537) without the decode: canonical key,
@@ -631,6 +675,11 @@ int fb_flow_slot_remap(fb_ctx* ctx, uint32_t* old_to_new, uint64_t cap, uint64_t
  * per-process key, src/sessions.rs:23 + dashmap RandomState, so it has no reproducible hash). */
 uint64_t fb_flow_hash(const fb_session_key* key);
 
+/* Every flow's fb_flow_time (timed contexts), with its table slot (join with fb_flow_rec.slot of an
+ * export: the orders differ).  Device form: asynchronous, *d_n = records; host form: synchronous. */
+int fb_flow_export_times_dev(fb_ctx* ctx, fb_flow_time* d_out, uint64_t cap, uint64_t* d_n, void* stream);
+int fb_flow_export_times(fb_ctx* ctx, fb_flow_time* out, uint64_t cap, uint64_t* n, void* stream);
+
 /* ---- multi-GPU session table (BASELINE configs[4]) ------------------------------
  * The reference runs one capture task per interface into ONE shared DashMap (src/capture.rs:946-1016,
  * src/packets.rs:329-535); W ranks that each parse a contiguous packet-index shard into their own
@@ -674,6 +723,22 @@ int fb_flow_export_merge_map_dev(fb_ctx* ctx, uint32_t world, uint32_t rank, con
  * (device u64) = keys.  d_out: room for n records.  DEVICE pointers, asynchronous. */
 int fb_flow_merge_dev(fb_ctx* ctx, const fb_flow_mrec* d_in, uint64_t n, fb_flow_rec* d_out, uint64_t* d_n,
                       void* stream);
+/* Routed global table (every kind of session state exact, the capture-time state of timed contexts
+ * included): instead of merging per-rank tables, each rank parses its shard (fb_parse_classify_dev,
+ * no update) and routes every SESSION record to the owner of its key BEFORE the update; the owner
+ * then runs ONE update call per global batch over what it received -- every rank's group in rank
+ * order, i.e. the flow's packets in global order -- so its table is exactly the single-table state of
+ * its flows (history, conn_state, timeouts).  This groups a rank's n_session (*d_stats, at most max_n)
+ * dense records by owner (stable), makes pkt_index global (+ shard_first: the index of the shard's
+ * first frame in the global batch), and with d_ts (the shard's frame times) writes each record's
+ * capture time to d_ts_out beside it; d_counts[world] = group sizes.  The host moves the groups
+ * (all-to-all), scatters the received times into a global-batch-sized array by pkt_index for
+ * fb_set_frame_times, and calls fb_flow_update_records_dev on the received records (with a stats
+ * struct whose n_session is their count; an owner that received none still makes the call, so update
+ * calls stay global batches).  DEVICE pointers, asynchronous. */
+int fb_route_records_dev(fb_ctx* ctx, const fb_pkt_out* d_recs, const fb_batch_stats* d_stats, uint32_t max_n,
+                         uint32_t world, uint64_t shard_first, const uint64_t* d_ts, fb_pkt_out* d_out,
+                         uint64_t* d_ts_out, uint64_t* d_counts, void* stream);
 /* The owner rank fb_flow_export_merge_dev assigns a key to. */
 uint32_t fb_flow_owner(const fb_session_key* key, uint32_t world);
 

@@ -58,6 +58,9 @@ def lib():
         L.orc_flows_free.argtypes = [P]
         L.orc_flows_clear.argtypes = [P]
         L.orc_flows_update.argtypes = [P, P, U64, P]
+        L.orc_flows_update_timed.argtypes = [P, P, U64, P, P]
+        L.orc_flows_export_times.restype = U64
+        L.orc_flows_export_times.argtypes = [P, P, P, U64]
         L.orc_flows_count.restype = U64
         L.orc_flows_count.argtypes = [P]
         L.orc_flows_export_sorted.restype = U64
@@ -189,10 +192,29 @@ class Flows:
     def __init__(self):
         self.h = C.c_void_p(lib().orc_flows_new())
 
-    def update(self, recs, stats=None):
+    def update(self, recs, stats=None, ts=None):
+        """One update call.  ts (timed tables): the batch's per-frame capture timestamps (uint64 ns,
+        indexed by pkt_index)."""
         recs = np.ascontiguousarray(recs, dtype=PKT_OUT_DTYPE)
-        lib().orc_flows_update(self.h, recs.ctypes.data if recs.size else None, recs.size,
-                               stats.ctypes.data if stats is not None else None)
+        if ts is None:
+            lib().orc_flows_update(self.h, recs.ctypes.data if recs.size else None, recs.size,
+                                   stats.ctypes.data if stats is not None else None)
+        else:
+            ts = np.ascontiguousarray(ts, dtype=np.uint64)
+            lib().orc_flows_update_timed(self.h, recs.ctypes.data if recs.size else None, recs.size,
+                                         stats.ctypes.data if stats is not None else None,
+                                         ts.ctypes.data if ts.size else None)
+        self._keep = ts
+
+    def export_times(self, with_ref=False):
+        """FLOW_TIME_DTYPE per flow in export_sorted order; with_ref: also the reference's own f64
+        (total_segment_interarrival, segment_interarrival) per flow, [F, 2]."""
+        from flodbadd_amd._native import FLOW_TIME_DTYPE
+        n = self.count()
+        out = np.zeros(max(n, 1), dtype=FLOW_TIME_DTYPE)
+        ref = np.zeros((max(n, 1), 2), dtype=np.float64)
+        m = lib().orc_flows_export_times(self.h, out.ctypes.data, ref.ctypes.data, n)
+        return (out[:m], ref[:m]) if with_ref else out[:m]
 
     def count(self):
         return lib().orc_flows_count(self.h)

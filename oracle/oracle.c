@@ -366,6 +366,9 @@ typedef struct orc_flow {
     int ended; /* end_time.is_some() */
     int used;
     uint32_t char_call[4]; /* update call of the first S, s, H, h (FB_CALL_NONE: none), for the merge */
+    fb_flow_time tm;       /* timed contexts: capture-time state (packets.rs:137-186, 352-426) */
+    double ref_total_s;    /* the reference's own f64 running sum total_segment_interarrival */
+    double ref_ia_s;       /* and its segment_interarrival */
 } orc_flow;
 
 struct orc_flows {
@@ -442,19 +445,65 @@ static uint32_t hist_bit(char c) {
     return (c && p) ? (uint32_t)(p - FB_HIST_CHARS) : 16u;
 }
 
-static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st);
+static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st, const uint64_t* ts);
 
 void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* st) {
-    for (uint64_t i = 0; i < n; ++i) flow_upsert(f, &recs[i], st);
+    for (uint64_t i = 0; i < n; ++i) flow_upsert(f, &recs[i], st, NULL);
     f->batch++;
 }
 
-/* One SessionPacketData through the DashMap upsert (src/packets.rs:329-535). */
-static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
+void orc_flows_update_timed(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* st,
+                            const uint64_t* ts) {
+    for (uint64_t i = 0; i < n; ++i) flow_upsert(f, &recs[i], st, ts);
+    f->batch++;
+}
+
+/* (now - then).num_milliseconds(): chrono's TimeDelta between two instants, truncated toward zero
+ * (timestamps are ns since an epoch, as i64 -- DateTime<Utc>'s range) */
+static int64_t ms_between(uint64_t now, uint64_t then) { return ((int64_t)now - (int64_t)then) / 1000000; }
+
+/* The segment state of update_session_stats (src/packets.rs:137-186) at capture time `now`. */
+static void segment_update(orc_flow* s, int tcp_psh, uint64_t now) {
+    fb_flow_time* t = &s->tm;
+    const double since_s = (double)ms_between(now, t->last_activity_ns) / 1000.0; /* 138 */
+    const int timeout = since_s >= 5.0;                                              /* segment_timeout */
+    const int is_end = tcp_psh || (t->in_segment && timeout);                       /* 140-149 */
+    if (!t->in_segment) {                                                            /* 151-154 */
+        t->in_segment = 1;
+        t->current_segment_start_ns = now;
+    }
+    if (is_end && t->in_segment) {                                                   /* 156-186 */
+        const uint64_t prev = t->last_segment_end_ns;
+        t->segment_count += 1;
+        t->in_segment = 0;
+        t->last_segment_end_ns = now;
+        if (prev != FB_SEEN_NONE) {
+            const int64_t ia_ms = ms_between(t->current_segment_start_ns, prev);
+            const double seg_ia = (double)ia_ms / 1000.0;
+            if (seg_ia >= 0.0) {
+                t->total_segment_interarrival_ms += ia_ms;
+                s->ref_total_s += seg_ia;
+                s->ref_ia_s = t->segment_count > 1 ? s->ref_total_s / (double)(t->segment_count - 1) : 0.0;
+                t->segment_interarrival_div = t->segment_count > 1 ? t->segment_count - 1 : 0;
+            } /* else: warn! and skip (src/packets.rs:172-179) */
+        }
+        if (timeout) {
+            t->in_segment = 1;
+            t->current_segment_start_ns = now;
+        }
+    }
+    t->last_activity_ns = now; /* 189 */
+}
+
+/* One SessionPacketData through the DashMap upsert (src/packets.rs:329-535); `ts` (timed): the
+ * batch's per-frame capture timestamps, ts[pkt_index] = the packet's `now`. */
+static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st, const uint64_t* ts) {
     {
         if ((f->count + 1) * 2 > f->cap) grow(f);
         orc_flow* s = find_slot(f->slots, f->cap, &r->key);
         const uint64_t pos = ((uint64_t)f->batch << 32) | r->pkt_index; /* stands for `now` */
+        const int tcp_psh = (r->meta & FB_META_HAS_FLAGS) && r->key.protocol == 6 && (r->tcp_flags & TCP_PSH);
+        const int inserted = !s->used;
         if (!s->used) { /* Entry::Vacant, src/packets.rs:344 */
             memset(s, 0, sizeof(*s));
             s->used = 1;
@@ -479,13 +528,33 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
             s->rec.resp_pkts += 1;
             s->rec.resp_ip_bytes += r->ip_packet_length;
         }
-        /* segment detection without the wall-clock timeout (src/packets.rs:137-160 update, 370-376 and
-           414-420 insert): a TCP packet with PSH ends the segment -- segment_count += 1, in_segment =
-           false --; any other packet leaves the flow in a segment (a new one starts when it was not) */
-        {
-            const int psh = (r->meta & FB_META_HAS_FLAGS) && r->key.protocol == 6 && (r->tcp_flags & TCP_PSH);
-            if (psh) s->rec.segment_count += 1;
-            s->rec.in_segment = psh ? 0 : 1;
+        if (!ts) {
+            /* segment detection without the wall-clock timeout (src/packets.rs:137-160 update, 370-376
+               and 414-420 insert): a TCP packet with PSH ends the segment -- segment_count += 1,
+               in_segment = false --; any other packet leaves the flow in a segment (a new one starts
+               when it was not) */
+            if (tcp_psh) s->rec.segment_count += 1;
+            s->rec.in_segment = tcp_psh ? 0 : 1;
+        } else {
+            const uint64_t now = ts[r->pkt_index];
+            fb_flow_time* t = &s->tm;
+            if (inserted) { /* SessionStats at insert (src/packets.rs:352-380, 414-420) */
+                t->start_time_ns = t->last_activity_ns = t->current_segment_start_ns = now;
+                t->end_time_ns = t->last_segment_end_ns = FB_SEEN_NONE;
+                t->in_segment = 1;
+                if (tcp_psh) {
+                    t->segment_count = 1;
+                    t->in_segment = 0;
+                    t->last_segment_end_ns = now;
+                }
+            } else {
+                segment_update(s, tcp_psh, now);
+            }
+            /* end_time at the first FIN/RST (src/packets.rs:195-198, 423-426) */
+            if ((r->meta & FB_META_HAS_FLAGS) && (r->tcp_flags & (TCP_FIN | TCP_RST)) && t->end_time_ns == FB_SEEN_NONE)
+                t->end_time_ns = now;
+            s->rec.segment_count = t->segment_count;
+            s->rec.in_segment = t->in_segment;
         }
         if (r->meta & FB_META_HAS_FLAGS) { /* history push, src/packets.rs:187-198, 410-426 */
             if (s->hist_len + 1 > s->hist_cap) {
@@ -509,6 +578,24 @@ static void flow_upsert(orc_flows* f, const fb_pkt_out* r, fb_batch_stats* st) {
 }
 
 uint64_t orc_flows_count(const orc_flows* f) { return f->count; }
+
+uint64_t orc_flows_export_times(const orc_flows* f, fb_flow_time* out, double* ref_f64, uint64_t cap) {
+    /* in the order of orc_flows_export_sorted (derived Ord of the keys) */
+    fb_flow_rec* recs = (fb_flow_rec*)malloc((f->count ? f->count : 1) * sizeof(fb_flow_rec));
+    const uint64_t m = orc_flows_export_sorted(f, recs, f->count);
+    uint64_t k = 0;
+    for (; k < m && k < cap; ++k) {
+        const orc_flow* s = find_slot(f->slots, f->cap, &recs[k].key);
+        out[k] = s->tm;
+        out[k].slot = 0;
+        if (ref_f64) {
+            ref_f64[2 * k] = s->ref_total_s;
+            ref_f64[2 * k + 1] = s->ref_ia_s;
+        }
+    }
+    free(recs);
+    return k;
+}
 
 static int ip_cmp(uint32_t fam, const uint32_t* a, const uint32_t* b) {
     int nw = fam == 2 ? 1 : 4;
@@ -1145,7 +1232,7 @@ uint64_t orc_pipeline_mt(const orc_cfg* c, orc_flows** tables, int threads, cons
         for (uint32_t i = a; i < b; ++i) idx[cnt[(size_t)t * T + own[i]]++] = i;
 #pragma omp barrier
         memset(&ts[t], 0, sizeof(ts[t]));
-        for (uint64_t k = beg[t]; k < beg[t + 1]; ++k) flow_upsert(tables[t], &scratch[idx[k]], &ts[t]);
+        for (uint64_t k = beg[t]; k < beg[t + 1]; ++k) flow_upsert(tables[t], &scratch[idx[k]], &ts[t], NULL);
         tables[t]->batch++;
     }
     for (int t = 0; t < T; ++t) {

@@ -89,6 +89,13 @@ void orc_flows_clear(orc_flows* f);
 /* Upsert records in order; adds new/updated counts into stats (may be NULL). */
 /* One call = one flow-table update (the high word of fb_flow_rec positions, FB_SEEN_NONE etc.). */
 void orc_flows_update(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* stats);
+/* The same with capture timestamps (ts[pkt_index] ns): segment state with the 5-s timeout and the
+ * capture-time fields of fb_flow_time (src/packets.rs:137-200, 352-426). */
+void orc_flows_update_timed(orc_flows* f, const fb_pkt_out* recs, uint64_t n, fb_batch_stats* stats,
+                            const uint64_t* ts);
+/* fb_flow_time per flow in orc_flows_export_sorted order (slot 0); ref_f64 (optional, 2 per flow):
+ * the reference's own f64 total_segment_interarrival and segment_interarrival. */
+uint64_t orc_flows_export_times(const orc_flows* f, fb_flow_time* out, double* ref_f64, uint64_t cap);
 uint64_t orc_flows_count(const orc_flows* f);
 /* Export sorted by the derived Ord of Session (src/sessions.rs:23-30). Returns count. */
 uint64_t orc_flows_export_sorted(const orc_flows* f, fb_flow_rec* out, uint64_t cap);

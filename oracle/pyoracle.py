@@ -163,9 +163,12 @@ class SessionTable:
         self.new = 0
         self.updated = 0
 
-    def process(self, c):
+    def process(self, c, now=None):
+        """now: the packet's capture time in ns (timed state: the 5-s segment timeout and the
+        capture-time fields, src/packets.rs:137-200, 352-426), or None (positional model)."""
         key = c["key"]
         s = self.sessions.get(key)
+        inserted = s is None
         if s is None:
             # is_local_src/dst and is_self_src/dst are stored once, at insert (src/packets.rs:429-435)
             s = dict(outbound_bytes=0, inbound_bytes=0, orig_pkts=0, resp_pkts=0, orig_ip_bytes=0,
@@ -181,17 +184,55 @@ class SessionTable:
         s[side[0]] += c["plen"]
         s[side[1]] += 1
         s[side[2]] += c["iplen"]
-        # segment end on TCP PSH (src/packets.rs:140-160 / 414-420; no wall-clock timeout here)
         psh = c["flags"] is not None and c["key"][0] == 6 and bool(c["flags"] & PSH)
-        s["segment_count"] += 1 if psh else 0
-        s["in_segment"] = not psh
+        if now is None:
+            # segment end on TCP PSH (src/packets.rs:140-160 / 414-420; no wall-clock timeout here)
+            s["segment_count"] += 1 if psh else 0
+            s["in_segment"] = not psh
+        elif inserted:  # src/packets.rs:352-380, 414-420
+            s.update(start=now, last=now, end=None, seg_start=now, seg_end=None, ia_total=0.0, ia=0.0,
+                     ia_ms=0, div=0, in_segment=not psh, segment_count=1 if psh else 0)
+            if psh:
+                s["seg_end"] = now
+        else:  # update_session_stats, src/packets.rs:137-189
+            def ms(a, b):  # chrono num_milliseconds: truncation toward zero
+                d = a - b
+                return d // 1000000 if d >= 0 else -((-d) // 1000000)
+            timeout = ms(now, s["last"]) / 1000.0 >= 5.0
+            is_end = psh or (s["in_segment"] and timeout)
+            if not s["in_segment"]:
+                s["in_segment"], s["seg_start"] = True, now
+            if is_end and s["in_segment"]:
+                prev = s["seg_end"]
+                s["segment_count"] += 1
+                s["in_segment"], s["seg_end"] = False, now
+                if prev is not None:
+                    ia_ms = ms(s["seg_start"], prev)
+                    if ia_ms / 1000.0 >= 0.0:
+                        s["ia_total"] += ia_ms / 1000.0
+                        s["ia_ms"] += ia_ms
+                        s["div"] = s["segment_count"] - 1 if s["segment_count"] > 1 else 0
+                        s["ia"] = s["ia_total"] / (s["segment_count"] - 1) if s["segment_count"] > 1 else 0.0
+                if timeout:
+                    s["in_segment"], s["seg_start"] = True, now
+            s["last"] = now
+        if now is not None and c["flags"] is not None and c["flags"] & (FIN | RST) and s["end"] is None:
+            s["end"] = now
         if c["flags"] is not None:
             s["history"] += c["hist"]
             if c["flags"] & (FIN | RST) and s["conn_state"] is None:
                 s["conn_state"] = conn_state(s["history"])
 
 
-def run_batch(cfg, frames, offsets, table=None):
+def table_times(table):
+    """Timed SessionTable -> {key: fb_flow_time fields}: start, last, end (None), segment start, last
+    segment end (None), total interarrival (integer ms and the f64 running sum), divisor, segment
+    count, in_segment."""
+    return {k: (s["start"], s["last"], s["end"], s["seg_start"], s["seg_end"], s["ia_ms"], s["ia_total"], s["div"],
+                s["segment_count"], s["in_segment"]) for k, s in table.sessions.items()}
+
+
+def run_batch(cfg, frames, offsets, table=None, ts=None):
     """Whole-batch restatement: per frame class + emitted session records (dicts) + dns tuples."""
     classes, records, dns = [], [], []
     stats = dict(total_processed=0, tcp_processed=0, udp_processed=0, ipv4_processed=0, ipv6_processed=0,
@@ -226,7 +267,7 @@ def run_batch(cfg, frames, offsets, table=None):
                 stats["n_session"] += 1
                 records.append(c)
                 if table is not None:
-                    table.process(c)
+                    table.process(c, None if ts is None else int(ts[i]))
     return classes, records, dns, stats
 
 

@@ -32,11 +32,22 @@ def key_of(k):
     return Session(Protocol[k[0]], ipaddress.ip_address(k[1]), k[2], ipaddress.ip_address(k[3]), k[4])
 
 
-def check_case(case, records, flows, histories=None):
+def times_of(case, base_ns=1_700_000_000 * 10**9):
+    """Timed cases: the per-packet capture timestamps (ns) of the reference test's sleeps
+    (packets[i]["t_ms"] ms after a fixed epoch instant), indexed like the packets; None untimed."""
+    if not case.get("timed"):
+        return None
+    import numpy as np
+    return np.array([base_ns + int(round(p["t_ms"] * 1e6)) for p in case["packets"]], dtype=np.uint64)
+
+
+def check_case(case, records, flows, histories=None, times=None):
     """Assert everything the reference asserts for this case.  The flow table's ordered state
     (hist_len, conn_state) must agree with the history derived from the packet-ordered records;
     `histories` ({table slot: str}, from fb_flow_history_dev) is checked against it too."""
-    sess = {i.session: i for i in flows_to_sessions(flows, histories=histories)}
+    if case.get("timed") and times is None:
+        raise AssertionError("%s: a timed case needs the flows' capture-time records" % case["name"])
+    sess = {i.session: i for i in flows_to_sessions(flows, histories=histories, times=times)}
     hist = histories_from_records(records)
     for k, info in sess.items():
         h, cs = hist.get(k, ("", None))
@@ -66,7 +77,13 @@ def check_case(case, records, flows, histories=None):
         if "in_segment" in e:
             assert st.in_segment == e["in_segment"], (name, "in_segment", st.in_segment)
         if "last_segment_end_set" in e:
-            assert (st.segment_count > 0) == e["last_segment_end_set"], (name, "last_segment_end", st.segment_count)
+            assert st.last_segment_end_set == e["last_segment_end_set"], (name, "last_segment_end", st.segment_count)
+        if "segment_interarrival_gt" in e:
+            assert st.segment_interarrival > e["segment_interarrival_gt"], (name, "interarrival", st.segment_interarrival)
+        if "segment_interarrival_ge" in e:
+            assert st.segment_interarrival >= e["segment_interarrival_ge"], (name, "interarrival", st.segment_interarrival)
+        if "end_time_set" in e:
+            assert (st.end_time_ns is not None) == e["end_time_set"], (name, "end_time", st.end_time_ns)
         h, cs = hist.get(k, ("", None))
         if "history" in e:
             assert h == e["history"], (name, h)

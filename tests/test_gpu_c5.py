@@ -261,3 +261,68 @@ def test_two_process_gloo_device_merge(tmp_path, layout):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r)).view(N.FLOW_REC_DTYPE)
         assert len(got) == len(ref), (r, len(got), len(ref))
         assert _rows(got).tobytes() == _rows(ref).tobytes(), r
+
+
+def _routed_child(rank, world, port, outdir):
+    """Rank `rank` of a gloo group on GPU 0 with a TIMED context: each global batch of SIZES is parsed
+    shard by shard, every record routed to its key's owner (fb_route_records_dev) and applied there
+    with its capture time (flodbadd_amd.distributed.RoutedSessionTable)."""
+    import torch
+    import torch.distributed as dist
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.distributed import RoutedSessionTable
+    from flodbadd_amd.sessions import SessionFilter
+    from test_gpu_timed import frame_times
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 16, timed=True)
+    try:
+        rt = RoutedSessionTable(dist, cap)
+        for k, size in enumerate(SIZES):
+            first, count = shard_range(size, rank, world)
+            fr, of = _sched_batch(k, first, count)
+            ts = frame_times(size, seed=50 + k, call=k)[first: first + count]
+            rt.process(fr, of, first, size, ts=ts)
+        flows, times = rt.global_table(with_times=True)
+        np.save(os.path.join(outdir, "f%d.npy" % rank), flows.view(np.uint8))
+        np.save(os.path.join(outdir, "t%d.npy" % rank), times.view(np.uint8))
+    finally:
+        cap.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_process_routed_timed_global_table(tmp_path):
+    """The routed global table (records to their key's owner before the update) on timed contexts,
+    two processes over gloo: with unequal batches and an empty shard, every rank's gathered table --
+    counters, positions, history length / set, conn_state and every capture-time field incl. the
+    5-s segment timeout -- equals ONE timed oracle table fed the global stream, byte for byte."""
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_gpu_timed import frame_times
+    world = 2
+    mp.start_processes(_routed_child, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    fl = coracle.Flows()
+    for k, size in enumerate(SIZES):
+        fr, of = _sched_batch(k, 0, size)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+        fl.update(out, ts=frame_times(size, seed=50 + k, call=k))
+    er, et = fl.export_sorted(), fl.export_times()
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "f%d.npy" % r)).view(N.FLOW_REC_DTYPE)
+        gt = np.load(os.path.join(tmp_path, "t%d.npy" % r)).view(N.FLOW_TIME_DTYPE)
+        assert len(got) == len(er) == len(gt), (r, len(got), len(er))
+        order = np.lexsort(np.ascontiguousarray(got).view(np.uint8).reshape(len(got), -1)[:, :40].T[::-1])
+        got, gt = got[order], gt[order]
+        eo = np.lexsort(np.ascontiguousarray(er).view(np.uint8).reshape(len(er), -1)[:, :40].T[::-1])
+        e_r, e_t = er[eo], et[eo]
+        got = got.copy()
+        got["slot"] = 0
+        e_r = e_r.copy()
+        e_r["slot"] = 0
+        gt = gt.copy()
+        gt["slot"] = 0
+        assert got.tobytes() == e_r.tobytes(), r
+        assert gt.tobytes() == e_t.tobytes(), r
+    assert (et["segment_count"] > 0).any() and (et["end_time_ns"] != N.FB_SEEN_NONE).any()

@@ -156,7 +156,10 @@ from flodbadd_amd.sessions import packets_to_parsed  # noqa: E402
 _KATS = kat.load()
 
 
-@pytest.mark.parametrize("case", _KATS["cases"], ids=[c["name"] for c in _KATS["cases"]])
+_UNTIMED = [c for c in _KATS["cases"] if not c.get("timed")]  # (timed cases: tests/test_gpu_timed.py)
+
+
+@pytest.mark.parametrize("case", _UNTIMED, ids=[c["name"] for c in _UNTIMED])
 def test_reference_kat_on_gpu(gpu_capture, case):
     """process_parsed_packet KATs (src/packets.rs, tests/metrics_test.rs, src/capture.rs) on the
     GPU: keys, counters, derived f64s, history; records byte-identical to the oracle's."""

@@ -20,16 +20,60 @@ def oracle_process(case):
     recs, cls, st = coracle.process_parsed(cfg, packets_to_parsed(kat.packets_of(case)))
     flows = coracle.Flows()
     fst = np.zeros(1, dtype=N.STATS_DTYPE)
-    flows.update(recs, fst)
+    flows.update(recs, fst, ts=kat.times_of(case))
     return recs, flows, st
 
 
 @pytest.mark.parametrize("case", KATS["cases"], ids=[c["name"] for c in KATS["cases"]])
 def test_oracle_reference_kat(case):
     recs, flows, st = oracle_process(case)
-    kat.check_case(case, recs, flows.export_sorted())
+    kat.check_case(case, recs, flows.export_sorted(), times=flows.export_times() if case.get("timed") else None)
     # PACKET_STATS counts every packet before the filter (src/packets.rs:211-227)
     assert int(st[0]["total_processed"]) == len(case["packets"])
+
+
+TIMED = [c for c in KATS["cases"] if c.get("timed")]
+
+
+def test_timed_cases_present():
+    """The clock-dependent asserts are transcribed: the >= 5 s gap (TCP and UDP) and the interarrival."""
+    names = {c["name"] for c in TIMED}
+    assert {"test_packet_statistics/timed_final", "test_udp_segment_timeout/timed_after_pkt2"} <= names
+    final = next(c for c in TIMED if c["name"] == "test_packet_statistics/timed_final")
+    assert final["expect"]["sessions"][0]["segment_count"] == 2
+
+
+@pytest.mark.parametrize("case", TIMED, ids=[c["name"] for c in TIMED])
+def test_timed_kat_c_oracle_equals_python_oracle(case):
+    """The C restatement's capture-time state equals the independent Python restatement's
+    (pyoracle.SessionTable with `now`), field by field -- and its exact integer interarrival sum in
+    ms / 1000 equals the reference's own f64 running sum (both restatements keep it) to 1e-12 s."""
+    from flodbadd_amd.sessions import Session
+    recs, flows, _ = oracle_process(case)
+    ts = kat.times_of(case)
+    t, ref = flows.export_times(with_ref=True)
+    fr = flows.export_sorted()
+    table = pyoracle.SessionTable()
+    for i, p in enumerate(kat.packets_of(case)):
+        pc = pyoracle.Config.from_bitmap(coracle.default_bitmap(), session_filter=int(kat.filter_of(case)),
+                                         own_ips=case["own_ips"])
+        import ipaddress
+        c = pyoracle.classify(pc, ("tcp" if int(p.session.protocol) == 6 else "udp", int(p.session.protocol),
+                                   p.session.src_ip, p.session.src_port, p.session.dst_ip, p.session.dst_port,
+                                   p.packet_length, p.ip_packet_length, p.flags))
+        if c["klass"] != "filtered":
+            table.process(c, int(ts[i]))
+    py = pyoracle.table_times(table)
+    none = lambda v: None if int(v) == N.FB_SEEN_NONE else int(v)  # noqa: E731
+    for r, x, (rt, ri) in zip(fr, t, ref):
+        k = Session.from_key(r)
+        e = py[(int(k.protocol), k.src_ip, k.src_port, k.dst_ip, k.dst_port)]
+        got = (int(x["start_time_ns"]), int(x["last_activity_ns"]), none(x["end_time_ns"]),
+               int(x["current_segment_start_ns"]), none(x["last_segment_end_ns"]),
+               int(x["total_segment_interarrival_ms"]), e[6], int(x["segment_interarrival_div"]),
+               int(x["segment_count"]), bool(x["in_segment"]))
+        assert got == e, (case["name"], got, e)
+        assert abs(rt - e[6]) <= 1e-12 and abs(int(x["total_segment_interarrival_ms"]) / 1000.0 - rt) <= 1e-12
 
 
 @pytest.mark.parametrize("case", KATS["cases"], ids=[c["name"] for c in KATS["cases"]])
