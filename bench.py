@@ -529,6 +529,44 @@ def c5_conservation(merged, records, local_flows, global_flows, unique_keys):
                 ip_bytes=int(merged["ip_bytes"]), local_flows=[int(x) for x in local_flows], unique_keys=unique_keys)
 
 
+def c5_routed(N, lib, device, gpu_index, frames, offs, shard_first, global_n, world, dist, group, merged):
+    """The routed global table (flodbadd_amd.distributed.RoutedSessionTable: every record to its key's
+    owner before the update) over the same shard on a fresh context: its per-batch route / all_to_all /
+    owner-update times, and its gathered table, which must equal the merged table of the export /
+    merge path byte for byte (two independent constructions of the one global table; a difference
+    raises and fails the run)."""
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.distributed import RoutedSessionTable, sort_by_ord
+    from flodbadd_amd.sessions import SessionFilter
+    n = len(offs) - 1
+    cap = FlodbaddGpuCapture(gpu_index, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 21,
+                             max_batch_packets=n, grow=False)
+    try:
+        rt = RoutedSessionTable(dist, cap, group=group, device=device)
+        rt.process(frames, offs, shard_first, global_n)  # warm-up (communicators, scratch)
+        cap.clear_all_sessions()
+        dist.barrier(group=group)
+        timing = {}
+        t0 = time.perf_counter()
+        rt.process(frames, offs, shard_first, global_n, timing=timing)
+        dist.barrier(group=group)
+        el = time.perf_counter() - t0
+        table = rt.global_table()
+    finally:
+        cap.close()
+    m = np.ascontiguousarray(merged.cpu().numpy()).view(N.FLOW_REC_DTYPE).reshape(-1)
+    a, b = sort_by_ord(table.copy()), sort_by_ord(m.copy())
+    a["slot"] = 0
+    b["slot"] = 0
+    if len(a) != len(b) or a.tobytes() != b.tobytes():
+        raise RuntimeError("routed global table (%d flows) differs from the merged one (%d flows)" % (len(a), len(b)))
+    return dict(batch_ms=round(el * 1e3, 3), Mpackets_s=round(global_n / el / 1e6, 1),
+                stages_ms={k: round(v, 3) for k, v in timing.items() if k.endswith("_ms")},
+                records_sent_to_other_ranks=int(timing.get("records_out", 0)), equals_merged_table=True,
+                note="per global batch: parse + route (fb_route_records_dev), all_to_all of the records, the "
+                     "owner's update (fb_flow_update_records_dev); gathered table == the export/merge path's")
+
+
 def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     """BASELINE config C5 after the timed region: rank r's shard of a world x per_rank frame batch
     (C4 mix, flow pool 2^20; packets [r * per_rank, (r+1) * per_rank)) through the fused parse +
@@ -602,12 +640,15 @@ def c5_flow_reduce(N, lib, ctx, per_rank, rank, world, dist, group, device):
     cols = merged[:, 5:11].sum(dim=0).tolist() if len(merged) else [0] * 6  # fb_flow_rec counters
     uniq = int(torch.unique(merged[:, :5], dim=0).shape[0]) if len(merged) else 0
     rs = rs.tolist()
+    cdev = C.c_int(0)
+    N.check(lib.fb_ctx_device(ctx, C.byref(cdev)))
+    routed = c5_routed(N, lib, device, cdev.value, frames, offs, shard_first, n * world, world, dist, group, merged)
     conserved = c5_conservation(
         dict(packets=cols[2] + cols[3], payload_bytes=cols[0] + cols[1], ip_bytes=cols[4] + cols[5]),
         dict(packets=rs[0], payload_bytes=rs[1], ip_bytes=rs[2]),
         [int(x.item()) for x in lfs], int(len(merged)), uniq)
     return dict(ranks_in_group=dist.get_world_size(group), frames_per_rank=n, total_frames=n * world,
-                conservation=conserved,
+                conservation=conserved, routed=routed,
                 local_flows=local, global_flows=int(len(merged)),
                 flow_update_ms=round(flow_ms, 3), update_Mpackets_s=round(world * n / float(t[0]) / 1e3, 1),
                 export_merge_ms=round(el * 1e3, 3), export_merge_first_call_ms=round(first * 1e3, 3),

@@ -325,20 +325,21 @@ class RoutedSessionTable:
             tt = np.array([by[int(r["slot"])] for r in recs], dtype=self.N.FLOW_TIME_DTYPE) if len(recs) else \
                 np.zeros(0, dtype=self.N.FLOW_TIME_DTYPE)
             rows.append(np.ascontiguousarray(tt).view(np.int64).reshape(len(tt), 8))
-        mine = torch.from_numpy(np.concatenate(rows, axis=1) if len(rows) > 1 else rows[0])
+        mine = torch.from_numpy(np.ascontiguousarray(np.concatenate(rows, axis=1) if len(rows) > 1 else rows[0]))
         width = mine.shape[1]
         if self.world == 1:
             allr = mine
-        else:
-            n = torch.tensor([mine.shape[0]], dtype=torch.int64)
+        else:  # (on the group's device: RCCL takes device tensors, gloo host ones)
+            mine = mine.to(self.dev)
+            n = torch.tensor([mine.shape[0]], dtype=torch.int64, device=self.dev)
             sizes = [torch.zeros_like(n) for _ in range(self.world)]
             self.dist.all_gather(sizes, n, group=self.group)
             sizes = [int(x.item()) for x in sizes]
-            pad = torch.zeros((max(sizes + [1]), width), dtype=torch.int64)
+            pad = torch.zeros((max(sizes + [1]), width), dtype=torch.int64, device=self.dev)
             pad[: mine.shape[0]] = mine
             got = [torch.zeros_like(pad) for _ in range(self.world)]
             self.dist.all_gather(got, pad, group=self.group)
-            allr = torch.cat([g[:sz] for g, sz in zip(got, sizes)])
+            allr = torch.cat([g[:sz] for g, sz in zip(got, sizes)]).cpu()
         a = allr.numpy()
         flows = np.ascontiguousarray(a[:, :REC_WORDS]).view(FLOW_REC_DTYPE).reshape(-1)
         if not with_times:
