@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--zipf", type=float, default=None)
+    ap.add_argument("--sync", action="store_true", help="fb_process_seg_dev (one stream) instead of the async call")
     args = ap.parse_args()
     from flodbadd_amd import _native as N
     from flodbadd_amd import synth
@@ -42,8 +43,8 @@ def main():
 
     def call(i):
         b = sets[i & 1]
-        N.check(lib.fb_process_seg_async_dev(ctx, b[0].ptr, fr.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr, None, b[4].ptr,
-                                             s.ptr))
+        fn = lib.fb_process_seg_dev if args.sync else lib.fb_process_seg_async_dev
+        N.check(fn(ctx, b[0].ptr, fr.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr, None, b[4].ptr, s.ptr))
     for i in range(args.warmup):
         call(i)
     N.check(lib.fb_flow_join(ctx, s.ptr))
