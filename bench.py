@@ -56,7 +56,7 @@ def plan_launches(k, bpl):
 
 
 def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, dist, flow=False, mode="seg", bpl=1,
-               synth_kw=None, pipelined=False, stage_extras=True, records=True):
+               synth_kw=None, pipelined=False, stage_extras=True, records=True, timed=False):
     """Time `steps` steps (one step = one batch through the hot path).  mode "seg":
     fb_parse_classify_seg_dev (records compacted per 64-frame wavefront segment, no
     cross-workgroup dependency); mode "dense": fb_parse_classify_dev (the same kernel + the
@@ -87,6 +87,10 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
             d_dns = N.DeviceBuffer(n * N.DNS_OUT_DTYPE.itemsize)
         d_st = N.DeviceBuffer(N.STATS_DTYPE.itemsize)
         bufs.append((d_fr, d_off, d_out, d_dns, d_st))
+    # timed contexts (flow): every buffer set's frame capture times (~2 us apart, set j one second later)
+    d_ts = [N.DeviceBuffer(8 * n).upload(
+        (1_700_000_000 * 10 ** 9 + j * 10 ** 9 + 2000 * np.arange(n, dtype=np.uint64)).astype(np.uint64))
+        for j in range(rotate)] if timed else None
 
     def descriptors(first, count):
         d = np.zeros(count, dtype=N.SEG_BATCH_DTYPE)
@@ -124,6 +128,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
 
     def step(i):
         d_fr, d_off, d_out, d_dns, d_st = bufs[i % rotate]
+        if d_ts is not None:
+            N.check(lib.fb_set_frame_times(ctx, d_ts[i % rotate].ptr))
         if mode == "seg" and flow:
             # fb_process_seg_dev: parse + session upsert in one call (the parse also hands each
             # record's table partition to the update's histogram pass); pipelined: the async form
@@ -240,8 +246,8 @@ def run_config(N, lib, ctx, config_id, n, steps, warmup, rotate, rank, world, di
     N.check(lib.fb_set_session_records(ctx, 1))
     if not records:  # no session record is written: the parse's bytes are the headers, offsets, DNS records
         algo -= 56 * int(st[0]["n_session"])
-    for b in bufs:
-        for x in b:
+    for b in bufs + (d_ts or []):
+        for x in (b if isinstance(b, tuple) else (b,)):
             x.free()
     return dict(frames=frames, offs=offs, elapsed=elapsed, local_elapsed=local_elapsed, ev_ms=ev_ms,
                 algo_bytes=algo, stage=stage,
@@ -871,6 +877,30 @@ def c4_line(N, lib, ctx, steps, warmup, rank, world, dist, cpu_seconds):
     out["c4_1m"] = dict(value=round(world * m * s1 / r1["elapsed"] / 1e6, 2), unit="Mpackets/s",
                         ms_per_call=round(r1["elapsed"] * 1e3 / s1, 4), steps=s1, frames_per_call=m,
                         note="the C4 mix in 1M-frame fb_process_seg_async_dev calls (table-only, pipelined)")
+    # the same C4 line on a timed context (capture timestamps: the 5-s segment timeout and the capture
+    # times per flow, fb_time.hip) -- its own context, the table's time plane beside it
+    tcfg = N.FbConfig()
+    tcfg.abi_version = N.FB_ABI_VERSION
+    tcfg.filter = N.FB_FILTER_GLOBAL_ONLY
+    tcfg.max_batch_packets = n
+    tcfg.flow_capacity = 1 << 21
+    tcfg.flags = N.FB_CFG_FIXED_TABLE | N.FB_CFG_TIMED
+    cdev = C.c_int(0)
+    N.check(lib.fb_ctx_device(ctx, C.byref(cdev)))
+    tctx = lib.fb_create(cdev.value, C.byref(tcfg))
+    if tctx:
+        tctx = C.c_void_p(tctx)
+        try:
+            rt = run_config(N, lib, tctx, 4, n, steps, warmup, 2, rank, world, dist, flow=True, mode="seg",
+                            pipelined=True, records=False, stage_extras=False, timed=True)
+            out["c4_timed"] = dict(value=round(world * n * steps / rt["elapsed"] / 1e6, 2), unit="Mpackets/s",
+                                   ms_per_step=round(rt["elapsed"] * 1e3 / steps, 4), steps=steps,
+                                   note="the C4 line on a timed context (FB_CFG_TIMED): per-frame capture times, "
+                                        "the capture-time pass after each update")
+        finally:
+            lib.fb_destroy(tctx)
+    else:
+        out["c4_timed"] = {"error": lib.fb_last_error().decode()[:200]}
     if rank == 0 and world == 1 and cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline_c4(r["frames"], r["offs"], cpu_seconds)
     return out
