@@ -60,6 +60,7 @@ FLOW_TIME_DTYPE = np.dtype([
 assert FLOW_TIME_DTYPE.itemsize == 64
 FB_SEGMENT_TIMEOUT_MS = 5000
 FB_CFG_TIMED = 2
+FB_QUEUE_SHARED = 1
 # fb_session_flags (fb_flow_rec.session_flags: SessionInfo.is_local_src/dst, is_self_src/dst and
 # dst_service is Some, at insert)
 SESSION_LOCAL_SRC, SESSION_LOCAL_DST, SESSION_SELF_SRC, SESSION_SELF_DST, SESSION_DST_SERVICE = 1, 2, 4, 8, 16
@@ -243,6 +244,7 @@ GPU_SYMBOLS = [
     ("fb_set_device", _I, [_I]),
     ("fb_ctx_device", _I, [_P, C.POINTER(C.c_int)]),
     ("fb_seg_queue_create", _P, [_P, _U32, _U32]),
+    ("fb_seg_queue_create_ex", _P, [_P, _U32, _U32, _U32]),
     ("fb_seg_queue_submit", _I, [_P, _P, _PU64]),
     ("fb_seg_queue_query", _I, [_P, _U64]),
     ("fb_seg_queue_wait", _I, [_P, _U64]),

@@ -854,6 +854,14 @@ static int queue_gone_error(fb_seg_queue* q) {
 }
 
 fb_seg_queue* fb_seg_queue_create(fb_ctx* c, uint32_t depth, uint32_t idle_ms) {
+    return fb_seg_queue_create_ex(c, depth, idle_ms, 0u);
+}
+
+fb_seg_queue* fb_seg_queue_create_ex(fb_ctx* c, uint32_t depth, uint32_t idle_ms, uint32_t flags) {
+    if (flags & ~FB_QUEUE_SHARED) {
+        set_err(FB_ERR_INVAL, "unknown queue flags 0x%x", flags);
+        return nullptr;
+    }
     if (!c) {
         set_err(FB_ERR_INVAL, "ctx is NULL");
         return nullptr;
@@ -935,7 +943,10 @@ fb_seg_queue* fb_seg_queue_create(fb_ctx* c, uint32_t depth, uint32_t idle_ms) {
     // every block must be resident at once: a batch completes when every block has passed it
     int occ = 0;
     if (occupancy_parse_seg_queue(&occ) != hipSuccess || occ < 1) occ = 1;
-    const uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(FB_QUEUE_BPC, occ) * cus));
+    // FB_QUEUE_SHARED: one block per CU, so the session-table update kernels (K1 96 KB + K2 80 KB of
+    // LDS, 80 / 128 VGPRs) fit beside it on every CU (two blocks leave ~66 KB of LDS)
+    const int bpc = (flags & FB_QUEUE_SHARED) ? 1 : FB_QUEUE_BPC;
+    const uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(bpc, occ) * cus));
     q->grid = grid;
     q->idle_ns = (uint64_t)(idle_ms ? idle_ms : 5000u) * 1000000ull;
     q->created = std::chrono::steady_clock::now();

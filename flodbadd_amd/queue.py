@@ -71,6 +71,12 @@ class DeviceSegBatch:
         st = self._st.download(np.zeros(1, dtype=N.STATS_DTYPE))
         return raw, seg, cls, st
 
+    def update_table(self, capture, stream=None):
+        """Apply this (completed) batch's SESSION records to `capture`'s session table
+        (fb_flow_update_seg_dev on `stream`, asynchronous) -- beside a queue created shared."""
+        N.check(N.gpu_lib().fb_flow_update_seg_dev(capture.ctx, self._out.ptr, self._seg.ptr, self.n, self._st.ptr,
+                                                   stream))
+
     def result(self):
         """(SESSION records in packet order, DNS records, classes or None, stats)."""
         raw, seg, cls, st = self.raw()
@@ -87,9 +93,12 @@ class SegQueue:
     """fb_seg_queue_* over a FlodbaddGpuCapture's context (its filter, service table, LAN prefixes
     and own IPs as they are at creation)."""
 
-    def __init__(self, capture, depth=8, idle_ms=0):
+    def __init__(self, capture, depth=8, idle_ms=0, shared=False):
+        """shared: FB_QUEUE_SHARED -- one workgroup per CU, leaving room for the context's table
+        update kernels beside the resident parse (a loop applying each completed batch to the table)."""
         self._lib = N.gpu_lib()
-        q = self._lib.fb_seg_queue_create(capture.ctx, int(depth), int(idle_ms))
+        q = self._lib.fb_seg_queue_create_ex(capture.ctx, int(depth), int(idle_ms),
+                                             N.FB_QUEUE_SHARED if shared else 0)
         if not q:
             raise N.FbError(N.FB_ERR_INVAL, self._lib.fb_last_error().decode(errors="replace"))
         self._q = C.c_void_p(q)

@@ -480,6 +480,15 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, 
 #define FB_QUEUE_MAX_SUBMISSIONS (0xFFFFFFFFull - FB_QUEUE_MAX_DEPTH)
 typedef struct fb_seg_queue fb_seg_queue;
 fb_seg_queue* fb_seg_queue_create(fb_ctx* ctx, uint32_t depth /* 1..FB_QUEUE_MAX_DEPTH, 0 = 8 */, uint32_t idle_ms);
+/* FB_QUEUE_SHARED: the kernel takes ONE workgroup per CU instead of two, leaving room on every CU
+ * for the session-table update kernels, so a host can apply each completed batch to the context's
+ * table (fb_flow_update_seg_dev on the batch's d_out / d_seg, on a stream of its own) while the
+ * queue keeps parsing -- one batch per call WITH the upsert.  The update must then allocate nothing
+ * (hipFree would wait for the queue): create the context with FB_CFG_FIXED_TABLE and
+ * max_batch_packets >= the largest batch, and run no history / enrichment / export that grows
+ * scratch while the queue lives. */
+#define FB_QUEUE_SHARED 1u
+fb_seg_queue* fb_seg_queue_create_ex(fb_ctx* ctx, uint32_t depth, uint32_t idle_ms, uint32_t flags);
 /* Blocks only while `depth` batches are in flight (until the oldest of them completes). */
 int fb_seg_queue_submit(fb_seg_queue* q, const fb_seg_batch* batch, uint64_t* ticket);
 /* Lower this queue's submission limit below FB_QUEUE_MAX_SUBMISSIONS (tests of the limit; a host

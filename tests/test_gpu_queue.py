@@ -243,3 +243,54 @@ def test_queue_large_batch_between_small_ones():
     finally:
         q.close()
         cap.close()
+
+
+@pytest.mark.timeout(180)
+def test_shared_queue_builds_the_session_table():
+    """One batch per call WITH the upsert: a queue created shared (FB_QUEUE_SHARED, one workgroup per
+    CU) parses C4-mix batches while each completed batch is applied to the context's session table on
+    a stream of its own (fb_flow_update_seg_dev, K1 / K2 beside the resident kernel); three rotating
+    buffer sets, a set reloaded only after its update completed.  The table equals the oracle's fed
+    the same batches in order, row for row, and each update ran while the queue lived (no wait for
+    the kernel's idle exit)."""
+    import time as _t
+    from oracle import coracle
+    from test_gpu_parity import rows_sorted
+    n_max = 120000
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.GlobalOnly, flow_capacity=1 << 17,
+                             max_batch_packets=n_max, grow=False)
+    batches = [synth.generate(4, 100000 + 977 * k, first=k * 200000, n_flows=40000) for k in range(9)]
+    sets = [DeviceSegBatch(*batches[0], max_frames=n_max, max_bytes=max(b[0].nbytes for b in batches))
+            for _ in range(3)]
+    lib = N.gpu_lib()
+    stream, evs = N.Stream(), [N.Event() for _ in range(3)]
+    q = SegQueue(cap, depth=4, idle_ms=4000, shared=True)
+    ref = coracle.Flows()
+    upd_ms = []
+    try:
+        for k, (fr, of) in enumerate(batches):
+            b = sets[k % 3]
+            if k >= 3:
+                evs[k % 3].wait_spin()  # its previous batch's update is done
+            b.load(fr, of)
+            b.fill_outputs()
+            t = q.submit(b)
+            q.wait(t)
+            t0 = _t.perf_counter()
+            b.update_table(cap, stream.ptr)
+            evs[k % 3].record(stream)
+            evs[k % 3].wait_spin()
+            upd_ms.append((_t.perf_counter() - t0) * 1e3)
+            out, _, _, st = b.result()
+            assert int(st[0]["error"]) == 0
+            ref.update(coracle.parse_classify(coracle.make_cfg(1), fr, of)[0])
+        stream.sync()
+    finally:
+        q.close()
+        for b in sets:
+            b.free()
+    try:
+        assert rows_sorted(cap.export_flows()) == rows_sorted(ref.export_sorted())
+        assert max(upd_ms) < 2000, upd_ms  # (an update stuck behind the kernel would wait out idle_ms)
+    finally:
+        cap.close()
