@@ -18,30 +18,27 @@
 //   reset_i = T_i || !in_{i-1}     (current_segment_start := t_i; the insert: always)
 // and at an end the interarrival term is (segment start as of i) - (previous end), where the start
 // is t_i when !in_{i-1} (the segment opened at i) and otherwise the start current before i.  So one
-// stable sort of the batch's records by table slot (they arrive in packet order) and two device-wide
-// inclusive scans -- the latest reset / end / run head at or before each packet (max of index + 1:
-// a flow's packets are contiguous, so a value below its run's head means "none in this batch, use
-// the time plane") and the running end count -- give every packet its inputs, a second scan the
-// accepted interarrival sum, and the run's last packet writes the flow's new FlowTime:
-//   K_keys   one thread per record slot: the record's key (record or update entry), its table slot
-//            (probe of the updated table), sort key = slot (cap: no flow -> sorts last), value =
-//            pkt_index << 1 | P
-//   sort     rocPRIM LSD radix sort of (slot, value) pairs over log2(cap) + 1 bits (stable: the
-//            packet order inside a slot stays)
-//   K_flags  per sorted packet: its capture time, T, in, end, reset (its own and its predecessor's:
-//            the predecessor's `in` needs the packet before that), the scan input
-//   scan 1   (head, reset, end) max, end count sum
-//   K_ia     per packet that ends a segment after an earlier end: the interarrival term (ms) if
-//            accepted (>= 0, src/packets.rs:165), and the divisor segment_count - 1 then
-//   scan 2   accepted ms sum, last accepted index max
-//   K_write  per run's last packet: the flow's FlowTime (start / end from the table's positions of
-//            this call, last = the run's last packet)
-// Bytes per record: 8 B (sort pairs, 3 passes of 2 x 8 B) + 8 B timestamp + 16 + 16 B scan words
-// + the table probe (a 128-B slot line) -- an auxiliary pass, not the headline path.
+// stable sort of the batch's records by table slot (they arrive in packet order) makes each flow's
+// packets one contiguous run, and two chained segmented scans over the runs give every packet its
+// inputs -- scan A: the latest reset / end in the run at or before it, the run's ends so far, its
+// head; scan B: the accepted interarrival sum and the latest accepted term with its divisor -- and
+// the run's last packet writes the flow's new FlowTime:
+//   k_time_keys  one thread per record slot: the record's key (record or update entry), its table
+//                slot (probe of the updated table), sort key = slot (cap: no flow -> sorts last),
+//                value = pkt_index << 1 | P
+//   sort         rocPRIM LSD radix sort of (slot, value) pairs over log2(cap) + 1 bits (stable: the
+//                packet order inside a slot stays)
+//   k_time_runs  ONE launch over tiles of 1,024 sorted packets taken in ticket order: per packet its
+//                time, T / in / end / reset (its predecessor's `in` from the packet before that),
+//                scan A (thread, wave, block, then the tile's prefix by decoupled look-back), the
+//                interarrival term, scan B the same way, and the runs' last packets write the plane
+//                (start / end from the table's positions of this call)
+// Bytes per record: the record or entry (56 / 32 B) + the table probe (a 128-B slot line) + 4 B of
+// sort key and value out; the sort 3 passes x 16 B; the fused pass 8 B in + the timestamp gathers
+// (8 B, up to four per packet, mostly cached) -- an auxiliary pass, not the headline path.
 #include <cstring>  // (rocPRIM's texture-cache iterator needs memset declared)
 
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include "fb_internal.h"
 
@@ -50,7 +47,6 @@ namespace fbk {
 namespace {
 
 constexpr uint32_t kTmThreads = 256;
-constexpr uint32_t kTmInvalidDiv = 0u;
 
 // chrono's (a - b).num_milliseconds(): the signed difference truncated toward zero
 __device__ __forceinline__ long long ms_between(unsigned long long a, unsigned long long b) {
@@ -60,26 +56,39 @@ __device__ __forceinline__ bool timeout_of(unsigned long long now, unsigned long
     return ms_between(now, last) >= (long long)FB_SEGMENT_TIMEOUT_MS;
 }
 
-struct ScanA {  // scan 1 word: index + 1 of the latest run head / reset / end at or before, ends so far
+// Segmented scan words of the fused pass (k_time_runs): values since the latest run head at or before
+// an element, so nothing needs the run's head position to discount earlier runs.
+//   SegA: head index + 1 (0: no head in the segment) | the run is a new flow's (bit 31); the latest
+//         reset / end (index + 1, 0: none in the run); the run's ends so far
+//   SegB: the run's accepted interarrival ms so far; the latest accepted term (index + 1); its
+//         divisor | head bit 30
+struct SegA {
     uint32_t h, r, e, c;
 };
-struct ScanAOp {
-    __device__ __host__ ScanA operator()(const ScanA& a, const ScanA& b) const {
-        return ScanA{a.h > b.h ? a.h : b.h, a.r > b.r ? a.r : b.r, a.e > b.e ? a.e : b.e, a.c + b.c};
-    }
-};
-struct ScanB {  // scan 2 word: accepted interarrival ms so far, index + 1 of the latest accepted term
+struct SegB {
     long long s;
-    uint32_t a, pad;
+    uint32_t a, d;
 };
-struct ScanBOp {
-    __device__ __host__ ScanB operator()(const ScanB& x, const ScanB& y) const {
-        return ScanB{x.s + y.s, x.a > y.a ? x.a : y.a, 0u};
-    }
-};
+constexpr uint32_t kInsRun = 0x80000000u;
+__device__ __forceinline__ bool segA_head(const SegA& x) { return (x.h & ~kInsRun) != 0u; }
+__device__ __forceinline__ SegA segA_op(const SegA& x, const SegA& y) {
+    if (segA_head(y)) return y;
+    return SegA{x.h, x.r > y.r ? x.r : y.r, x.e > y.e ? x.e : y.e, x.c + y.c};
+}
+// SegB's head flag rides in bit 30 of d (a is 0 for a segment without a term)
+constexpr uint32_t kBHead = 0x40000000u;
+__device__ __forceinline__ SegB segB_op(const SegB& x, const SegB& y) {
+    if (y.d & kBHead) return y;
+    SegB o;
+    o.s = x.s + y.s;
+    const bool take_y = y.a > x.a;
+    o.a = take_y ? y.a : x.a;
+    o.d = ((take_y ? y.d : x.d) & ~kBHead) | (x.d & kBHead);
+    return o;
+}
 
-// per sorted packet flags (K_flags)
-constexpr uint8_t kFP = 1u, kFT = 2u, kFIn = 4u, kFHead = 8u, kFIns = 16u, kFEnd = 32u, kFInPrev = 64u;
+// per sorted packet flags
+constexpr uint8_t kFP = 1u, kFT = 2u, kFIn = 4u, kFHead = 8u, kFIns = 16u, kFEnd = 32u, kFInPrev = 64u, kFReset = 128u;
 
 // The table slot of `key` (the update just inserted every key it took), or `cap` if absent (a record
 // the table could not take: its flow is not in the table).
@@ -146,133 +155,308 @@ __global__ __launch_bounds__(kTmThreads) void k_time_keys(const FlowParams P, ui
     vals[i] = val;
 }
 
-// The sorted packets: capture time, T / in / end / reset flags and the scan-1 input.
-__global__ __launch_bounds__(kTmThreads) void k_time_flags(const uint32_t* keys, const uint32_t* vals, uint32_t n,
-                                                           uint32_t cap, const FlowSlot* T, const FlowTime* plane,
-                                                           const unsigned long long* ts, uint32_t batch,
-                                                           unsigned long long* t_out, uint8_t* f_out, ScanA* a_out) {
-    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = keys[i];
-    if (s >= cap) {  // no flow: neutral scan word
-        f_out[i] = 0u;
-        a_out[i] = ScanA{0u, 0u, 0u, 0u};
-        return;
-    }
-    const unsigned long long pos_hi = (unsigned long long)batch << 32;
-    // element j's (T, in, insert) given its predecessor; `hd` whether j heads its run
-    auto state = [&](uint32_t j, bool hd, unsigned long long tj, unsigned long long tprev_elem, bool& T_, bool& in_,
-                     bool& ins_) {
-        const bool P_ = vals[j] & 1u;
-        ins_ = false;
-        unsigned long long tprev = tprev_elem;
-        if (hd) {
-            ins_ = T[s].first_seen == (pos_hi | (vals[j] >> 1));  // the flow's insert is this packet
-            tprev = plane[s].last_activity_ns;
+// ---------------------------------------------------------------------------------------------
+// The fused pass over the sorted packets (one launch, tiles of kRunTile packets taken in ticket order,
+// two chained decoupled look-backs): per packet its flags, the segmented scan A (latest reset / end,
+// ends so far, the run's head), then its interarrival term and the segmented scan B (accepted sum,
+// latest accepted term and its divisor), and the run's last packet writes the flow's FlowTime.
+constexpr uint32_t kRunThreads = 256, kRunItems = 4, kRunTile = kRunThreads * kRunItems;
+// status bits per scan (A: bits 0-2, B: bits 16-18): aggregate published, inclusive published, the
+// aggregate holds a run head (a segmented value: everything before it is irrelevant)
+constexpr uint32_t kStAgg = 1u, kStInc = 2u, kStHead = 4u;
+
+struct RunStatus {  // per tile: status bits (zeroed before the launch), then the values
+    uint32_t* flag;
+    SegA* a_agg;
+    SegA* a_inc;
+    SegB* b_agg;
+    SegB* b_inc;
+    uint32_t* ticket;
+};
+
+__device__ __forceinline__ uint32_t st_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_publish(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane shuffles of the scan words.
+__device__ __forceinline__ SegA shfl_down(const SegA& x, int o) {
+    return SegA{(uint32_t)__shfl_down(x.h, o, 64), (uint32_t)__shfl_down(x.r, o, 64), (uint32_t)__shfl_down(x.e, o, 64),
+                (uint32_t)__shfl_down(x.c, o, 64)};
+}
+__device__ __forceinline__ SegB shfl_down(const SegB& x, int o) {
+    return SegB{__shfl_down(x.s, o, 64), (uint32_t)__shfl_down(x.a, o, 64), (uint32_t)__shfl_down(x.d, o, 64)};
+}
+
+// The exclusive prefix of tile `t` for one scan, by one wavefront: lane L looks at tile t-1-L-64k
+// (lane 0 the nearest), every lane waits for its tile's status, the nearest tile with an inclusive
+// value ends the walk, and the window's values are folded in tile order (the all-zero word is the
+// identity of both operators).  shift: 0 (A) or 16 (B) in the status word.
+template <class V, class Op>
+__device__ V lookback(const RunStatus& S, uint32_t t, uint32_t shift, const V* agg, const V* inc, Op op) {
+    const uint32_t lane = threadIdx.x & 63u;
+    V acc{};
+    bool have = false;
+    for (int j0 = (int)t - 1; j0 >= 0; j0 -= 64) {
+        const int j = j0 - (int)lane;
+        uint32_t f = 0u;
+        if (j >= 0)
+            while (((f = st_load(S.flag + j)) >> shift & 3u) == 0u) __builtin_amdgcn_s_sleep(1);
+        // the walk ends at the nearest tile with an inclusive value or a run head in its aggregate
+        const unsigned long long full = __ballot(j >= 0 && ((f >> shift) & (kStInc | kStHead)));
+        const uint32_t stop = full ? (uint32_t)__builtin_ctzll(full) : 64u;
+        V v{};
+        if (j >= 0 && lane <= stop) v = (lane == stop && ((f >> shift) & kStInc)) ? inc[j] : agg[j];
+        // fold: lane L holds tiles [L, L + o) after step o (higher lanes are earlier tiles)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const V w = shfl_down(v, o);
+            if ((lane & (2u * o - 1u)) == 0u) v = op(w, v);
         }
-        T_ = !ins_ && timeout_of(tj, tprev);
+        // (lane 0 holds the window folded in tile order)
+        acc = have ? op(v, acc) : v;
+        have = true;
+        if (full) break;
+    }
+    return acc;  // meaningful in lane 0
+}
+
+__device__ __forceinline__ unsigned long long t_of(const uint32_t* vals, const unsigned long long* ts, uint32_t j) {
+    return ts[vals[j] >> 1];
+}
+
+__global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys, const uint32_t* vals, uint32_t n,
+                                                          uint32_t cap, const FlowSlot* T, FlowTime* plane,
+                                                          const unsigned long long* ts, uint32_t batch, RunStatus S) {
+    __shared__ uint32_t s_tile;
+    __shared__ SegA s_wa[kRunThreads / 64];
+    __shared__ SegB s_wb[kRunThreads / 64];
+    __shared__ SegA s_pa;
+    __shared__ SegB s_pb;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(S.ticket, 1u);  // tiles in start order: the look-back waits only on running ones
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t base = tile * kRunTile + tid * kRunItems;
+    const unsigned long long pos_hi = (unsigned long long)batch << 32;
+
+    // element j's (T, in, insert) given its predecessor element (or the plane at a run head)
+    auto state = [&](uint32_t j, uint32_t sj, bool hd, unsigned long long tj, bool& T_, bool& in_, bool& ins_) {
+        const bool P_ = vals[j] & 1u;
+        unsigned long long tprev;
+        if (hd) {
+            ins_ = T[sj].first_seen == (pos_hi | (vals[j] >> 1));  // the flow's insert is this packet
+            tprev = ins_ ? tj : plane[sj].last_activity_ns;
+        } else {
+            ins_ = false;
+            tprev = t_of(vals, ts, j - 1u);
+        }
+        T_ = !ins_ && ms_between(tj, tprev) >= (long long)FB_SEGMENT_TIMEOUT_MS;
         in_ = ins_ ? !P_ : (T_ || !P_);
     };
-    const bool head = i == 0u || keys[i - 1u] != s;
-    const unsigned long long t = ts[vals[i] >> 1];
-    const unsigned long long t1 = head ? 0ull : ts[vals[i - 1u] >> 1];
-    bool Ti, ini, insi;
-    state(i, head, t, t1, Ti, ini, insi);
-    bool in_prev;
-    if (head) {
-        in_prev = insi ? false : plane[s].in_segment != 0u;
-    } else {
-        const bool head1 = i == 1u || keys[i - 2u] != s;
-        const unsigned long long t2 = head1 ? 0ull : ts[vals[i - 2u] >> 1];
-        bool T1, in1, ins1;
-        state(i - 1u, head1, t1, t2, T1, in1, ins1);
-        in_prev = in1;
-    }
-    const bool P_ = vals[i] & 1u;
-    const bool end = insi ? P_ : (P_ || (in_prev && Ti));
-    const bool reset = insi || Ti || !in_prev;
-    t_out[i] = t;
-    f_out[i] = (uint8_t)((P_ ? kFP : 0u) | (Ti ? kFT : 0u) | (ini ? kFIn : 0u) | (head ? kFHead : 0u) |
-                         (insi ? kFIns : 0u) | (end ? kFEnd : 0u) | (in_prev ? kFInPrev : 0u));
-    a_out[i] = ScanA{head ? i + 1u : 0u, reset ? i + 1u : 0u, end ? i + 1u : 0u, end ? 1u : 0u};
-}
 
-// Interarrival terms: at an end that follows an earlier end (in this batch or the plane's).
-__global__ __launch_bounds__(kTmThreads) void k_time_ia(const uint32_t* keys, uint32_t n, uint32_t cap,
-                                                        const FlowTime* plane, const unsigned long long* t,
-                                                        const uint8_t* f, const ScanA* A, ScanB* b_out,
-                                                        uint32_t* div) {
-    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i >= n) return;
-    ScanB out{0ll, 0u, 0u};
-    const uint32_t s = keys[i];
-    const uint8_t fl = f[i];
-    if (s < cap && (fl & kFEnd) && !(fl & kFIns)) {
-        const uint32_t H = A[i].h - 1u;  // the run's head
-        const bool ins_run = f[H] & kFIns;
-        const ScanA prev = i > H ? A[i - 1u] : ScanA{0u, 0u, 0u, 0u};
-        // previous end: in this run before i, else the plane's (a new flow's run has none before)
-        unsigned long long prev_end = FB_SEEN_NONE;
-        if (prev.e > H) prev_end = t[prev.e - 1u];
-        else if (!ins_run) prev_end = plane[s].last_segment_end_ns;
-        if (prev_end != FB_SEEN_NONE) {
-            unsigned long long start;  // current_segment_start as of packet i (src/packets.rs:151-154)
-            if (!(fl & kFInPrev)) start = t[i];
-            else if (prev.r > H) start = t[prev.r - 1u];
-            else start = plane[s].current_segment_start_ns;
-            const long long ia = ms_between(start, prev_end);
-            if (ia >= 0) {  // (double)ia / 1000.0 >= 0.0 (src/packets.rs:165)
-                const uint32_t before = (i > H ? prev.c - (H > 0u ? A[H - 1u].c : 0u) : 0u) +
-                                        (ins_run ? 0u : plane[s].segment_count);
-                out = ScanB{ia, i + 1u, 0u};
-                div[i] = before;  // segment_count after this end, minus 1
+    uint32_t key[kRunItems];
+    uint8_t fl[kRunItems];
+    unsigned long long tt[kRunItems];
+    SegA xa[kRunItems];
+#pragma unroll
+    for (uint32_t k = 0; k < kRunItems; ++k) {
+        const uint32_t i = base + k;
+        key[k] = i < n ? keys[i] : cap;
+        fl[k] = 0u;
+        tt[k] = 0ull;
+        xa[k] = SegA{0u, 0u, 0u, 0u};
+        if (key[k] >= cap) continue;  // (no flow: sorts last, a neutral word)
+        const uint32_t s = key[k];
+        const bool head = i == 0u || keys[i - 1u] != s;
+        const unsigned long long t = t_of(vals, ts, i);
+        bool Ti, ini, insi, in_prev;
+        state(i, s, head, t, Ti, ini, insi);
+        if (head) {
+            in_prev = insi ? false : plane[s].in_segment != 0u;
+        } else {
+            bool T1, in1, ins1;
+            state(i - 1u, s, i == 1u || keys[i - 2u] != s, t_of(vals, ts, i - 1u), T1, in1, ins1);
+            in_prev = in1;
+        }
+        const bool P_ = vals[i] & 1u;
+        const bool end = insi ? P_ : (P_ || (in_prev && Ti));
+        const bool reset = insi || Ti || !in_prev;
+        tt[k] = t;
+        fl[k] = (uint8_t)((P_ ? kFP : 0u) | (Ti ? kFT : 0u) | (ini ? kFIn : 0u) | (head ? kFHead : 0u) |
+                          (insi ? kFIns : 0u) | (end ? kFEnd : 0u) | (in_prev ? kFInPrev : 0u) | (reset ? kFReset : 0u));
+        xa[k] = SegA{head ? ((i + 1u) | (insi ? kInsRun : 0u)) : 0u, reset ? i + 1u : 0u, end ? i + 1u : 0u,
+                     end ? 1u : 0u};
+    }
+    // ---- scan A: thread-sequential, wave, block, then the tile's prefix by look-back
+    SegA ia[kRunItems];  // inclusive within the thread's items
+    ia[0] = xa[0];
+#pragma unroll
+    for (uint32_t k = 1; k < kRunItems; ++k) ia[k] = segA_op(ia[k - 1], xa[k]);
+    SegA tot = ia[kRunItems - 1];
+    SegA wincl = tot;  // wave inclusive scan of the thread totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        SegA y;
+        y.h = __shfl_up(wincl.h, o, 64);
+        y.r = __shfl_up(wincl.r, o, 64);
+        y.e = __shfl_up(wincl.e, o, 64);
+        y.c = __shfl_up(wincl.c, o, 64);
+        if (lane >= (uint32_t)o) wincl = segA_op(y, wincl);
+    }
+    if (lane == 63u) s_wa[wave] = wincl;
+    SegA wexcl;  // exclusive within the wave
+    wexcl.h = __shfl_up(wincl.h, 1, 64);
+    wexcl.r = __shfl_up(wincl.r, 1, 64);
+    wexcl.e = __shfl_up(wincl.e, 1, 64);
+    wexcl.c = __shfl_up(wincl.c, 1, 64);
+    __syncthreads();
+    if (wave == 0u) {
+        SegA agg = s_wa[0];
+        for (uint32_t w = 1; w < kRunThreads / 64; ++w) agg = segA_op(agg, s_wa[w]);
+        SegA prefix{0u, 0u, 0u, 0u};
+        if (tile == 0u) {
+            if (lane == 0u) {
+                S.a_inc[0] = agg;
+                st_publish(S.flag, kStInc);
+            }
+        } else {
+            if (lane == 0u) {
+                S.a_agg[tile] = agg;
+                st_publish(S.flag + tile, kStAgg | (segA_head(agg) ? kStHead : 0u));
+            }
+            prefix = lookback(S, tile, 0u, S.a_agg, S.a_inc, segA_op);
+            if (lane == 0u) {
+                S.a_inc[tile] = segA_op(prefix, agg);
+                st_publish(S.flag + tile, kStInc);
             }
         }
+        if (lane == 0u) s_pa = prefix;
     }
-    b_out[i] = out;
-}
-
-// Each run's last packet: the flow's new time record.
-__global__ __launch_bounds__(kTmThreads) void k_time_write(const uint32_t* keys, const uint32_t* vals, uint32_t n,
-                                                           uint32_t cap, const FlowSlot* T, FlowTime* plane,
-                                                           const unsigned long long* ts, uint32_t batch,
-                                                           const unsigned long long* t, const uint8_t* f,
-                                                           const ScanA* A, const ScanB* B, const uint32_t* div) {
-    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = keys[i];
-    if (s >= cap || (i + 1u < n && keys[i + 1u] == s)) return;  // not a run's last packet
-    const uint32_t H = A[i].h - 1u;
-    const bool ins = f[H] & kFIns;
-    FlowTime o;
-    if (ins) {
-        o.start_time_ns = t[H];
-        o.end_time_ns = FB_SEEN_NONE;
-        o.current_segment_start_ns = t[H];
-        o.last_segment_end_ns = FB_SEEN_NONE;
-        o.total_segment_interarrival_ms = 0ll;
-        o.segment_interarrival_div = kTmInvalidDiv;
-        o.segment_count = 0u;
-    } else {
-        o = plane[s];
+    __syncthreads();
+    {
+        SegA pre = s_pa;  // everything before this thread's first item
+        for (uint32_t w = 0; w < wave; ++w) pre = segA_op(pre, s_wa[w]);
+        if (lane > 0u) pre = segA_op(pre, wexcl);
+        SegA ex[kRunItems];  // exclusive per item (= inclusive of the element before)
+        ex[0] = pre;
+#pragma unroll
+        for (uint32_t k = 1; k < kRunItems; ++k) ex[k] = segA_op(pre, ia[k - 1]);
+#pragma unroll
+        for (uint32_t k = 0; k < kRunItems; ++k) {
+            ia[k] = segA_op(pre, ia[k]);  // inclusive, global
+            xa[k] = ex[k];
+        }
     }
-    const ScanA a = A[i];
-    const uint32_t c0 = H > 0u ? A[H - 1u].c : 0u;
-    o.segment_count += a.c - c0;
-    if (a.r > H) o.current_segment_start_ns = t[a.r - 1u];
-    if (a.e > H) o.last_segment_end_ns = t[a.e - 1u];
-    const long long s0 = H > 0u ? B[H - 1u].s : 0ll;
-    o.total_segment_interarrival_ms += B[i].s - s0;
-    if (B[i].a > H) o.segment_interarrival_div = div[B[i].a - 1u];
-    o.last_activity_ns = t[i];
-    o.in_segment = (f[i] & kFIn) ? 1u : 0u;
-    // end_time at the flow's first FIN/RST, which the update placed in end_seen (src/packets.rs:195-198)
-    const unsigned long long es = T[s].end_seen;
-    if (es != FB_SEEN_NONE && (es >> 32) == (unsigned long long)batch && o.end_time_ns == FB_SEEN_NONE)
-        o.end_time_ns = ts[es & 0xFFFFFFFFull];
-    o.reserved[0] = o.reserved[1] = o.reserved[2] = 0u;
-    o.slot = 0u;
-    plane[s] = o;
+    // ---- interarrival terms and scan B
+    SegB xb[kRunItems];
+#pragma unroll
+    for (uint32_t k = 0; k < kRunItems; ++k) {
+        const uint32_t i = base + k;
+        xb[k] = SegB{0ll, 0u, (fl[k] & kFHead) ? kBHead : 0u};
+        if (key[k] >= cap || !(fl[k] & kFEnd) || (fl[k] & kFIns)) continue;
+        const uint32_t s = key[k];
+        const SegA& inc = ia[k];
+        const bool ins_run = inc.h & kInsRun;
+        const bool head = fl[k] & kFHead;
+        const SegA prev = head ? SegA{0u, 0u, 0u, 0u} : xa[k];  // the run's state before packet i
+        unsigned long long prev_end = FB_SEEN_NONE;
+        if (prev.e) prev_end = t_of(vals, ts, prev.e - 1u);
+        else if (!ins_run) prev_end = plane[s].last_segment_end_ns;
+        if (prev_end == FB_SEEN_NONE) continue;
+        unsigned long long start;  // current_segment_start as of packet i (src/packets.rs:151-154)
+        if (!(fl[k] & kFInPrev)) start = tt[k];
+        else if (prev.r) start = t_of(vals, ts, prev.r - 1u);
+        else start = plane[s].current_segment_start_ns;
+        const long long ia_ms = ms_between(start, prev_end);
+        if (ia_ms < 0) continue;  // (double)ia / 1000.0 >= 0.0, src/packets.rs:165
+        const uint32_t before = prev.c + (ins_run ? 0u : plane[s].segment_count);
+        xb[k] = SegB{ia_ms, i + 1u, before | (head ? kBHead : 0u)};
+    }
+    SegB ib[kRunItems];
+    ib[0] = xb[0];
+#pragma unroll
+    for (uint32_t k = 1; k < kRunItems; ++k) ib[k] = segB_op(ib[k - 1], xb[k]);
+    SegB wb = ib[kRunItems - 1];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        SegB y;
+        y.s = __shfl_up(wb.s, o, 64);
+        y.a = __shfl_up(wb.a, o, 64);
+        y.d = __shfl_up(wb.d, o, 64);
+        if (lane >= (uint32_t)o) wb = segB_op(y, wb);
+    }
+    if (lane == 63u) s_wb[wave] = wb;
+    SegB wbx;
+    wbx.s = __shfl_up(wb.s, 1, 64);
+    wbx.a = __shfl_up(wb.a, 1, 64);
+    wbx.d = __shfl_up(wb.d, 1, 64);
+    __syncthreads();
+    if (wave == 0u) {
+        SegB agg = s_wb[0];
+        for (uint32_t w = 1; w < kRunThreads / 64; ++w) agg = segB_op(agg, s_wb[w]);
+        SegB prefix{0ll, 0u, 0u};
+        if (tile == 0u) {
+            if (lane == 0u) {
+                S.b_inc[0] = agg;
+                st_publish(S.flag, kStInc << 16);
+            }
+        } else {
+            if (lane == 0u) {
+                S.b_agg[tile] = agg;
+                st_publish(S.flag + tile, (kStAgg | ((agg.d & kBHead) ? kStHead : 0u)) << 16);
+            }
+            prefix = lookback(S, tile, 16u, S.b_agg, S.b_inc, segB_op);
+            if (lane == 0u) {
+                S.b_inc[tile] = segB_op(prefix, agg);
+                st_publish(S.flag + tile, kStInc << 16);
+            }
+        }
+        if (lane == 0u) s_pb = prefix;
+    }
+    __syncthreads();
+    SegB preb = s_pb;
+    for (uint32_t w = 0; w < wave; ++w) preb = segB_op(preb, s_wb[w]);
+    if (lane > 0u) preb = segB_op(preb, wbx);
+    // ---- each run's last packet: the flow's new time record
+#pragma unroll
+    for (uint32_t k = 0; k < kRunItems; ++k) {
+        const uint32_t i = base + k;
+        const uint32_t s = key[k];
+        if (s >= cap || (i + 1u < n && keys[i + 1u] == s)) continue;
+        const SegA a = ia[k];
+        const SegB b = segB_op(preb, ib[k]);
+        const uint32_t H = (a.h & ~kInsRun) - 1u;
+        const bool ins = a.h & kInsRun;
+        FlowTime o;
+        if (ins) {
+            o.start_time_ns = t_of(vals, ts, H);
+            o.end_time_ns = FB_SEEN_NONE;
+            o.current_segment_start_ns = o.start_time_ns;
+            o.last_segment_end_ns = FB_SEEN_NONE;
+            o.total_segment_interarrival_ms = 0ll;
+            o.segment_interarrival_div = 0u;
+            o.segment_count = 0u;
+        } else {
+            o = plane[s];
+        }
+        o.segment_count += a.c;
+        if (a.r) o.current_segment_start_ns = t_of(vals, ts, a.r - 1u);
+        if (a.e) o.last_segment_end_ns = t_of(vals, ts, a.e - 1u);
+        o.total_segment_interarrival_ms += b.s;
+        if (b.a) o.segment_interarrival_div = b.d & ~kBHead;
+        o.last_activity_ns = tt[k];
+        o.in_segment = (fl[k] & kFIn) ? 1u : 0u;
+        // end_time at the flow's first FIN/RST, which the update placed in end_seen (src/packets.rs:195-198)
+        const unsigned long long es = T[s].end_seen;
+        if (es != FB_SEEN_NONE && (es >> 32) == (unsigned long long)batch && o.end_time_ns == FB_SEEN_NONE)
+            o.end_time_ns = ts[es & 0xFFFFFFFFull];
+        o.reserved[0] = o.reserved[1] = o.reserved[2] = 0u;
+        o.slot = 0u;
+        plane[s] = o;
+    }
 }
 
 // Growth: the time records follow their flows (remap[old slot] = new slot, ~0u: empty).
@@ -316,31 +500,26 @@ __global__ __launch_bounds__(256) void k_time_export(const FlowSlot* T, const Fl
 
 // ---------------------------------------------------------------------------------------------
 struct TimeScratch {
-    uint32_t *keys, *keys2, *vals, *vals2, *div;
-    unsigned long long* t;
-    uint8_t* f;
-    ScanA* a;
-    ScanA* a2;
-    ScanB* b;
-    ScanB* b2;
+    uint32_t *keys, *keys2, *vals, *vals2;
+    RunStatus st;
+    uint32_t tiles;
     void* tmp;
     size_t tmp_bytes;
 };
 static size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
-static size_t lib_tmp_bytes(uint32_t n, uint32_t bits) {
-    size_t a = 0, b = 0, c = 0;
+static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
+    size_t a = 0;
     rocprim::radix_sort_pairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                               (uint32_t*)nullptr, n, 0u, bits, (hipStream_t)0);
-    rocprim::inclusive_scan(nullptr, b, (ScanA*)nullptr, (ScanA*)nullptr, n, ScanAOp(), (hipStream_t)0);
-    rocprim::inclusive_scan(nullptr, c, (ScanB*)nullptr, (ScanB*)nullptr, n, ScanBOp(), (hipStream_t)0);
-    return std::max(a, std::max(b, c));
+    return a;
 }
 
 uint64_t time_scratch_bytes(uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
-    return al256(m * 4) * 5 + al256(m * 8) + al256(m) + al256(m * sizeof(ScanA)) * 2 + al256(m * sizeof(ScanB)) * 2 +
-           al256(lib_tmp_bytes(n, cap_bits + 1u));
+    const size_t tiles = (m + kRunTile - 1) / kRunTile;
+    return al256(m * 4) * 4 + al256(tiles * 4) + al256(tiles * sizeof(SegA)) * 2 + al256(tiles * sizeof(SegB)) * 2 +
+           al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
 }
 
 static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
@@ -348,18 +527,18 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
     auto take = [&](size_t b) { char* q = p; p += al256(b); return q; };
     TimeScratch s;
+    s.tiles = (uint32_t)((m + kRunTile - 1) / kRunTile);
     s.keys = (uint32_t*)take(m * 4);
     s.keys2 = (uint32_t*)take(m * 4);
     s.vals = (uint32_t*)take(m * 4);
     s.vals2 = (uint32_t*)take(m * 4);
-    s.div = (uint32_t*)take(m * 4);
-    s.t = (unsigned long long*)take(m * 8);
-    s.f = (uint8_t*)take(m);
-    s.a = (ScanA*)take(m * sizeof(ScanA));
-    s.a2 = (ScanA*)take(m * sizeof(ScanA));
-    s.b = (ScanB*)take(m * sizeof(ScanB));
-    s.b2 = (ScanB*)take(m * sizeof(ScanB));
-    s.tmp_bytes = lib_tmp_bytes(n, cap_bits + 1u);
+    s.st.flag = (uint32_t*)take(s.tiles * 4);
+    s.st.a_agg = (SegA*)take(s.tiles * sizeof(SegA));
+    s.st.a_inc = (SegA*)take(s.tiles * sizeof(SegA));
+    s.st.b_agg = (SegB*)take(s.tiles * sizeof(SegB));
+    s.st.b_inc = (SegB*)take(s.tiles * sizeof(SegB));
+    s.st.ticket = (uint32_t*)take(8);
+    s.tmp_bytes = sort_tmp_bytes(n, cap_bits + 1u);
     s.tmp = take(s.tmp_bytes);
     return s;
 }
@@ -378,20 +557,10 @@ hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t ca
     size_t tb = s.tmp_bytes;
     e = rocprim::radix_sort_pairs(s.tmp, tb, s.keys, s.keys2, s.vals, s.vals2, n_slots, 0u, bits + 1u, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_flags, dim3(g), dim3(kTmThreads), 0, st, s.keys2, s.vals2, n_slots, c, p.table, plane, ts,
-                       p.batch, s.t, s.f, s.a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tb = s.tmp_bytes;
-    e = rocprim::inclusive_scan(s.tmp, tb, s.a, s.a2, n_slots, ScanAOp(), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_ia, dim3(g), dim3(kTmThreads), 0, st, s.keys2, n_slots, c, plane, s.t, s.f, s.a2, s.b,
-                       s.div);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tb = s.tmp_bytes;
-    e = rocprim::inclusive_scan(s.tmp, tb, s.b, s.b2, n_slots, ScanBOp(), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_write, dim3(g), dim3(kTmThreads), 0, st, s.keys2, s.vals2, n_slots, c, p.table, plane, ts,
-                       p.batch, s.t, s.f, s.a2, s.b2, s.div);
+    if ((e = hipMemsetAsync(s.st.flag, 0, s.tiles * 4ull, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(s.st.ticket, 0, 8, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.keys2, s.vals2, n_slots, c, p.table,
+                       plane, ts, p.batch, s.st);
     return hipGetLastError();
 }
 

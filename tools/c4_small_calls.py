@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--zipf", type=float, default=None)
     ap.add_argument("--sync", action="store_true", help="fb_process_seg_dev (one stream) instead of the async call")
+    ap.add_argument("--timed", action="store_true", help="a timed context (FB_CFG_TIMED) with per-frame capture times")
     args = ap.parse_args()
     from flodbadd_amd import _native as N
     from flodbadd_amd import synth
@@ -30,7 +31,7 @@ def main():
     cfg.filter = N.FB_FILTER_GLOBAL_ONLY
     cfg.max_batch_packets = args.frames
     cfg.flow_capacity = 1 << 21
-    cfg.flags = N.FB_CFG_FIXED_TABLE
+    cfg.flags = N.FB_CFG_FIXED_TABLE | (N.FB_CFG_TIMED if args.timed else 0)
     ctx = C.c_void_p(lib.fb_create(0, C.byref(cfg)))
     kw = dict(zipf=1, zipf_s=args.zipf) if args.zipf else {}
     n = args.frames
@@ -40,9 +41,13 @@ def main():
              N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize)) for _ in range(2)]
     N.check(lib.fb_set_session_records(ctx, 0))
     s = N.Stream()
+    tsb = [N.DeviceBuffer(8 * n).upload((1_700_000_000 * 10 ** 9 + j * 10 ** 9 + 2000 * np.arange(n, dtype=np.uint64))
+                                        .astype(np.uint64)) for j in range(2)] if args.timed else None
 
     def call(i):
         b = sets[i & 1]
+        if tsb:
+            N.check(lib.fb_set_frame_times(ctx, tsb[i & 1].ptr))
         fn = lib.fb_process_seg_dev if args.sync else lib.fb_process_seg_async_dev
         N.check(fn(ctx, b[0].ptr, fr.nbytes, b[1].ptr, n, b[2].ptr, b[3].ptr, None, b[4].ptr, s.ptr))
     for i in range(args.warmup):
