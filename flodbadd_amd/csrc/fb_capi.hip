@@ -1509,17 +1509,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
     p.char_call = c->d_char_call;
     c->part_recs = nullptr;
-    HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
-    if (split) {
-        // (K1t stays on the update stream: beside the next batch's parse it takes ~95 us instead of
-        // 10, but on the parse stream it delays that parse instead -- C4 12.85 vs 12.57 Gpps)
-        HIP_TRY(hipEventRecord(c->ev_parsed, s_bucket));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_parsed, 0));
-    }
-    HIP_TRY(launch_flow_apply(p, chunks, s));
-    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), c->d_mbox,
-                               ++c->upd_seq, s));
-    if (c->timed) {  // the capture-time pass over the placed records (fb_time.hip)
+    if (c->timed) {  // the capture-time pass's scratch (K2 writes each record's slot into it)
         const uint32_t slots = p.max_recs < n_slots ? p.max_recs : n_slots;
         uint32_t bits = 0;
         while ((1ull << bits) < c->table_cap) ++bits;
@@ -1534,6 +1524,21 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
                 return set_err(FB_ERR_NOMEM, "capture-time scratch (%llu bytes)", (unsigned long long)need);
             c->tscratch_bytes = need;
         }
+        p.tslot = time_slot_array(c->d_tscratch);
+        p.hot = nullptr;  // no combined entries: every record is a plain entry K2 places
+    }
+    HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));
+    if (split) {
+        // (K1t stays on the update stream: beside the next batch's parse it takes ~95 us instead of
+        // 10, but on the parse stream it delays that parse instead -- C4 12.85 vs 12.57 Gpps)
+        HIP_TRY(hipEventRecord(c->ev_parsed, s_bucket));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_parsed, 0));
+    }
+    HIP_TRY(launch_flow_apply(p, chunks, s));
+    HIP_TRY(launch_flow_finish(d_stats, c->d_partials, c->flow_parts, c->d_error + (c->epoch & 3u), c->d_mbox,
+                               ++c->upd_seq, s));
+    if (c->timed) {  // the capture-time pass over the placed records (fb_time.hip)
+        const uint32_t slots = p.max_recs < n_slots ? p.max_recs : n_slots;
         HIP_TRY(launch_time_update(p, slots, c->table_cap, c->d_time, c->next_ts, c->d_tscratch, s));
         HIP_TRY(hipEventRecord(c->ev_tscratch, s));
         c->next_ts = nullptr;

@@ -1255,6 +1255,12 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                         r < 0 ? 0u
                               : P.ent ? hist_word(sl, hist_code((fe[3].z >> 16) & 1u, fe[3].z & 0xFFu), fe[3].y)
                                       : hist_word(sl, v0);
+                    if (P.tslot) {  // timed contexts: the record slot's table slot for the capture-time pass
+                        // (an update entry's record slot: its segment's 64 slots + its rank, unit 0 word 7)
+                        const uint32_t rs = P.ent ? ((v0 & kEntUnitMask) / kUpdUnitsPerSeg) * 64u + (r0[1].w >> 26)
+                                                  : (v0 & kEntRecMask);
+                        P.tslot[rs] = r < 0 ? ~0u : part * kFlowSlots + sl;
+                    }
                 }
 #pragma unroll
                 for (uint32_t w = 0; w < 4u; ++w) r0[w] = r1[w];

@@ -283,6 +283,8 @@ struct FlowParams {
                                 // K1c / K2 read instead of the records
     uint4* char_call = nullptr; // [capacity] per slot: the update call of the flow's first S, s, H, h
                                 // (FB_CALL_NONE: none), for the multi-GPU merge (fb_flow_merge_dev)
+    uint32_t* tslot = nullptr;  // timed contexts: [record slots] K2 writes each applied record's table slot
+                                // (~0u: not taken); K1c's combining is off then (every record a plain entry)
     uint32_t* order = nullptr;  // [parts + kK2Lead + 1] K2's partition order: per partition its entries
                                 // (K1t's sums; bit 31: one of K2's leading workgroups takes it), the
                                 // leading partitions, their count (zeroed by K1)
@@ -573,6 +575,7 @@ hipError_t launch_merge(const fb_flow_mrec* in, unsigned long long n, fb_flow_re
 // (its record slots, n_slots of them), brings each touched flow's FlowTime forward; ts = the batch's
 // capture timestamps by frame index; scratch: time_scratch_bytes(n_slots, log2(cap)).
 uint64_t time_scratch_bytes(uint32_t n_slots, uint32_t cap_bits);
+uint32_t* time_slot_array(void* scratch);  // the scratch's first array: FlowParams::tslot of the update
 hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t cap, FlowTime* plane,
                               const unsigned long long* ts, void* scratch, hipStream_t s);
 hipError_t launch_time_remap(const FlowTime* old, const uint32_t* remap, unsigned long long old_cap, FlowTime* nw,

@@ -23,9 +23,10 @@
 // inputs -- scan A: the latest reset / end in the run at or before it, the run's ends so far, its
 // head; scan B: the accepted interarrival sum and the latest accepted term with its divisor -- and
 // the run's last packet writes the flow's new FlowTime:
-//   k_time_keys  one thread per record slot: the record's key (record or update entry), its table
-//                slot (probe of the updated table), sort key = slot (cap: no flow -> sorts last),
-//                value = pkt_index << 1 | P
+//   k_time_keys  one thread per record slot: its table slot (K2 wrote it per applied record:
+//                FlowParams::tslot; K1c's combining is off on a timed context, so every record is a
+//                plain entry), sort key = slot (cap: no flow -> sorts last), value = pkt_index << 1 | P
+//                (from the record or update entry)
 //   sort         rocPRIM LSD radix sort of (slot, value) pairs over log2(cap) + 1 bits (stable: the
 //                packet order inside a slot stays)
 //   k_time_runs  ONE launch over tiles of 1,024 sorted packets taken in ticket order: per packet its
@@ -33,8 +34,8 @@
 //                scan A (thread, wave, block, then the tile's prefix by decoupled look-back), the
 //                interarrival term, scan B the same way, and the runs' last packets write the plane
 //                (start / end from the table's positions of this call)
-// Bytes per record: the record or entry (56 / 32 B) + the table probe (a 128-B slot line) + 4 B of
-// sort key and value out; the sort 3 passes x 16 B; the fused pass 8 B in + the timestamp gathers
+// Bytes per record: K2's 4-B slot store, the record's flags / pkt_index (8 of its 56 / 32 B) + 4 B of
+// slot in, 8 B of sort key and value out; the sort 3 passes x 16 B; the fused pass 8 B in + the timestamp gathers
 // (8 B, up to four per packet, mostly cached) -- an auxiliary pass, not the headline path.
 #include <cstring>  // (rocPRIM's texture-cache iterator needs memset declared)
 
@@ -90,30 +91,6 @@ __device__ __forceinline__ SegB segB_op(const SegB& x, const SegB& y) {
 // per sorted packet flags
 constexpr uint8_t kFP = 1u, kFT = 2u, kFIn = 4u, kFHead = 8u, kFIns = 16u, kFEnd = 32u, kFInPrev = 64u, kFReset = 128u;
 
-// The table slot of `key` (the update just inserted every key it took), or `cap` if absent (a record
-// the table could not take: its flow is not in the table).
-__device__ __forceinline__ uint32_t table_slot(const FlowSlot* T, uint32_t part_shift, const uint32_t key[10],
-                                               uint32_t cap) {
-    const unsigned long long h = flow_hash_words(key);
-    const uint32_t part = part_of(h, part_shift);
-    const uint32_t want = (uint32_t)h | 2u;
-    uint32_t j = (uint32_t)h & (kFlowSlots - 1u);
-    const FlowSlot* P = T + (size_t)part * kFlowSlots;
-    for (uint32_t probe = 0; probe < kFlowSlots; ++probe) {
-        const FlowSlot& s = P[j];
-        const uint32_t tag = s.tag;
-        if (tag == 0u) return cap;
-        if (tag == want) {
-            bool eq = (s.key[9] & 0xFFFFu) == (key[9] & 0xFFFFu);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) eq &= s.key[k] == key[k];
-            if (eq) return part * kFlowSlots + j;
-        }
-        j = (j + 1u) & (kFlowSlots - 1u);
-    }
-    return cap;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -123,32 +100,35 @@ __global__ __launch_bounds__(kTmThreads) void k_time_keys(const FlowParams P, ui
     if (i >= n) return;
     const uint32_t nrec = batch_records(P);
     bool ok = i < nrec;
-    uint32_t w = i;
-    if (ok && P.rec_part) {  // update entries of the fused parse (fb_internal.h UpdEnt)
+    uint32_t pkt = 0u, flags = 0u, proto = 0u;
+    bool has_flags = false;
+    if (ok && P.rec_part) {  // update entries of the fused parse (fb_internal.h UpdEnt): unit 0 only
         ok = !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
-        const uint32_t pw = ok ? P.rec_part[i] : 0u;
-        w = (i >> 6) * kUpdUnitsPerSeg + ((pw >> kRecUnitShift) & 127u) | ((pw & kRecV6) ? kEntV6 : 0u);
+        if (ok) {
+            const uint32_t pw = P.rec_part[i];
+            const uint4* u = P.ent + (size_t)((i >> 6) * kUpdUnitsPerSeg + ((pw >> kRecUnitShift) & 127u)) * 2u;
+            const uint4 A = u[0], B = u[1];
+            proto = A.w & 0xFFu;
+            pkt = B.z;
+            flags = (B.w >> 8) & 0xFFu;
+            has_flags = (B.w >> 16) & 1u;
+        }
     } else if (ok) {
         ok = slot_valid(P, i);
+        if (ok) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + i);
+            proto = q[9] & 0xFFu;           // protocol byte of the key (offset 36)
+            const uint2 m = ld_u2(q + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
+            flags = m.x & 0xFFu;
+            has_flags = (m.x >> 8) & FB_META_HAS_FLAGS;
+            pkt = m.y;
+        }
     }
     uint32_t key = cap, val = 0u;
     if (ok) {
-        uint4 e[4];
-        if (P.rec_part) {
-            uint4 r[4];
-            raw_entry(P, w, r);
-            entry_of(true, r, w, e);
-        } else {
-            uint4 r[4];
-            raw_entry(P, w, r);
-            entry_of(false, r, w, e);
-        }
-        const uint32_t k[10] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x, e[2].y & 0xFFFFu};
-        const uint32_t pkt = e[3].x, hinfo = e[3].z;
-        const uint32_t flags = (hinfo >> 8) & 0xFFu;
-        const bool has_flags = (hinfo >> 16) & 1u;
-        const bool psh = has_flags && (k[9] & 0xFFu) == 6u && (flags & kTcpPsh);
-        key = table_slot(P.table, P.part_shift, k, cap);
+        const uint32_t sl = P.tslot[i];  // the record's table slot, written by K2 (~0u: not taken)
+        const bool psh = has_flags && proto == 6u && (flags & kTcpPsh);
+        key = sl < cap ? sl : cap;
         val = pkt << 1 | (psh ? 1u : 0u);
     }
     keys[i] = key;
@@ -500,7 +480,7 @@ __global__ __launch_bounds__(256) void k_time_export(const FlowSlot* T, const Fl
 
 // ---------------------------------------------------------------------------------------------
 struct TimeScratch {
-    uint32_t *keys, *keys2, *vals, *vals2;
+    uint32_t *tslot, *keys, *keys2, *vals, *vals2;
     RunStatus st;
     uint32_t tiles;
     void* tmp;
@@ -518,7 +498,7 @@ static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
 uint64_t time_scratch_bytes(uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
     const size_t tiles = (m + kRunTile - 1) / kRunTile;
-    return al256(m * 4) * 4 + al256(tiles * 4) + al256(tiles * sizeof(SegA)) * 2 + al256(tiles * sizeof(SegB)) * 2 +
+    return al256(m * 4) * 5 + al256(tiles * 4) + al256(tiles * sizeof(SegA)) * 2 + al256(tiles * sizeof(SegB)) * 2 +
            al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
 }
 
@@ -528,6 +508,7 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     auto take = [&](size_t b) { char* q = p; p += al256(b); return q; };
     TimeScratch s;
     s.tiles = (uint32_t)((m + kRunTile - 1) / kRunTile);
+    s.tslot = (uint32_t*)take(m * 4);  // (first: time_slot_array)
     s.keys = (uint32_t*)take(m * 4);
     s.keys2 = (uint32_t*)take(m * 4);
     s.vals = (uint32_t*)take(m * 4);
@@ -542,6 +523,8 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     s.tmp = take(s.tmp_bytes);
     return s;
 }
+
+uint32_t* time_slot_array(void* scratch) { return static_cast<uint32_t*>(scratch); }
 
 hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t cap, FlowTime* plane,
                               const unsigned long long* ts, void* scratch, hipStream_t st) {
