@@ -313,6 +313,73 @@ def queue_line(N, lib, ctx, config_id, n, steps, warmup, rotate, depth=8):
                      "submission to completion, DESIGN 3.7: the first batches' fill is inside the timed region)")
 
 
+def queue_table_line(N, lib, ctx, n=1 << 20, steps=100, warmup=8, rotate=4, depth=4):
+    """One batch per call WITH the session-table upsert through the resident queue: a queue created
+    shared (FB_QUEUE_SHARED, one workgroup per CU) parses C4-mix batches of n frames while each
+    completed batch is applied to the context's table on a stream of its own (fb_flow_update_seg_dev
+    beside the resident kernel); `rotate` device buffer sets, a set resubmitted only after its last
+    update completed.  Host wall clock from the first submission to the last update's completion."""
+    from flodbadd_amd import synth
+    frames, offs = synth.generate(4, n, first=0)
+    nseg = (n + N.FB_SEG_FRAMES - 1) // N.FB_SEG_FRAMES
+    sets, descs = [], []
+    for _ in range(rotate):
+        b = (N.DeviceBuffer(frames.nbytes).upload(frames), N.DeviceBuffer(offs.nbytes).upload(offs),
+             N.DeviceBuffer(nseg * N.SEG_BYTES), N.DeviceBuffer(nseg * 4), N.DeviceBuffer(N.STATS_DTYPE.itemsize))
+        d = np.zeros(1, dtype=N.SEG_BATCH_DTYPE)
+        d[0] = (b[0].ptr.value, frames.nbytes, b[1].ptr.value, n, 0, b[2].ptr.value, b[3].ptr.value, 0, b[4].ptr.value)
+        sets.append(b)
+        descs.append(d)
+    upd = N.Stream()
+    evs = [N.Event() for _ in range(rotate)]
+    N.check(lib.fb_flow_clear(ctx, None))
+    N.check(lib.fb_stream_sync(None))
+    q = lib.fb_seg_queue_create_ex(ctx, depth, 0, N.FB_QUEUE_SHARED)
+    if not q:
+        raise RuntimeError("fb_seg_queue_create_ex: %s" % lib.fb_last_error().decode())
+    q = C.c_void_p(q)
+    ptrs = [C.c_void_p(d.ctypes.data) for d in descs]
+    tk = C.c_uint64()
+    submit, wait = lib.fb_seg_queue_submit, lib.fb_seg_queue_wait
+
+    def run(k0, count):
+        """Batches k0 .. k0 + count - 1: submit batch i, then apply batch i - 1 once it completed."""
+        tickets = {}
+        for i in range(k0, k0 + count + 1):
+            if i < k0 + count:
+                if i - k0 >= rotate:
+                    evs[i % rotate].wait_spin()  # the set's previous batch is applied
+                N.check(submit(q, ptrs[i % rotate], C.byref(tk)))
+                tickets[i] = tk.value
+            if i > k0:
+                j = i - 1
+                N.check(wait(q, tickets.pop(j)))
+                b = sets[j % rotate]
+                N.check(lib.fb_flow_update_seg_dev(ctx, b[2].ptr, b[3].ptr, n, b[4].ptr, upd.ptr))
+                evs[j % rotate].record(upd)
+        upd.sync()
+    try:
+        run(0, warmup)
+        t0 = time.perf_counter()
+        run(warmup, steps)
+        el = time.perf_counter() - t0
+    finally:
+        N.check(lib.fb_seg_queue_destroy(q))
+    st = sets[(warmup + steps - 1) % rotate][4].download(np.zeros(1, dtype=N.STATS_DTYPE))
+    cnt = C.c_uint64()
+    N.check(lib.fb_flow_count(ctx, C.byref(cnt), None))
+    for b in sets:
+        for x in b:
+            x.free()
+    if int(st[0]["error"]) or int(st[0]["new_sessions"]) + int(st[0]["updated_sessions"]) != int(st[0]["n_session"]):
+        raise RuntimeError("queue + table batch stats inconsistent: %s" % st)
+    N.check(lib.fb_flow_clear(ctx, None))
+    return dict(value=round(n * steps / el / 1e6, 2), unit="Mpackets/s", ms_per_batch=round(el * 1e3 / steps, 4),
+                steps=steps, frames_per_batch=n, flows_in_table=int(cnt.value),
+                note="C4-mix batches one per call through a shared resident queue (FB_QUEUE_SHARED), each "
+                     "completed batch applied to the session table on its own stream beside it")
+
+
 def enrich_timing(N, lib, ctx, flows, stream, reps=5):
     """New-session enrichment (fb_flow_enrich_dev) over every flow of the C4 table against
     IPtoASN-sized synthetic tables: 500k IPv4 + 100k IPv6 ASN ranges, 50k blacklist ranges in 32
@@ -1150,6 +1217,11 @@ def main():
                 extra["single_batch_queue"] = qr
             except Exception as e:  # reported beside the line; the headline does not depend on it
                 extra["single_batch_queue"] = {"error": repr(e)[:300]}
+            if args.config == 2 and world == 1:
+                try:
+                    extra["single_batch_queue_table"] = queue_table_line(N, lib, ctx)
+                except Exception as e:
+                    extra["single_batch_queue_table"] = {"error": repr(e)[:300]}
     # N > 1: the scaling line needs only the headline path (the other layout is timed at N = 1)
     if not args.no_other_mode and world == 1:
         other = "dense" if args.mode == "seg" else "seg"

@@ -140,26 +140,53 @@ __global__ __launch_bounds__(kTmThreads) void k_time_keys(const FlowParams P, ui
 // two chained decoupled look-backs): per packet its flags, the segmented scan A (latest reset / end,
 // ends so far, the run's head), then its interarrival term and the segmented scan B (accepted sum,
 // latest accepted term and its divisor), and the run's last packet writes the flow's FlowTime.
+//
+// A tile publishes each scan's aggregate, then its inclusive value, as two 64-bit words with RELAXED
+// agent-scope atomic stores, each word carrying a 2-bit status (1 aggregate, 2 inclusive) beside its
+// half of the value: a reader takes a value only when both of its words carry the status, so no
+// release / acquire fence is needed (on gfx950 an agent-scope release writes back, and an acquire
+// invalidates, the XCD's L2 -- per tile, that made this pass ~8x slower than its memory traffic).
 constexpr uint32_t kRunThreads = 256, kRunItems = 4, kRunTile = kRunThreads * kRunItems;
-// status bits per scan (A: bits 0-2, B: bits 16-18): aggregate published, inclusive published, the
-// aggregate holds a run head (a segmented value: everything before it is irrelevant)
-constexpr uint32_t kStAgg = 1u, kStInc = 2u, kStHead = 4u;
+constexpr unsigned long long kStAgg = 1ull, kStInc = 2ull;
 
-struct RunStatus {  // per tile: status bits (zeroed before the launch), then the values
-    uint32_t* flag;
-    SegA* a_agg;
-    SegA* a_inc;
-    SegB* b_agg;
-    SegB* b_inc;
+struct RunStatus {  // per tile 8 words: A aggregate, A inclusive, B aggregate, B inclusive (zeroed per launch)
+    unsigned long long* w;
     uint32_t* ticket;
 };
-
-__device__ __forceinline__ uint32_t st_load(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+constexpr unsigned long long kM27 = (1ull << 27) - 1ull, kM28 = (1ull << 28) - 1ull;
+__device__ __forceinline__ void pack(const SegA& x, unsigned long long st, unsigned long long (&w)[2]) {
+    w[0] = st | (unsigned long long)x.h << 2 | ((unsigned long long)x.r & kM27) << 34;  // h: 27 bits + bit 31
+    w[1] = st | ((unsigned long long)x.e & kM27) << 2 | ((unsigned long long)x.c & kM27) << 29;
 }
-__device__ __forceinline__ void st_publish(uint32_t* p, uint32_t v) {
-    __hip_atomic_fetch_or(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ SegA unpack_a(const unsigned long long (&w)[2]) {
+    return SegA{(uint32_t)(w[0] >> 2), (uint32_t)((w[0] >> 34) & kM27), (uint32_t)((w[1] >> 2) & kM27),
+                (uint32_t)((w[1] >> 29) & kM27)};
 }
+constexpr unsigned long long kM46 = (1ull << 46) - 1ull;
+__device__ __forceinline__ void pack(const SegB& x, unsigned long long st, unsigned long long (&w)[2]) {
+    // s: 46 bits (accepted interarrivals are >= 0), a: 27 bits, d: 28 bits (divisor + head bit 30 -> 27)
+    const unsigned long long d = (x.d & kM27) | ((x.d & kBHead) ? (1ull << 27) : 0ull);
+    w[0] = st | ((unsigned long long)x.s & kM46) << 2 | ((unsigned long long)x.a & 0xFFFFull) << 48;
+    w[1] = st | (((unsigned long long)x.a >> 16) & 0x7FFull) << 2 | (d & kM28) << 13;
+}
+__device__ __forceinline__ SegB unpack_b(const unsigned long long (&w)[2]) {
+    const uint32_t d = (uint32_t)((w[1] >> 13) & kM28);
+    return SegB{(long long)((w[0] >> 2) & kM46), (uint32_t)((w[0] >> 48) | ((w[1] >> 2) & 0x7FFull) << 16),
+                (d & (uint32_t)kM27) | ((d >> 27) ? kBHead : 0u)};
+}
+__device__ __forceinline__ void st_put(unsigned long long* p, const unsigned long long (&w)[2]) {
+    __hip_atomic_store(p, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool st_get(const unsigned long long* p, unsigned long long st, unsigned long long (&w)[2]) {
+    w[0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w[1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (w[0] & 3ull) == st && (w[1] & 3ull) == st;
+}
+__device__ __forceinline__ bool has_head(const SegA& x) { return segA_head(x); }
+__device__ __forceinline__ bool has_head(const SegB& x) { return (x.d & kBHead) != 0u; }
+__device__ __forceinline__ SegA unpack(const unsigned long long (&w)[2], const SegA*) { return unpack_a(w); }
+__device__ __forceinline__ SegB unpack(const unsigned long long (&w)[2], const SegB*) { return unpack_b(w); }
 
 // Lane shuffles of the scan words.
 __device__ __forceinline__ SegA shfl_down(const SegA& x, int o) {
@@ -170,46 +197,75 @@ __device__ __forceinline__ SegB shfl_down(const SegB& x, int o) {
     return SegB{__shfl_down(x.s, o, 64), (uint32_t)__shfl_down(x.a, o, 64), (uint32_t)__shfl_down(x.d, o, 64)};
 }
 
-// The exclusive prefix of tile `t` for one scan, by one wavefront: lane L looks at tile t-1-L-64k
-// (lane 0 the nearest), every lane waits for its tile's status, the nearest tile with an inclusive
-// value ends the walk, and the window's values are folded in tile order (the all-zero word is the
-// identity of both operators).  shift: 0 (A) or 16 (B) in the status word.
+// The exclusive prefix of tile `t` for one scan (words at offset `off` of each tile's 8: 0 A, 4 B), by
+// one wavefront: lane L looks at tile t-1-L-64k (lane 0 the nearest); the walk ends at the nearest
+// tile whose inclusive value is published or whose aggregate holds a run head (a segmented value),
+// waiting only for that tile and the nearer ones; the window is folded in tile order (the all-zero
+// word is the identity of both operators).
 template <class V, class Op>
-__device__ V lookback(const RunStatus& S, uint32_t t, uint32_t shift, const V* agg, const V* inc, Op op) {
+__device__ V lookback(const RunStatus& S, uint32_t t, uint32_t off, Op op) {
     const uint32_t lane = threadIdx.x & 63u;
     V acc{};
     bool have = false;
     for (int j0 = (int)t - 1; j0 >= 0; j0 -= 64) {
         const int j = j0 - (int)lane;
-        uint32_t f = 0u;
-        if (j >= 0)
-            while (((f = st_load(S.flag + j)) >> shift & 3u) == 0u) __builtin_amdgcn_s_sleep(1);
-        // the walk ends at the nearest tile with an inclusive value or a run head in its aggregate
-        const unsigned long long full = __ballot(j >= 0 && ((f >> shift) & (kStInc | kStHead)));
-        const uint32_t stop = full ? (uint32_t)__builtin_ctzll(full) : 64u;
+        bool ready = j < 0, inc = false;
         V v{};
-        if (j >= 0 && lane <= stop) v = (lane == stop && ((f >> shift) & kStInc)) ? inc[j] : agg[j];
+        uint32_t stop;
+        for (;;) {
+            if (!ready) {
+                unsigned long long w[2];
+                const unsigned long long* base = S.w + (size_t)j * 8u + off;
+                if (st_get(base + 2, kStInc, w)) {
+                    v = unpack(w, (const V*)nullptr);
+                    ready = inc = true;
+                } else if (st_get(base, kStAgg, w)) {
+                    v = unpack(w, (const V*)nullptr);
+                    ready = true;
+                }
+            }
+            const unsigned long long rdy = __ballot(ready);
+            const unsigned long long hit = __ballot(ready && j >= 0 && (inc || has_head(v)));
+            const uint32_t not_ready = ~rdy ? (uint32_t)__builtin_ctzll(~rdy) : 64u;
+            const uint32_t first_hit = hit ? (uint32_t)__builtin_ctzll(hit) : 64u;
+            if (first_hit < not_ready || not_ready == 64u) {
+                stop = first_hit;  // (64: the whole window, no end of the walk in it)
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (j < 0 || lane > stop) v = V{};
         // fold: lane L holds tiles [L, L + o) after step o (higher lanes are earlier tiles)
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const V w = shfl_down(v, o);
             if ((lane & (2u * o - 1u)) == 0u) v = op(w, v);
         }
-        // (lane 0 holds the window folded in tile order)
-        acc = have ? op(v, acc) : v;
+        acc = have ? op(v, acc) : v;  // (lane 0 holds the window folded in tile order)
         have = true;
-        if (full) break;
+        if (stop < 64u) break;
     }
     return acc;  // meaningful in lane 0
 }
 
-__device__ __forceinline__ unsigned long long t_of(const uint32_t* vals, const unsigned long long* ts, uint32_t j) {
-    return ts[vals[j] >> 1];
+// The capture time of sorted packet j: gathered once into sorted order (k_time_gather), so the fused
+// pass reads it coalesced (a packet reads its own and its two predecessors').
+__device__ __forceinline__ unsigned long long t_of(const uint32_t* vals, const unsigned long long* tsort, uint32_t j) {
+    (void)vals;
+    return tsort[j];
+}
+
+__global__ __launch_bounds__(kTmThreads) void k_time_gather(const uint32_t* keys, const uint32_t* vals, uint32_t n,
+                                                            uint32_t cap, const unsigned long long* ts,
+                                                            unsigned long long* tsort) {
+    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
+    if (i < n) tsort[i] = keys[i] < cap ? ts[vals[i] >> 1] : 0ull;
 }
 
 __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys, const uint32_t* vals, uint32_t n,
                                                           uint32_t cap, const FlowSlot* T, FlowTime* plane,
-                                                          const unsigned long long* ts, uint32_t batch, RunStatus S) {
+                                                          const unsigned long long* ts, const unsigned long long* tsort,
+                                                          uint32_t batch, RunStatus S) {
     __shared__ uint32_t s_tile;
     __shared__ SegA s_wa[kRunThreads / 64];
     __shared__ SegB s_wb[kRunThreads / 64];
@@ -231,7 +287,7 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
             tprev = ins_ ? tj : plane[sj].last_activity_ns;
         } else {
             ins_ = false;
-            tprev = t_of(vals, ts, j - 1u);
+            tprev = t_of(vals, tsort, j - 1u);
         }
         T_ = !ins_ && ms_between(tj, tprev) >= (long long)FB_SEGMENT_TIMEOUT_MS;
         in_ = ins_ ? !P_ : (T_ || !P_);
@@ -251,14 +307,14 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         if (key[k] >= cap) continue;  // (no flow: sorts last, a neutral word)
         const uint32_t s = key[k];
         const bool head = i == 0u || keys[i - 1u] != s;
-        const unsigned long long t = t_of(vals, ts, i);
+        const unsigned long long t = t_of(vals, tsort, i);
         bool Ti, ini, insi, in_prev;
         state(i, s, head, t, Ti, ini, insi);
         if (head) {
             in_prev = insi ? false : plane[s].in_segment != 0u;
         } else {
             bool T1, in1, ins1;
-            state(i - 1u, s, i == 1u || keys[i - 2u] != s, t_of(vals, ts, i - 1u), T1, in1, ins1);
+            state(i - 1u, s, i == 1u || keys[i - 2u] != s, t_of(vals, tsort, i - 1u), T1, in1, ins1);
             in_prev = in1;
         }
         const bool P_ = vals[i] & 1u;
@@ -297,20 +353,21 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         SegA agg = s_wa[0];
         for (uint32_t w = 1; w < kRunThreads / 64; ++w) agg = segA_op(agg, s_wa[w]);
         SegA prefix{0u, 0u, 0u, 0u};
+        unsigned long long pw[2];
         if (tile == 0u) {
             if (lane == 0u) {
-                S.a_inc[0] = agg;
-                st_publish(S.flag, kStInc);
+                pack(agg, kStInc, pw);
+                st_put(S.w + 2, pw);
             }
         } else {
             if (lane == 0u) {
-                S.a_agg[tile] = agg;
-                st_publish(S.flag + tile, kStAgg | (segA_head(agg) ? kStHead : 0u));
+                pack(agg, kStAgg, pw);
+                st_put(S.w + (size_t)tile * 8u, pw);
             }
-            prefix = lookback(S, tile, 0u, S.a_agg, S.a_inc, segA_op);
+            prefix = lookback<SegA>(S, tile, 0u, segA_op);
             if (lane == 0u) {
-                S.a_inc[tile] = segA_op(prefix, agg);
-                st_publish(S.flag + tile, kStInc);
+                pack(segA_op(prefix, agg), kStInc, pw);
+                st_put(S.w + (size_t)tile * 8u + 2u, pw);
             }
         }
         if (lane == 0u) s_pa = prefix;
@@ -343,12 +400,12 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         const bool head = fl[k] & kFHead;
         const SegA prev = head ? SegA{0u, 0u, 0u, 0u} : xa[k];  // the run's state before packet i
         unsigned long long prev_end = FB_SEEN_NONE;
-        if (prev.e) prev_end = t_of(vals, ts, prev.e - 1u);
+        if (prev.e) prev_end = t_of(vals, tsort, prev.e - 1u);
         else if (!ins_run) prev_end = plane[s].last_segment_end_ns;
         if (prev_end == FB_SEEN_NONE) continue;
         unsigned long long start;  // current_segment_start as of packet i (src/packets.rs:151-154)
         if (!(fl[k] & kFInPrev)) start = tt[k];
-        else if (prev.r) start = t_of(vals, ts, prev.r - 1u);
+        else if (prev.r) start = t_of(vals, tsort, prev.r - 1u);
         else start = plane[s].current_segment_start_ns;
         const long long ia_ms = ms_between(start, prev_end);
         if (ia_ms < 0) continue;  // (double)ia / 1000.0 >= 0.0, src/packets.rs:165
@@ -378,20 +435,21 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         SegB agg = s_wb[0];
         for (uint32_t w = 1; w < kRunThreads / 64; ++w) agg = segB_op(agg, s_wb[w]);
         SegB prefix{0ll, 0u, 0u};
+        unsigned long long pw[2];
         if (tile == 0u) {
             if (lane == 0u) {
-                S.b_inc[0] = agg;
-                st_publish(S.flag, kStInc << 16);
+                pack(agg, kStInc, pw);
+                st_put(S.w + 6, pw);
             }
         } else {
             if (lane == 0u) {
-                S.b_agg[tile] = agg;
-                st_publish(S.flag + tile, (kStAgg | ((agg.d & kBHead) ? kStHead : 0u)) << 16);
+                pack(agg, kStAgg, pw);
+                st_put(S.w + (size_t)tile * 8u + 4u, pw);
             }
-            prefix = lookback(S, tile, 16u, S.b_agg, S.b_inc, segB_op);
+            prefix = lookback<SegB>(S, tile, 4u, segB_op);
             if (lane == 0u) {
-                S.b_inc[tile] = segB_op(prefix, agg);
-                st_publish(S.flag + tile, kStInc << 16);
+                pack(segB_op(prefix, agg), kStInc, pw);
+                st_put(S.w + (size_t)tile * 8u + 6u, pw);
             }
         }
         if (lane == 0u) s_pb = prefix;
@@ -412,7 +470,7 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         const bool ins = a.h & kInsRun;
         FlowTime o;
         if (ins) {
-            o.start_time_ns = t_of(vals, ts, H);
+            o.start_time_ns = t_of(vals, tsort, H);
             o.end_time_ns = FB_SEEN_NONE;
             o.current_segment_start_ns = o.start_time_ns;
             o.last_segment_end_ns = FB_SEEN_NONE;
@@ -423,8 +481,8 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
             o = plane[s];
         }
         o.segment_count += a.c;
-        if (a.r) o.current_segment_start_ns = t_of(vals, ts, a.r - 1u);
-        if (a.e) o.last_segment_end_ns = t_of(vals, ts, a.e - 1u);
+        if (a.r) o.current_segment_start_ns = t_of(vals, tsort, a.r - 1u);
+        if (a.e) o.last_segment_end_ns = t_of(vals, tsort, a.e - 1u);
         o.total_segment_interarrival_ms += b.s;
         if (b.a) o.segment_interarrival_div = b.d & ~kBHead;
         o.last_activity_ns = tt[k];
@@ -481,6 +539,7 @@ __global__ __launch_bounds__(256) void k_time_export(const FlowSlot* T, const Fl
 // ---------------------------------------------------------------------------------------------
 struct TimeScratch {
     uint32_t *tslot, *keys, *keys2, *vals, *vals2;
+    unsigned long long* tsort;
     RunStatus st;
     uint32_t tiles;
     void* tmp;
@@ -498,8 +557,7 @@ static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
 uint64_t time_scratch_bytes(uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
     const size_t tiles = (m + kRunTile - 1) / kRunTile;
-    return al256(m * 4) * 5 + al256(tiles * 4) + al256(tiles * sizeof(SegA)) * 2 + al256(tiles * sizeof(SegB)) * 2 +
-           al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
+    return al256(m * 4) * 5 + al256(m * 8) + al256(tiles * 64) + al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
 }
 
 static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
@@ -513,11 +571,8 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     s.keys2 = (uint32_t*)take(m * 4);
     s.vals = (uint32_t*)take(m * 4);
     s.vals2 = (uint32_t*)take(m * 4);
-    s.st.flag = (uint32_t*)take(s.tiles * 4);
-    s.st.a_agg = (SegA*)take(s.tiles * sizeof(SegA));
-    s.st.a_inc = (SegA*)take(s.tiles * sizeof(SegA));
-    s.st.b_agg = (SegB*)take(s.tiles * sizeof(SegB));
-    s.st.b_inc = (SegB*)take(s.tiles * sizeof(SegB));
+    s.tsort = (unsigned long long*)take(m * 8);
+    s.st.w = (unsigned long long*)take(s.tiles * 64ull);
     s.st.ticket = (uint32_t*)take(8);
     s.tmp_bytes = sort_tmp_bytes(n, cap_bits + 1u);
     s.tmp = take(s.tmp_bytes);
@@ -540,10 +595,12 @@ hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t ca
     size_t tb = s.tmp_bytes;
     e = rocprim::radix_sort_pairs(s.tmp, tb, s.keys, s.keys2, s.vals, s.vals2, n_slots, 0u, bits + 1u, st);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(s.st.flag, 0, s.tiles * 4ull, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_time_gather, dim3(g), dim3(kTmThreads), 0, st, s.keys2, s.vals2, n_slots, c, ts, s.tsort);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(s.st.w, 0, s.tiles * 64ull, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(s.st.ticket, 0, 8, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.keys2, s.vals2, n_slots, c, p.table,
-                       plane, ts, p.batch, s.st);
+                       plane, ts, s.tsort, p.batch, s.st);
     return hipGetLastError();
 }
 

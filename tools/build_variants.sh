@@ -28,7 +28,7 @@ for f in glob.glob(sys.argv[1] + "/*.hip") + glob.glob(sys.argv[1] + "/*.h"):
 PY
   fi
   objs=""
-  for s in fb_parse fb_compact fb_flow fb_hist fb_capi fb_ring fb_enrich fb_dns fb_merge; do
+  for s in $(python3 -c "import sys; sys.path.insert(0, \"flodbadd_amd\"); import build; print(\" \".join(x[:-4] for x in build.HIP_SOURCES))"); do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -Iinclude -I$src -c $src/$s.hip \
       -o flodbadd_amd/build/var_${name}_$s.o &
     objs="$objs flodbadd_amd/build/var_${name}_$s.o"
