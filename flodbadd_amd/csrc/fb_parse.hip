@@ -1423,17 +1423,24 @@ __device__ __forceinline__ uint32_t q_grab(const QueueParams& Q, uint32_t slot, 
 // before its tail (the host stores them in the other order), so a stop seen with nothing new is final.
 __device__ __forceinline__ unsigned long long q_refill(const QueueParams& Q, uint32_t k) {
     const uint32_t lane = threadIdx.x & 63u, R = Q.depth;
-    unsigned long long dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    // Every load here is relaxed and the poller word is released relaxed: these run on every poll, and on
+    // gfx950 an agent release writes back (a system acquire invalidates) the XCD's L2 under the table
+    // update kernels running beside a shared queue (bench single_batch_queue_table: 2.1 ms per 1M-frame
+    // batch with acquire / release polls).  The tail and descriptor words are atomics (they bypass the
+    // non-coherent caches); ordering is paid once per publication: a system acquire before the host's
+    // descriptors are read, the device tail's release after they are copied.
+    unsigned long long dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t got = 0u;
     if (lane == 0u) got = atomicCAS(&Q.d->poller, 0u, blockIdx.x + 1u) == 0u ? 1u : 0u;
     if (!u1st(got)) return dt;
-    dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long hs =
-        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
     const unsigned long long tl =
-        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+        u1st64(lane == 0u ? __hip_atomic_load(&Q.h->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
     QTRACE(if (lane == 0u) atomicAdd(qt(Q, kQtPolls, k), 1ull));
     if (tl > dt) {  // descriptors dt .. tl-1 (at most R: the host waits for slot reuse)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope: the host's descriptor stores)
         const uint32_t words = (uint32_t)min(tl - dt, (unsigned long long)R) * 8u;
         for (uint32_t w = lane; w < words; w += 64u) {
             const unsigned long long j = dt + w / 8u;
@@ -1448,7 +1455,7 @@ __device__ __forceinline__ unsigned long long q_refill(const QueueParams& Q, uin
     } else if (lane == 0u && hs != 0ull) {
         __hip_atomic_store(&Q.d->stop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane == 0u) __hip_atomic_store(&Q.d->poller, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0u) __hip_atomic_store(&Q.d->poller, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return dt;
 }
 
@@ -1472,9 +1479,10 @@ __device__ __forceinline__ bool q_ensure(const QueueParams& Q, QLds* L, uint32_t
         const unsigned long long t0 = rt_now();
         unsigned long long dt;
         for (uint32_t spins = 0u;; ++spins) {
-            dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (relaxed poll)
             if (dt <= k) dt = q_refill(Q, k);
             if (dt > k) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, after the match
                 if (lane == 0u) atomicMax(&L->tail, (uint32_t)dt);
                 break;
             }
@@ -1662,7 +1670,7 @@ __device__ __forceinline__ QPos q_gen_slow(const QueueParams& Q, QLds* L, QGen* 
             if (g->gk >= g->known) {  // a peek at the device ring's tail (the poller keeps it current)
                 uint32_t t = 0u;
                 if (lane == 0u) {
-                    t = (uint32_t)__hip_atomic_load(&Q.d->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    t = (uint32_t)__hip_atomic_load(&Q.d->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // a peek
                     atomicMax(&L->tail, t);
                 }
                 g->known = u1st(t);
