@@ -1479,8 +1479,18 @@ __device__ __forceinline__ bool q_ensure(const QueueParams& Q, QLds* L, uint32_t
         const unsigned long long t0 = rt_now();
         unsigned long long dt;
         for (uint32_t spins = 0u;; ++spins) {
+            // Idle polling is paced: every poll is a memory-side access to one line (the device tail,
+            // the poller word), and a block's polls at s_sleep(2) -- 256 blocks of a shared queue, between
+            // batches -- queue on that line's channel under the table update kernels beside the queue.
+            // Past 64 polls (~0.1 ms with nothing published: the host is the slower side) only the first
+            // 64 blocks keep polling every ~7 us; the others look every ~27 us and never take the poller
+            // word (a batch's chunks are taken dynamically, so the early blocks start it alone).
+            const bool slow = spins >= 64u && blockIdx.x >= 64u;
+            if (slow) {
+                for (int z = 0; z < 6; ++z) __builtin_amdgcn_s_sleep(127);
+            }
             dt = __hip_atomic_load(&Q.d->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (relaxed poll)
-            if (dt <= k) dt = q_refill(Q, k);
+            if (dt <= k && !slow && (spins < 8u || (spins & 3u) == 0u)) dt = q_refill(Q, k);
             if (dt > k) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, after the match
                 if (lane == 0u) atomicMax(&L->tail, (uint32_t)dt);
@@ -1500,8 +1510,14 @@ __device__ __forceinline__ bool q_ensure(const QueueParams& Q, QLds* L, uint32_t
                 if (lane == 0u) __hip_atomic_store(&L->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return false;
             }
-            if (spins < 256u) __builtin_amdgcn_s_sleep(2);
-            else __builtin_amdgcn_s_sleep(127);  // (~3.4 us per poll once idle)
+            if (spins < 8u) {
+                __builtin_amdgcn_s_sleep(2);
+            } else if (spins < 64u) {
+                __builtin_amdgcn_s_sleep(32);
+            } else {
+                __builtin_amdgcn_s_sleep(127);  // (~6.8 us per poll once idle, a refill every 4th)
+                __builtin_amdgcn_s_sleep(127);
+            }
         }
         // lane j < 8 reads word j of the 64-B descriptor (fb_seg_batch) from the device ring
         const unsigned long long v =
