@@ -315,7 +315,7 @@ def queue_line(N, lib, ctx, config_id, n, steps, warmup, rotate, depth=8):
 
 def queue_table_line(N, lib, ctx, n=1 << 20, steps=100, warmup=8, rotate=4, depth=4):
     """One batch per call WITH the session-table upsert through the resident queue: a queue created
-    shared (FB_QUEUE_SHARED, one workgroup per CU) parses C4-mix batches of n frames while each
+    shared (FB_QUEUE_SHARED: one workgroup on each of an eighth of the CUs) parses C4-mix batches of n frames while each
     completed batch is applied to the context's table on a stream of its own (fb_flow_update_seg_dev
     beside the resident kernel); `rotate` device buffer sets, a set resubmitted only after its last
     update completed.  Host wall clock from the first submission to the last update's completion."""

@@ -944,9 +944,14 @@ fb_seg_queue* fb_seg_queue_create_ex(fb_ctx* c, uint32_t depth, uint32_t idle_ms
     int occ = 0;
     if (occupancy_parse_seg_queue(&occ) != hipSuccess || occ < 1) occ = 1;
     // FB_QUEUE_SHARED: one block per CU, so the session-table update kernels (K1 96 KB + K2 80 KB of
-    // LDS, 80 / 128 VGPRs) fit beside it on every CU (two blocks leave ~66 KB of LDS)
+    // LDS, 80 / 128 VGPRs) fit beside it (two blocks leave ~66 KB of LDS)
     const int bpc = (flags & FB_QUEUE_SHARED) ? 1 : FB_QUEUE_BPC;
-    const uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(bpc, occ) * cus));
+    uint32_t grid = std::min<uint32_t>(c->seg_grid, (uint32_t)(std::min(bpc, occ) * cus));
+    // ... and on only a share of the CUs (the dispatcher spreads a small grid one block per CU): K2's
+    // two 80-KB workgroups per CU need a CU's whole LDS, so every CU holding a queue block runs one.
+    // C4-mix 1M-frame batches + the update beside them: CUs / 1, 2, 4, 8, 16, 32 -> 1.8, 2.6, 3.3,
+    // 3.75, 2.3, 1.2 Gpps (past 8 the parse on too few CUs is the step; profiles/r06_shared_queue_div_sweep.txt)
+    if (flags & FB_QUEUE_SHARED) grid = std::max<uint32_t>(1u, grid / FB_QUEUE_SHARED_DIV);
     q->grid = grid;
     q->idle_ns = (uint64_t)(idle_ms ? idle_ms : 5000u) * 1000000ull;
     q->created = std::chrono::steady_clock::now();

@@ -484,6 +484,10 @@ enum QTrace : uint32_t { kQtPub = 0, kQtFirst, kQtArr0, kQtDone, kQtDrain, kQtPo
 #define FB_QUEUE_BPC 2
 #endif
 constexpr int kQueueWavesPerSimd = FB_QUEUE_BPC * 8 / 4 + 1;
+// FB_QUEUE_SHARED: blocks = CUs / FB_QUEUE_SHARED_DIV (one per CU on that share of the CUs)
+#ifndef FB_QUEUE_SHARED_DIV
+#define FB_QUEUE_SHARED_DIV 8
+#endif
 hipError_t launch_parse_seg_queue(const QueueParams& q, uint32_t grid, hipStream_t s);
 hipError_t occupancy_parse_seg_queue(int* blocks_per_cu);
 

@@ -94,7 +94,7 @@ class SegQueue:
     and own IPs as they are at creation)."""
 
     def __init__(self, capture, depth=8, idle_ms=0, shared=False):
-        """shared: FB_QUEUE_SHARED -- one workgroup per CU, leaving room for the context's table
+        """shared: FB_QUEUE_SHARED -- one workgroup on each of an eighth of the CUs, leaving the rest to the context's table
         update kernels beside the resident parse (a loop applying each completed batch to the table)."""
         self._lib = N.gpu_lib()
         q = self._lib.fb_seg_queue_create_ex(capture.ctx, int(depth), int(idle_ms),

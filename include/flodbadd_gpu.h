@@ -480,8 +480,9 @@ int fb_parse_classify_seg_batches_dev(fb_ctx* ctx, const fb_seg_batch* batches, 
 #define FB_QUEUE_MAX_SUBMISSIONS (0xFFFFFFFFull - FB_QUEUE_MAX_DEPTH)
 typedef struct fb_seg_queue fb_seg_queue;
 fb_seg_queue* fb_seg_queue_create(fb_ctx* ctx, uint32_t depth /* 1..FB_QUEUE_MAX_DEPTH, 0 = 8 */, uint32_t idle_ms);
-/* FB_QUEUE_SHARED: the kernel takes ONE workgroup per CU instead of two, leaving room on every CU
- * for the session-table update kernels, so a host can apply each completed batch to the context's
+/* FB_QUEUE_SHARED: the kernel takes one workgroup on each of an eighth of the CUs (instead of two on
+ * every CU), leaving the rest of the device to the session-table update kernels (K2's two 80-KB
+ * workgroups need a CU's whole LDS), so a host can apply each completed batch to the context's
  * table (fb_flow_update_seg_dev on the batch's d_out / d_seg, on a stream of its own) while the
  * queue keeps parsing -- one batch per call WITH the upsert.  The update must then allocate nothing
  * (hipFree would wait for the queue): create the context with FB_CFG_FIXED_TABLE and
