@@ -1514,7 +1514,7 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
     p.ent = p.rec_part ? c->ent_buf : nullptr;                                  // (with its update entries)
     p.char_call = c->d_char_call;
     c->part_recs = nullptr;
-    if (c->timed) {  // the capture-time pass's scratch (K2 writes each record's slot into it)
+    if (c->timed) {  // the capture-time pass's scratch (K2 writes its sort input into it)
         const uint32_t slots = p.max_recs < n_slots ? p.max_recs : n_slots;
         uint32_t bits = 0;
         while ((1ull << bits) < c->table_cap) ++bits;
@@ -1529,7 +1529,8 @@ static int flow_update(fb_ctx* c, const fb_pkt_out* d_recs, const uint32_t* d_se
                 return set_err(FB_ERR_NOMEM, "capture-time scratch (%llu bytes)", (unsigned long long)need);
             c->tscratch_bytes = need;
         }
-        p.tslot = time_slot_array(c->d_tscratch);
+        p.tkv = time_key_array(c->d_tscratch);
+        HIP_TRY(launch_time_prepare(c->d_tscratch, slots, s));
         p.hot = nullptr;  // no combined entries: every record is a plain entry K2 places
     }
     HIP_TRY(launch_flow_bucket(p, chunks, s_bucket));

@@ -1255,11 +1255,15 @@ __global__ __launch_bounds__(kFlowK2Threads, 2 * kFlowK2Threads / 256) void k_fl
                         r < 0 ? 0u
                               : P.ent ? hist_word(sl, hist_code((fe[3].z >> 16) & 1u, fe[3].z & 0xFFu), fe[3].y)
                                       : hist_word(sl, v0);
-                    if (P.tslot) {  // timed contexts: the record slot's table slot for the capture-time pass
-                        // (an update entry's record slot: its segment's 64 slots + its rank, unit 0 word 7)
+                    if (P.tkv) {  // timed contexts: the capture-time pass's sort input at the record slot
+                        // (an update entry's record slot: its segment's 64 slots + its rank, unit 0 word 7):
+                        // table slot << 32 | pkt_index << 1 | PSH (TCP with flags)
                         const uint32_t rs = P.ent ? ((v0 & kEntUnitMask) / kUpdUnitsPerSeg) * 64u + (r0[1].w >> 26)
                                                   : (v0 & kEntRecMask);
-                        P.tslot[rs] = r < 0 ? ~0u : part * kFlowSlots + sl;
+                        const uint32_t hi = fe[3].z;  // hist_char | tcp_flags << 8 | has_flags << 16
+                        const bool psh = ((hi >> 16) & 1u) && (fe[2].y & 0xFFu) == 6u && ((hi >> 8) & kTcpPsh);
+                        P.tkv[rs] = (unsigned long long)(r < 0 ? ~0u : part * kFlowSlots + sl) << 32 |
+                                    (fe[3].x << 1 | (psh ? 1u : 0u));
                     }
                 }
 #pragma unroll

@@ -283,8 +283,11 @@ struct FlowParams {
                                 // K1c / K2 read instead of the records
     uint4* char_call = nullptr; // [capacity] per slot: the update call of the flow's first S, s, H, h
                                 // (FB_CALL_NONE: none), for the multi-GPU merge (fb_flow_merge_dev)
-    uint32_t* tslot = nullptr;  // timed contexts: [record slots] K2 writes each applied record's table slot
-                                // (~0u: not taken); K1c's combining is off then (every record a plain entry)
+    unsigned long long* tkv = nullptr;  // timed contexts: [record slots] K2 writes at each applied
+                                // record's slot its table slot << 32 | pkt_index << 1 | PSH (~0u slot: not
+                                // taken) -- the capture-time pass's sort input, in record (= packet) order
+                                // (K2's own entry order is not: K1's scatter is not stable inside a
+                                // chunk); K1c's combining is off then (every record a plain entry)
     uint32_t* order = nullptr;  // [parts + kK2Lead + 1] K2's partition order: per partition its entries
                                 // (K1t's sums; bit 31: one of K2's leading workgroups takes it), the
                                 // leading partitions, their count (zeroed by K1)
@@ -579,7 +582,10 @@ hipError_t launch_merge(const fb_flow_mrec* in, unsigned long long n, fb_flow_re
 // (its record slots, n_slots of them), brings each touched flow's FlowTime forward; ts = the batch's
 // capture timestamps by frame index; scratch: time_scratch_bytes(n_slots, log2(cap)).
 uint64_t time_scratch_bytes(uint32_t n_slots, uint32_t cap_bits);
-uint32_t* time_slot_array(void* scratch);  // the scratch's first array: FlowParams::tslot of the update
+// the scratch's sort input (FlowParams::tkv, written by K2); launch_time_prepare marks every record
+// slot "no flow" before K2 (invalid slots and non-SESSION records get no entry)
+unsigned long long* time_key_array(void* scratch);
+hipError_t launch_time_prepare(void* scratch, uint32_t n_slots, hipStream_t s);
 hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t cap, FlowTime* plane,
                               const unsigned long long* ts, void* scratch, hipStream_t s);
 hipError_t launch_time_remap(const FlowTime* old, const uint32_t* remap, unsigned long long old_cap, FlowTime* nw,

@@ -23,19 +23,19 @@
 // inputs -- scan A: the latest reset / end in the run at or before it, the run's ends so far, its
 // head; scan B: the accepted interarrival sum and the latest accepted term with its divisor -- and
 // the run's last packet writes the flow's new FlowTime:
-//   k_time_keys  one thread per record slot: its table slot (K2 wrote it per applied record:
-//                FlowParams::tslot; K1c's combining is off on a timed context, so every record is a
-//                plain entry), sort key = slot (cap: no flow -> sorts last), value = pkt_index << 1 | P
-//                (from the record or update entry)
-//   sort         rocPRIM LSD radix sort of (slot, value) pairs over log2(cap) + 1 bits (stable: the
-//                packet order inside a slot stays)
+//   K2           writes the sort input at each applied record's slot (FlowParams::tkv): table slot
+//                << 32 | pkt_index << 1 | P; record slots without an entry keep launch_time_prepare's
+//                "no flow" word (~0: sorts last).  K1c's combining is off on a timed context, so every
+//                record is a plain entry
+//   sort         rocPRIM LSD radix sort of the 64-bit words on bits [32, 32 + log2(cap) + 1) (stable:
+//                the packet order inside a slot stays)
 //   k_time_runs  ONE launch over tiles of 1,024 sorted packets taken in ticket order: per packet its
 //                time, T / in / end / reset (its predecessor's `in` from the packet before that),
 //                scan A (thread, wave, block, then the tile's prefix by decoupled look-back), the
 //                interarrival term, scan B the same way, and the runs' last packets write the plane
 //                (start / end from the table's positions of this call)
-// Bytes per record: K2's 4-B slot store, the record's flags / pkt_index (8 of its 56 / 32 B) + 4 B of
-// slot in, 8 B of sort key and value out; the sort 3 passes x 16 B; the fused pass 8 B in + the timestamp gathers
+// Bytes per record: K2's 8-B sort input store (one per record, at its record slot); the sort 3 passes
+// x 16 B; the gather 8 B in, 8 B random, 8 B out; the fused pass 16 B in + the timestamp gathers
 // (8 B, up to four per packet, mostly cached) -- an auxiliary pass, not the headline path.
 #include <cstring>  // (rocPRIM's texture-cache iterator needs memset declared)
 
@@ -92,48 +92,6 @@ __device__ __forceinline__ SegB segB_op(const SegB& x, const SegB& y) {
 constexpr uint8_t kFP = 1u, kFT = 2u, kFIn = 4u, kFHead = 8u, kFIns = 16u, kFEnd = 32u, kFInPrev = 64u, kFReset = 128u;
 
 }  // namespace
-
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kTmThreads) void k_time_keys(const FlowParams P, uint32_t n, uint32_t cap,
-                                                          uint32_t* keys, uint32_t* vals) {
-    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t nrec = batch_records(P);
-    bool ok = i < nrec;
-    uint32_t pkt = 0u, flags = 0u, proto = 0u;
-    bool has_flags = false;
-    if (ok && P.rec_part) {  // update entries of the fused parse (fb_internal.h UpdEnt): unit 0 only
-        ok = !P.seg || (i & 63u) < (P.seg[i >> 6] & 0xFFFFu);
-        if (ok) {
-            const uint32_t pw = P.rec_part[i];
-            const uint4* u = P.ent + (size_t)((i >> 6) * kUpdUnitsPerSeg + ((pw >> kRecUnitShift) & 127u)) * 2u;
-            const uint4 A = u[0], B = u[1];
-            proto = A.w & 0xFFu;
-            pkt = B.z;
-            flags = (B.w >> 8) & 0xFFu;
-            has_flags = (B.w >> 16) & 1u;
-        }
-    } else if (ok) {
-        ok = slot_valid(P, i);
-        if (ok) {
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(P.recs + i);
-            proto = q[9] & 0xFFu;           // protocol byte of the key (offset 36)
-            const uint2 m = ld_u2(q + 12);  // flags | meta << 8 | hist_char << 16, pkt_index
-            flags = m.x & 0xFFu;
-            has_flags = (m.x >> 8) & FB_META_HAS_FLAGS;
-            pkt = m.y;
-        }
-    }
-    uint32_t key = cap, val = 0u;
-    if (ok) {
-        const uint32_t sl = P.tslot[i];  // the record's table slot, written by K2 (~0u: not taken)
-        const bool psh = has_flags && proto == 6u && (flags & kTcpPsh);
-        key = sl < cap ? sl : cap;
-        val = pkt << 1 | (psh ? 1u : 0u);
-    }
-    keys[i] = key;
-    vals[i] = val;
-}
 
 // ---------------------------------------------------------------------------------------------
 // The fused pass over the sorted packets (one launch, tiles of kRunTile packets taken in ticket order,
@@ -250,19 +208,22 @@ __device__ V lookback(const RunStatus& S, uint32_t t, uint32_t off, Op op) {
 
 // The capture time of sorted packet j: gathered once into sorted order (k_time_gather), so the fused
 // pass reads it coalesced (a packet reads its own and its two predecessors').
-__device__ __forceinline__ unsigned long long t_of(const uint32_t* vals, const unsigned long long* tsort, uint32_t j) {
-    (void)vals;
-    return tsort[j];
-}
+__device__ __forceinline__ unsigned long long t_of(const unsigned long long* tsort, uint32_t j) { return tsort[j]; }
 
-__global__ __launch_bounds__(kTmThreads) void k_time_gather(const uint32_t* keys, const uint32_t* vals, uint32_t n,
-                                                            uint32_t cap, const unsigned long long* ts,
-                                                            unsigned long long* tsort) {
+__global__ __launch_bounds__(kTmThreads) void k_time_gather(const unsigned long long* kv, uint32_t n, uint32_t cap,
+                                                            const unsigned long long* ts, unsigned long long* tsort) {
     const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i < n) tsort[i] = keys[i] < cap ? ts[vals[i] >> 1] : 0ull;
+    if (i < n) {
+        const unsigned long long w = kv[i];
+        tsort[i] = (uint32_t)(w >> 32) < cap ? ts[(uint32_t)w >> 1] : 0ull;
+    }
 }
 
-__global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys, const uint32_t* vals, uint32_t n,
+// the sorted words: table slot (>= cap: no flow), pkt_index << 1 | P
+#define TKEY(i) ((uint32_t)(kv[(i)] >> 32))
+#define TVAL(i) ((uint32_t)kv[(i)])
+
+__global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long long* kv, uint32_t n,
                                                           uint32_t cap, const FlowSlot* T, FlowTime* plane,
                                                           const unsigned long long* ts, const unsigned long long* tsort,
                                                           uint32_t batch, RunStatus S) {
@@ -280,14 +241,14 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
 
     // element j's (T, in, insert) given its predecessor element (or the plane at a run head)
     auto state = [&](uint32_t j, uint32_t sj, bool hd, unsigned long long tj, bool& T_, bool& in_, bool& ins_) {
-        const bool P_ = vals[j] & 1u;
+        const bool P_ = TVAL(j) & 1u;
         unsigned long long tprev;
         if (hd) {
-            ins_ = T[sj].first_seen == (pos_hi | (vals[j] >> 1));  // the flow's insert is this packet
+            ins_ = T[sj].first_seen == (pos_hi | (TVAL(j) >> 1));  // the flow's insert is this packet
             tprev = ins_ ? tj : plane[sj].last_activity_ns;
         } else {
             ins_ = false;
-            tprev = t_of(vals, tsort, j - 1u);
+            tprev = t_of(tsort, j - 1u);
         }
         T_ = !ins_ && ms_between(tj, tprev) >= (long long)FB_SEGMENT_TIMEOUT_MS;
         in_ = ins_ ? !P_ : (T_ || !P_);
@@ -300,24 +261,24 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
 #pragma unroll
     for (uint32_t k = 0; k < kRunItems; ++k) {
         const uint32_t i = base + k;
-        key[k] = i < n ? keys[i] : cap;
+        key[k] = i < n ? TKEY(i) : cap;
         fl[k] = 0u;
         tt[k] = 0ull;
         xa[k] = SegA{0u, 0u, 0u, 0u};
         if (key[k] >= cap) continue;  // (no flow: sorts last, a neutral word)
         const uint32_t s = key[k];
-        const bool head = i == 0u || keys[i - 1u] != s;
-        const unsigned long long t = t_of(vals, tsort, i);
+        const bool head = i == 0u || TKEY(i - 1u) != s;
+        const unsigned long long t = t_of(tsort, i);
         bool Ti, ini, insi, in_prev;
         state(i, s, head, t, Ti, ini, insi);
         if (head) {
             in_prev = insi ? false : plane[s].in_segment != 0u;
         } else {
             bool T1, in1, ins1;
-            state(i - 1u, s, i == 1u || keys[i - 2u] != s, t_of(vals, tsort, i - 1u), T1, in1, ins1);
+            state(i - 1u, s, i == 1u || TKEY(i - 2u) != s, t_of(tsort, i - 1u), T1, in1, ins1);
             in_prev = in1;
         }
-        const bool P_ = vals[i] & 1u;
+        const bool P_ = TVAL(i) & 1u;
         const bool end = insi ? P_ : (P_ || (in_prev && Ti));
         const bool reset = insi || Ti || !in_prev;
         tt[k] = t;
@@ -400,12 +361,12 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
         const bool head = fl[k] & kFHead;
         const SegA prev = head ? SegA{0u, 0u, 0u, 0u} : xa[k];  // the run's state before packet i
         unsigned long long prev_end = FB_SEEN_NONE;
-        if (prev.e) prev_end = t_of(vals, tsort, prev.e - 1u);
+        if (prev.e) prev_end = t_of(tsort, prev.e - 1u);
         else if (!ins_run) prev_end = plane[s].last_segment_end_ns;
         if (prev_end == FB_SEEN_NONE) continue;
         unsigned long long start;  // current_segment_start as of packet i (src/packets.rs:151-154)
         if (!(fl[k] & kFInPrev)) start = tt[k];
-        else if (prev.r) start = t_of(vals, tsort, prev.r - 1u);
+        else if (prev.r) start = t_of(tsort, prev.r - 1u);
         else start = plane[s].current_segment_start_ns;
         const long long ia_ms = ms_between(start, prev_end);
         if (ia_ms < 0) continue;  // (double)ia / 1000.0 >= 0.0, src/packets.rs:165
@@ -463,14 +424,14 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
     for (uint32_t k = 0; k < kRunItems; ++k) {
         const uint32_t i = base + k;
         const uint32_t s = key[k];
-        if (s >= cap || (i + 1u < n && keys[i + 1u] == s)) continue;
+        if (s >= cap || (i + 1u < n && TKEY(i + 1u) == s)) continue;
         const SegA a = ia[k];
         const SegB b = segB_op(preb, ib[k]);
         const uint32_t H = (a.h & ~kInsRun) - 1u;
         const bool ins = a.h & kInsRun;
         FlowTime o;
         if (ins) {
-            o.start_time_ns = t_of(vals, tsort, H);
+            o.start_time_ns = t_of(tsort, H);
             o.end_time_ns = FB_SEEN_NONE;
             o.current_segment_start_ns = o.start_time_ns;
             o.last_segment_end_ns = FB_SEEN_NONE;
@@ -481,8 +442,8 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* keys,
             o = plane[s];
         }
         o.segment_count += a.c;
-        if (a.r) o.current_segment_start_ns = t_of(vals, tsort, a.r - 1u);
-        if (a.e) o.last_segment_end_ns = t_of(vals, tsort, a.e - 1u);
+        if (a.r) o.current_segment_start_ns = t_of(tsort, a.r - 1u);
+        if (a.e) o.last_segment_end_ns = t_of(tsort, a.e - 1u);
         o.total_segment_interarrival_ms += b.s;
         if (b.a) o.segment_interarrival_div = b.d & ~kBHead;
         o.last_activity_ns = tt[k];
@@ -538,7 +499,7 @@ __global__ __launch_bounds__(256) void k_time_export(const FlowSlot* T, const Fl
 
 // ---------------------------------------------------------------------------------------------
 struct TimeScratch {
-    uint32_t *tslot, *keys, *keys2, *vals, *vals2;
+    unsigned long long *kv, *kv2;
     unsigned long long* tsort;
     RunStatus st;
     uint32_t tiles;
@@ -549,15 +510,15 @@ static size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
     size_t a = 0;
-    rocprim::radix_sort_pairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                              (uint32_t*)nullptr, n, 0u, bits, (hipStream_t)0);
+    rocprim::radix_sort_keys(nullptr, a, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n, 32u,
+                             32u + bits, (hipStream_t)0);
     return a;
 }
 
 uint64_t time_scratch_bytes(uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
     const size_t tiles = (m + kRunTile - 1) / kRunTile;
-    return al256(m * 4) * 5 + al256(m * 8) + al256(tiles * 64) + al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
+    return al256(m * 8) * 3 + al256(tiles * 64) + al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
 }
 
 static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
@@ -566,11 +527,8 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     auto take = [&](size_t b) { char* q = p; p += al256(b); return q; };
     TimeScratch s;
     s.tiles = (uint32_t)((m + kRunTile - 1) / kRunTile);
-    s.tslot = (uint32_t*)take(m * 4);  // (first: time_slot_array)
-    s.keys = (uint32_t*)take(m * 4);
-    s.keys2 = (uint32_t*)take(m * 4);
-    s.vals = (uint32_t*)take(m * 4);
-    s.vals2 = (uint32_t*)take(m * 4);
+    s.kv = (unsigned long long*)take(m * 8);  // (first: time_key_array)
+    s.kv2 = (unsigned long long*)take(m * 8);
     s.tsort = (unsigned long long*)take(m * 8);
     s.st.w = (unsigned long long*)take(s.tiles * 64ull);
     s.st.ticket = (uint32_t*)take(8);
@@ -579,7 +537,10 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     return s;
 }
 
-uint32_t* time_slot_array(void* scratch) { return static_cast<uint32_t*>(scratch); }
+unsigned long long* time_key_array(void* scratch) { return static_cast<unsigned long long*>(scratch); }
+hipError_t launch_time_prepare(void* scratch, uint32_t n_slots, hipStream_t s) {
+    return n_slots ? hipMemsetAsync(scratch, 0xFF, (size_t)n_slots * 8u, s) : hipSuccess;  // "no flow"
+}
 
 hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t cap, FlowTime* plane,
                               const unsigned long long* ts, void* scratch, hipStream_t st) {
@@ -589,17 +550,15 @@ hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t ca
     const uint32_t c = (uint32_t)cap;  // (<= 2^25: the sort key's "no flow" value is cap itself)
     TimeScratch s = carve(scratch, n_slots, bits);
     const uint32_t g = (n_slots + kTmThreads - 1u) / kTmThreads;
-    hipLaunchKernelGGL(k_time_keys, dim3(g), dim3(kTmThreads), 0, st, p, n_slots, c, s.keys, s.vals);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e;
     size_t tb = s.tmp_bytes;
-    e = rocprim::radix_sort_pairs(s.tmp, tb, s.keys, s.keys2, s.vals, s.vals2, n_slots, 0u, bits + 1u, st);
+    e = rocprim::radix_sort_keys(s.tmp, tb, s.kv, s.kv2, n_slots, 32u, 32u + bits + 1u, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_gather, dim3(g), dim3(kTmThreads), 0, st, s.keys2, s.vals2, n_slots, c, ts, s.tsort);
+    hipLaunchKernelGGL(k_time_gather, dim3(g), dim3(kTmThreads), 0, st, s.kv2, n_slots, c, ts, s.tsort);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipMemsetAsync(s.st.w, 0, s.tiles * 64ull, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(s.st.ticket, 0, 8, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.keys2, s.vals2, n_slots, c, p.table,
+    hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.kv2, n_slots, c, p.table,
                        plane, ts, s.tsort, p.batch, s.st);
     return hipGetLastError();
 }
