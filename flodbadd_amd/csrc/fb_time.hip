@@ -29,7 +29,7 @@
 //                record is a plain entry
 //   sort         rocPRIM LSD radix sort of the 64-bit words on bits [32, 32 + log2(cap) + 1) (stable:
 //                the packet order inside a slot stays)
-//   k_time_runs  ONE launch over tiles of 1,024 sorted packets taken in ticket order: per packet its
+//   k_time_runs  ONE launch over tiles of 2,048 sorted packets taken in ticket order: per packet its
 //                time, T / in / end / reset (its predecessor's `in` from the packet before that),
 //                scan A (thread, wave, block, then the tile's prefix by decoupled look-back), the
 //                interarrival term, scan B the same way, and the runs' last packets write the plane
@@ -104,7 +104,7 @@ constexpr uint8_t kFP = 1u, kFT = 2u, kFIn = 4u, kFHead = 8u, kFIns = 16u, kFEnd
 // half of the value: a reader takes a value only when both of its words carry the status, so no
 // release / acquire fence is needed (on gfx950 an agent-scope release writes back, and an acquire
 // invalidates, the XCD's L2 -- per tile, that made this pass ~8x slower than its memory traffic).
-constexpr uint32_t kRunThreads = 256, kRunItems = 4, kRunTile = kRunThreads * kRunItems;
+constexpr uint32_t kRunThreads = 512, kRunItems = 4, kRunTile = kRunThreads * kRunItems;
 constexpr unsigned long long kStAgg = 1ull, kStInc = 2ull;
 
 struct RunStatus {  // per tile 8 words: A aggregate, A inclusive, B aggregate, B inclusive (zeroed per launch)
@@ -239,49 +239,67 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
     const uint32_t base = tile * kRunTile + tid * kRunItems;
     const unsigned long long pos_hi = (unsigned long long)batch << 32;
 
-    // element j's (T, in, insert) given its predecessor element (or the plane at a run head)
-    auto state = [&](uint32_t j, uint32_t sj, bool hd, unsigned long long tj, bool& T_, bool& in_, bool& ins_) {
-        const bool P_ = TVAL(j) & 1u;
-        unsigned long long tprev;
-        if (hd) {
-            ins_ = T[sj].first_seen == (pos_hi | (TVAL(j) >> 1));  // the flow's insert is this packet
-            tprev = ins_ ? tj : plane[sj].last_activity_ns;
-        } else {
-            ins_ = false;
-            tprev = t_of(tsort, j - 1u);
-        }
-        T_ = !ins_ && ms_between(tj, tprev) >= (long long)FB_SEGMENT_TIMEOUT_MS;
-        in_ = ins_ ? !P_ : (T_ || !P_);
-    };
-
+    // Per packet i: its T / in / insert and its predecessor's `in` (from the packet before that, or the
+    // plane at a run head).  The loads go out together first -- key words, times and, for a packet at
+    // run position 0 or 1, the slot's first_seen and plane words, none behind another -- then the flags
+    // are computed (a timing-only split of this pass put ~35 % of it in the plane / table round trips).
     uint32_t key[kRunItems];
     uint8_t fl[kRunItems];
     unsigned long long tt[kRunItems];
     SegA xa[kRunItems];
+    unsigned long long tp[kRunItems], tpp[kRunItems], fs[kRunItems], la[kRunItems];
+    uint32_t vv[kRunItems], vp[kRunItems];
+    uint8_t pos[kRunItems], isg[kRunItems];  // run position: 0 head, 1 after the head, 2 later
 #pragma unroll
     for (uint32_t k = 0; k < kRunItems; ++k) {
         const uint32_t i = base + k;
         key[k] = i < n ? TKEY(i) : cap;
+        const uint32_t s = key[k];
+        const bool ok = s < cap;
+        const bool head = ok && (i == 0u || TKEY(i - 1u) != s);
+        const bool head1 = ok && !head && (i == 1u || TKEY(i - 2u) != s);
+        pos[k] = head ? 0u : head1 ? 1u : 2u;
+        tt[k] = ok ? t_of(tsort, i) : 0ull;
+        vv[k] = ok ? TVAL(i) : 0u;
+        tp[k] = ok && !head ? t_of(tsort, i - 1u) : 0ull;
+        vp[k] = ok && !head ? TVAL(i - 1u) : 0u;
+        tpp[k] = ok && !head && !head1 ? t_of(tsort, i - 2u) : 0ull;
+        const bool need = ok && (head || head1);
+        fs[k] = need ? T[s].first_seen : 0ull;
+        la[k] = need ? plane[s].last_activity_ns : 0ull;
+        isg[k] = need ? plane[s].in_segment : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kRunItems; ++k) {
+        const uint32_t i = base + k;
         fl[k] = 0u;
-        tt[k] = 0ull;
         xa[k] = SegA{0u, 0u, 0u, 0u};
         if (key[k] >= cap) continue;  // (no flow: sorts last, a neutral word)
-        const uint32_t s = key[k];
-        const bool head = i == 0u || TKEY(i - 1u) != s;
-        const unsigned long long t = t_of(tsort, i);
+        const bool head = pos[k] == 0u;
+        const unsigned long long t = tt[k];
+        const bool P_ = vv[k] & 1u;
         bool Ti, ini, insi, in_prev;
-        state(i, s, head, t, Ti, ini, insi);
         if (head) {
-            in_prev = insi ? false : plane[s].in_segment != 0u;
+            insi = fs[k] == (pos_hi | (vv[k] >> 1));  // the flow's insert is this packet
+            Ti = !insi && ms_between(t, la[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+            ini = insi ? !P_ : (Ti || !P_);
+            in_prev = insi ? false : isg[k] != 0u;
         } else {
-            bool T1, in1, ins1;
-            state(i - 1u, s, i == 1u || TKEY(i - 2u) != s, t_of(tsort, i - 1u), T1, in1, ins1);
-            in_prev = in1;
+            insi = false;
+            Ti = ms_between(t, tp[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+            ini = Ti || !P_;
+            const bool P1 = vp[k] & 1u;
+            if (pos[k] == 1u) {  // the predecessor is the run's head
+                const bool ins1 = fs[k] == (pos_hi | (vp[k] >> 1));
+                const bool T1 = !ins1 && ms_between(tp[k], la[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+                in_prev = ins1 ? !P1 : (T1 || !P1);
+            } else {
+                const bool T1 = ms_between(tp[k], tpp[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+                in_prev = T1 || !P1;
+            }
         }
-        const bool P_ = TVAL(i) & 1u;
         const bool end = insi ? P_ : (P_ || (in_prev && Ti));
         const bool reset = insi || Ti || !in_prev;
-        tt[k] = t;
         fl[k] = (uint8_t)((P_ ? kFP : 0u) | (Ti ? kFT : 0u) | (ini ? kFIn : 0u) | (head ? kFHead : 0u) |
                           (insi ? kFIns : 0u) | (end ? kFEnd : 0u) | (in_prev ? kFInPrev : 0u) | (reset ? kFReset : 0u));
         xa[k] = SegA{head ? ((i + 1u) | (insi ? kInsRun : 0u)) : 0u, reset ? i + 1u : 0u, end ? i + 1u : 0u,
