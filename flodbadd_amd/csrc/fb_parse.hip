@@ -1419,8 +1419,8 @@ __device__ __forceinline__ uint32_t q_grab(const QueueParams& Q, uint32_t slot, 
 
 // One block at a time (whichever takes the poller word) reads the host's tail over PCIe and copies
 // the new descriptors into the device ring -- 512 blocks polling the host each had every host access
-// wait ~1 ms.  Returns the device ring's tail as this wave last saw it.  The host's stop word is read
-// before its tail (the host stores them in the other order), so a stop seen with nothing new is final.
+// wait ~1 ms.  Returns the device ring's tail as this wave last saw it.  The host stores its tail before
+// its stop word, so a stop followed (behind an acquire) by a tail with nothing new is final.
 __device__ __forceinline__ unsigned long long q_refill(const QueueParams& Q, uint32_t k) {
     const uint32_t lane = threadIdx.x & 63u, R = Q.depth;
     // Every load here is relaxed and the poller word is released relaxed: these run on every poll, and on
@@ -1452,8 +1452,14 @@ __device__ __forceinline__ unsigned long long q_refill(const QueueParams& Q, uin
         QTRACE(const unsigned long long now_ = rt_now();
                for (unsigned long long j = dt + lane; j < tl; j += 64u) *qt(Q, kQtPub, j) = now_);
         dt = tl;
-    } else if (lane == 0u && hs != 0ull) {
-        __hip_atomic_store(&Q.d->stop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (hs != 0ull) {
+        // the two relaxed loads above may have been performed in either order: a stop is final only if
+        // the tail read after it (behind an acquire, so after the stop) still has nothing new -- the
+        // host stores its last tail before the stop (shutdown only: the fence's cost is paid once)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const unsigned long long tl2 =
+            u1st64(lane == 0u ? __hip_atomic_load(&Q.h->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+        if (lane == 0u && tl2 <= dt) __hip_atomic_store(&Q.d->stop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0u) __hip_atomic_store(&Q.d->poller, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return dt;

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -u
 cd "${GRAFT_REPO_ROOT}"
-R=$(pwd); OUT=$R/gpurun_out/r6j; mkdir -p "$OUT"; export TMPDIR=/tmp
+R=$(pwd); OUT=$R/gpurun_out/${RUN:-r6j}; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_queue.py -x -v --timeout 120 --timeout-method thread -m gpu > "$OUT/tests.log" 2>&1 || { tail -30 "$OUT/tests.log"; exit 1; }
 tail -2 "$OUT/tests.log"
 cd /tmp
