@@ -326,3 +326,58 @@ def test_two_process_routed_timed_global_table(tmp_path):
         assert got.tobytes() == e_r.tobytes(), r
         assert gt.tobytes() == e_t.tobytes(), r
     assert (et["segment_count"] > 0).any() and (et["end_time_ns"] != N.FB_SEEN_NONE).any()
+
+
+def _rccl_routed_child(rank, port, outdir):
+    """The routed table over RCCL (the "nccl" backend, device tensors) at world size 1: the record
+    routing, both all_to_all_single calls with split sizes and the gathered table take the code path
+    an 8-GPU run takes, in a fresh process (its own communicator)."""
+    import torch
+    import torch.distributed as dist
+    from flodbadd_amd.capture import FlodbaddGpuCapture
+    from flodbadd_amd.distributed import RoutedSessionTable
+    from flodbadd_amd.sessions import SessionFilter
+    from test_gpu_timed import frame_times
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    cap = FlodbaddGpuCapture(0, session_filter=SessionFilter.All, flow_capacity=1 << 16, timed=True)
+    try:
+        rt = RoutedSessionTable(dist, cap, device=dev)
+        for k, size in enumerate(SIZES):
+            fr, of = _sched_batch(k, 0, size)
+            rt.process(fr, of, 0, size, ts=frame_times(size, seed=50 + k, call=k))
+        flows, times = rt.global_table(with_times=True)
+        np.save(os.path.join(outdir, "f.npy"), flows.view(np.uint8))
+        np.save(os.path.join(outdir, "t.npy"), times.view(np.uint8))
+    finally:
+        cap.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_rccl_world1_routed_timed_table(tmp_path):
+    """RoutedSessionTable over RCCL at world size 1 (device tensors through all_to_all_single with
+    split sizes): the gathered table and its capture-time records equal the timed oracle's."""
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_gpu_timed import frame_times
+    mp.start_processes(_rccl_routed_child, args=(_free_port(), str(tmp_path)), nprocs=1, start_method="spawn")
+    fl = coracle.Flows()
+    for k, size in enumerate(SIZES):
+        fr, of = _sched_batch(k, 0, size)
+        out, _, _, _ = coracle.parse_classify(coracle.make_cfg(2), fr, of)
+        fl.update(out, ts=frame_times(size, seed=50 + k, call=k))
+    er, et = fl.export_sorted(), fl.export_times()
+    got = np.load(os.path.join(tmp_path, "f.npy")).view(N.FLOW_REC_DTYPE)
+    gt = np.load(os.path.join(tmp_path, "t.npy")).view(N.FLOW_TIME_DTYPE)
+    assert len(got) == len(er) == len(gt), (len(got), len(er))
+    key = lambda a: np.lexsort(np.ascontiguousarray(a).view(np.uint8).reshape(len(a), -1)[:, :40].T[::-1])
+    o, eo = key(got), key(er)
+    got, gt, e_r, e_t = got[o].copy(), gt[o].copy(), er[eo].copy(), et[eo]
+    got["slot"] = 0
+    gt["slot"] = 0
+    e_r["slot"] = 0
+    assert got.tobytes() == e_r.tobytes()
+    assert gt.tobytes() == e_t.tobytes()
