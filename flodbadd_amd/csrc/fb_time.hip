@@ -281,20 +281,20 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
         bool Ti, ini, insi, in_prev;
         if (head) {
             insi = fs[k] == (pos_hi | (vv[k] >> 1));  // the flow's insert is this packet
-            Ti = !insi && ms_between(t, la[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+            Ti = !insi && timeout_of(t, la[k]);
             ini = insi ? !P_ : (Ti || !P_);
             in_prev = insi ? false : isg[k] != 0u;
         } else {
             insi = false;
-            Ti = ms_between(t, tp[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+            Ti = timeout_of(t, tp[k]);
             ini = Ti || !P_;
             const bool P1 = vp[k] & 1u;
             if (pos[k] == 1u) {  // the predecessor is the run's head
                 const bool ins1 = fs[k] == (pos_hi | (vp[k] >> 1));
-                const bool T1 = !ins1 && ms_between(tp[k], la[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+                const bool T1 = !ins1 && timeout_of(tp[k], la[k]);
                 in_prev = ins1 ? !P1 : (T1 || !P1);
             } else {
-                const bool T1 = ms_between(tp[k], tpp[k]) >= (long long)FB_SEGMENT_TIMEOUT_MS;
+                const bool T1 = timeout_of(tp[k], tpp[k]);
                 in_prev = T1 || !P1;
             }
         }
@@ -528,8 +528,9 @@ static size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
     size_t a = 0;
-    rocprim::radix_sort_keys(nullptr, a, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n, 32u,
-                             32u + bits, (hipStream_t)0);
+    if (rocprim::radix_sort_keys(nullptr, a, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n, 32u,
+                                 32u + bits, (hipStream_t)0) != hipSuccess)
+        a = 0;  // (the sort itself then reports the error)
     return a;
 }
 
