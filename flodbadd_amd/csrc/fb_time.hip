@@ -27,19 +27,24 @@
 //                << 32 | pkt_index << 1 | P; record slots without an entry keep launch_time_prepare's
 //                "no flow" word (~0: sorts last).  K1c's combining is off on a timed context, so every
 //                record is a plain entry
-//   sort         rocPRIM LSD radix sort of the 64-bit words on bits [32, 32 + log2(cap) + 1) (stable:
-//                the packet order inside a slot stays)
+//   sort         rocPRIM onesweep LSD radix sort of (slot << 1 | P, capture time) pairs on the slot bits
+//                (stable: the packet order inside a slot stays), its inputs read from K2's words
+//                through transform iterators -- the time is ts[pkt_index], so the sort also gathers
+//                the times into sorted order (record slots follow packet order: a near-sequential read)
 //   k_time_runs  ONE launch over tiles of 2,048 sorted packets taken in ticket order: per packet its
 //                time, T / in / end / reset (its predecessor's `in` from the packet before that),
 //                scan A (thread, wave, block, then the tile's prefix by decoupled look-back), the
 //                interarrival term, scan B the same way, and the runs' last packets write the plane
 //                (start / end from the table's positions of this call)
-// Bytes per record: K2's 8-B sort input store (one per record, at its record slot); the sort 3 passes
-// x 16 B; the gather 8 B in, 8 B random, 8 B out; the fused pass 16 B in + the timestamp gathers
-// (8 B, up to four per packet, mostly cached) -- an auxiliary pass, not the headline path.
+// Bytes per record: K2's 8-B sort input store (one per record, at its record slot); the sort's
+// histogram 8 B, its first pass 8 + 8 in (word, time) and 12 out, its second 12 + 12; the fused pass
+// 12 B in + the timestamp reads (8 B, up to four per packet, mostly cached) -- an auxiliary pass, not
+// the headline path.  The insert test needs no pkt_index: a flow whose first_seen is of this batch was
+// inserted by this call, at its run's head.
 #include <cstring>  // (rocPRIM's texture-cache iterator needs memset declared)
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "fb_internal.h"
 
@@ -206,24 +211,32 @@ __device__ V lookback(const RunStatus& S, uint32_t t, uint32_t off, Op op) {
     return acc;  // meaningful in lane 0
 }
 
-// The capture time of sorted packet j: gathered once into sorted order (k_time_gather), so the fused
+// The capture time of sorted packet j: the sort carried it beside the key (its value), so the fused
 // pass reads it coalesced (a packet reads its own and its two predecessors').
 __device__ __forceinline__ unsigned long long t_of(const unsigned long long* tsort, uint32_t j) { return tsort[j]; }
 
-__global__ __launch_bounds__(kTmThreads) void k_time_gather(const unsigned long long* kv, uint32_t n, uint32_t cap,
-                                                            const unsigned long long* ts, unsigned long long* tsort) {
-    const uint32_t i = blockIdx.x * kTmThreads + threadIdx.x;
-    if (i < n) {
-        const unsigned long long w = kv[i];
-        tsort[i] = (uint32_t)(w >> 32) < cap ? ts[(uint32_t)w >> 1] : 0ull;
+// The sort's inputs, read straight from K2's words through rocPRIM transform iterators (no pass of
+// their own): the key table slot << 1 | P (a "no flow" word's slot ~0u gives 0x7FFFFFFF, past every
+// slot: it sorts last), the value the record's capture time ts[pkt_index] (record slots follow packet
+// order, so these reads walk the timestamp array nearly in order).
+struct TimeSortKey {
+    __host__ __device__ uint32_t operator()(unsigned long long w) const {
+        return (uint32_t)(w >> 32) << 1 | ((uint32_t)w & 1u);
     }
-}
+};
+struct TimeSortTs {
+    const unsigned long long* ts;
+    uint32_t cap;
+    __host__ __device__ unsigned long long operator()(unsigned long long w) const {
+        return (uint32_t)(w >> 32) < cap ? ts[(uint32_t)w >> 1] : 0ull;
+    }
+};
 
-// the sorted words: table slot (>= cap: no flow), pkt_index << 1 | P
-#define TKEY(i) ((uint32_t)(kv[(i)] >> 32))
-#define TVAL(i) ((uint32_t)kv[(i)])
+// the sorted keys: table slot (>= cap: no flow) << 1 | P
+#define TKEY(i) (ks[(i)] >> 1)
+#define TPSH(i) (ks[(i)] & 1u)
 
-__global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long long* kv, uint32_t n,
+__global__ __launch_bounds__(kRunThreads) void k_time_runs(const uint32_t* ks, uint32_t n,
                                                           uint32_t cap, const FlowSlot* T, FlowTime* plane,
                                                           const unsigned long long* ts, const unsigned long long* tsort,
                                                           uint32_t batch, RunStatus S) {
@@ -237,7 +250,6 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint32_t base = tile * kRunTile + tid * kRunItems;
-    const unsigned long long pos_hi = (unsigned long long)batch << 32;
 
     // Per packet i: its T / in / insert and its predecessor's `in` (from the packet before that, or the
     // plane at a run head).  The loads go out together first -- key words, times and, for a packet at
@@ -248,7 +260,7 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
     unsigned long long tt[kRunItems];
     SegA xa[kRunItems];
     unsigned long long tp[kRunItems], tpp[kRunItems], fs[kRunItems], la[kRunItems];
-    uint32_t vv[kRunItems], vp[kRunItems];
+    uint8_t vv[kRunItems], vp[kRunItems];  // P of the packet and of its predecessor
     uint8_t pos[kRunItems], isg[kRunItems];  // run position: 0 head, 1 after the head, 2 later
 #pragma unroll
     for (uint32_t k = 0; k < kRunItems; ++k) {
@@ -260,12 +272,12 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
         const bool head1 = ok && !head && (i == 1u || TKEY(i - 2u) != s);
         pos[k] = head ? 0u : head1 ? 1u : 2u;
         tt[k] = ok ? t_of(tsort, i) : 0ull;
-        vv[k] = ok ? TVAL(i) : 0u;
+        vv[k] = ok ? TPSH(i) : 0u;
         tp[k] = ok && !head ? t_of(tsort, i - 1u) : 0ull;
-        vp[k] = ok && !head ? TVAL(i - 1u) : 0u;
+        vp[k] = ok && !head ? TPSH(i - 1u) : 0u;
         tpp[k] = ok && !head && !head1 ? t_of(tsort, i - 2u) : 0ull;
         const bool need = ok && (head || head1);
-        fs[k] = need ? T[s].first_seen : 0ull;
+        fs[k] = need ? T[s].first_seen : FB_SEEN_NONE;
         la[k] = need ? plane[s].last_activity_ns : 0ull;
         isg[k] = need ? plane[s].in_segment : 0u;
     }
@@ -279,8 +291,12 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
         const unsigned long long t = tt[k];
         const bool P_ = vv[k] & 1u;
         bool Ti, ini, insi, in_prev;
+        // The flow was inserted by this call exactly when its first_seen is of this batch (the update
+        // keeps a new flow's first_seen at its earliest packet), and then its insert packet is the
+        // run's head: the run holds every applied packet of the flow, in packet order.
+        const bool new_flow = (fs[k] >> 32) == (unsigned long long)batch;
         if (head) {
-            insi = fs[k] == (pos_hi | (vv[k] >> 1));  // the flow's insert is this packet
+            insi = new_flow;  // the flow's insert is this packet
             Ti = !insi && timeout_of(t, la[k]);
             ini = insi ? !P_ : (Ti || !P_);
             in_prev = insi ? false : isg[k] != 0u;
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(kRunThreads) void k_time_runs(const unsigned long l
             ini = Ti || !P_;
             const bool P1 = vp[k] & 1u;
             if (pos[k] == 1u) {  // the predecessor is the run's head
-                const bool ins1 = fs[k] == (pos_hi | (vp[k] >> 1));
+                const bool ins1 = new_flow;  // (the head inserted the flow)
                 const bool T1 = !ins1 && timeout_of(tp[k], la[k]);
                 in_prev = ins1 ? !P1 : (T1 || !P1);
             } else {
@@ -516,8 +532,38 @@ __global__ __launch_bounds__(256) void k_time_export(const FlowSlot* T, const Fl
 }
 
 // ---------------------------------------------------------------------------------------------
+// The sort: rocPRIM's onesweep LSD radix sort of (key, time) pairs on the key's slot bits [1, 2 +
+// log2(cap)), FB_TIME_RADIX_BITS per pass (11: a 2^21-slot table's 22 bits in two passes instead of
+// three at rocPRIM's default 8), tiles of 1024 x 16 pairs (2,048 digits need the larger tiles: 8
+// items per thread 1,819 us per timed 10.5M-frame C4 call, 12 1,779, 16 1,740, 20 1,757, 24 1,802,
+// 32 1,967; 8-bit digits 1,851, 10-bit 1,849; profiles/r06_timed_sort_pairs_ab.txt).
+#ifndef FB_TIME_RADIX_BITS
+#define FB_TIME_RADIX_BITS 11
+#endif
+#ifndef FB_TIME_SORT_BLOCK
+#define FB_TIME_SORT_BLOCK 1024
+#endif
+#ifndef FB_TIME_SORT_ITEMS
+#define FB_TIME_SORT_ITEMS 16
+#endif
+using TimeSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<FB_TIME_SORT_BLOCK, FB_TIME_SORT_ITEMS>,
+                                        rocprim::kernel_config<FB_TIME_SORT_BLOCK, FB_TIME_SORT_ITEMS>,
+                                        FB_TIME_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+using TimeKeyIt = rocprim::transform_iterator<const unsigned long long*, TimeSortKey, uint32_t>;
+using TimeTsIt = rocprim::transform_iterator<const unsigned long long*, TimeSortTs, unsigned long long>;
+
+static hipError_t time_sort(void* tmp, size_t& tmp_bytes, const unsigned long long* kv, uint32_t* ks,
+                            unsigned long long* tsort, const unsigned long long* ts, uint32_t cap, uint32_t n,
+                            uint32_t bits, hipStream_t st) {
+    return rocprim::radix_sort_pairs<TimeSortConfig>(tmp, tmp_bytes, TimeKeyIt(kv, TimeSortKey{}), ks,
+                                                     TimeTsIt(kv, TimeSortTs{ts, cap}), tsort, n, 1u, 1u + bits, st);
+}
+
 struct TimeScratch {
-    unsigned long long *kv, *kv2;
+    unsigned long long* kv;
+    uint32_t* ks;
     unsigned long long* tsort;
     RunStatus st;
     uint32_t tiles;
@@ -528,8 +574,7 @@ static size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
     size_t a = 0;
-    if (rocprim::radix_sort_keys(nullptr, a, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n, 32u,
-                                 32u + bits, (hipStream_t)0) != hipSuccess)
+    if (time_sort(nullptr, a, nullptr, nullptr, nullptr, nullptr, 0u, n, bits, (hipStream_t)0) != hipSuccess)
         a = 0;  // (the sort itself then reports the error)
     return a;
 }
@@ -537,7 +582,7 @@ static size_t sort_tmp_bytes(uint32_t n, uint32_t bits) {
 uint64_t time_scratch_bytes(uint32_t n, uint32_t cap_bits) {
     const size_t m = std::max<uint32_t>(n, 1u);
     const size_t tiles = (m + kRunTile - 1) / kRunTile;
-    return al256(m * 8) * 3 + al256(tiles * 64) + al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
+    return al256(m * 8) * 2 + al256(m * 4) + al256(tiles * 64) + al256(8) + al256(sort_tmp_bytes(n, cap_bits + 1u));
 }
 
 static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
@@ -547,7 +592,7 @@ static TimeScratch carve(void* base, uint32_t n, uint32_t cap_bits) {
     TimeScratch s;
     s.tiles = (uint32_t)((m + kRunTile - 1) / kRunTile);
     s.kv = (unsigned long long*)take(m * 8);  // (first: time_key_array)
-    s.kv2 = (unsigned long long*)take(m * 8);
+    s.ks = (uint32_t*)take(m * 4);
     s.tsort = (unsigned long long*)take(m * 8);
     s.st.w = (unsigned long long*)take(s.tiles * 64ull);
     s.st.ticket = (uint32_t*)take(8);
@@ -568,16 +613,13 @@ hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t ca
     while ((1ull << bits) < cap) ++bits;
     const uint32_t c = (uint32_t)cap;  // (<= 2^25: the sort key's "no flow" value is cap itself)
     TimeScratch s = carve(scratch, n_slots, bits);
-    const uint32_t g = (n_slots + kTmThreads - 1u) / kTmThreads;
     hipError_t e;
     size_t tb = s.tmp_bytes;
-    e = rocprim::radix_sort_keys(s.tmp, tb, s.kv, s.kv2, n_slots, 32u, 32u + bits + 1u, st);
+    e = time_sort(s.tmp, tb, s.kv, s.ks, s.tsort, ts, c, n_slots, bits + 1u, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_gather, dim3(g), dim3(kTmThreads), 0, st, s.kv2, n_slots, c, ts, s.tsort);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipMemsetAsync(s.st.w, 0, s.tiles * 64ull, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(s.st.ticket, 0, 8, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.kv2, n_slots, c, p.table,
+    hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.ks, n_slots, c, p.table,
                        plane, ts, s.tsort, p.batch, s.st);
     return hipGetLastError();
 }
