@@ -617,8 +617,8 @@ hipError_t launch_time_update(const FlowParams& p, uint32_t n_slots, uint64_t ca
     size_t tb = s.tmp_bytes;
     e = time_sort(s.tmp, tb, s.kv, s.ks, s.tsort, ts, c, n_slots, bits + 1u, st);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(s.st.w, 0, s.tiles * 64ull, st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(s.st.ticket, 0, 8, st)) != hipSuccess) return e;
+    // the tiles' status words and the ticket after them (carve keeps them adjacent): one memset
+    if ((e = hipMemsetAsync(s.st.w, 0, (size_t)((char*)s.st.ticket - (char*)s.st.w) + 8u, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_time_runs, dim3(s.tiles), dim3(kRunThreads), 0, st, s.ks, n_slots, c, p.table,
                        plane, ts, s.tsort, p.batch, s.st);
     return hipGetLastError();

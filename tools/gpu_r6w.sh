@@ -1,12 +1,12 @@
 #!/bin/bash
-# Timed pipelined call: parse k+1 held until K2 k (product) vs free (variant); timed tests first
+# Timed C4 pipelined call A/B: product vs variants (VARS), timed tests first, then an async kernel trace
 set -u
 cd "${GRAFT_REPO_ROOT}"
-R=$(pwd); OUT=$R/gpurun_out/r6w; mkdir -p "$OUT"; export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_timed.py tests/test_gpu_c5.py -x -q --timeout 120 --timeout-method thread > "$OUT/timed_tests.txt" 2>&1 || { tail -30 "$OUT/timed_tests.txt"; exit 1; }
+R=$(pwd); OUT=$R/gpurun_out/${RUN:-r6w}; mkdir -p "$OUT"; export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_timed.py -x -q --timeout 120 ${TESTS_K:-} --timeout-method thread > "$OUT/timed_tests.txt" 2>&1 || { tail -30 "$OUT/timed_tests.txt"; exit 1; }
 tail -2 "$OUT/timed_tests.txt"
 for rep in 1 2; do
-for v in prod free; do
+for v in ${VARS:-prod nt}; do
   if [ $v = prod ]; then L=""; else L="$R/flodbadd_amd/build/var_$v.so"; fi
   FLODBADD_GPU_LIB=$L timeout -k 10 120 python3 tools/c4_small_calls.py --frames 10485760 --calls 20 --warmup 3 --timed > "$OUT/c4t_$v.log" 2>&1 || { cat "$OUT/c4t_$v.log"; exit 1; }
   echo "$rep $v $(cat $OUT/c4t_$v.log)"
